@@ -1,0 +1,165 @@
+"""bench.py -- headline benchmark of the MI355X engine (BASELINE.json metric).
+
+Workload (BASELINE.json configs / SURVEY.md §8d "Headline"): the vert-cor.R sign family,
+MASS::mvrnorm Gaussian DGP mu=(.5,.5) sigma=(2,2), rho=0.5, eps=(1,1), n=1e5, alpha=.05,
+normalise=T, ci_mode auto (mixquant CIs), NI+INT per replicate.  One step = one fused
+launch of R replicates per GPU (+ the per-cell accumulation kernel); every step runs fresh
+replicate indices (a Monte-Carlo sweep of the cell), so nothing is cached or skipped.
+Multi-GPU: one process per GPU, replicates sharded per rank (weak scaling: R per GPU
+per step), accumulators all-gathered once at the end (the only collective).
+
+Prints ONE JSON line (rank 0).
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "distributed-correlation_amd"))
+sys.path.insert(0, ROOT)
+
+METRIC = "MC replicates/sec (Gaussian n=1e5, NI+INT CIs) at 1/8 MI355X + % roofline"
+FP64_PEAK_TFLOPS = 78.6          # MI355X FP64 vector (spec); SURVEY §8d: 3.93e13 FMA lane-ops/s
+W_SAMPLE = {"gaussian": 260, "bernoulli": 120, "bounded_factor": 292}  # SURVEY §8d pinned weights
+W_BATCH = 183
+W_REP = 2.0e5
+
+
+def work_units(cell, m, k):
+    """Pinned algorithmic work per replicate: w*n + 183*k + 2e5."""
+    return W_SAMPLE[cell.dgp] * cell.n + W_BATCH * k + W_REP
+
+
+def cpu_baseline(cell, seconds: float = 12.0):
+    """The oracle's fused restatement (C, 1 thread) on a bounded sample of the workload."""
+    import numpy as np
+    from oracle.oracle import sim_reps
+    c = cell.to_c()
+    t0 = time.perf_counter()
+    done = 0
+    while True:
+        sim_reps(c, 10_000_000 + done, 10_000_000 + done + 2, threads=1)
+        done += 2
+        el = time.perf_counter() - t0
+        if el >= seconds or done >= 2000:
+            break
+    return {"value": done / el, "unit": "replicates/s", "cores": 1, "kind": "port",
+            "sample": f"{done} replicates of the headline cell (n={cell.n}) in {el:.1f} s, "
+                      "oracle/dcor_oracle.c fused restatement, 1 thread (mclapply granularity: "
+                      "one core per cell)"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--reps", type=int, default=8192, help="replicates per GPU per step")
+    ap.add_argument("--n", type=int, default=100_000)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+
+    import dcor
+    from dcor import _lib
+    from dcor.dist import gather_accums, merge_ranked
+    from dcor.sim import accum_from_bytes, accumulate, finalize, headline_cell, simulate
+
+    cell = headline_cell(args.n)
+    k, m = dcor.api.batch_geometry(cell.n, cell.eps1, cell.eps2, "sign")
+    R = args.reps
+    stream = torch.cuda.current_stream()
+    buf = torch.empty((R, 6), dtype=torch.float64, device="cuda")
+    accs = []
+
+    def step(s):
+        r0 = (s * world + rank) * R
+        simulate(cell, R, r0, out=buf, stream=stream)
+        return accumulate(buf, cell.rho, stream=stream)
+
+    for s in range(args.warmup):
+        step(1_000_000 + s)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(args.steps)]
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for s in range(args.steps):
+        ev[s][0].record(stream)
+        r0 = (s * world + rank) * R
+        simulate(cell, R, r0, out=buf, stream=stream)
+        ev[s][1].record(stream)
+        accs.append(accumulate(buf, cell.rho, stream=stream))
+    host = [accum_from_bytes(a.cpu().numpy().tobytes()) for a in accs]
+    local_acc = [merge_from(host, 0), merge_from(host, 1)]
+    if world > 1:
+        merged = merge_ranked(gather_accums(local_acc))
+    else:
+        merged = local_acc
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    kern_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
+
+    total_reps = R * args.steps * world
+    value = total_reps / el
+    W = work_units(cell, m, k)
+    achieved = R * W * 2.0 / (kern_ms * 1e-3) / 1e12  # fp64-equivalent TFLOP/s per GPU
+    summ = {"NI": finalize(merged[0], cell.rho), "INT": finalize(merged[1], cell.rho)}
+
+    if rank == 0:
+        res = {
+            "metric": METRIC, "value": value, "unit": "replicates/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": el * 1e3 / args.steps,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic (on-device Philox draws of the reference DGP)",
+            "config": {"workload": "vert-cor.R sign family, Gaussian mvrnorm mu=(.5,.5) sigma=(2,2), "
+                                   "rho=.5, eps=(1,1), NI+INT CIs (mixquant)",
+                       "n": cell.n, "m": m, "k": k, "replicates_per_gpu_per_step": R,
+                       "parallelism": f"replicate-shard x{world}"},
+            "roofline": {"bound": "valu_fp64", "achieved": achieved, "peak": FP64_PEAK_TFLOPS,
+                         "unit": "TFLOP/s", "frac": achieved / FP64_PEAK_TFLOPS, "traffic": None,
+                         "kernel": "k_sign_fused", "kernel_ms_avg": kern_ms,
+                         "work_units_per_rep": W,
+                         "note": "achieved = R * W_rep(SURVEY §8d pinned weights) * 2 / kernel time"},
+            "summary": {"coverage_NI": summ["NI"]["coverage"], "coverage_INT": summ["INT"]["coverage"],
+                        "ci_len_NI": summ["NI"]["ci_length"], "ci_len_INT": summ["INT"]["ci_length"]},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            res["cpu_baseline"] = cpu_baseline(cell, args.cpu_seconds)
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def merge_from(host, meth):
+    from dcor.sim import merge
+    return merge([h[meth] for h in host])
+
+
+if __name__ == "__main__":
+    main()

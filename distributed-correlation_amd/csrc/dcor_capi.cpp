@@ -1,0 +1,645 @@
+// dcor_capi.cpp -- host side of the C-ABI declared in include/dcor.h.
+//
+// Validates arguments the way the reference's stopifnot() calls do, evaluates every
+// data-independent scalar of the estimators once (R operation order, cited), and
+// launches the gfx950 kernels.  There is no CPU compute path: without a visible
+// device every compute entry fails with DCOR_ENODEV.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <vector>
+
+#include "../../include/dcor.h"
+#include "dcor_engine.h"
+
+using namespace dcor;
+
+namespace {
+
+thread_local char g_err[512] = "";
+
+int fail(int code, const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+  return code;
+}
+
+int hip_fail(hipError_t e, const char* what) {
+  return fail(DCOR_EHIP, "%s: %s", what, hipGetErrorString(e));
+}
+
+#define HIPCHK(expr)                                   \
+  do {                                                 \
+    hipError_t e_ = (expr);                            \
+    if (e_ != hipSuccess) return hip_fail(e_, #expr);  \
+  } while (0)
+
+int need_device() {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) {
+    (void)hipGetLastError();
+    return fail(DCOR_ENODEV, "no HIP device visible: the dcor engine has no CPU path");
+  }
+  return DCOR_OK;
+}
+
+double r_min(double a, double b) { return (std::isnan(a) || std::isnan(b)) ? NAN : (a < b ? a : b); }
+double r_max(double a, double b) { return (std::isnan(a) || std::isnan(b)) ? NAN : (a > b ? a : b); }
+
+struct DevBuf {  // RAII device allocation for the host-pointer entry points
+  void* p = nullptr;
+  ~DevBuf() { if (p) (void)hipFree(p); }
+  hipError_t alloc(size_t bytes) { return hipMalloc(&p, bytes ? bytes : 8); }
+  template <class T> T* as() const { return static_cast<T*>(p); }
+};
+
+template <class T>
+int upload(DevBuf& b, const T* h, size_t count) {
+  HIPCHK(b.alloc(sizeof(T) * count));
+  if (h && count) HIPCHK(hipMemcpy(b.p, h, sizeof(T) * count, hipMemcpyHostToDevice));
+  else if (count) HIPCHK(hipMemset(b.p, 0, sizeof(T) * count));
+  return DCOR_OK;
+}
+
+// MixConst for sort(x)[ceiling(p*nsim)], p = 1 - alpha/2.
+int make_mix(int64_t nsim, double alpha, MixConst& mx) {
+  if (nsim < 1 || nsim > 2048) return fail(DCOR_EINVAL, "nsim must be in [1, 2048] (got %lld)", (long long)nsim);
+  const double pos = std::ceil((1.0 - alpha / 2.0) * (double)nsim);
+  mx.nsim = (int32_t)nsim;
+  mx.pos = (pos >= 1 && pos <= (double)nsim) ? (int32_t)pos - 1 : -1;
+  mx.P = 1;
+  while (mx.P < mx.nsim) mx.P <<= 1;
+  mx.pad = 0;
+  return DCOR_OK;
+}
+
+// MASS::mvrnorm factor A = V diag(sqrt(ev)) of the 2x2 covariance (vert-cor.R:389-394).
+void mvrnorm_factor(const double sigma[2], double rho, double A[4]) {
+  const double s11 = sigma[0] * sigma[0];
+  const double s12 = sigma[0] * sigma[1] * rho;
+  const double s22 = sigma[1] * sigma[1];
+  const double mid = (s11 + s22) / 2.0, hd = (s11 - s22) / 2.0;
+  const double d = std::sqrt(hd * hd + s12 * s12);
+  const double l1 = mid + d, l2 = mid - d;
+  double v0, v1;
+  if (s12 == 0.0) {
+    if (s11 > s22) { v0 = 1.0; v1 = 0.0; } else { v0 = 0.0; v1 = 1.0; }
+  } else {
+    if (s11 >= s22) { v0 = l1 - s22; v1 = s12; } else { v0 = s12; v1 = l1 - s11; }
+    const double nr = std::sqrt(v0 * v0 + v1 * v1);
+    v0 /= nr; v1 /= nr;
+    if (v1 < 0) { v0 = -v0; v1 = -v1; }
+  }
+  const double a1 = std::sqrt(l1 > 0 ? l1 : 0.0), a2 = std::sqrt(l2 > 0 ? l2 : 0.0);
+  A[0] = v0 * a1; A[1] = -v1 * a2;
+  A[2] = v1 * a1; A[3] = v0 * a2;
+}
+
+int make_dgp(const dcor_cell& c, DgpConst& g) {
+  std::memset(&g, 0, sizeof(g));
+  g.dgp = c.dgp;
+  if (c.dgp == DCOR_DGP_GAUSSIAN) {
+    double A[4];
+    mvrnorm_factor(c.sigma, c.rho, A);
+    g.mu0 = c.mu[0]; g.mu1 = c.mu[1];
+    g.a00 = A[0]; g.a01 = A[1]; g.a10 = A[2]; g.a11 = A[3];
+  } else if (c.dgp == DCOR_DGP_BERNOULLI) {
+    if (!(std::fabs(c.rho) <= 1)) return fail(DCOR_EINVAL, "gen_bernoulli: |rho| <= 1 required (vert-cor.R:79)");
+    const double p11 = 0.25 + c.rho / 4, p10 = 0.25 - c.rho / 4, p01 = p10;  // vert-cor.R:80-83
+    g.thr0 = p01 / 0.5; g.thr1 = p11 / 0.5;
+  } else if (c.dgp == DCOR_DGP_BOUNDED_FACTOR) {
+    if (!(c.rho >= 0 && c.rho <= 1)) return fail(DCOR_EINVAL, "gen_bounded_factor: rho in [0,1] required");
+    g.cU = std::sqrt(3.0 * c.rho); g.cE = std::sqrt(3.0 * (1.0 - c.rho));  // ver-cor-subG.R:148-149
+    g.cU2 = g.cU - -g.cU; g.cE2 = g.cE - -g.cE;
+  } else {
+    return fail(DCOR_EINVAL, "unknown dgp %d", c.dgp);
+  }
+  return DCOR_OK;
+}
+
+int check_common(int64_t n, double eps1, double eps2, double alpha) {
+  if (n < 1 || n > 0x7fffffffLL) return fail(DCOR_EINVAL, "n must be in [1, 2^31) (got %lld)", (long long)n);
+  if (!(eps1 > 0) || !(eps2 > 0) || !std::isfinite(eps1) || !std::isfinite(eps2))
+    return fail(DCOR_EINVAL, "eps1 > 0 and eps2 > 0 required (vert-cor.R:264)");
+  if (!(alpha > 0 && alpha < 1)) return fail(DCOR_EINVAL, "alpha must be in (0,1)");
+  return DCOR_OK;
+}
+
+// ci_NI_signbatch + ci_INT_signflip scalars (vert-cor.R:204-317).
+// allow_k0: INT-only single calls (ci_INT_signflip has no batch requirement).
+int make_sign(int64_t n, double eps1, double eps2, double alpha, int normalise, int mode,
+              int64_t nsim, bool allow_k0, SignConst& c) {
+  std::memset(&c, 0, sizeof(c));
+  if (int st = check_common(n, eps1, eps2, alpha)) return st;
+  const double nd = (double)n;
+  const double md = std::ceil(8.0 / (eps1 * eps2));                     // :207
+  const double kd = std::floor(nd / md);                                 // :208
+  if (!(kd >= 1) && !allow_k0)
+    return fail(DCOR_EKLT1, "ci_NI_signbatch: k = floor(n/m) = %g < 1 (n=%lld, m=%g; vert-cor.R:209)", kd, (long long)n, md);
+  if (md > 0x7fffffff) return fail(DCOR_EINVAL, "batch size m too large");
+  c.n = n; c.m = (int32_t)md; c.k = kd >= 1 ? (int64_t)kd : 0;
+  c.nd = nd; c.md = md; c.kd = kd;
+  c.normalise = normalise ? 1 : 0;
+  const double L = std::sqrt(2.0 * std::log(nd));                        // :212
+  c.L = L;
+  c.s_mu_x = 2.0 * L / (nd * (eps1 / 2));                                // :335-336
+  c.s_m2_x = 2.0 * (L * L) / (nd * (eps1 / 2));                          // :339-340
+  c.s_mu_y = 2.0 * L / (nd * (eps2 / 2));
+  c.s_m2_y = 2.0 * (L * L) / (nd * (eps2 / 2));
+  c.bx = 2.0 / (md * eps1);                                              // :230
+  c.by = 2.0 / (md * eps2);                                              // :231
+  c.inv_k = 1.0 / kd;                                                    // :234
+  c.crit = dcor_qnorm(1.0 - alpha / 2.0);                                // :242
+  c.sqrt_k = std::sqrt(kd);
+  c.sender_is_X = (eps1 >= eps2) ? 1 : 0;                                // :275
+  const double eps_s = c.sender_is_X ? eps1 : eps2, eps_r = c.sender_is_X ? eps2 : eps1;
+  const double es = std::exp(eps_s);
+  c.pflip = es / (es + 1.0);                                             // :174
+  c.scale_Z = 2.0 * (es + 1.0) / (nd * (es - 1.0) * eps_r);              // :186-187
+  c.coefZ = (es + 1.0) / (nd * (es - 1.0));                              // :190-191
+  const double q = (es - 1.0) / (es + 1.0);
+  c.q2 = q * q;                                                          // :284
+  c.ratio = (es + 1.0) / (es - 1.0);                                     // :289
+  c.inv_sqrt_n = 1.0 / std::sqrt(nd);
+  c.eps_r = eps_r;
+  c.w_laplace = (2.0 / (nd * eps_r)) * c.ratio * std::log(1.0 / alpha);  // :305-308
+  int md_ = mode;
+  if (md_ == DCOR_MODE_AUTO) md_ = (std::sqrt(nd) * eps_r > 0.5) ? DCOR_MODE_NORMAL : DCOR_MODE_LAPLACE;  // :294-296
+  else if (md_ != DCOR_MODE_NORMAL && md_ != DCOR_MODE_LAPLACE) return fail(DCOR_EINVAL, "ci_mode must be auto/normal/laplace");
+  c.mode_normal = (md_ == DCOR_MODE_NORMAL) ? 1 : 0;
+  if (int st = make_mix(nsim, alpha, c.mix)) return st;
+  return DCOR_OK;
+}
+
+// correlation_NI_subG + ci_INT_subG scalars (ver-cor-subG.R:25-108; HRS variant
+// real-data-sims.R:115-147,176-252 when hrs).
+int make_subg(int64_t n, double eps1, double eps2, double eta1, double eta2, double alpha,
+              int hrs, double lam_x, double lam_y, double lam_s, double lam_o, double lam_r,
+              double delta, int64_t nsim, SubgConst& c, double* lo_out, double* crit_sqrt2_s) {
+  std::memset(&c, 0, sizeof(c));
+  if (int st = check_common(n, eps1, eps2, alpha)) return st;
+  if (hrs && n < 2) return fail(DCOR_EINVAL, "n >= 2 required (real-data-sims.R:121)");
+  const double nd = (double)n;
+  c.n = n; c.nd = nd;
+  c.l1 = (hrs && !std::isnan(lam_x)) ? lam_x : dcor_lambda_n(nd, eta1);  // :30 / rds:123
+  c.l2 = (hrs && !std::isnan(lam_y)) ? lam_y : dcor_lambda_n(nd, eta2);
+  double md = std::ceil(8.0 / (eps1 * eps2));                            // :37
+  if (md > nd) md = nd;
+  double kd = std::floor(nd / md);                                       // :38
+  if (hrs) {
+    if (kd < 2) { kd = 2; md = std::floor(nd / kd); }                    // rds:130
+  } else if (!(kd >= 1)) {
+    return fail(DCOR_EKLT1, "correlation_NI_subG: k < 1 (ver-cor-subG.R:38)");
+  }
+  c.m = (int32_t)md; c.k = (int64_t)kd; c.md = md; c.kd = kd;
+  c.bx = 2.0 * c.l1 / (md * eps1);                                       // :48
+  c.by = 2.0 * c.l2 / (md * eps2);                                       // :49
+  c.m_over_k = md / kd;                                                  // :51
+  c.crit = dcor_qnorm(1.0 - alpha / 2.0);                                // :57
+  c.sqrt_k = std::sqrt(kd);
+  c.sender_is_X = (eps1 >= eps2) ? 1 : 0;                                // :76
+  const double eps_s = c.sender_is_X ? eps1 : eps2, eps_r = c.sender_is_X ? eps2 : eps1;
+  const double eta_s = c.sender_is_X ? eta1 : eta2, eta_r = c.sender_is_X ? eta2 : eta1;
+  double lo_ = NAN;
+  if (!hrs) {
+    double lam[2];
+    dcor_lambda_int_n(nd, eta_s, eta_r, eps_s, lam);                     // :83-85
+    c.ls = lam[0]; c.lr = lam[1];
+  } else {
+    const double dl = std::isnan(delta) ? 1.0 / nd : delta;              // rds:199
+    double ls = lam_s;
+    lo_ = lam_o;
+    if (std::isnan(ls) || std::isnan(lo_)) {                             // rds:202-208
+      double lam[2];
+      dcor_lambda_int_n(nd, eta_s, eta_r, eps_s, lam);
+      if (std::isnan(ls)) ls = lam[0];
+      if (std::isnan(lo_)) lo_ = dcor_lambda_n(nd, c.sender_is_X ? eta2 : eta1);
+    }
+    double lr = lam_r;
+    if (std::isnan(lr)) lr = dcor_lambda_receiver_from_noise(ls, lo_, eps_s, dl);  // rds:211-218
+    c.ls = ls; c.lr = lr;
+  }
+  c.bs = 2.0 * c.ls / (eps_s);                                           // :89
+  c.s_central = 2.0 * c.lr / (nd * eps_r);                               // :91
+  c.sn2x2 = 2.0 * (c.s_central * c.s_central);                           // :99
+  c.sqrt_n = std::sqrt(nd);
+  c.eps_r = eps_r;
+  if (lo_out) *lo_out = lo_;
+  if (crit_sqrt2_s) *crit_sqrt2_s = c.crit * std::sqrt(2.0) * (2.0 * c.lr / (nd * eps_r));  // rds:238
+  if (int st = make_mix(nsim, alpha, c.mix)) return st;
+  return DCOR_OK;
+}
+
+}  // namespace
+
+// ===================================================================== ABI
+extern "C" {
+
+const char* dcor_version(void) { return "dcor-mi355x 0.1.0 (gfx950)"; }
+
+int dcor_last_error(char* buf, size_t len) {
+  if (buf && len) {
+    std::strncpy(buf, g_err, len - 1);
+    buf[len - 1] = 0;
+  }
+  return (int)std::strlen(g_err);
+}
+
+int dcor_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) { (void)hipGetLastError(); return 0; }
+  return n;
+}
+
+double dcor_lambda_n(double n, double eta) {  // ver-cor-subG.R:1
+  return r_min(2.0 * eta * std::sqrt(std::log(n)), 2.0 * std::sqrt(3.0));
+}
+
+void dcor_lambda_int_n(double n, double eta_s, double eta_r, double eps_s, double out[2]) {
+  out[0] = r_min(2.0 * eta_s * std::sqrt(std::log(n)), 2.0 * std::sqrt(3.0));  // ver-cor-subG.R:4
+  out[1] = 5.0 * r_max(eta_r, 1.0) * r_min(std::log(n), 6.0) / (r_min(eps_s, 1.0));  // :5
+}
+
+double dcor_lambda_receiver_from_noise(double lam_s, double lam_o, double eps_s, double delta) {
+  const double b_s = 2.0 * lam_s / eps_s;  // real-data-sims.R:172
+  return (lam_s + b_s * std::log(1.0 / delta)) * lam_o;
+}
+
+double dcor_lambda_from_priv(double lo, double hi, double mean, double sd) {
+  const double sig = r_max(sd, 1e-8);  // real-data-sims.R:104
+  return r_max(std::fabs((lo - mean) / sig), std::fabs((hi - mean) / sig));
+}
+
+double dcor_qnorm(double p) {
+  // Lower-tail solve on min(p, 1-p): Abramowitz-Stegun 26.2.23 start, Halley on erfc.
+  if (std::isnan(p) || p < 0 || p > 1) return NAN;
+  if (p == 0) return -INFINITY;
+  if (p == 1) return INFINITY;
+  const double pp = (p < 0.5) ? p : 1.0 - p;
+  const double t = std::sqrt(-2.0 * std::log(pp));
+  double x = -(t - (2.515517 + 0.802853 * t + 0.010328 * t * t) /
+                       (1.0 + 1.432788 * t + 0.189269 * t * t + 0.001308 * t * t * t));
+  for (int it = 0; it < 6; ++it) {
+    const double e = 0.5 * std::erfc(-x / 1.4142135623730951) - pp;
+    const double u = e * 2.5066282746310002 * std::exp(0.5 * x * x);
+    x = x - u / (1.0 + 0.5 * x * u);
+  }
+  return (p < 0.5) ? x : -x;
+}
+
+int dcor_batch_geometry(int64_t n, double eps1, double eps2, int family, int hrs, int64_t km[2]) {
+  const double nd = (double)n;
+  double md = std::ceil(8.0 / (eps1 * eps2));
+  if (family == DCOR_FAMILY_SUBG && md > nd) md = nd;
+  double kd = std::floor(nd / md);
+  if (family == DCOR_FAMILY_SUBG && hrs && kd < 2) { kd = 2; md = std::floor(nd / kd); }
+  km[0] = (int64_t)kd; km[1] = (int64_t)md;
+  if (!(kd >= 1)) return fail(DCOR_EKLT1, "k = floor(n/m) < 1");
+  return DCOR_OK;
+}
+
+int dcor_sim_launch(const dcor_cell* cell, int64_t rep_begin, int64_t rep_count,
+                    dcor_rep_out* d_out, void* stream) {
+  if (!cell || (rep_count > 0 && !d_out)) return fail(DCOR_EINVAL, "null argument");
+  if (rep_begin < 0 || rep_count < 0 || rep_begin + rep_count > 0xffffffffLL)
+    return fail(DCOR_EINVAL, "replicate range must lie in [0, 2^32)");
+  if (rep_count > 0x7fffffffLL) return fail(DCOR_EINVAL, "rep_count too large for one launch");
+  if (int st = need_device()) return st;
+  const dcor_cell& c = *cell;
+  DgpConst g;
+  if (int st = make_dgp(c, g)) return st;
+  int rc;
+  if (c.family == DCOR_FAMILY_SIGN) {
+    SignConst k;
+    if (int st = make_sign(c.n, c.eps1, c.eps2, c.alpha, c.normalise, c.ci_mode, c.nsim, false, k)) return st;
+    k.g = g; k.rep_begin = rep_begin;
+    k.k0 = (uint32_t)c.seed; k.k1 = (uint32_t)(c.seed >> 32);
+    rc = launch_sign_fused(k, rep_count, d_out, stream);
+  } else if (c.family == DCOR_FAMILY_SUBG) {
+    SubgConst k;
+    if (int st = make_subg(c.n, c.eps1, c.eps2, c.eta1, c.eta2, c.alpha, 0, NAN, NAN, NAN, NAN,
+                           NAN, NAN, c.nsim, k, nullptr, nullptr)) return st;
+    k.g = g; k.rep_begin = rep_begin;
+    k.k0 = (uint32_t)c.seed; k.k1 = (uint32_t)(c.seed >> 32);
+    rc = launch_subg_fused(k, rep_count, d_out, stream);
+  } else {
+    return fail(DCOR_EINVAL, "unknown family %d", c.family);
+  }
+  if (rc) return hip_fail((hipError_t)rc, "sim kernel launch");
+  return DCOR_OK;
+}
+
+int dcor_accumulate_launch(const dcor_rep_out* d_out, int64_t count, double rho,
+                           dcor_accum* d_acc, void* stream) {
+  if (!d_acc || (count > 0 && !d_out) || count < 0) return fail(DCOR_EINVAL, "bad accumulate arguments");
+  if (int st = need_device()) return st;
+  const int rc = launch_accumulate(d_out, count, rho, d_acc, stream);
+  if (rc) return hip_fail((hipError_t)rc, "accumulate launch");
+  return DCOR_OK;
+}
+
+static void dd_add_host(double* a, const double* b) {  // a += b (double-double)
+  auto two_sum = [](double x, double y, double& s, double& e) {
+    s = x + y;
+    const double bb = s - x;
+    e = (x - (s - bb)) + (y - bb);
+  };
+  double s, e, t, f;
+  two_sum(a[0], b[0], s, e);
+  two_sum(a[1], b[1], t, f);
+  e += t;
+  double s2, e2;
+  two_sum(s, e, s2, e2);
+  e2 += f;
+  two_sum(s2, e2, a[0], a[1]);
+}
+
+void dcor_accum_merge(dcor_accum* dst, const dcor_accum* src) {
+  dst->n += src->n; dst->n_cover += src->n_cover; dst->n_cover_na += src->n_cover_na;
+  dst->n_na_est += src->n_na_est; dst->n_na_ci += src->n_na_ci;
+  dd_add_host(dst->est, src->est); dd_add_host(dst->est2, src->est2);
+  dd_add_host(dst->se2, src->se2); dd_add_host(dst->len, src->len);
+  dd_add_host(dst->lo, src->lo); dd_add_host(dst->hi, src->hi);
+}
+
+void dcor_accum_finalize(const dcor_accum* a, double rho, dcor_summary* out) {
+  // vert-cor.R:422-430: mse = mean(se2), bias = mean(est) - rho, var = var(est),
+  // coverage = mean(cover), ci_length = mean(up - lo); NA propagates like R's mean/var.
+  const double n = (double)a->n;
+  const long double est = (long double)a->est[0] + a->est[1];
+  const long double est2 = (long double)a->est2[0] + a->est2[1];
+  const bool nae = a->n_na_est > 0, nac = a->n_na_ci > 0;
+  out->mse = nae || a->n == 0 ? NAN : (double)(((long double)a->se2[0] + a->se2[1]) / n);
+  out->bias = nae || a->n == 0 ? NAN : (double)(est / n) - rho;
+  out->var = (nae || a->n < 2) ? NAN : (double)((est2 - est * est / n) / (n - 1));
+  out->coverage = (a->n_cover_na > 0 || a->n == 0) ? NAN : (double)a->n_cover / n;
+  out->ci_length = nac || a->n == 0 ? NAN : (double)(((long double)a->len[0] + a->len[1]) / n);
+}
+
+int dcor_grid_run(const dcor_cell* cells, int ncells, int64_t B, dcor_accum* h_acc,
+                  dcor_rep_out* h_detail) {
+  if (!cells || ncells < 0 || B < 1 || !h_acc) return fail(DCOR_EINVAL, "bad grid arguments");
+  if (int st = need_device()) return st;
+  DevBuf out, acc;
+  HIPCHK(out.alloc(sizeof(dcor_rep_out) * (size_t)B));
+  HIPCHK(acc.alloc(sizeof(dcor_accum) * 2));
+  for (int i = 0; i < ncells; ++i) {
+    if (int st = dcor_sim_launch(&cells[i], 0, B, out.as<dcor_rep_out>(), nullptr)) return st;
+    if (int st = dcor_accumulate_launch(out.as<dcor_rep_out>(), B, cells[i].rho,
+                                        acc.as<dcor_accum>(), nullptr)) return st;
+    HIPCHK(hipMemcpy(h_acc + 2 * i, acc.p, sizeof(dcor_accum) * 2, hipMemcpyDeviceToHost));
+    if (h_detail)
+      HIPCHK(hipMemcpy(h_detail + (size_t)i * B, out.p, sizeof(dcor_rep_out) * (size_t)B,
+                       hipMemcpyDeviceToHost));
+  }
+  return DCOR_OK;
+}
+
+int dcor_premat_sign_launch(const dcor_premat_sign* d, dcor_rep_out* d_out, void* stream) {
+  if (!d || !d_out || d->reps < 0) return fail(DCOR_EINVAL, "null argument");
+  if (!d->X || !d->Y || !d->lap_ni_sc || !d->lap_ni_x || !d->lap_ni_y || !d->lap_int_sc ||
+      !d->flips || !d->lap_z || !d->mix_z || !d->mix_l)
+    return fail(DCOR_EINVAL, "premat_sign: every input array is required");
+  if (int st = need_device()) return st;
+  PrematSignConst p;
+  std::memset(&p, 0, sizeof(p));
+  if (int st = make_sign(d->n, d->eps1, d->eps2, d->alpha, d->normalise, d->ci_mode, d->nsim,
+                         false, p.s)) return st;
+  p.X = d->X; p.Y = d->Y; p.xy_stride = d->xy_stride;
+  p.lap_ni_sc = d->lap_ni_sc; p.lap_ni_x = d->lap_ni_x; p.lap_ni_y = d->lap_ni_y;
+  p.lap_int_sc = d->lap_int_sc; p.flips = d->flips; p.flip_words = (d->n + 31) / 32;
+  p.lap_z = d->lap_z; p.mix_z = d->mix_z; p.mix_l = d->mix_l;
+  const int rc = launch_premat_sign(p, d->reps, d_out, stream);
+  if (rc) return hip_fail((hipError_t)rc, "premat_sign launch");
+  return DCOR_OK;
+}
+
+static int premat_subg_const(const dcor_premat_subg* d, PrematSubgConst& p) {
+  std::memset(&p, 0, sizeof(p));
+  if (int st = make_subg(d->n, d->eps1, d->eps2, d->eta1, d->eta2, d->alpha, d->hrs, d->lam_x,
+                         d->lam_y, d->lam_s, d->lam_o, d->lam_r, d->delta, d->nsim, p.s, &p.lo_,
+                         &p.crit_sqrt2_s)) return st;
+  p.hrs = d->hrs ? 1 : 0;
+  p.X = d->X; p.Y = d->Y; p.xy_stride = d->xy_stride; p.perm = d->perm;
+  p.lap_ni_x = d->lap_ni_x; p.lap_ni_y = d->lap_ni_y; p.lap_local = d->lap_local;
+  p.lap_central = d->lap_central; p.mix_z = d->mix_z; p.mix_l = d->mix_l;
+  return DCOR_OK;
+}
+
+int dcor_premat_subg_launch(const dcor_premat_subg* d, dcor_rep_out* d_out, void* stream) {
+  if (!d || !d_out || d->reps < 0) return fail(DCOR_EINVAL, "null argument");
+  if (!d->X || !d->Y || !d->lap_ni_x || !d->lap_ni_y || !d->lap_local || !d->lap_central ||
+      !d->mix_z || !d->mix_l)
+    return fail(DCOR_EINVAL, "premat_subg: every input array except perm is required");
+  if (int st = need_device()) return st;
+  PrematSubgConst p;
+  if (int st = premat_subg_const(d, p)) return st;
+  const int rc = launch_premat_subg(p, d->reps, d_out, stream);
+  if (rc) return hip_fail((hipError_t)rc, "premat_subg launch");
+  return DCOR_OK;
+}
+
+// ------------------------------------------- single-call host-pointer forms
+static int run_premat_sign_1(const double* X, const double* Y, int64_t n, double eps1,
+                             double eps2, double alpha, int normalise, int mode, bool int_only,
+                             const double* lap_ni_sc, const double* lap_x, const double* lap_y,
+                             const double* lap_int_sc, const uint8_t* flips, double lap_z,
+                             const double* mix_z, const double* mix_l, int64_t nsim,
+                             dcor_rep_out* res) {
+  if (!X || !Y) return fail(DCOR_EINVAL, "X and Y are required");
+  if (int st = need_device()) return st;
+  PrematSignConst p;
+  std::memset(&p, 0, sizeof(p));
+  if (int st = make_sign(n, eps1, eps2, alpha, normalise, mode, nsim > 0 ? nsim : 1, int_only, p.s)) return st;
+  const int64_t k = p.s.k;
+  std::vector<uint32_t> fw((size_t)((n + 31) / 32), 0u);
+  if (flips)
+    for (int64_t i = 0; i < n; ++i) if (flips[i]) fw[(size_t)(i >> 5)] |= (1u << (i & 31));
+  DevBuf bX, bY, bnsc, blx, bly, bisc, bfl, bz, bmz, bml, bout;
+  if (int st = upload(bX, X, (size_t)n)) return st;
+  if (int st = upload(bY, Y, (size_t)n)) return st;
+  if (int st = upload(bnsc, lap_ni_sc, 4)) return st;
+  if (int st = upload(blx, lap_x, (size_t)k)) return st;
+  if (int st = upload(bly, lap_y, (size_t)k)) return st;
+  if (int st = upload(bisc, lap_int_sc, 4)) return st;
+  if (int st = upload(bfl, fw.data(), fw.size())) return st;
+  if (int st = upload(bz, &lap_z, 1)) return st;
+  const size_t ns = (size_t)p.s.mix.nsim;
+  if (int st = upload(bmz, mix_z, mix_z ? ns : ns)) return st;
+  if (int st = upload(bml, mix_l, ns)) return st;
+  HIPCHK(bout.alloc(sizeof(dcor_rep_out)));
+  p.X = bX.as<double>(); p.Y = bY.as<double>(); p.xy_stride = 0;
+  p.lap_ni_sc = bnsc.as<double>(); p.lap_ni_x = blx.as<double>(); p.lap_ni_y = bly.as<double>();
+  p.lap_int_sc = bisc.as<double>(); p.flips = bfl.as<uint32_t>(); p.flip_words = (n + 31) / 32;
+  p.lap_z = bz.as<double>(); p.mix_z = bmz.as<double>(); p.mix_l = bml.as<double>();
+  const int rc = launch_premat_sign(p, 1, bout.as<dcor_rep_out>(), nullptr);
+  if (rc) return hip_fail((hipError_t)rc, "premat_sign launch");
+  HIPCHK(hipMemcpy(res, bout.p, sizeof(dcor_rep_out), hipMemcpyDeviceToHost));
+  return DCOR_OK;
+}
+
+int dcor_ci_ni_signbatch(const double* X, const double* Y, int64_t n, double eps1, double eps2,
+                         double alpha, int normalise, const double lap_sc[4],
+                         const double* lap_x, const double* lap_y, double out[3]) {
+  if (!out || !lap_x || !lap_y || (normalise && !lap_sc)) return fail(DCOR_EINVAL, "null argument");
+  dcor_rep_out r;
+  if (int st = run_premat_sign_1(X, Y, n, eps1, eps2, alpha, normalise, DCOR_MODE_LAPLACE, false,
+                                 lap_sc, lap_x, lap_y, lap_sc, nullptr, 0.0, nullptr, nullptr, 1, &r))
+    return st;
+  out[0] = r.ni_hat; out[1] = r.ni_lo; out[2] = r.ni_hi;
+  return DCOR_OK;
+}
+
+int dcor_ci_int_signflip(const double* X, const double* Y, int64_t n, double eps1, double eps2,
+                         double alpha, int mode, int normalise, const double lap_sc[4],
+                         const uint8_t* flips, double lap_z, const double* mix_z,
+                         const double* mix_l, int64_t nsim, double out[3]) {
+  if (!out || !flips || (normalise && !lap_sc)) return fail(DCOR_EINVAL, "null argument");
+  dcor_rep_out r;
+  if (int st = run_premat_sign_1(X, Y, n, eps1, eps2, alpha, normalise, mode, true, lap_sc,
+                                 nullptr, nullptr, lap_sc, flips, lap_z, mix_z, mix_l, nsim, &r))
+    return st;
+  out[0] = r.int_hat; out[1] = r.int_lo; out[2] = r.int_hi;
+  return DCOR_OK;
+}
+
+static int run_premat_subg_1(const double* X, const double* Y, int64_t n, double eps1,
+                             double eps2, double eta1, double eta2, double alpha, int hrs,
+                             double lam_x, double lam_y, double lam_s, double lam_o,
+                             double lam_r, double delta, const int32_t* perm,
+                             const double* lap_x, const double* lap_y, const double* lap_local,
+                             double lap_central, const double* mix_z, const double* mix_l,
+                             int64_t nsim, dcor_rep_out* res) {
+  if (!X || !Y) return fail(DCOR_EINVAL, "X and Y are required");
+  if (int st = need_device()) return st;
+  dcor_premat_subg d;
+  std::memset(&d, 0, sizeof(d));
+  d.n = n; d.reps = 1; d.eps1 = eps1; d.eps2 = eps2; d.eta1 = eta1; d.eta2 = eta2; d.alpha = alpha;
+  d.hrs = hrs; d.lam_x = lam_x; d.lam_y = lam_y; d.lam_s = lam_s; d.lam_o = lam_o;
+  d.lam_r = lam_r; d.delta = delta; d.nsim = nsim > 0 ? nsim : 1;
+  PrematSubgConst p;
+  if (int st = premat_subg_const(&d, p)) return st;
+  const int64_t k = p.s.k, m = p.s.m;
+  DevBuf bX, bY, bp, blx, bly, bll, bc, bmz, bml, bout;
+  if (int st = upload(bX, X, (size_t)n)) return st;
+  if (int st = upload(bY, Y, (size_t)n)) return st;
+  if (perm) { if (int st = upload(bp, perm, (size_t)(k * m))) return st; }
+  if (int st = upload(blx, lap_x, (size_t)k)) return st;
+  if (int st = upload(bly, lap_y, (size_t)k)) return st;
+  if (int st = upload(bll, lap_local, (size_t)n)) return st;
+  if (int st = upload(bc, &lap_central, 1)) return st;
+  const size_t ns = (size_t)p.s.mix.nsim;
+  if (int st = upload(bmz, mix_z, ns)) return st;
+  if (int st = upload(bml, mix_l, ns)) return st;
+  HIPCHK(bout.alloc(sizeof(dcor_rep_out)));
+  p.X = bX.as<double>(); p.Y = bY.as<double>(); p.xy_stride = 0;
+  p.perm = perm ? bp.as<int32_t>() : nullptr;
+  p.lap_ni_x = blx.as<double>(); p.lap_ni_y = bly.as<double>(); p.lap_local = bll.as<double>();
+  p.lap_central = bc.as<double>(); p.mix_z = bmz.as<double>(); p.mix_l = bml.as<double>();
+  const int rc = launch_premat_subg(p, 1, bout.as<dcor_rep_out>(), nullptr);
+  if (rc) return hip_fail((hipError_t)rc, "premat_subg launch");
+  HIPCHK(hipMemcpy(res, bout.p, sizeof(dcor_rep_out), hipMemcpyDeviceToHost));
+  return DCOR_OK;
+}
+
+int dcor_correlation_ni_subg(const double* X, const double* Y, int64_t n, double eps1,
+                             double eps2, double eta1, double eta2, double alpha, int hrs,
+                             double lam_x, double lam_y, const int32_t* perm,
+                             const double* lap_x, const double* lap_y, double out[3]) {
+  if (!out || !lap_x || !lap_y) return fail(DCOR_EINVAL, "null argument");
+  dcor_rep_out r;
+  if (int st = run_premat_subg_1(X, Y, n, eps1, eps2, eta1, eta2, alpha, hrs, lam_x, lam_y, NAN,
+                                 NAN, NAN, NAN, perm, lap_x, lap_y, nullptr, 0.0, nullptr,
+                                 nullptr, 1, &r)) return st;
+  out[0] = r.ni_hat; out[1] = r.ni_lo; out[2] = r.ni_hi;
+  return DCOR_OK;
+}
+
+int dcor_ci_int_subg(const double* X, const double* Y, int64_t n, double eps1, double eps2,
+                     double eta1, double eta2, double alpha, int hrs, double lam_s,
+                     double lam_o, double lam_r, double delta, const double* lap_local,
+                     double lap_central, const double* mix_z, const double* mix_l,
+                     int64_t nsim, double out[3]) {
+  if (!out || !lap_local || !mix_z || !mix_l) return fail(DCOR_EINVAL, "null argument");
+  dcor_rep_out r;
+  if (int st = run_premat_subg_1(X, Y, n, eps1, eps2, eta1, eta2, alpha, hrs, NAN, NAN, lam_s,
+                                 lam_o, lam_r, delta, nullptr, nullptr, nullptr, lap_local,
+                                 lap_central, mix_z, mix_l, nsim, &r)) return st;
+  out[0] = r.int_hat; out[1] = r.int_lo; out[2] = r.int_hi;
+  return DCOR_OK;
+}
+
+int dcor_mixquant(const double* z, const double* l, int64_t nsim, double c, double p,
+                  double* out) {
+  if (!z || !l || !out) return fail(DCOR_EINVAL, "null argument");
+  if (nsim < 1 || nsim > 2048) return fail(DCOR_EINVAL, "nsim must be in [1, 2048]");
+  if (int st = need_device()) return st;
+  const double pos = std::ceil(p * (double)nsim);  // ceiling(p*nsim)
+  const int32_t ip = (pos >= 1 && pos <= (double)nsim) ? (int32_t)pos - 1 : -1;
+  DevBuf bz, bl, bo;
+  if (int st = upload(bz, z, (size_t)nsim)) return st;
+  if (int st = upload(bl, l, (size_t)nsim)) return st;
+  HIPCHK(bo.alloc(sizeof(double)));
+  const int rc = launch_mixquant(bz.as<double>(), bl.as<double>(), (int32_t)nsim, c, ip,
+                                 bo.as<double>(), nullptr);
+  if (rc) return hip_fail((hipError_t)rc, "mixquant launch");
+  HIPCHK(hipMemcpy(out, bo.p, sizeof(double), hipMemcpyDeviceToHost));
+  return DCOR_OK;
+}
+
+int dcor_priv_standardize(const double* v, int64_t n, double eps_norm, double L_raw,
+                          const double lap[2], double* out) {
+  if (!v || !lap || !out || n < 1) return fail(DCOR_EINVAL, "bad argument");
+  if (int st = need_device()) return st;
+  const double nd = (double)n;
+  const double s_mu = 2.0 * L_raw / (nd * (eps_norm / 2));           // vert-cor.R:336
+  const double s_m2 = 2.0 * (L_raw * L_raw) / (nd * (eps_norm / 2));  // vert-cor.R:340
+  DevBuf bv, bl, bo;
+  if (int st = upload(bv, v, (size_t)n)) return st;
+  if (int st = upload(bl, lap, 2)) return st;
+  HIPCHK(bo.alloc(sizeof(double) * (size_t)n));
+  const int rc = launch_priv_standardize(bv.as<double>(), n, L_raw, s_mu, s_m2, bl.as<double>(),
+                                         bo.as<double>(), nullptr);
+  if (rc) return hip_fail((hipError_t)rc, "priv_standardize launch");
+  HIPCHK(hipMemcpy(out, bo.p, sizeof(double) * (size_t)n, hipMemcpyDeviceToHost));
+  return DCOR_OK;
+}
+
+int dcor_dp_sd(const double* x, int64_t n, double lo, double hi, double eps1, double eps2,
+               const double lap[2], double out[2]) {
+  if (!x || !lap || !out || n < 1) return fail(DCOR_EINVAL, "bad argument");
+  if (int st = need_device()) return st;
+  const double nd = (double)n;
+  const double s_mu = (hi - lo) / (nd * eps1);                // real-data-sims.R:69
+  const double s_m2 = (hi * hi - lo * lo) / (nd * eps2);      // real-data-sims.R:80
+  DevBuf bx, bl, bo;
+  if (int st = upload(bx, x, (size_t)n)) return st;
+  if (int st = upload(bl, lap, 2)) return st;
+  HIPCHK(bo.alloc(sizeof(double) * 2));
+  const int rc = launch_dp_sd(bx.as<double>(), n, lo, hi, s_mu, s_m2, bl.as<double>(),
+                              bo.as<double>(), nullptr);
+  if (rc) return hip_fail((hipError_t)rc, "dp_sd launch");
+  HIPCHK(hipMemcpy(out, bo.p, sizeof(double) * 2, hipMemcpyDeviceToHost));
+  return DCOR_OK;
+}
+
+int dcor_draws_launch(int kind, uint64_t seed, int site, int64_t rep_begin, int64_t reps,
+                      int64_t count, double* d_out, void* stream) {
+  if (kind < 0 || kind > 2 || reps < 0 || count < 0 || (reps * count > 0 && !d_out))
+    return fail(DCOR_EINVAL, "bad draws arguments");
+  if (reps > 65535) return fail(DCOR_EINVAL, "draws: at most 65535 replicates per launch");
+  if (rep_begin < 0 || rep_begin + reps > 0xffffffffLL || (count + 1) / 2 > 0xffffffffLL)
+    return fail(DCOR_EINVAL, "draws: counter range exceeds 2^32");
+  if (int st = need_device()) return st;
+  const int rc = launch_draws(kind, (uint32_t)seed, (uint32_t)(seed >> 32), (uint32_t)site,
+                              rep_begin, reps, count, d_out, stream);
+  if (rc) return hip_fail((hipError_t)rc, "draws launch");
+  return DCOR_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,296 @@
+// dcor_device.h -- gfx950 device primitives for the DP-correlation Monte-Carlo engine.
+//
+//  * Philox4x32-10 counter RNG (key = per-cell seed, counter = (index, rep, site, 0)),
+//    the draw-site contract of include/dcor.h.
+//  * Uniform / normal / Laplace transforms in fp64 built only from IEEE basic ops and
+//    explicit fma(), compiled with -ffp-contract=off, so a draw is a pure function of
+//    (seed, rep, site, index) -- identical on any GPU count and reproducible bit for bit
+//    by the CPU restatement in oracle/.
+//  * Wave64 / workgroup reductions (DPP shuffles + LDS), double-double accumulators.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define DCOR_BLOCK 256
+#define DCOR_WAVES (DCOR_BLOCK / 64)
+
+namespace dcor {
+
+// ------------------------------------------------------------------ Philox
+struct U4 { uint32_t w0, w1, w2, w3; };
+
+__device__ __forceinline__ U4 philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
+                                     uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint32_t hi0 = __umulhi(0xD2511F53u, c0), lo0 = 0xD2511F53u * c0;
+    const uint32_t hi1 = __umulhi(0xCD9E8D57u, c2), lo1 = 0xCD9E8D57u * c2;
+    const uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+    c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
+    k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
+  }
+  return U4{c0, c1, c2, c3};
+}
+
+__device__ __forceinline__ U4 draw(uint32_t idx, uint32_t rep, uint32_t site, uint32_t k0,
+                                   uint32_t k1) {
+  return philox(idx, rep, site, 0u, k0, k1);
+}
+
+// (2x+1) * 2^-53 with x the top 52 bits of (a, b): in (0, 1), exact.
+__device__ __forceinline__ double u53(uint32_t a, uint32_t b) {
+  const uint64_t x = ((uint64_t)a << 20) | (uint64_t)(b >> 12);
+  return (double)(2 * x + 1) * 0x1p-53;
+}
+
+// fdlibm-style log for positive normal x (same code as oracle/orc_log).
+__device__ __forceinline__ double dlog(double x) {
+  const double ln2_hi = 6.93147180369123816490e-01, ln2_lo = 1.90821492927058770002e-10,
+               Lg1 = 6.666666666666735130e-01, Lg2 = 3.999999999940941908e-01,
+               Lg3 = 2.857142874366239149e-01, Lg4 = 2.222219843214978396e-01,
+               Lg5 = 1.818357216161805012e-01, Lg6 = 1.531383769920937332e-01,
+               Lg7 = 1.479819860511658591e-01;
+  const uint64_t bits = __double_as_longlong(x);
+  int32_t hx = (int32_t)(bits >> 32);
+  const uint32_t lx = (uint32_t)bits;
+  int32_t k = ((hx >> 20) & 0x7ff) - 1023;
+  hx &= 0x000fffff;
+  const int32_t i = (hx + 0x95f64) & 0x100000;
+  hx |= (i ^ 0x3ff00000);
+  k += (i >> 20);
+  const double mnt = __longlong_as_double((long long)(((uint64_t)(uint32_t)hx << 32) | lx));
+  const double f = mnt - 1.0;
+  const double s = f / (2.0 + f);
+  const double dk = (double)k;
+  const double z = s * s, w = z * z;
+  const double t1 = w * fma(w, fma(w, Lg6, Lg4), Lg2);
+  const double t2 = z * fma(w, fma(w, fma(w, Lg7, Lg5), Lg3), Lg1);
+  const double R = t2 + t1;
+  const double hfsq = 0.5 * f * f;
+  return dk * ln2_hi - ((hfsq - (s * (hfsq + R) + dk * ln2_lo)) - f);
+}
+
+// sin(pi t), cos(pi t) for t with 2t exactly representable (same as oracle/orc_sincospi).
+__device__ __forceinline__ void dsincospi(double t, double* sp, double* cp) {
+  const double S1 = -1.66666666666666324348e-01, S2 = 8.33333333332248946124e-03,
+               S3 = -1.98412698298579493134e-04, S4 = 2.75573137070700676789e-06,
+               S5 = -2.50507602534068634195e-08, S6 = 1.58969099521155010221e-10,
+               C1 = 4.16666666666666019037e-02, C2 = -1.38888888888741095749e-03,
+               C3 = 2.48015872894767294178e-05, C4 = -2.75573143513906633035e-07,
+               C5 = 2.08757232129817482790e-09, C6 = -1.13596475577881948265e-11,
+               PIO2_HI = 1.57079632679489655800e+00, PIO2_LO = 6.12323399573676603587e-17;
+  const double t2 = 2.0 * t;
+  const double j = rint(t2);
+  const double r = t2 - j;
+  const double x = fma(r, PIO2_HI, r * PIO2_LO);
+  const double z = x * x;
+  const double v = z * x;
+  const double rs = fma(z, fma(z, fma(z, S6, S5), S4), S3);
+  const double sn = x + v * fma(z, fma(z, rs, S2), S1);
+  const double rc = z * fma(z, fma(z, fma(z, fma(z, fma(z, C6, C5), C4), C3), C2), C1);
+  const double hz = 0.5 * z;
+  const double wc = 1.0 - hz;
+  const double cs = wc + (((1.0 - wc) - hz) + z * rc);
+  const int q = ((int)j) & 3;
+  const double a = (q & 1) ? cs : sn;   // |sin| source
+  const double b = (q & 1) ? sn : cs;   // |cos| source
+  *sp = (q & 2) ? -a : a;
+  *cp = ((q + 1) & 2) ? -b : b;
+}
+
+__device__ __forceinline__ double unit_laplace(double u) {
+  const double up = u - 0.5;
+  const double g = dlog(1.0 - 2.0 * fabs(up));
+  return (up > 0) ? -g : g;
+}
+
+__device__ __forceinline__ void normal_pair(const U4& w, double* z1, double* z2) {
+  const double u1 = u53(w.w0, w.w1);
+  const double u2 = u53(w.w2, w.w3);
+  const double r = sqrt(-2.0 * dlog(u1));
+  double s, c;
+  dsincospi(2.0 * u2, &s, &c);
+  *z1 = r * c;
+  *z2 = r * s;
+}
+
+// ------------------------------------------------------------- R helpers
+__device__ __forceinline__ double rclip(double x, double L) {  // pmax(pmin(x, L), -L)
+  if (x != x) return x;
+  const double t = (x < L) ? x : L;
+  return (t > -L) ? t : -L;
+}
+__device__ __forceinline__ double rclip_lohi(double x, double lo, double hi) {  // pmin(pmax(x,lo),hi)
+  if (x != x) return x;
+  const double t = (x > lo) ? x : lo;
+  return (t < hi) ? t : hi;
+}
+__device__ __forceinline__ double rmax(double a, double b) {
+  return (a != a || b != b) ? __longlong_as_double(0x7ff8000000000000LL) : (a > b ? a : b);
+}
+__device__ __forceinline__ double rmin(double a, double b) {
+  return (a != a || b != b) ? __longlong_as_double(0x7ff8000000000000LL) : (a < b ? a : b);
+}
+__device__ __forceinline__ double dnan() { return __longlong_as_double(0x7ff8000000000000LL); }
+
+// ------------------------------------------------------- double-double
+struct DD { double hi, lo; };
+__device__ __forceinline__ DD two_sum(double a, double b) {
+  const double s = a + b;
+  const double bb = s - a;
+  const double e = (a - (s - bb)) + (b - bb);
+  return DD{s, e};
+}
+__device__ __forceinline__ void dd_acc(DD& acc, double x) {  // acc += x
+  const DD t = two_sum(acc.hi, x);
+  const double lo = acc.lo + t.lo;
+  const DD r = two_sum(t.hi, lo);
+  acc = r;
+}
+__device__ __forceinline__ DD dd_add(DD a, DD b) {
+  const DD s = two_sum(a.hi, b.hi);
+  const DD t = two_sum(a.lo, b.lo);
+  double lo = s.lo + t.hi;
+  DD r = two_sum(s.hi, lo);
+  lo = r.lo + t.lo;
+  return two_sum(r.hi, lo);
+}
+__device__ __forceinline__ DD two_prod(double a, double b) {
+  const double p = a * b;
+  return DD{p, fma(a, b, -p)};
+}
+__device__ __forceinline__ DD dd_mul_d(DD a, double b) {
+  DD p = two_prod(a.hi, b);
+  p.lo = fma(a.lo, b, p.lo);
+  return two_sum(p.hi, p.lo);
+}
+__device__ __forceinline__ DD dd_mul(DD a, DD b) {
+  DD p = two_prod(a.hi, b.hi);
+  p.lo = fma(a.hi, b.lo, p.lo);
+  p.lo = fma(a.lo, b.hi, p.lo);
+  return two_sum(p.hi, p.lo);
+}
+__device__ __forceinline__ DD dd_div_d(DD a, double b) {
+  const double q1 = a.hi / b;
+  const DD p = two_prod(q1, b);
+  const DD r = dd_add(a, DD{-p.hi, -p.lo});
+  const double q2 = r.hi / b;
+  return two_sum(q1, q2);
+}
+__device__ __forceinline__ DD dd_neg(DD a) { return DD{-a.hi, -a.lo}; }
+
+// sample variance (n-1) from double-double sum and sum of squares
+__device__ __forceinline__ double dd_var(DD s1, DD s2, double n) {
+  if (!(n >= 2)) return dnan();
+  const DD mean = dd_div_d(s1, n);
+  const DD c = dd_add(s2, dd_neg(dd_mul(s1, mean)));
+  const DD v = dd_div_d(c, n - 1.0);
+  return v.hi + v.lo;
+}
+
+// ------------------------------------------------------------ reductions
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ long long wave_sum_i(long long v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ DD wave_sum_dd(DD v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    DD w{__shfl_xor(v.hi, o, 64), __shfl_xor(v.lo, o, 64)};
+    // combine in a lane-order independent way: lower lane is left operand
+    const bool low = ((threadIdx.x & o) == 0);
+    v = low ? dd_add(v, w) : dd_add(w, v);
+  }
+  return v;
+}
+
+// Workgroup sums of NV doubles; result broadcast to every thread. Scratch: NV*DCOR_WAVES.
+template <int NV>
+__device__ __forceinline__ void block_sum(double (&v)[NV], double* scratch) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) v[i] = wave_sum(v[i]);
+  if (lane == 0) {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) scratch[i * DCOR_WAVES + wv] = v[i];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    double s = 0.0;
+#pragma unroll
+    for (int w = 0; w < DCOR_WAVES; ++w) s += scratch[i * DCOR_WAVES + w];
+    v[i] = s;
+  }
+  __syncthreads();
+}
+
+template <int NV>
+__device__ __forceinline__ void block_sum_dd(DD (&v)[NV], double* scratch) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) v[i] = wave_sum_dd(v[i]);
+  if (lane == 0) {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      scratch[(2 * i) * DCOR_WAVES + wv] = v[i].hi;
+      scratch[(2 * i + 1) * DCOR_WAVES + wv] = v[i].lo;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    DD s{scratch[(2 * i) * DCOR_WAVES], scratch[(2 * i + 1) * DCOR_WAVES]};
+#pragma unroll
+    for (int w = 1; w < DCOR_WAVES; ++w)
+      s = dd_add(s, DD{scratch[(2 * i) * DCOR_WAVES + w], scratch[(2 * i + 1) * DCOR_WAVES + w]});
+    v[i] = s;
+  }
+  __syncthreads();
+}
+
+__device__ __forceinline__ long long block_sum_i(long long v, long long* scratch) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  v = wave_sum_i(v);
+  if (lane == 0) scratch[wv] = v;
+  __syncthreads();
+  long long s = 0;
+#pragma unroll
+  for (int w = 0; w < DCOR_WAVES; ++w) s += scratch[w];
+  __syncthreads();
+  return s;
+}
+
+// ------------------------------------------------------------- mixquant
+// R: sort(x)[pos] (0-based pos) with NaN dropped.  Bitonic sort of P (power of two
+// >= nsim) keys in LDS; NaN becomes +inf and is counted.  Caller fills keys[0..nsim)
+// and calls with all threads; returns the selected value to every thread.
+__device__ __forceinline__ double lds_select(double* keys, int nsim, int P, int pos,
+                                             int* nan_count) {
+  for (int i = nsim + threadIdx.x; i < P; i += DCOR_BLOCK) keys[i] = __longlong_as_double(0x7ff0000000000000LL);
+  __syncthreads();
+  for (int k = 2; k <= P; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int t = threadIdx.x; t < (P >> 1); t += DCOR_BLOCK) {
+        const int i = ((t & ~(j - 1)) << 1) | (t & (j - 1));
+        const int l = i | j;
+        const double a = keys[i], b = keys[l];
+        const bool asc = ((i & k) == 0);
+        if ((a > b) == asc) { keys[i] = b; keys[l] = a; }
+      }
+      __syncthreads();
+    }
+  }
+  const int valid = nsim - *nan_count;
+  const double r = (pos >= 0 && pos < valid) ? keys[pos] : dnan();
+  __syncthreads();
+  return r;
+}
+
+}  // namespace dcor

@@ -1,0 +1,97 @@
+// dcor_engine.h -- launch-time constant blocks shared by the host C-ABI and the kernels.
+//
+// Every data-independent scalar of the R estimators (lambda, m, k, Laplace scales,
+// qnorm, exp(eps_s) ratios, mixquant order-statistic index ...) is evaluated ONCE on
+// the host with the R operation order (see dcor_capi.cpp) and handed to the kernel by
+// value, so the per-replicate kernel only does the data-dependent arithmetic.
+#pragma once
+#include <stdint.h>
+
+#include "../../include/dcor.h"
+
+namespace dcor {
+
+struct DgpConst {
+  int32_t dgp;
+  int32_t pad;
+  double mu0, mu1, a00, a01, a10, a11;  // Gaussian: X = mu + A z  (MASS::mvrnorm)
+  double thr0, thr1;                    // Bernoulli: p01/0.5, p11/0.5
+  double cU, cU2, cE, cE2;              // bounded factor: -c + (c - -c) * u
+};
+
+struct MixConst {
+  int32_t nsim, pos, P, pad;  // R: sort(x)[ceiling(p*nsim)] -> 0-based pos; P = pow2 >= nsim
+};
+
+// Sign family: ci_NI_signbatch + ci_INT_signflip (vert-cor.R:204-317).
+struct SignConst {
+  int64_t n, k;
+  int64_t rep_begin;
+  uint32_t k0, k1;          // Philox key (seed lo, hi)
+  int32_t m, normalise, sender_is_X, mode_normal;
+  DgpConst g;
+  MixConst mix;
+  double nd, md, kd;
+  double L;                                   // sqrt(2*log(n))
+  double s_mu_x, s_m2_x, s_mu_y, s_m2_y;      // priv_standardize Laplace scales
+  double bx, by;                              // 2/(m*eps1), 2/(m*eps2)
+  double inv_k, crit, sqrt_k;
+  double pflip;                               // exp(eps_s)/(exp(eps_s)+1)
+  double scale_Z, coefZ, q2, ratio, inv_sqrt_n, eps_r, w_laplace;
+};
+
+// Sub-G family: correlation_NI_subG + ci_INT_subG (ver-cor-subG.R:25-108).
+struct SubgConst {
+  int64_t n, k;
+  int64_t rep_begin;
+  uint32_t k0, k1;
+  int32_t m, sender_is_X;
+  DgpConst g;
+  MixConst mix;
+  double nd, md, kd;
+  double l1, l2;                    // lambda_n(n, eta1/2)
+  double bx, by;                    // 2*l1/(m*eps1), 2*l2/(m*eps2)
+  double m_over_k, crit, sqrt_k;
+  double ls, lr, bs;                // lambda_s, lambda_r, 2*lambda_s/eps_s
+  double s_central, sn2x2;          // 2*lr/(n*eps_r), 2*(s_central^2)
+  double sqrt_n, eps_r;
+};
+
+// Pre-materialised sign family.
+struct PrematSignConst {
+  SignConst s;          // scalars (dgp/key unused)
+  const double* X; const double* Y; int64_t xy_stride;
+  const double* lap_ni_sc; const double* lap_ni_x; const double* lap_ni_y;
+  const double* lap_int_sc; const uint32_t* flips; int64_t flip_words;
+  const double* lap_z; const double* mix_z; const double* mix_l;
+};
+
+// Pre-materialised sub-G (simulation or HRS variant).
+struct PrematSubgConst {
+  SubgConst s;
+  int32_t hrs, pad;
+  double lo_;                        // HRS: lambda_other (clip of the non-sender)
+  double crit_sqrt2_s;               // HRS: qnorm*sqrt(2)*(2*lr/(n*eps_r))  (sd==0 branch)
+  const double* X; const double* Y; int64_t xy_stride;
+  const int32_t* perm;
+  const double* lap_ni_x; const double* lap_ni_y; const double* lap_local;
+  const double* lap_central; const double* mix_z; const double* mix_l;
+};
+
+// Kernel launchers (dcor_kernels.hip).  Return hipError_t as int.
+int launch_sign_fused(const SignConst& c, int64_t reps, dcor_rep_out* out, void* stream);
+int launch_subg_fused(const SubgConst& c, int64_t reps, dcor_rep_out* out, void* stream);
+int launch_premat_sign(const PrematSignConst& c, int64_t reps, dcor_rep_out* out, void* stream);
+int launch_premat_subg(const PrematSubgConst& c, int64_t reps, dcor_rep_out* out, void* stream);
+int launch_accumulate(const dcor_rep_out* d_out, int64_t count, double rho, dcor_accum* acc,
+                      void* stream);
+int launch_mixquant(const double* z, const double* l, int32_t nsim, double c, int32_t pos,
+                    double* out, void* stream);
+int launch_priv_standardize(const double* v, int64_t n, double L, double s_mu, double s_m2,
+                            const double* lap2, double* out, void* stream);
+int launch_draws(int kind, uint32_t k0, uint32_t k1, uint32_t site, int64_t rep_begin,
+                 int64_t reps, int64_t count, double* out, void* stream);
+int launch_dp_sd(const double* x, int64_t n, double lo, double hi, double s_mu, double s_m2,
+                 const double* lap2, double* out2, void* stream);
+
+}  // namespace dcor

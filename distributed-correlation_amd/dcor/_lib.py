@@ -1,0 +1,171 @@
+"""ctypes binding of include/dcor.h (libdcor.so, built in-tree for gfx950).
+
+The shared object is the product: every compute entry runs on the GPU.  If it is
+missing this module raises at import time -- there is no Python/CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import math
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libdcor.so")
+
+DCOR_OK, DCOR_EINVAL, DCOR_EKLT1, DCOR_EHIP, DCOR_ENOMEM, DCOR_ENODEV = 0, 1, 2, 3, 4, 5
+FAMILY_SIGN, FAMILY_SUBG = 0, 1
+DGP_GAUSSIAN, DGP_BERNOULLI, DGP_BOUNDED_FACTOR = 0, 1, 2
+MODE_AUTO, MODE_NORMAL, MODE_LAPLACE = 0, 1, 2
+SITE_DGP_A, SITE_DGP_B, SITE_FLIP, SITE_NI_LAP, SITE_SCALAR, SITE_MIX_Z, SITE_MIX_L = 1, 2, 3, 4, 5, 6, 7
+
+_MODES = {"auto": MODE_AUTO, "normal": MODE_NORMAL, "laplace": MODE_LAPLACE}
+
+
+class DcorError(RuntimeError):
+    """A non-zero dcor status; `.code` is the DCOR_E* value."""
+
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"dcor error {code}: {msg}")
+        self.code = code
+
+
+class KLessThanOne(DcorError, ValueError):
+    """k = floor(n/m) < 1: the reference's stopifnot(k >= 1)."""
+
+
+class Cell(C.Structure):
+    _fields_ = [
+        ("family", C.c_int32), ("dgp", C.c_int32), ("n", C.c_int64),
+        ("rho", C.c_double), ("eps1", C.c_double), ("eps2", C.c_double), ("alpha", C.c_double),
+        ("mu", C.c_double * 2), ("sigma", C.c_double * 2),
+        ("eta1", C.c_double), ("eta2", C.c_double),
+        ("normalise", C.c_int32), ("ci_mode", C.c_int32), ("nsim", C.c_int64),
+        ("seed", C.c_uint64),
+    ]
+
+
+class RepOut(C.Structure):
+    _fields_ = [(f, C.c_double) for f in ("ni_hat", "ni_lo", "ni_hi", "int_hat", "int_lo", "int_hi")]
+
+
+class Accum(C.Structure):
+    _fields_ = [("n", C.c_int64), ("n_cover", C.c_int64), ("n_cover_na", C.c_int64),
+                ("n_na_est", C.c_int64), ("n_na_ci", C.c_int64), ("reserved", C.c_int64 * 3)] + [
+        (f, C.c_double * 2) for f in ("est", "est2", "se2", "len", "lo", "hi")]
+
+
+class Summary(C.Structure):
+    _fields_ = [(f, C.c_double) for f in ("mse", "bias", "var", "coverage", "ci_length")]
+
+
+_P = C.c_void_p
+
+
+class PrematSign(C.Structure):
+    _fields_ = [
+        ("n", C.c_int64), ("reps", C.c_int64),
+        ("eps1", C.c_double), ("eps2", C.c_double), ("alpha", C.c_double),
+        ("normalise", C.c_int32), ("ci_mode", C.c_int32), ("nsim", C.c_int64),
+        ("X", _P), ("Y", _P), ("xy_stride", C.c_int64),
+        ("lap_ni_sc", _P), ("lap_ni_x", _P), ("lap_ni_y", _P), ("lap_int_sc", _P),
+        ("flips", _P), ("lap_z", _P), ("mix_z", _P), ("mix_l", _P),
+    ]
+
+
+class PrematSubg(C.Structure):
+    _fields_ = [
+        ("n", C.c_int64), ("reps", C.c_int64),
+        ("eps1", C.c_double), ("eps2", C.c_double), ("eta1", C.c_double), ("eta2", C.c_double),
+        ("alpha", C.c_double), ("hrs", C.c_int32), ("reserved", C.c_int32),
+        ("lam_x", C.c_double), ("lam_y", C.c_double),
+        ("lam_s", C.c_double), ("lam_o", C.c_double), ("lam_r", C.c_double), ("delta", C.c_double),
+        ("nsim", C.c_int64),
+        ("X", _P), ("Y", _P), ("xy_stride", C.c_int64), ("perm", _P),
+        ("lap_ni_x", _P), ("lap_ni_y", _P), ("lap_local", _P), ("lap_central", _P),
+        ("mix_z", _P), ("mix_l", _P),
+    ]
+
+
+_D = C.POINTER(C.c_double)
+_I64 = C.POINTER(C.c_int64)
+
+# name -> (restype, argtypes); this list IS the exported ABI (checked against the header
+# by tests/test_abi.py).
+SIGNATURES = {
+    "dcor_version": (C.c_char_p, []),
+    "dcor_last_error": (C.c_int, [C.c_char_p, C.c_size_t]),
+    "dcor_device_count": (C.c_int, []),
+    "dcor_lambda_n": (C.c_double, [C.c_double, C.c_double]),
+    "dcor_lambda_int_n": (None, [C.c_double, C.c_double, C.c_double, C.c_double, _D]),
+    "dcor_lambda_receiver_from_noise": (C.c_double, [C.c_double] * 4),
+    "dcor_lambda_from_priv": (C.c_double, [C.c_double] * 4),
+    "dcor_qnorm": (C.c_double, [C.c_double]),
+    "dcor_sim_launch": (C.c_int, [C.POINTER(Cell), C.c_int64, C.c_int64, _P, _P]),
+    "dcor_accumulate_launch": (C.c_int, [_P, C.c_int64, C.c_double, _P, _P]),
+    "dcor_accum_merge": (None, [C.POINTER(Accum), C.POINTER(Accum)]),
+    "dcor_accum_finalize": (None, [C.POINTER(Accum), C.c_double, C.POINTER(Summary)]),
+    "dcor_grid_run": (C.c_int, [C.POINTER(Cell), C.c_int, C.c_int64, C.POINTER(Accum), C.POINTER(RepOut)]),
+    "dcor_premat_sign_launch": (C.c_int, [C.POINTER(PrematSign), _P, _P]),
+    "dcor_premat_subg_launch": (C.c_int, [C.POINTER(PrematSubg), _P, _P]),
+    "dcor_batch_geometry": (C.c_int, [C.c_int64, C.c_double, C.c_double, C.c_int, C.c_int, _I64]),
+    "dcor_ci_ni_signbatch": (C.c_int, [_D, _D, C.c_int64, C.c_double, C.c_double, C.c_double,
+                                       C.c_int, _D, _D, _D, _D]),
+    "dcor_ci_int_signflip": (C.c_int, [_D, _D, C.c_int64, C.c_double, C.c_double, C.c_double,
+                                       C.c_int, C.c_int, _D, C.POINTER(C.c_uint8), C.c_double,
+                                       _D, _D, C.c_int64, _D]),
+    "dcor_correlation_ni_subg": (C.c_int, [_D, _D, C.c_int64, C.c_double, C.c_double, C.c_double,
+                                           C.c_double, C.c_double, C.c_int, C.c_double,
+                                           C.c_double, C.POINTER(C.c_int32), _D, _D, _D]),
+    "dcor_ci_int_subg": (C.c_int, [_D, _D, C.c_int64, C.c_double, C.c_double, C.c_double,
+                                   C.c_double, C.c_double, C.c_int, C.c_double, C.c_double,
+                                   C.c_double, C.c_double, _D, C.c_double, _D, _D, C.c_int64, _D]),
+    "dcor_mixquant": (C.c_int, [_D, _D, C.c_int64, C.c_double, C.c_double, _D]),
+    "dcor_priv_standardize": (C.c_int, [_D, C.c_int64, C.c_double, C.c_double, _D, _D]),
+    "dcor_draws_launch": (C.c_int, [C.c_int, C.c_uint64, C.c_int, C.c_int64, C.c_int64, C.c_int64,
+                                    _P, _P]),
+    "dcor_dp_sd": (C.c_int, [_D, C.c_int64, C.c_double, C.c_double, C.c_double, C.c_double, _D, _D]),
+}
+
+
+def _load() -> C.CDLL:
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"{LIB_PATH} is missing: build the gfx950 engine first "
+            "(python -c 'import __graft_entry__ as g; g.build()'); there is no CPU fallback")
+    lib = C.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        f = getattr(lib, name)
+        f.restype = res
+        f.argtypes = args
+    return lib
+
+
+lib = _load()
+
+
+def last_error() -> str:
+    buf = C.create_string_buffer(512)
+    lib.dcor_last_error(buf, 512)
+    return buf.value.decode(errors="replace")
+
+
+def check(status: int) -> None:
+    if status != DCOR_OK:
+        msg = last_error()
+        if status == DCOR_EKLT1:
+            raise KLessThanOne(status, msg)
+        raise DcorError(status, msg)
+
+
+def mode_code(mode) -> int:
+    if isinstance(mode, int):
+        return mode
+    if isinstance(mode, (list, tuple)):  # R's match.arg default c("auto", ...) -> first
+        mode = mode[0]
+    if mode not in _MODES:
+        raise ValueError(f"mode must be one of {sorted(_MODES)}")
+    return _MODES[mode]
+
+
+def nan_if_none(x) -> float:
+    return math.nan if x is None else float(x)

@@ -1,0 +1,225 @@
+"""Fused Monte-Carlo engine: grid cells, replicate drivers and summaries.
+
+Replaces run_sim_one (vert-cor.R:356-444; ver-cor-subG.R:159-222) and the
+expand.grid + mclapply grid drivers (vert-cor.R:486-597; ver-cor-subG.R:245-335).
+Replicates run on the GPU (one workgroup each) from counter-based Philox streams
+keyed by the cell seed, so a replicate's numbers depend only on (seed, rep) and
+any split over launches or GPUs reproduces them bit for bit.
+torch supplies device memory and the stream; all compute is in libdcor.so.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import itertools
+import math
+from dataclasses import dataclass, field
+from typing import Optional, Sequence
+
+import numpy as np
+
+from . import _lib
+from ._lib import check, lib
+
+DETAIL_COLS = ("ni_hat", "ni_low", "ni_up", "int_hat", "int_low", "int_up")
+
+
+@dataclass
+class CellSpec:
+    """One (family, distribution, rho, eps, n) grid cell + run_sim_one arguments."""
+    n: int
+    rho: float
+    eps1: float
+    eps2: float
+    family: str = "sign"            # "sign" (vert-cor.R) or "subG" (ver-cor-subG.R)
+    dgp: str = "gaussian"           # "gaussian" | "bernoulli" | "bounded_factor"
+    alpha: float = 0.05
+    mu: Sequence[float] = (0.0, 0.0)
+    sigma: Sequence[float] = (1.0, 1.0)
+    eta1: float = 1.0
+    eta2: float = 1.0
+    normalise: bool = True
+    ci_mode: str = "auto"
+    nsim: int = 1000
+    seed: int = 2025
+
+    def to_c(self) -> _lib.Cell:
+        c = _lib.Cell()
+        c.family = _lib.FAMILY_SUBG if self.family == "subG" else _lib.FAMILY_SIGN
+        c.dgp = {"gaussian": _lib.DGP_GAUSSIAN, "bernoulli": _lib.DGP_BERNOULLI,
+                 "bounded_factor": _lib.DGP_BOUNDED_FACTOR}[self.dgp]
+        c.n = int(self.n)
+        c.rho, c.eps1, c.eps2, c.alpha = float(self.rho), float(self.eps1), float(self.eps2), float(self.alpha)
+        c.mu[0], c.mu[1] = float(self.mu[0]), float(self.mu[1])
+        c.sigma[0], c.sigma[1] = float(self.sigma[0]), float(self.sigma[1])
+        c.eta1, c.eta2 = float(self.eta1), float(self.eta2)
+        c.normalise = int(bool(self.normalise))
+        c.ci_mode = _lib.mode_code(self.ci_mode)
+        c.nsim = int(self.nsim)
+        c.seed = int(self.seed) & 0xFFFFFFFFFFFFFFFF
+        return c
+
+
+def _torch():
+    import torch
+    if not torch.cuda.is_available():
+        raise _lib.DcorError(_lib.DCOR_ENODEV, "no GPU visible: the dcor engine has no CPU path")
+    return torch
+
+
+def _stream_ptr(stream) -> int:
+    torch = _torch()
+    s = torch.cuda.current_stream() if stream is None else stream
+    return int(s.cuda_stream)
+
+
+def simulate(cell: CellSpec, reps: int, rep_begin: int = 0, out=None, stream=None):
+    """Replicates [rep_begin, rep_begin+reps) of `cell` -> float64 tensor [reps, 6] on the GPU
+    (columns DETAIL_COLS).  Asynchronous on `stream` (default: torch's current stream)."""
+    torch = _torch()
+    if out is None:
+        out = torch.empty((reps, 6), dtype=torch.float64, device="cuda")
+    assert out.is_cuda and out.dtype == torch.float64 and out.is_contiguous() and out.shape[0] >= reps
+    c = cell.to_c()
+    check(lib.dcor_sim_launch(C.byref(c), int(rep_begin), int(reps), C.c_void_p(out.data_ptr()),
+                              C.c_void_p(_stream_ptr(stream))))
+    return out
+
+
+def accumulate(records, rho: float, stream=None):
+    """Deterministic per-method accumulators of device records -> (2, 20) int64/float view
+    returned as a list of two _lib.Accum (host)."""
+    torch = _torch()
+    n = records.shape[0]
+    acc = torch.empty(2 * C.sizeof(_lib.Accum), dtype=torch.uint8, device="cuda")
+    check(lib.dcor_accumulate_launch(C.c_void_p(records.data_ptr()), int(n), float(rho),
+                                     C.c_void_p(acc.data_ptr()), C.c_void_p(_stream_ptr(stream))))
+    return acc
+
+
+def accum_from_bytes(buf: bytes):
+    a = (_lib.Accum * 2).from_buffer_copy(buf)
+    return [a[0], a[1]]
+
+
+def merge(accums):
+    """Merge a rank-ordered list of Accum (double-double sums; deterministic)."""
+    out = _lib.Accum()
+    for a in accums:
+        lib.dcor_accum_merge(C.byref(out), C.byref(a))
+    return out
+
+
+def finalize(acc: _lib.Accum, rho: float) -> dict:
+    s = _lib.Summary()
+    lib.dcor_accum_finalize(C.byref(acc), float(rho), C.byref(s))
+    return {"mse": s.mse, "bias": s.bias, "var": s.var, "coverage": s.coverage, "ci_length": s.ci_length}
+
+
+def detail_frame(rec: np.ndarray, rho: float) -> dict:
+    """run_sim_one's `detail` (vert-cor.R:367-417) from the six per-replicate numbers."""
+    rec = np.asarray(rec, dtype=np.float64).reshape(-1, 6)
+    d = {"repl": np.arange(1, rec.shape[0] + 1)}
+    for i, name in enumerate(DETAIL_COLS):
+        d[name] = rec[:, i]
+    for m in ("ni", "int"):
+        lo, up, hat = d[f"{m}_low"], d[f"{m}_up"], d[f"{m}_hat"]
+        d[f"{m}_se2"] = (hat - rho) ** 2
+        with np.errstate(invalid="ignore"):
+            cov = (rho >= lo) & (rho <= up)
+        cov = cov.astype(float)
+        cov[np.isnan(lo) | np.isnan(up)] = np.nan
+        d[f"{m}_cover"] = cov
+        d[f"{m}_ci_len"] = up - lo
+    return d
+
+
+def run_cell(cell: CellSpec, B: int, detail: bool = True, chunk: int = 1 << 16, stream=None) -> dict:
+    """All B replicates of one cell on the current GPU -> {'detail', 'summary'}."""
+    torch = _torch()
+    recs = []
+    accs = []
+    buf = torch.empty((min(B, chunk), 6), dtype=torch.float64, device="cuda")
+    for r0 in range(0, B, chunk):
+        nr = min(chunk, B - r0)
+        simulate(cell, nr, r0, out=buf, stream=stream)
+        a = accumulate(buf[:nr], cell.rho, stream=stream)
+        accs.extend(accum_from_bytes(a.cpu().numpy().tobytes()))
+        if detail:
+            recs.append(buf[:nr].cpu().numpy().copy())
+    ni = merge(accs[0::2])
+    it = merge(accs[1::2])
+    summary = {"NI": finalize(ni, cell.rho), "INT": finalize(it, cell.rho)}
+    res = {"summary": summary, "accum": (ni, it)}
+    if detail:
+        res["detail"] = detail_frame(np.concatenate(recs), cell.rho)
+    return res
+
+
+# ---------------------------------------------------------- R-shaped drivers
+def run_sim_one(n, rho, eps1, eps2, mu=(0.0, 0.0), sigma=(1.0, 1.0), B=1000, alpha=0.05,
+                ci_mode="auto", normalise=True, seed=2025, dgp="gaussian") -> dict:
+    """run_sim_one of vert-cor.R:356-444 (sign family; dgp='bernoulli' wires gen_bernoulli)."""
+    cell = CellSpec(n=n, rho=rho, eps1=eps1, eps2=eps2, family="sign", dgp=dgp, alpha=alpha,
+                    mu=mu, sigma=sigma, normalise=normalise, ci_mode=ci_mode, seed=seed)
+    return run_cell(cell, B)
+
+
+def run_sim_one_subG(n, rho, eps1, eps2, dgp_fun="bounded_factor", dgp_args=None, B=1000,
+                     alpha=0.05, use_subG=True, ci_mode="auto", seed=2025) -> dict:
+    """run_sim_one of ver-cor-subG.R:159-222.  use_subG=FALSE routes to the sign family."""
+    args = dict(dgp_args or {})
+    cell = CellSpec(n=n, rho=rho, eps1=eps1, eps2=eps2, family="subG" if use_subG else "sign",
+                    dgp=dgp_fun, alpha=alpha, ci_mode=ci_mode, seed=seed,
+                    mu=args.get("mu", (0.0, 0.0)), sigma=args.get("sigma", (1.0, 1.0)))
+    return run_cell(cell, B)
+
+
+# ------------------------------------------------------------------- grids
+def expand_grid(n_grid, rho_grid, eps_pairs, **kw) -> list:
+    """expand.grid(n, rho, eps_idx) with n fastest; seed = 1e6 + i (vert-cor.R:507-552)."""
+    cells = []
+    i = 0
+    for e in eps_pairs:
+        for rho in rho_grid:
+            for n in n_grid:
+                i += 1
+                cells.append(CellSpec(n=n, rho=rho, eps1=e[0], eps2=e[1], seed=1_000_000 + i, **kw))
+    return cells
+
+
+def vert_cor_grid() -> list:
+    """144-cell sign-family grid of vert-cor.R:486-499 (B = 250 there)."""
+    return expand_grid([1000, 1500, 2500, 4000, 6000, 9000],
+                       [0, 0.15, 0.3, 0.4, 0.5, 0.65, 0.8, 0.9],
+                       [(0.5, 0.5), (1.0, 1.0), (1.5, 0.5)],
+                       family="sign", dgp="gaussian", mu=(0.5, 0.5), sigma=(2.0, 2.0))
+
+
+def subg_grid() -> list:
+    """120-cell sub-G grid of ver-cor-subG.R:245-258 (bounded factor, B = 250)."""
+    return expand_grid([2500, 4000, 6000, 9000, 12000],
+                       [0, 0.15, 0.3, 0.4, 0.5, 0.65, 0.8, 0.9],
+                       [(0.5, 0.5), (1.0, 1.0), (1.5, 0.5)],
+                       family="subG", dgp="bounded_factor")
+
+
+def paper_grid(n_grid=(200, 400, 800, 1600, 3200)) -> list:
+    """Legacy paper axes of vert-cor.R:19-40 crossed with both families (BASELINE C4)."""
+    eps = [(0.2, 0.2), (0.5, 0.5), (1.0, 1.0), (1.5, 0.5), (0.5, 1.5)]
+    rho = [0.0, 0.3, 0.8]
+    out = []
+    for fam, dgp, kw in (("sign", "gaussian", {}), ("sign", "bernoulli", {}),
+                         ("subG", "gaussian", {}), ("subG", "bounded_factor", {})):
+        out += expand_grid(list(n_grid), rho, eps, family=fam, dgp=dgp, **kw)
+    return out
+
+
+def headline_cell(n: int = 100_000) -> CellSpec:
+    """BASELINE.json headline: sign family, mvrnorm mu=(.5,.5) sigma=(2,2), rho=.5, eps=(1,1)."""
+    return CellSpec(n=n, rho=0.5, eps1=1.0, eps2=1.0, family="sign", dgp="gaussian",
+                    mu=(0.5, 0.5), sigma=(2.0, 2.0), alpha=0.05, normalise=True, ci_mode="auto",
+                    seed=1_000_073)
+
+
+def run_grid(cells, B: int, detail: bool = False) -> list:
+    return [run_cell(c, B, detail=detail) for c in cells]

@@ -1,0 +1,231 @@
+/*
+ * dcor.h -- C-ABI of the MI355X (gfx950) engine for the Monte-Carlo hot path of
+ * abhinavc3/distributed-correlation (DP correlation across two servers, NI + INT).
+ *
+ * Drop-in boundary.  The reference's surface is a set of R closures
+ * (vert-cor.R, ver-cor-subG.R, real-data-sims.R); its R wrappers call these
+ * entry points through `.Call`.  Plain C types only: no torch,
+ * no C++ across the ABI.  Every compute entry point runs on the GPU; there is no
+ * CPU fallback (a missing device is an error, DCOR_ENODEV / DCOR_EHIP).
+ *
+ * Conventions
+ *  - Status: every entry returns int (DCOR_OK = 0).  The message of the last
+ *    failure on the calling thread is read with dcor_last_error().
+ *  - Ownership: inputs are borrowed for the duration of the call; outputs go to
+ *    caller-allocated buffers.  `*_launch` entries take DEVICE pointers and a
+ *    hipStream_t (as void*) and are asynchronous; all other entries take HOST
+ *    pointers and are synchronous.
+ *  - Noise: explicit-input entries take UNIT-scale draws (Laplace(0,1), flip bits,
+ *    mixquant normals/Laplace); the entry scales them exactly as the R code scales
+ *    its own draws (scale * unit is bit-identical to extraDistr::rlaplace's
+ *    mu - sigma*sign(u)*log(1-2|u|) at mu = 0).
+ *  - NA: a statistic R would return as NA (e.g. sd of k = 1 batch products) is
+ *    returned as NaN.
+ */
+#ifndef DCOR_H
+#define DCOR_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DCOR_OK 0
+#define DCOR_EINVAL 1  /* bad n / eps / lengths: the reference's stopifnot()          */
+#define DCOR_EKLT1 2   /* fewer than one full batch (vert-cor.R:127,209; subG.R:38)    */
+#define DCOR_EHIP 3    /* HIP runtime error                                            */
+#define DCOR_ENOMEM 4
+#define DCOR_ENODEV 5  /* no gfx950 device visible                                     */
+
+enum { DCOR_FAMILY_SIGN = 0, DCOR_FAMILY_SUBG = 1 };
+enum { DCOR_DGP_GAUSSIAN = 0, DCOR_DGP_BERNOULLI = 1, DCOR_DGP_BOUNDED_FACTOR = 2 };
+enum { DCOR_MODE_AUTO = 0, DCOR_MODE_NORMAL = 1, DCOR_MODE_LAPLACE = 2 };
+
+/* One (distribution, rho, eps, n) grid cell.  Replaces one row of
+ * expand.grid(n, rho, eps_idx) plus run_sim_one's arguments
+ * (vert-cor.R:356-362,507-511,542-552; ver-cor-subG.R:159-167,265-288). */
+typedef struct dcor_cell {
+  int32_t family;    /* DCOR_FAMILY_SIGN: ci_NI_signbatch + ci_INT_signflip          */
+                     /* DCOR_FAMILY_SUBG: correlation_NI_subG + ci_INT_subG          */
+  int32_t dgp;       /* DCOR_DGP_*                                                    */
+  int64_t n;         /* samples per replicate                                         */
+  double rho, eps1, eps2, alpha;
+  double mu[2], sigma[2]; /* Gaussian DGP (MASS::mvrnorm), vert-cor.R:389-394          */
+  double eta1, eta2;      /* sub-G calibration, ver-cor-subG.R:26                      */
+  int32_t normalise;      /* sign family priv_standardize switch, vert-cor.R:211       */
+  int32_t ci_mode;        /* DCOR_MODE_*, vert-cor.R:294-296                           */
+  int64_t nsim;           /* mixquant draws (1000; 2000 in real-data-sims.R:161)       */
+  uint64_t seed;          /* per-cell seed (R: 1e6 + i, vert-cor.R:552): Philox key    */
+} dcor_cell;
+
+/* Per-replicate result: the six numbers of one row of run_sim_one's `detail`
+ * (vert-cor.R:401-417); se2 / cover / ci_len derive from these and rho. */
+typedef struct dcor_rep_out {
+  double ni_hat, ni_lo, ni_hi;
+  double int_hat, int_lo, int_hi;
+} dcor_rep_out;
+
+/* Per-(cell, method) summary accumulator, mergeable across replicate ranges and
+ * GPUs (sums are double-double {hi, lo}).  Finalised by dcor_accum_finalize into
+ * run_sim_one's summary row (vert-cor.R:422-430; ver-cor-subG.R:208-210). */
+typedef struct dcor_accum {
+  int64_t n;          /* replicates accumulated                                      */
+  int64_t n_cover;    /* cover TRUE  (rho >= lo && rho <= hi, R three-valued logic)  */
+  int64_t n_cover_na; /* cover NA                                                    */
+  int64_t n_na_est;   /* estimate NA                                                 */
+  int64_t n_na_ci;    /* lo or hi NA                                                 */
+  int64_t reserved[3];
+  double est[2], est2[2], se2[2], len[2], lo[2], hi[2];
+} dcor_accum;
+
+/* mse, bias, var, coverage, ci_length: the summary columns. */
+typedef struct dcor_summary {
+  double mse, bias, var, coverage, ci_length;
+} dcor_summary;
+
+/* ------------------------------------------------------------------------ */
+const char* dcor_version(void);
+int dcor_last_error(char* buf, size_t len);
+/* Number of visible HIP devices (0 on a host without GPU; never fails). */
+int dcor_device_count(void);
+
+/* ---- calibration scalars (host closed forms) ----------------------------- */
+/* lambda_n, ver-cor-subG.R:1 (= real-data-sims.R:109). */
+double dcor_lambda_n(double n, double eta);
+/* lambda_INT_n, ver-cor-subG.R:3-7 (= real-data-sims.R:154-158). out = {lambda_s, lambda_r}. */
+void dcor_lambda_int_n(double n, double eta_s, double eta_r, double eps_s, double out[2]);
+/* lambda_receiver_from_noise, real-data-sims.R:170-174. */
+double dcor_lambda_receiver_from_noise(double lam_s, double lam_o, double eps_s, double delta);
+/* lambda_from_priv, real-data-sims.R:103-106. */
+double dcor_lambda_from_priv(double lo, double hi, double mean, double sd);
+/* qnorm(p) (R's qnorm, used as qnorm(1 - alpha/2)). */
+double dcor_qnorm(double p);
+
+/* ---- fused Monte-Carlo engine (the hot path) ----------------------------- */
+/* Replicates [rep_begin, rep_begin + rep_count) of one cell, one workgroup per
+ * replicate: Philox DGP -> clip -> reduce -> Laplace -> NI + INT estimate + CI.
+ * Replaces run_sim_one's loop body (vert-cor.R:392-419; ver-cor-subG.R:174-198).
+ * d_out: rep_count device records.  Per-replicate results depend only on
+ * (seed, rep), never on the range split, so any sharding over GPUs is exact. */
+int dcor_sim_launch(const dcor_cell* cell, int64_t rep_begin, int64_t rep_count,
+                    dcor_rep_out* d_out, void* stream);
+/* Deterministic per-method accumulation of `count` records into d_acc[0] (NI)
+ * and d_acc[1] (INT) (overwrites).  Replaces the summarise() closures
+ * (vert-cor.R:422-437; ver-cor-subG.R:201-217). */
+int dcor_accumulate_launch(const dcor_rep_out* d_out, int64_t count, double rho,
+                           dcor_accum* d_acc, void* stream);
+/* Host helpers over accumulators. */
+void dcor_accum_merge(dcor_accum* dst, const dcor_accum* src);
+void dcor_accum_finalize(const dcor_accum* acc, double rho, dcor_summary* out);
+/* Whole grid on the current device, synchronous, host buffers: the one `.Call`
+ * that replaces the mclapply grid (vert-cor.R:534-553; ver-cor-subG.R:294-295).
+ * h_acc: 2*ncells accumulators (NI, INT per cell); h_detail: NULL or ncells*B. */
+int dcor_grid_run(const dcor_cell* cells, int ncells, int64_t B, dcor_accum* h_acc,
+                  dcor_rep_out* h_detail);
+
+/* ---- pre-materialised (explicit-input) batch mode: HBM streaming --------- */
+/* Sign family, R replicates.  Per-replicate arrays are laid out rep-major with
+ * the given strides (a stride of 0 shares one array across replicates). */
+typedef struct dcor_premat_sign {
+  int64_t n, reps;
+  double eps1, eps2, alpha;
+  int32_t normalise, ci_mode;
+  int64_t nsim;
+  const double* X;          /* [reps][xy_stride] (xy_stride 0: shared)            */
+  const double* Y;
+  int64_t xy_stride;
+  const double* lap_ni_sc;  /* [reps][4]  mu_X, m2_X, mu_Y, m2_Y (vert-cor.R:214-215) */
+  const double* lap_ni_x;   /* [reps][k]  (vert-cor.R:230)                        */
+  const double* lap_ni_y;   /* [reps][k]  (vert-cor.R:231)                        */
+  const double* lap_int_sc; /* [reps][4]  fresh standardisation (vert-cor.R:271-272) */
+  const uint32_t* flips;    /* [reps][ceil(n/32)] bit i of word i/32 = S_i (vert-cor.R:175) */
+  const double* lap_z;      /* [reps]     Z (vert-cor.R:188)                      */
+  const double* mix_z;      /* [reps][nsim] rnorm(nsim)  (vert-cor.R:47)          */
+  const double* mix_l;      /* [reps][nsim] rexp*(2*rbinom-1)                     */
+} dcor_premat_sign;
+
+/* Sub-Gaussian family (simulation variant, hrs = 0, ver-cor-subG.R:25-108) or the
+ * HRS variant (hrs = 1, real-data-sims.R:115-147,176-252). */
+typedef struct dcor_premat_subg {
+  int64_t n, reps;
+  double eps1, eps2, eta1, eta2, alpha;
+  int32_t hrs, reserved;
+  double lam_x, lam_y;                 /* NI overrides (NaN: lambda_n)             */
+  double lam_s, lam_o, lam_r, delta;   /* INT overrides (NaN: defaults)            */
+  int64_t nsim;
+  const double* X;
+  const double* Y;
+  int64_t xy_stride;
+  const int32_t* perm;      /* hrs: [reps][k*m] 0-based sample.int(n,k*m)-1; else NULL */
+  const double* lap_ni_x;   /* [reps][k]                                          */
+  const double* lap_ni_y;   /* [reps][k]                                          */
+  const double* lap_local;  /* [reps][n]  rLap(n, 2*lambda_s/eps_s)               */
+  const double* lap_central;/* [reps]                                             */
+  const double* mix_z;      /* [reps][nsim]                                       */
+  const double* mix_l;      /* [reps][nsim]                                       */
+} dcor_premat_subg;
+
+int dcor_premat_sign_launch(const dcor_premat_sign* d, dcor_rep_out* d_out, void* stream);
+int dcor_premat_subg_launch(const dcor_premat_subg* d, dcor_rep_out* d_out, void* stream);
+
+/* Batch geometry (m, k) the estimators use; family selects the guard
+ * (sub-G: m>n => m=n; HRS: k<2 => k=2, m=floor(n/2)).  Returns DCOR_EKLT1 if k<1. */
+int dcor_batch_geometry(int64_t n, double eps1, double eps2, int family, int hrs,
+                        int64_t km[2]);
+
+/* ---- single-call host-pointer forms: the R `.Call` targets --------------- */
+/* ci_NI_signbatch (vert-cor.R:204-255). out = {rho_hat, lo, hi}. */
+int dcor_ci_ni_signbatch(const double* X, const double* Y, int64_t n, double eps1,
+                         double eps2, double alpha, int normalise, const double lap_sc[4],
+                         const double* lap_x, const double* lap_y, double out[3]);
+/* ci_INT_signflip (vert-cor.R:260-317); flips one byte (0/1) per sample. */
+int dcor_ci_int_signflip(const double* X, const double* Y, int64_t n, double eps1,
+                         double eps2, double alpha, int mode, int normalise,
+                         const double lap_sc[4], const uint8_t* flips, double lap_z,
+                         const double* mix_z, const double* mix_l, int64_t nsim,
+                         double out[3]);
+/* correlation_NI_subG (ver-cor-subG.R:25-62; hrs: real-data-sims.R:115-147). */
+int dcor_correlation_ni_subg(const double* X, const double* Y, int64_t n, double eps1,
+                             double eps2, double eta1, double eta2, double alpha, int hrs,
+                             double lam_x, double lam_y, const int32_t* perm,
+                             const double* lap_x, const double* lap_y, double out[3]);
+/* ci_INT_subG (ver-cor-subG.R:67-108; hrs: real-data-sims.R:176-252). */
+int dcor_ci_int_subg(const double* X, const double* Y, int64_t n, double eps1, double eps2,
+                     double eta1, double eta2, double alpha, int hrs, double lam_s,
+                     double lam_o, double lam_r, double delta, const double* lap_local,
+                     double lap_central, const double* mix_z, const double* mix_l,
+                     int64_t nsim, double out[3]);
+/* mixquant (ver-cor-subG.R:8-13): sort(z + c*l)[ceiling(p*nsim)]. */
+int dcor_mixquant(const double* z, const double* l, int64_t nsim, double c, double p,
+                  double* out);
+/* priv_standardize (vert-cor.R:322-348): the DP mean / second-moment helper. */
+int dcor_priv_standardize(const double* v, int64_t n, double eps_norm, double L_raw,
+                          const double lap[2], double* out);
+/* dp_sd (real-data-sims.R:73-84): out = {mean, sd}; lap = {mean, m2} unit draws. */
+int dcor_dp_sd(const double* x, int64_t n, double lo, double hi, double eps1, double eps2,
+               const double lap[2], double out[2]);
+
+/* On-device unit draws from the engine's Philox streams (pre-materialised inputs
+ * generated in HBM, e.g. the HRS noise of BASELINE config C5).  kind: 0 unit Laplace,
+ * 1 standard normal (Box-Muller pairs), 2 uniform (0,1).  Element e of replicate r uses
+ * block (e/2, r, site) and words (0,1) / (2,3) for e even / odd.  d_out: [reps][count]. */
+int dcor_draws_launch(int kind, uint64_t seed, int site, int64_t rep_begin, int64_t reps,
+                      int64_t count, double* d_out, void* stream);
+
+/* Draw-site contract of the fused engine (DESIGN.md "RNG"): Philox4x32-10 with
+ * key = (seed lo32, seed hi32), counter = (index, rep, site, 0). */
+enum {
+  DCOR_SITE_DGP_A = 1,   /* Gaussian pair / Bernoulli pair-of-samples / U,E1      */
+  DCOR_SITE_DGP_B = 2,   /* bounded-factor E2 (w0,w1) ; sub-G local Laplace (w2,w3) */
+  DCOR_SITE_FLIP = 3,    /* sign-family INT flips, 4 samples per block            */
+  DCOR_SITE_NI_LAP = 4,  /* batch j: Laplace X (w0,w1), Y (w2,w3)                  */
+  DCOR_SITE_SCALAR = 5,  /* blocks 0..4: NI mu/m2 X, NI mu/m2 Y, INT mu/m2 X, INT mu/m2 Y, Z */
+  DCOR_SITE_MIX_Z = 6,   /* mixquant normals, 2 per block                         */
+  DCOR_SITE_MIX_L = 7    /* mixquant unit Laplace, 2 per block                    */
+};
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DCOR_H */

@@ -1,0 +1,713 @@
+/*
+ * dcor_oracle.c -- CPU restatement of the reference hot path (TEST INFRASTRUCTURE).
+ *
+ * Not product code: only tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg load the shared object built from this file.
+ *
+ * Parity status: "parity unpinned" -- the reference is R with no tests or golden
+ * vectors and R is absent here.  Each function cites the R lines
+ * it restates.  R semantics reproduced:
+ *   sum()   : long-double accumulator, rounded once          (R summary.c rsum)
+ *   mean()  : LD sum / n, then s += sum(x - s)/n in LD       (R summary.c real_mean)
+ *   var()   : mean as above (stored as double), LD sum of (x-m)^2 / (n-1)  (R cov.c)
+ *   rowMeans: LD row sums / p, rounded once                  (R array.c do_colsum)
+ *   max/min : NA/NaN propagate (C fmax does not, so r_max/r_min are used)
+ *   sign(0) = 0; pmax(pmin(x, L), -L) is the clip; x^2 is x*x.
+ * Compiled with -ffp-contract=off so every expression rounds as written.
+ */
+#include "dcor_oracle.h"
+
+#include <math.h>
+#include <pthread.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../include/dcor.h"
+
+typedef long double LD;
+
+/* ------------------------------------------------------------------ R core */
+double orc_r_sum(const double* x, int64_t n) {
+  LD s = 0.0L;
+  for (int64_t i = 0; i < n; ++i) s += x[i];
+  return (double)s;
+}
+
+double orc_r_mean(const double* x, int64_t n) {
+  LD s = 0.0L;
+  for (int64_t i = 0; i < n; ++i) s += x[i];
+  s /= (LD)n;
+  if (isfinite((double)s)) {
+    LD t = 0.0L;
+    for (int64_t i = 0; i < n; ++i) t += ((LD)x[i] - s);
+    s += t / (LD)n;
+  }
+  return (double)s;
+}
+
+double orc_r_var(const double* x, int64_t n) {
+  if (n < 2) return NAN; /* R: var of one value is NA */
+  LD s = 0.0L;
+  for (int64_t i = 0; i < n; ++i) s += x[i];
+  LD tmp = s / (LD)n;
+  if (isfinite((double)tmp)) {
+    LD t = 0.0L;
+    for (int64_t i = 0; i < n; ++i) t += ((LD)x[i] - tmp);
+    tmp = tmp + t / (LD)n;
+  }
+  const LD xm = (LD)(double)tmp; /* xm[] is a double array in cov.c */
+  LD acc = 0.0L;
+  for (int64_t i = 0; i < n; ++i) acc += ((LD)x[i] - xm) * ((LD)x[i] - xm);
+  return (double)(acc / (LD)(n - 1));
+}
+
+static double r_sign(double x) { return isnan(x) ? x : (x > 0 ? 1.0 : (x < 0 ? -1.0 : 0.0)); }
+static double r_max(double a, double b) { return (isnan(a) || isnan(b)) ? NAN : (a > b ? a : b); }
+static double r_min(double a, double b) { return (isnan(a) || isnan(b)) ? NAN : (a < b ? a : b); }
+/* pmax(pmin(x, L), -L) */
+static double r_clip(double x, double L) {
+  if (isnan(x)) return x;
+  double t = (x < L) ? x : L;
+  return (t > -L) ? t : -L;
+}
+/* pmin(pmax(x, lo), hi) (real-data-sims.R order) */
+static double r_clip_lohi(double x, double lo, double hi) {
+  if (isnan(x)) return x;
+  double t = (x > lo) ? x : lo;
+  return (t < hi) ? t : hi;
+}
+
+/* qnorm: Abramowitz-Stegun 26.2.23 start + Halley steps on erfc.  Only ever
+ * evaluated at 1 - alpha/2; checked against scipy.special.ndtri in tests. */
+double orc_qnorm(double p) {
+  if (isnan(p) || p < 0 || p > 1) return NAN;
+  if (p == 0) return -INFINITY;
+  if (p == 1) return INFINITY;
+  const double pp = (p < 0.5) ? p : 1.0 - p; /* exact (Sterbenz) */
+  const double t = sqrt(-2.0 * log(pp));
+  double x = -(t - (2.515517 + 0.802853 * t + 0.010328 * t * t) /
+                       (1.0 + 1.432788 * t + 0.189269 * t * t + 0.001308 * t * t * t));
+  for (int it = 0; it < 6; ++it) { /* lower tail: F(x) = erfc(-x/sqrt2)/2 */
+    const double e = 0.5 * erfc(-x / 1.4142135623730951) - pp;
+    const double u = e * 2.5066282746310002 * exp(0.5 * x * x);
+    x = x - u / (1.0 + 0.5 * x * u);
+  }
+  return (p < 0.5) ? x : -x;
+}
+
+/* ------------------------------------------------ calibration (subG.R:1-7) */
+double orc_lambda_n(double n, double eta) {
+  const double a = 2.0 * eta * sqrt(log(n));
+  const double b = 2.0 * sqrt(3.0);
+  return r_min(a, b);
+}
+
+void orc_lambda_int_n(double n, double eta_s, double eta_r, double eps_s, double out[2]) {
+  out[0] = r_min(2.0 * eta_s * sqrt(log(n)), 2.0 * sqrt(3.0));
+  out[1] = 5.0 * r_max(eta_r, 1.0) * r_min(log(n), 6.0) / (r_min(eps_s, 1.0));
+}
+
+/* ----------------------------------------------------------- mixquant ---- */
+static int cmp_dbl(const void* a, const void* b) {
+  const double x = *(const double*)a, y = *(const double*)b;
+  return (x < y) ? -1 : (x > y);
+}
+
+double orc_mixquant(const double* z, const double* l, int64_t nsim, double c, double p) {
+  double* x = (double*)malloc(sizeof(double) * (size_t)(nsim > 0 ? nsim : 1));
+  int64_t m = 0;
+  for (int64_t i = 0; i < nsim; ++i) {
+    const double v = z[i] + c * l[i]; /* rnorm + (c*rexp)*(2*rbinom-1) */
+    if (!isnan(v)) x[m++] = v;        /* sort() drops NA */
+  }
+  qsort(x, (size_t)m, sizeof(double), cmp_dbl);
+  const double pos = ceil(p * (double)nsim); /* ceiling(p*nsim), 1-based */
+  double r = NAN;
+  if (pos >= 1 && pos <= (double)m) r = x[(int64_t)pos - 1];
+  free(x);
+  return r;
+}
+
+/* -------------------------------------------------- sign family ----------- */
+void orc_priv_standardize(const double* v, int64_t n, double eps_norm, double L_raw,
+                          const double lap[2], double* out) {
+  /* vert-cor.R:322-348 */
+  double* xc = (double*)malloc(sizeof(double) * (size_t)n);
+  double* x2 = (double*)malloc(sizeof(double) * (size_t)n);
+  for (int64_t i = 0; i < n; ++i) xc[i] = r_clip(v[i], L_raw);          /* :328 */
+  const double eps_mu = eps_norm / 2, eps_m2 = eps_norm / 2;            /* :331-332 */
+  const double dn = (double)n;
+  const double mu = orc_r_mean(xc, n) + (2.0 * L_raw / (dn * eps_mu)) * lap[0]; /* :335-336 */
+  for (int64_t i = 0; i < n; ++i) x2[i] = xc[i] * xc[i];
+  const double m2 = orc_r_mean(x2, n) + (2.0 * (L_raw * L_raw) / (dn * eps_m2)) * lap[1]; /* :339-340 */
+  const double var = r_max(m2 - mu * mu, 1e-12);                       /* :343 */
+  const double sd = sqrt(var);                                          /* :344 */
+  for (int64_t i = 0; i < n; ++i) out[i] = (xc[i] - mu) / sd;           /* :347 */
+  free(xc);
+  free(x2);
+}
+
+int orc_ci_ni_signbatch(const double* X, const double* Y, int64_t n, double eps1, double eps2,
+                        double alpha, int normalise, const double lap_sc[4],
+                        const double* lap_x, const double* lap_y, double out[3]) {
+  /* vert-cor.R:204-255 */
+  const double dn = (double)n;
+  const double m = ceil(8.0 / (eps1 * eps2));                          /* :207 */
+  const double kd = floor(dn / m);                                     /* :208 */
+  if (!(kd >= 1)) return DCOR_EKLT1;                                   /* :209 */
+  const int64_t k = (int64_t)kd, mi = (int64_t)m;
+  double* Xn = (double*)malloc(sizeof(double) * (size_t)n);
+  double* Yn = (double*)malloc(sizeof(double) * (size_t)n);
+  if (normalise) {                                                     /* :211-216 */
+    const double L = sqrt(2.0 * log(dn));
+    orc_priv_standardize(X, n, eps1, L, lap_sc + 0, Xn);
+    orc_priv_standardize(Y, n, eps2, L, lap_sc + 2, Yn);
+  } else {
+    memcpy(Xn, X, sizeof(double) * (size_t)n);
+    memcpy(Yn, Y, sizeof(double) * (size_t)n);
+  }
+  double* T = (double*)malloc(sizeof(double) * (size_t)k);
+  double* sx = (double*)malloc(sizeof(double) * (size_t)mi);
+  double* sy = (double*)malloc(sizeof(double) * (size_t)mi);
+  for (int64_t j = 0; j < k; ++j) {                                    /* :222-227 */
+    for (int64_t r = 0; r < mi; ++r) {
+      sx[r] = r_sign(Xn[j * mi + r]);
+      sy[r] = r_sign(Yn[j * mi + r]);
+    }
+    const double xb = orc_r_mean(sx, mi), yb = orc_r_mean(sy, mi);
+    const double xt = xb + (2.0 / (m * eps1)) * lap_x[j];              /* :230 */
+    const double yt = yb + (2.0 / (m * eps2)) * lap_y[j];              /* :231 */
+    T[j] = m * xt * yt;                                                /* :233 */
+  }
+  const double eta = (1.0 / kd) * orc_r_sum(T, k);                     /* :234 */
+  const double rho = sin(M_PI * eta / 2.0);                            /* :235 */
+  const double S = sqrt(orc_r_var(T, k));                              /* :239 */
+  const double crit = orc_qnorm(1.0 - alpha / 2.0);                    /* :242 */
+  out[0] = rho;
+  out[1] = sin(M_PI / 2.0 * r_max(eta - crit * S / sqrt(kd), -1.0));   /* :251 */
+  out[2] = sin(M_PI / 2.0 * r_min(eta + crit * S / sqrt(kd), 1.0));    /* :252 */
+  free(T); free(sx); free(sy); free(Xn); free(Yn);
+  return DCOR_OK;
+}
+
+int orc_ci_int_signflip(const double* X, const double* Y, int64_t n, double eps1, double eps2,
+                        double alpha, int mode, int normalise, const double lap_sc[4],
+                        const uint8_t* flips, double lap_z, const double* mix_z,
+                        const double* mix_l, int64_t nsim, double out[3], int* mode_out) {
+  /* vert-cor.R:260-317 */
+  if (!(eps1 > 0 && eps2 > 0) || n < 1) return DCOR_EINVAL;          /* :264 */
+  const double dn = (double)n;
+  double* Xn = (double*)malloc(sizeof(double) * (size_t)n);
+  double* Yn = (double*)malloc(sizeof(double) * (size_t)n);
+  if (normalise) {                                                     /* :268-273 */
+    const double L = sqrt(2.0 * log(dn));
+    orc_priv_standardize(X, n, eps1, L, lap_sc + 0, Xn);
+    orc_priv_standardize(Y, n, eps2, L, lap_sc + 2, Yn);
+  } else {
+    memcpy(Xn, X, sizeof(double) * (size_t)n);
+    memcpy(Yn, Y, sizeof(double) * (size_t)n);
+  }
+  const int sender_is_X = (eps1 >= eps2);                              /* :275 */
+  const double eps_s = sender_is_X ? eps1 : eps2;
+  const double eps_r = sender_is_X ? eps2 : eps1;
+  /* correlation_INT_signflip, vert-cor.R:164-195 */
+  double* core = (double*)malloc(sizeof(double) * (size_t)n);
+  for (int64_t i = 0; i < n; ++i) {                                    /* :178-182 */
+    const double f = 2.0 * (double)flips[i] - 1.0;
+    core[i] = sender_is_X ? f * r_sign(Xn[i]) * r_sign(Yn[i]) : f * r_sign(Yn[i]) * r_sign(Xn[i]);
+  }
+  const double sum_core = orc_r_sum(core, n);                          /* :183 */
+  const double es = exp(eps_s);
+  const double scale_Z = 2.0 * (es + 1.0) / (dn * (es - 1.0) * eps_r); /* :186-187 */
+  const double Z = scale_Z * lap_z;                                    /* :188 */
+  const double eta0 = (es + 1.0) / (dn * (es - 1.0)) * sum_core + Z;   /* :190-191 */
+  const double rho = sin(M_PI * eta0 / 2.0);                           /* :194 */
+  /* CI, vert-cor.R:281-313 */
+  const double eta = 1.0 - acos(rho) * 2.0 / M_PI;                     /* :281 */
+  const double q = (es - 1.0) / (es + 1.0);
+  const double h = 1.0 - acos(rho) * 2.0 / M_PI;
+  const double s2 = 1.0 - (q * q) * (h * h);                           /* :284 */
+  const double ratio = (es + 1.0) / (es - 1.0);                        /* :289 */
+  const double se_eta = 1.0 / sqrt(dn) * sqrt(s2) * ratio;             /* :291 */
+  int md = mode;
+  if (md == DCOR_MODE_AUTO) md = (sqrt(dn) * eps_r > 0.5) ? DCOR_MODE_NORMAL : DCOR_MODE_LAPLACE; /* :294-296 */
+  double w;
+  if (md == DCOR_MODE_NORMAL) {                                        /* :298-302 */
+    const double cstar = 2.0 / (sqrt(dn * s2) * eps_r);
+    w = orc_mixquant(mix_z, mix_l, nsim, cstar, 1.0 - alpha / 2.0) * se_eta;
+  } else {                                                             /* :303-309 */
+    w = (2.0 / (dn * eps_r)) * ratio * log(1.0 / alpha);
+  }
+  out[0] = rho;
+  out[1] = sin(M_PI / 2.0 * r_max(eta - w, -1.0));                     /* :312 */
+  out[2] = sin(M_PI / 2.0 * r_min(eta + w, 1.0));                      /* :313 */
+  if (mode_out) *mode_out = md;
+  free(core); free(Xn); free(Yn);
+  return DCOR_OK;
+}
+
+/* ---------------------------------------------------- sub-G family -------- */
+int orc_ni_subg(const double* X, const double* Y, int64_t n, double eps1, double eps2,
+                double eta1, double eta2, double alpha, int hrs, double lam_x, double lam_y,
+                const int32_t* perm, const double* lap_x, const double* lap_y,
+                double out[3], int64_t km_out[2]) {
+  /* ver-cor-subG.R:25-62 ; hrs: real-data-sims.R:115-147 */
+  if (n < (hrs ? 2 : 1)) return DCOR_EINVAL;
+  const double dn = (double)n;
+  const double l1 = (hrs && !isnan(lam_x)) ? lam_x : orc_lambda_n(dn, eta1); /* :30 / :123 */
+  const double l2 = (hrs && !isnan(lam_y)) ? lam_y : orc_lambda_n(dn, eta2);
+  double m = ceil(8.0 / (eps1 * eps2));                                /* :37 */
+  if (m > dn) m = dn;
+  double kd = floor(dn / m);                                           /* :38 */
+  if (hrs) {
+    if (kd < 2) { kd = 2; m = floor(dn / kd); }                        /* rds:130 */
+  } else if (!(kd >= 1)) {
+    return DCOR_EKLT1;
+  }
+  const int64_t k = (int64_t)kd, mi = (int64_t)m;
+  if (hrs && !perm) return DCOR_EINVAL;
+  double* prod = (double*)malloc(sizeof(double) * (size_t)k);
+  double* T = (double*)malloc(sizeof(double) * (size_t)k);
+  for (int64_t j = 0; j < k; ++j) {                                    /* :40-45 rowMeans */
+    LD sx = 0.0L, sy = 0.0L;
+    for (int64_t r = 0; r < mi; ++r) {
+      const int64_t idx = hrs ? (int64_t)perm[j * mi + r] : j * mi + r;
+      sx += r_clip(X[idx], l1);                                        /* :33 */
+      sy += r_clip(Y[idx], l2);                                        /* :34 */
+    }
+    const double xb = (double)(sx / (LD)mi), yb = (double)(sy / (LD)mi);
+    const double xt = xb + (2.0 * l1 / (m * eps1)) * lap_x[j];         /* :48 */
+    const double yt = yb + (2.0 * l2 / (m * eps2)) * lap_y[j];         /* :49 */
+    prod[j] = xt * yt;
+    T[j] = m * xt * yt;                                                /* :55 */
+  }
+  const double rho = (m / kd) * orc_r_sum(prod, k);                    /* :51-52 */
+  const double se = sqrt(orc_r_var(T, k)) / sqrt(kd);                  /* :56 */
+  const double crit = orc_qnorm(1.0 - alpha / 2.0);                    /* :57 */
+  out[0] = rho;
+  out[1] = r_max(rho - crit * se, -1.0);                               /* :58 */
+  out[2] = r_min(rho + crit * se, 1.0);                                /* :59 */
+  if (km_out) { km_out[0] = k; km_out[1] = mi; }
+  free(prod); free(T);
+  return DCOR_OK;
+}
+
+int orc_int_subg(const double* X, const double* Y, int64_t n, double eps1, double eps2,
+                 double eta1, double eta2, double alpha, int hrs, double lam_s, double lam_o,
+                 double lam_r, double delta, const double* lap_local, double lap_central,
+                 const double* mix_z, const double* mix_l, int64_t nsim,
+                 double out[3], double lam_out[3]) {
+  /* ver-cor-subG.R:67-108 ; hrs: real-data-sims.R:176-252 */
+  if (n < (hrs ? 2 : 1)) return DCOR_EINVAL;
+  const double dn = (double)n;
+  const int sender_is_X = (eps1 >= eps2);                              /* :76 */
+  const double eps_s = sender_is_X ? eps1 : eps2, eps_r = sender_is_X ? eps2 : eps1;
+  const double eta_s = sender_is_X ? eta1 : eta2, eta_r = sender_is_X ? eta2 : eta1;
+  const double* S = sender_is_X ? X : Y;
+  const double* O = sender_is_X ? Y : X;
+  double ls, lo_, lr;
+  if (!hrs) {
+    double lam[2];
+    orc_lambda_int_n(dn, eta_s, eta_r, eps_s, lam);                    /* :83-85 */
+    ls = lam[0]; lr = lam[1]; lo_ = NAN;
+  } else {
+    const double dl = isnan(delta) ? 1.0 / dn : delta;                 /* rds:199 */
+    ls = lam_s; lo_ = lam_o;
+    if (isnan(ls) || isnan(lo_)) {                                     /* rds:202-208 */
+      double lam[2];
+      orc_lambda_int_n(dn, eta_s, eta_r, eps_s, lam);
+      if (isnan(ls)) ls = lam[0];
+      if (isnan(lo_)) lo_ = orc_lambda_n(dn, sender_is_X ? eta2 : eta1);
+    }
+    lr = lam_r;
+    if (isnan(lr)) lr = orc_lambda_receiver_from_noise(ls, lo_, eps_s, dl); /* rds:211-218 */
+  }
+  double* Uc = (double*)malloc(sizeof(double) * (size_t)n);
+  const double bs = 2.0 * ls / (eps_s);
+  for (int64_t i = 0; i < n; ++i) {
+    const double sc = r_clip(S[i], ls);                                /* :88 / rds:222 */
+    const double ov = hrs ? r_clip(O[i], lo_) : O[i];                  /* rds:223 */
+    const double U = (sc + bs * lap_local[i]) * ov;                    /* :89 / rds:224 */
+    Uc[i] = r_clip(U, lr);                                             /* :90 / rds:232 */
+  }
+  const double rho = orc_r_mean(Uc, n) + (2.0 * lr / (dn * eps_r)) * lap_central; /* :91 */
+  const double sdU = sqrt(orc_r_var(Uc, n));
+  double width;
+  if (!hrs) {
+    const double sn = 2.0 * lr / (dn * eps_r);
+    const double se_norm = sqrt(sdU * sdU + 2.0 * (sn * sn));          /* :99 */
+    const double cstar = 2.0 / (sqrt(dn) * sdU * eps_r);               /* :100 */
+    width = orc_mixquant(mix_z, mix_l, nsim, cstar, 1.0 - alpha / 2.0) * se_norm / sqrt(dn); /* :101 */
+  } else if (sdU == 0) {                                               /* rds:237-238 */
+    width = orc_qnorm(1.0 - alpha / 2.0) * sqrt(2.0) * (2.0 * lr / (dn * eps_r));
+  } else {                                                             /* rds:240-241 */
+    const double cstar = (2.0 * lr) / (sqrt(dn) * sdU * eps_r);
+    width = orc_mixquant(mix_z, mix_l, nsim, cstar, 1.0 - alpha / 2.0) * (sdU / sqrt(dn));
+  }
+  out[0] = rho;
+  out[1] = r_max(rho - width, -1.0);                                   /* :102 */
+  out[2] = r_min(rho + width, 1.0);                                    /* :103 */
+  if (lam_out) { lam_out[0] = ls; lam_out[1] = lo_; lam_out[2] = lr; }
+  free(Uc);
+  return DCOR_OK;
+}
+
+/* ------------------------------------------------------------ HRS helpers */
+double orc_dp_mean(const double* x, int64_t n, double lo, double hi, double eps, double lap) {
+  /* real-data-sims.R:64-70 (x assumed NA-free) */
+  if (n < 1) return NAN;
+  double* xc = (double*)malloc(sizeof(double) * (size_t)n);
+  for (int64_t i = 0; i < n; ++i) xc[i] = r_clip_lohi(x[i], lo, hi);
+  const double r = orc_r_mean(xc, n) + ((hi - lo) / ((double)n * eps)) * lap;
+  free(xc);
+  return r;
+}
+
+void orc_dp_sd(const double* x, int64_t n, double lo, double hi, double eps1, double eps2,
+               const double lap[2], double out[2]) {
+  /* real-data-sims.R:73-84 */
+  double* xc = (double*)malloc(sizeof(double) * (size_t)n);
+  double* x2 = (double*)malloc(sizeof(double) * (size_t)n);
+  for (int64_t i = 0; i < n; ++i) xc[i] = r_clip_lohi(x[i], lo, hi);
+  const double mu = orc_dp_mean(xc, n, lo, hi, eps1, lap[0]);
+  for (int64_t i = 0; i < n; ++i) x2[i] = xc[i] * xc[i];
+  const double m2 = orc_r_mean(x2, n) + ((hi * hi - lo * lo) / ((double)n * eps2)) * lap[1];
+  out[0] = mu;
+  out[1] = sqrt(r_max(m2 - mu * mu, 0.0));
+  free(xc); free(x2);
+}
+
+void orc_standardize_dp(const double* x, int64_t n, double mean, double sd, double lo,
+                        double hi, double* out) {
+  /* real-data-sims.R:87-90 */
+  const double s = r_max(sd, 1e-8);
+  for (int64_t i = 0; i < n; ++i) out[i] = (r_clip_lohi(x[i], lo, hi) - mean) / s;
+}
+
+double orc_lambda_from_priv(double lo, double hi, double mean, double sd) {
+  /* real-data-sims.R:103-106 */
+  const double sig = r_max(sd, 1e-8);
+  return r_max(fabs((lo - mean) / sig), fabs((hi - mean) / sig));
+}
+
+double orc_lambda_receiver_from_noise(double lam_s, double lam_o, double eps_s, double delta) {
+  /* real-data-sims.R:170-174 */
+  const double b_s = 2.0 * lam_s / eps_s;
+  return (lam_s + b_s * log(1.0 / delta)) * lam_o;
+}
+
+/* ------------------------------------------------------------------ DGPs */
+void orc_mvrnorm_factor(const double mu[2], const double sigma[2], double rho, double A[4]) {
+  (void)mu;
+  /* Sigma as built at vert-cor.R:389-390; eigen(Sigma, symmetric=TRUE), values
+   * decreasing; vector sign convention v2 = (-v1[1], v1[0]), v1[1] >= 0
+   * (matches R's output for [[1,.5],[.5,1]] and diag(2); not otherwise pinned). */
+  const double s11 = sigma[0] * sigma[0];
+  const double s12 = sigma[0] * sigma[1] * rho;
+  const double s22 = sigma[1] * sigma[1];
+  const double mid = (s11 + s22) / 2.0;
+  const double hd = (s11 - s22) / 2.0;
+  const double d = sqrt(hd * hd + s12 * s12);
+  const double l1 = mid + d, l2 = mid - d;
+  double v0, v1;
+  if (s12 == 0.0) {
+    if (s11 > s22) { v0 = 1.0; v1 = 0.0; } else { v0 = 0.0; v1 = 1.0; }
+  } else {
+    if (s11 >= s22) { v0 = l1 - s22; v1 = s12; } else { v0 = s12; v1 = l1 - s11; }
+    const double nr = sqrt(v0 * v0 + v1 * v1);
+    v0 /= nr; v1 /= nr;
+    if (v1 < 0) { v0 = -v0; v1 = -v1; }
+  }
+  const double a1 = sqrt(l1 > 0 ? l1 : 0.0), a2 = sqrt(l2 > 0 ? l2 : 0.0);
+  A[0] = v0 * a1;   A[1] = -v1 * a2;
+  A[2] = v1 * a1;   A[3] = v0 * a2;
+}
+
+void orc_mvrnorm_apply(const double* z1, const double* z2, int64_t n, const double mu[2],
+                       const double A[4], double* X, double* Y) {
+  for (int64_t i = 0; i < n; ++i) {
+    X[i] = mu[0] + (A[0] * z1[i] + A[1] * z2[i]);
+    Y[i] = mu[1] + (A[2] * z1[i] + A[3] * z2[i]);
+  }
+}
+
+void orc_gen_bernoulli(const double* u, const double* v, int64_t n, double rho, double* X,
+                       double* Y) {
+  /* vert-cor.R:78-98 */
+  const double p11 = 0.25 + rho / 4, p10 = 0.25 - rho / 4, p01 = p10;
+  for (int64_t i = 0; i < n; ++i) {
+    X[i] = (u[i] < 0.5) ? 1.0 : 0.0;
+    Y[i] = (X[i] == 0.0) ? (v[i] < (p01 / 0.5) ? 1.0 : 0.0) : (v[i] < (p11 / 0.5) ? 1.0 : 0.0);
+  }
+}
+
+void orc_gen_bounded_factor(const double* u, const double* e1, const double* e2, int64_t n,
+                            double rho, double* X, double* Y) {
+  /* ver-cor-subG.R:141-154 ; runif(n, a, b) = a + (b - a) * u */
+  const double cU = sqrt(3.0 * rho), cE = sqrt(3.0 * (1.0 - rho));
+  for (int64_t i = 0; i < n; ++i) {
+    const double U = -cU + (cU - -cU) * u[i];
+    const double E1 = -cE + (cE - -cE) * e1[i];
+    const double E2 = -cE + (cE - -cE) * e2[i];
+    X[i] = U + E1;
+    Y[i] = U + E2;
+  }
+}
+
+/* ------------------------------------------------------ RNG restatement -- */
+void orc_philox4x32_10(const uint32_t ctr[4], uint32_t k0, uint32_t k1, uint32_t out[4]) {
+  uint32_t x0 = ctr[0], x1 = ctr[1], x2 = ctr[2], x3 = ctr[3];
+  for (int r = 0; r < 10; ++r) {
+    const uint64_t p0 = (uint64_t)0xD2511F53u * x0;
+    const uint64_t p1 = (uint64_t)0xCD9E8D57u * x2;
+    const uint32_t y0 = (uint32_t)(p1 >> 32) ^ x1 ^ k0;
+    const uint32_t y2 = (uint32_t)(p0 >> 32) ^ x3 ^ k1;
+    x0 = y0; x1 = (uint32_t)p1; x2 = y2; x3 = (uint32_t)p0;
+    k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
+  }
+  out[0] = x0; out[1] = x1; out[2] = x2; out[3] = x3;
+}
+
+double orc_u53(uint32_t a, uint32_t b) {
+  const uint64_t x = ((uint64_t)a << 20) | (uint64_t)(b >> 12); /* 52 bits */
+  return (double)(2 * x + 1) * 0x1p-53;                          /* (0,1), exact */
+}
+
+/* fdlibm-style natural log for positive normal x (the engine's log). */
+double orc_log(double x) {
+  static const double ln2_hi = 6.93147180369123816490e-01, ln2_lo = 1.90821492927058770002e-10,
+                      Lg1 = 6.666666666666735130e-01, Lg2 = 3.999999999940941908e-01,
+                      Lg3 = 2.857142874366239149e-01, Lg4 = 2.222219843214978396e-01,
+                      Lg5 = 1.818357216161805012e-01, Lg6 = 1.531383769920937332e-01,
+                      Lg7 = 1.479819860511658591e-01;
+  uint64_t bits;
+  memcpy(&bits, &x, 8);
+  int32_t hx = (int32_t)(bits >> 32);
+  const uint32_t lx = (uint32_t)bits;
+  int32_t k = ((hx >> 20) & 0x7ff) - 1023;
+  hx &= 0x000fffff;
+  const int32_t i = (hx + 0x95f64) & 0x100000;
+  hx |= (i ^ 0x3ff00000);
+  k += (i >> 20);
+  bits = ((uint64_t)(uint32_t)hx << 32) | lx;
+  double mnt;
+  memcpy(&mnt, &bits, 8);
+  const double f = mnt - 1.0;
+  const double s = f / (2.0 + f);
+  const double dk = (double)k;
+  const double z = s * s, w = z * z;
+  const double t1 = w * fma(w, fma(w, Lg6, Lg4), Lg2);
+  const double t2 = z * fma(w, fma(w, fma(w, Lg7, Lg5), Lg3), Lg1);
+  const double R = t2 + t1;
+  const double hfsq = 0.5 * f * f;
+  return dk * ln2_hi - ((hfsq - (s * (hfsq + R) + dk * ln2_lo)) - f);
+}
+
+/* sin(pi t), cos(pi t) for t with 2t exactly representable. */
+void orc_sincospi(double t, double* sp, double* cp) {
+  static const double S1 = -1.66666666666666324348e-01, S2 = 8.33333333332248946124e-03,
+                      S3 = -1.98412698298579493134e-04, S4 = 2.75573137070700676789e-06,
+                      S5 = -2.50507602534068634195e-08, S6 = 1.58969099521155010221e-10,
+                      C1 = 4.16666666666666019037e-02, C2 = -1.38888888888741095749e-03,
+                      C3 = 2.48015872894767294178e-05, C4 = -2.75573143513906633035e-07,
+                      C5 = 2.08757232129817482790e-09, C6 = -1.13596475577881948265e-11,
+                      PIO2_HI = 1.57079632679489655800e+00, PIO2_LO = 6.12323399573676603587e-17;
+  const double t2 = 2.0 * t;
+  const double j = rint(t2);
+  const double r = t2 - j;
+  const double x = fma(r, PIO2_HI, r * PIO2_LO);
+  const double z = x * x;
+  const double v = z * x;
+  const double rs = fma(z, fma(z, fma(z, S6, S5), S4), S3);
+  const double sn = x + v * fma(z, fma(z, rs, S2), S1) ;
+  const double rc = z * fma(z, fma(z, fma(z, fma(z, fma(z, C6, C5), C4), C3), C2), C1);
+  const double hz = 0.5 * z;
+  const double wc = 1.0 - hz;
+  const double cs = wc + (((1.0 - wc) - hz) + z * rc);
+  const int q = ((int)j) & 3;
+  double s, c;
+  if (q == 0) { s = sn; c = cs; }
+  else if (q == 1) { s = cs; c = -sn; }
+  else if (q == 2) { s = -sn; c = -cs; }
+  else { s = -cs; c = sn; }
+  *sp = s; *cp = c;
+}
+
+double orc_unit_laplace(double u) {
+  /* extraDistr::rlaplace(1, 0, 1) restated on one uniform: -sign(u')*log(1-2|u'|) */
+  const double up = u - 0.5;
+  const double g = orc_log(1.0 - 2.0 * fabs(up));
+  return (up > 0) ? -g : g;
+}
+
+void orc_normal_pair(const uint32_t w[4], double* z1, double* z2) {
+  const double u1 = orc_u53(w[0], w[1]);
+  const double u2 = orc_u53(w[2], w[3]);
+  const double r = sqrt(-2.0 * orc_log(u1));
+  double s, c;
+  orc_sincospi(2.0 * u2, &s, &c);
+  *z1 = r * c;
+  *z2 = r * s;
+}
+
+static void blk(uint64_t seed, uint32_t idx, uint32_t rep, uint32_t site, uint32_t w[4]) {
+  const uint32_t ctr[4] = {idx, rep, site, 0u};
+  orc_philox4x32_10(ctr, (uint32_t)seed, (uint32_t)(seed >> 32), w);
+}
+
+void orc_gen_normals(uint64_t seed, int64_t rep, int site, int64_t count, double* z) {
+  for (int64_t j = 0; 2 * j < count; ++j) {
+    uint32_t w[4];
+    blk(seed, (uint32_t)j, (uint32_t)rep, (uint32_t)site, w);
+    double a, b;
+    orc_normal_pair(w, &a, &b);
+    z[2 * j] = a;
+    if (2 * j + 1 < count) z[2 * j + 1] = b;
+  }
+}
+
+void orc_gen_laplace(uint64_t seed, int64_t rep, int site, int64_t count, double* l) {
+  for (int64_t j = 0; 2 * j < count; ++j) {
+    uint32_t w[4];
+    blk(seed, (uint32_t)j, (uint32_t)rep, (uint32_t)site, w);
+    l[2 * j] = orc_unit_laplace(orc_u53(w[0], w[1]));
+    if (2 * j + 1 < count) l[2 * j + 1] = orc_unit_laplace(orc_u53(w[2], w[3]));
+  }
+}
+
+/* ------------------------------------------- fused replicate restatement - */
+static void gen_xy(const dcor_cell* c, int64_t rep, double* X, double* Y, double* lap_local) {
+  const int64_t n = c->n;
+  double A[4];
+  if (c->dgp == DCOR_DGP_GAUSSIAN) orc_mvrnorm_factor(c->mu, c->sigma, c->rho, A);
+  const double cU = sqrt(3.0 * c->rho), cE = sqrt(3.0 * (1.0 - c->rho));
+  const double p11 = 0.25 + c->rho / 4, p10 = 0.25 - c->rho / 4, p01 = p10;
+  for (int64_t i = 0; i < n; ++i) {
+    uint32_t w[4];
+    if (c->dgp == DCOR_DGP_GAUSSIAN) {
+      blk(c->seed, (uint32_t)i, (uint32_t)rep, DCOR_SITE_DGP_A, w);
+      double z1, z2;
+      orc_normal_pair(w, &z1, &z2);
+      X[i] = c->mu[0] + (A[0] * z1 + A[1] * z2);
+      Y[i] = c->mu[1] + (A[2] * z1 + A[3] * z2);
+    } else if (c->dgp == DCOR_DGP_BERNOULLI) {
+      blk(c->seed, (uint32_t)(i >> 1), (uint32_t)rep, DCOR_SITE_DGP_A, w);
+      const int b = 2 * (int)(i & 1);
+      const double u = (double)w[b] * 0x1p-32, v = (double)w[b + 1] * 0x1p-32;
+      X[i] = (u < 0.5) ? 1.0 : 0.0;
+      Y[i] = (X[i] == 0.0) ? (v < (p01 / 0.5) ? 1.0 : 0.0) : (v < (p11 / 0.5) ? 1.0 : 0.0);
+    } else {
+      blk(c->seed, (uint32_t)i, (uint32_t)rep, DCOR_SITE_DGP_A, w);
+      const double u = orc_u53(w[0], w[1]), e1 = orc_u53(w[2], w[3]);
+      uint32_t w2[4];
+      blk(c->seed, (uint32_t)i, (uint32_t)rep, DCOR_SITE_DGP_B, w2);
+      const double e2 = orc_u53(w2[0], w2[1]);
+      const double U = -cU + (cU - -cU) * u;
+      X[i] = U + (-cE + (cE - -cE) * e1);
+      Y[i] = U + (-cE + (cE - -cE) * e2);
+    }
+    if (lap_local) {
+      uint32_t w2[4];
+      blk(c->seed, (uint32_t)i, (uint32_t)rep, DCOR_SITE_DGP_B, w2);
+      lap_local[i] = orc_unit_laplace(orc_u53(w2[2], w2[3]));
+    }
+  }
+}
+
+int orc_sim_rep(const void* cellp, int64_t rep, double out[6]) {
+  const dcor_cell* c = (const dcor_cell*)cellp;
+  const int64_t n = c->n;
+  if (n < 1 || !(c->eps1 > 0) || !(c->eps2 > 0)) return DCOR_EINVAL;
+  const int64_t nsim = c->nsim;
+  const int subg = (c->family == DCOR_FAMILY_SUBG);
+  double* X = (double*)malloc(sizeof(double) * (size_t)n);
+  double* Y = (double*)malloc(sizeof(double) * (size_t)n);
+  double* ll = subg ? (double*)malloc(sizeof(double) * (size_t)n) : NULL;
+  gen_xy(c, rep, X, Y, ll);
+  /* batch geometry and NI Laplace draws */
+  double m = ceil(8.0 / (c->eps1 * c->eps2));
+  if (subg && m > (double)n) m = (double)n;
+  const double kd = floor((double)n / m);
+  const int64_t k = kd >= 1 ? (int64_t)kd : 1;
+  double* lx = (double*)malloc(sizeof(double) * (size_t)k);
+  double* ly = (double*)malloc(sizeof(double) * (size_t)k);
+  for (int64_t j = 0; j < k; ++j) {
+    uint32_t w[4];
+    blk(c->seed, (uint32_t)j, (uint32_t)rep, DCOR_SITE_NI_LAP, w);
+    lx[j] = orc_unit_laplace(orc_u53(w[0], w[1]));
+    ly[j] = orc_unit_laplace(orc_u53(w[2], w[3]));
+  }
+  double sc[10];
+  for (int b = 0; b < 5; ++b) {
+    uint32_t w[4];
+    blk(c->seed, (uint32_t)b, (uint32_t)rep, DCOR_SITE_SCALAR, w);
+    sc[2 * b] = orc_unit_laplace(orc_u53(w[0], w[1]));
+    sc[2 * b + 1] = orc_unit_laplace(orc_u53(w[2], w[3]));
+  }
+  double* mz = (double*)malloc(sizeof(double) * (size_t)(nsim + 1));
+  double* ml = (double*)malloc(sizeof(double) * (size_t)(nsim + 1));
+  orc_gen_normals(c->seed, rep, DCOR_SITE_MIX_Z, nsim, mz);
+  orc_gen_laplace(c->seed, rep, DCOR_SITE_MIX_L, nsim, ml);
+  int st;
+  if (!subg) {
+    st = orc_ci_ni_signbatch(X, Y, n, c->eps1, c->eps2, c->alpha, c->normalise, sc, lx, ly, out);
+    if (st == DCOR_OK) {
+      const int sender_is_X = (c->eps1 >= c->eps2);
+      const double es = exp(sender_is_X ? c->eps1 : c->eps2);
+      const double p = es / (es + 1.0);
+      uint8_t* fl = (uint8_t*)malloc((size_t)n);
+      for (int64_t i = 0; i < n; ++i) {
+        uint32_t w[4];
+        blk(c->seed, (uint32_t)(i >> 2), (uint32_t)rep, DCOR_SITE_FLIP, w);
+        fl[i] = ((double)w[i & 3] * 0x1p-32 < p) ? 1 : 0;
+      }
+      int md;
+      st = orc_ci_int_signflip(X, Y, n, c->eps1, c->eps2, c->alpha, c->ci_mode, c->normalise,
+                               sc + 4, fl, sc[8], mz, ml, nsim, out + 3, &md);
+      free(fl);
+    }
+  } else {
+    st = orc_ni_subg(X, Y, n, c->eps1, c->eps2, c->eta1, c->eta2, c->alpha, 0, NAN, NAN, NULL,
+                     lx, ly, out, NULL);
+    if (st == DCOR_OK)
+      st = orc_int_subg(X, Y, n, c->eps1, c->eps2, c->eta1, c->eta2, c->alpha, 0, NAN, NAN, NAN,
+                        NAN, ll, sc[8], mz, ml, nsim, out + 3, NULL);
+  }
+  free(X); free(Y); free(ll); free(lx); free(ly); free(mz); free(ml);
+  return st;
+}
+
+typedef struct { const void* cell; int64_t r0, r1; double* out; int st; } job_t;
+
+static void* worker(void* p) {
+  job_t* j = (job_t*)p;
+  j->st = 0;
+  for (int64_t r = j->r0; r < j->r1; ++r) {
+    const int s = orc_sim_rep(j->cell, r, j->out + 6 * r);
+    if (s) j->st = s;
+  }
+  return NULL;
+}
+
+int orc_sim_reps(const void* cell, int64_t r0, int64_t r1, int threads, double* out) {
+  /* out indexed by absolute replicate - r0 */
+  if (threads < 1) threads = 1;
+  double* base = out - 6 * r0;
+  pthread_t th[256];
+  job_t jobs[256];
+  if (threads > 256) threads = 256;
+  const int64_t total = r1 - r0;
+  for (int t = 0; t < threads; ++t) {
+    jobs[t].cell = cell;
+    jobs[t].r0 = r0 + total * t / threads;
+    jobs[t].r1 = r0 + total * (t + 1) / threads;
+    jobs[t].out = base;
+    pthread_create(&th[t], NULL, worker, &jobs[t]);
+  }
+  int st = 0;
+  for (int t = 0; t < threads; ++t) {
+    pthread_join(th[t], NULL);
+    if (jobs[t].st) st = jobs[t].st;
+  }
+  return st;
+}

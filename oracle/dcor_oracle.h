@@ -1,0 +1,129 @@
+/*
+ * dcor_oracle.h -- CPU restatement of the reference's Monte-Carlo hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Nothing in the product (distributed-correlation_amd/)
+ * includes, links or calls this.  Only tests/, __graft_entry__.smoke() and the
+ * cpu_baseline leg of bench.py may load it, and only as the checker.
+ *
+ * PARITY STATUS: "parity unpinned".  The reference (abhinavc3/distributed-correlation
+ * @ 2025-12-05) is R code with no tests, no golden vectors and no fixtures for this
+ * path, and R is absent from this image.  This file restates the R
+ * functions line by line (cited below) with R's arithmetic semantics (long-double
+ * sum/mean/var, `mean`'s correction pass, left-to-right operation order), and is
+ * cross-checked against an independent numpy restatement (tests/golden/) and
+ * closed-form known-answer tests.
+ *
+ * All noise is an explicit input (unit-scale Laplace draws, flip bits, mixquant
+ * normal / Laplace vectors), so every function here is deterministic.
+ */
+#ifndef DCOR_ORACLE_H
+#define DCOR_ORACLE_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- R arithmetic semantics -------------------------------------------- */
+double orc_r_sum(const double* x, int64_t n);   /* R sum(): long-double accumulator      */
+double orc_r_mean(const double* x, int64_t n);  /* R mean(): LD sum / n + correction pass */
+double orc_r_var(const double* x, int64_t n);   /* R var(): cov.c two-pass, n-1           */
+double orc_qnorm(double p);                      /* standard normal quantile              */
+
+/* ---- calibration (ver-cor-subG.R:1-7) ------------------------------------ */
+double orc_lambda_n(double n, double eta);
+void   orc_lambda_int_n(double n, double eta_s, double eta_r, double eps_s, double out[2]);
+
+/* ---- mixquant (ver-cor-subG.R:8-13, vert-cor.R:44-48, real-data-sims.R:161-164)
+ * x_i = z_i + c*l_i where l_i = rexp_i*(2*rbinom_i-1) (a unit Laplace draw);
+ * returns sort(x)[ceiling(p*nsim)] (R drops NaN in sort; NaN if index too big). */
+double orc_mixquant(const double* z, const double* l, int64_t nsim, double c, double p);
+
+/* ---- sign family (vert-cor.R) -------------------------------------------- */
+/* priv_standardize (vert-cor.R:322-348); lap = {mu, m2} unit Laplace draws. */
+void orc_priv_standardize(const double* v, int64_t n, double eps_norm, double L_raw,
+                          const double lap[2], double* out);
+
+/* ci_NI_signbatch (vert-cor.R:204-255).
+ * lap_sc = {mu_X, m2_X, mu_Y, m2_Y} unit Laplace (used iff normalise),
+ * lap_x/lap_y = k unit Laplace each.  out = {rho_hat, lo, hi}.
+ * returns 0, or 2 (k < 1, the stopifnot at vert-cor.R:209). */
+int orc_ci_ni_signbatch(const double* X, const double* Y, int64_t n, double eps1, double eps2,
+                        double alpha, int normalise, const double lap_sc[4],
+                        const double* lap_x, const double* lap_y, double out[3]);
+
+/* ci_INT_signflip (vert-cor.R:260-317) incl. correlation_INT_signflip (164-195).
+ * lap_sc = fresh {mu_X, m2_X, mu_Y, m2_Y}; flips[i] in {0,1} (rbinom(n,1,p));
+ * lap_z unit Laplace; mix_z/mix_l nsim each (used iff mode resolves to normal).
+ * mode: 0 auto, 1 normal, 2 laplace; *mode_out = resolved (1/2). */
+int orc_ci_int_signflip(const double* X, const double* Y, int64_t n, double eps1, double eps2,
+                        double alpha, int mode, int normalise, const double lap_sc[4],
+                        const uint8_t* flips, double lap_z, const double* mix_z,
+                        const double* mix_l, int64_t nsim, double out[3], int* mode_out);
+
+/* ---- sub-Gaussian family (ver-cor-subG.R, real-data-sims.R) -------------- */
+/* correlation_NI_subG.  hrs=0: ver-cor-subG.R:25-62 (contiguous batches, lambda_n,
+ * m>n => m=n).  hrs=1: real-data-sims.R:115-147 (lambda overrides, k<2 guard, batch
+ * rows from perm[k*m] 0-based = sample.int(n, k*m)-1).  lam_x/lam_y: NaN = default.
+ * out = {rho_hat, lo, hi}; km_out = {k, m} (may be NULL). */
+int orc_ni_subg(const double* X, const double* Y, int64_t n, double eps1, double eps2,
+                double eta1, double eta2, double alpha, int hrs, double lam_x, double lam_y,
+                const int32_t* perm, const double* lap_x, const double* lap_y,
+                double out[3], int64_t km_out[2]);
+
+/* ci_INT_subG.  hrs=0: ver-cor-subG.R:67-108.  hrs=1: real-data-sims.R:176-252
+ * (lam_s/lam_o/lam_r/delta overrides, NaN = default; other variable clipped;
+ * c* with lambda_r; sampling-only se; sd(Uc)==0 branch).
+ * lap_local[n], lap_central unit Laplace; mix_z/mix_l nsim each.
+ * lam_out = {lambda_sender, lambda_other(or NaN), lambda_receiver} (may be NULL). */
+int orc_int_subg(const double* X, const double* Y, int64_t n, double eps1, double eps2,
+                 double eta1, double eta2, double alpha, int hrs, double lam_s, double lam_o,
+                 double lam_r, double delta, const double* lap_local, double lap_central,
+                 const double* mix_z, const double* mix_l, int64_t nsim,
+                 double out[3], double lam_out[3]);
+
+/* ---- HRS DP helpers (real-data-sims.R:64-106,170-174) -------------------- */
+double orc_dp_mean(const double* x, int64_t n, double lo, double hi, double eps, double lap);
+void   orc_dp_sd(const double* x, int64_t n, double lo, double hi, double eps1, double eps2,
+                 const double lap[2], double out_mean_sd[2]);
+void   orc_standardize_dp(const double* x, int64_t n, double mean, double sd, double lo,
+                          double hi, double* out);
+double orc_lambda_from_priv(double lo, double hi, double mean, double sd);
+double orc_lambda_receiver_from_noise(double lam_s, double lam_o, double eps_s, double delta);
+
+/* ---- DGPs from explicit uniforms / normals -------------------------------- */
+/* MASS::mvrnorm, 2-d (vert-cor.R:389-394): X = mu + A z, A = V diag(sqrt(ev)). */
+void orc_mvrnorm_factor(const double mu[2], const double sigma[2], double rho, double A[4]);
+void orc_mvrnorm_apply(const double* z1, const double* z2, int64_t n, const double mu[2],
+                       const double A[4], double* X, double* Y);
+/* gen_bernoulli (vert-cor.R:78-98) from uniforms u, v. */
+void orc_gen_bernoulli(const double* u, const double* v, int64_t n, double rho, double* X,
+                       double* Y);
+/* gen_bounded_factor (ver-cor-subG.R:141-154) from uniforms on [0,1). */
+void orc_gen_bounded_factor(const double* u, const double* e1, const double* e2, int64_t n,
+                            double rho, double* X, double* Y);
+
+/* ---- counter-based RNG restatement (the engine's draw-site contract) ----- */
+void   orc_philox4x32_10(const uint32_t ctr[4], uint32_t k0, uint32_t k1, uint32_t out[4]);
+double orc_u53(uint32_t a, uint32_t b);
+double orc_log(double x);
+void   orc_sincospi(double t, double* s, double* c);
+double orc_unit_laplace(double u);
+void   orc_normal_pair(const uint32_t w[4], double* z1, double* z2);
+
+/* One fused replicate, generated from the (seed, rep) Philox streams exactly as
+ * the GPU engine draws them, then fed through the estimators above.
+ * cell layout = dcor_cell in include/dcor.h.  out = {ni_hat, ni_lo, ni_hi,
+ * int_hat, int_lo, int_hi}.  Returns status. */
+int orc_sim_rep(const void* cell, int64_t rep, double out[6]);
+/* Replicates [r0, r1) on `threads` host threads (pthreads). */
+int orc_sim_reps(const void* cell, int64_t r0, int64_t r1, int threads, double* out);
+
+/* Draw the explicit noise a replicate consumes (for tests): see orc_sim_rep. */
+void orc_gen_normals(uint64_t seed, int64_t rep, int site, int64_t count, double* z);
+void orc_gen_laplace(uint64_t seed, int64_t rep, int site, int64_t count, double* l);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,134 @@
+"""GPU parity: the HIP path (through the C-ABI) against the CPU oracle on identical inputs.
+
+Bar: estimators and CI endpoints within 1e-12 relative (ATOL 1e-13 floor for values
+that cancel to 0); integer-valued work (batch sign counts, flip sums, Philox draws)
+bit-exact.  Oracle parity status: unpinned (oracle/dcor_oracle.h)."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+from helpers import assert_close, sign_case, subg_case
+
+pytestmark = pytest.mark.gpu
+
+EPS_PAIRS = [(0.5, 0.5), (1.0, 1.0), (1.5, 0.5), (0.5, 1.5), (0.2, 0.2)]
+
+
+@pytest.fixture(scope="module")
+def dc():
+    import torch
+    assert torch.cuda.is_available()
+    import dcor
+    return dcor
+
+
+@pytest.fixture(scope="module")
+def orc():
+    from oracle import oracle
+    return oracle
+
+
+# --------------------------------------------------------------- RNG streams
+@pytest.mark.parametrize("kind,site", [(1, 6), (0, 7), (0, 4), (1, 1)])
+def test_draws_bitexact(dc, orc, kind, site):
+    import torch
+    from dcor import _lib
+    seed, r0, reps, count = 1_000_073, 5, 3, 4099
+    out = torch.empty((reps, count), dtype=torch.float64, device="cuda")
+    _lib.check(_lib.lib.dcor_draws_launch(kind, seed, site, r0, reps, count,
+                                          C.c_void_p(out.data_ptr()), None))
+    got = out.cpu().numpy()
+    for r in range(reps):
+        ref = (orc.gen_normals if kind == 1 else orc.gen_laplace)(seed, r0 + r, site, count)
+        assert np.array_equal(got[r], ref), f"stream mismatch kind={kind} site={site} rep={r0 + r}"
+
+
+# ------------------------------------------------------- explicit-input sign
+@pytest.mark.parametrize("n", [10, 1000, 10_000, 100_000])
+@pytest.mark.parametrize("eps", EPS_PAIRS)
+def test_sign_single(dc, orc, n, eps):
+    eps1, eps2 = eps
+    g = np.random.default_rng(n * 7 + int(eps1 * 10) * 3 + int(eps2 * 10))
+    cs = sign_case(g, n, eps1, eps2)
+    if cs["k"] >= 1:
+        st, ref = orc.ci_ni_signbatch(cs["X"], cs["Y"], eps1, eps2, 0.05, 1, cs["lap_ni_sc"],
+                                      cs["lap_x"], cs["lap_y"])
+        assert st == 0
+        got = dc.ci_NI_signbatch(cs["X"], cs["Y"], eps1, eps2, noise={
+            "lap_sc": cs["lap_ni_sc"], "lap_x": cs["lap_x"], "lap_y": cs["lap_y"]})
+        assert_close([got["rho_hat"], *got["ci"]], ref, what=f"NI sign n={n} eps={eps}")
+    else:
+        with pytest.raises(dc.KLessThanOne):
+            dc.ci_NI_signbatch(cs["X"], cs["Y"], eps1, eps2, noise={
+                "lap_sc": cs["lap_ni_sc"], "lap_x": cs["lap_x"], "lap_y": cs["lap_y"]})
+    for mode in (0, 1, 2):
+        st, ref, md = orc.ci_int_signflip(cs["X"], cs["Y"], eps1, eps2, 0.05, mode, 1,
+                                          cs["lap_int_sc"], cs["flips"], cs["lap_z"],
+                                          cs["mix_z"], cs["mix_l"])
+        assert st == 0
+        got = dc.ci_INT_signflip(cs["X"], cs["Y"], eps1, eps2, mode=["auto", "normal", "laplace"][mode],
+                                 noise={"lap_sc": cs["lap_int_sc"], "flips": cs["flips"],
+                                        "lap_z": cs["lap_z"], "mix_z": cs["mix_z"],
+                                        "mix_l": cs["mix_l"]})
+        assert_close([got["rho_hat"], *got["ci"]], ref, what=f"INT sign n={n} eps={eps} mode={mode}")
+        assert got["mode"] == ("normal" if md == 1 else "laplace")
+
+
+# ------------------------------------------------------- explicit-input sub-G
+@pytest.mark.parametrize("n", [10, 1000, 10_000, 100_000])
+@pytest.mark.parametrize("eps", EPS_PAIRS)
+@pytest.mark.parametrize("hrs", [False, True])
+def test_subg_single(dc, orc, n, eps, hrs):
+    eps1, eps2 = eps
+    g = np.random.default_rng(n * 11 + int(eps1 * 10) * 5 + int(eps2 * 10) + 999 * hrs)
+    cs = subg_case(g, n, eps1, eps2, nsim=2000 if hrs else 1000, hrs=hrs)
+    lamx, lamy = (2.2, 2.6) if hrs else (np.nan, np.nan)
+    st, ref, km = orc.ni_subg(cs["X"], cs["Y"], eps1, eps2, hrs=int(hrs), lam_x=lamx, lam_y=lamy,
+                              perm=cs["perm"], lap_x=cs["lap_x"], lap_y=cs["lap_y"])
+    assert st == 0
+    got = dc.correlation_NI_subG(cs["X"], cs["Y"], eps1, eps2, hrs=hrs,
+                                 lambda_X=None if not hrs else lamx,
+                                 lambda_Y=None if not hrs else lamy, perm=cs["perm"],
+                                 noise={"lap_x": cs["lap_x"], "lap_y": cs["lap_y"]})
+    assert_close([got["rho_hat"], *got["ci"]], ref, what=f"NI subG n={n} eps={eps} hrs={hrs}")
+    kw = dict(lam_s=2.2, lam_o=2.6) if hrs else {}
+    st, ref, lam = orc.int_subg(cs["X"], cs["Y"], eps1, eps2, hrs=int(hrs), lap_local=cs["lap_local"],
+                                lap_central=cs["lap_central"], mix_z=cs["mix_z"], mix_l=cs["mix_l"], **kw)
+    assert st == 0
+    got = dc.ci_INT_subG(cs["X"], cs["Y"], eps1, eps2, hrs=hrs,
+                         lambda_sender=kw.get("lam_s"), lambda_other=kw.get("lam_o"),
+                         noise={"lap_local": cs["lap_local"], "lap_central": cs["lap_central"],
+                                "mix_z": cs["mix_z"], "mix_l": cs["mix_l"]})
+    assert_close([got["rho_hat"], *got["ci"]], ref, what=f"INT subG n={n} eps={eps} hrs={hrs}")
+
+
+# ------------------------------------------------------------ fused engine
+FUSED_CELLS = [
+    dict(n=1000, rho=0.5, eps1=1.0, eps2=1.0, family="sign", dgp="gaussian", mu=(0.5, 0.5), sigma=(2.0, 2.0)),
+    dict(n=4000, rho=0.9, eps1=1.5, eps2=0.5, family="sign", dgp="gaussian", mu=(0.5, 0.5), sigma=(2.0, 2.0)),
+    dict(n=3000, rho=0.0, eps1=0.5, eps2=1.5, family="sign", dgp="gaussian"),
+    dict(n=2000, rho=0.3, eps1=1.0, eps2=1.0, family="sign", dgp="bernoulli"),
+    dict(n=2500, rho=0.65, eps1=1.5, eps2=0.5, family="subG", dgp="bounded_factor"),
+    dict(n=2500, rho=0.3, eps1=0.5, eps2=0.5, family="subG", dgp="gaussian"),
+    dict(n=1600, rho=0.8, eps1=1.0, eps2=1.0, family="sign", dgp="gaussian", ci_mode="laplace"),
+    dict(n=1000, rho=0.4, eps1=1.0, eps2=1.0, family="sign", dgp="gaussian", normalise=False),
+]
+
+
+@pytest.mark.parametrize("spec", FUSED_CELLS)
+def test_fused_vs_oracle(dc, orc, spec):
+    from dcor.sim import CellSpec, simulate
+    cell = CellSpec(seed=1_000_000 + spec["n"] % 97, **spec)
+    got = simulate(cell, 24, rep_begin=3).cpu().numpy()
+    ref = orc.sim_reps(cell.to_c(), 3, 27)
+    assert_close(got, ref, what=f"fused {spec}")
+
+
+def test_fused_split_invariance(dc):
+    """Per-replicate results do not depend on how the replicate range is split."""
+    from dcor.sim import headline_cell, simulate
+    cell = headline_cell(20_000)
+    a = simulate(cell, 96).cpu().numpy()
+    b = np.concatenate([simulate(cell, 40, 0).cpu().numpy(), simulate(cell, 56, 40).cpu().numpy()])
+    assert np.array_equal(a, b)
