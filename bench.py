@@ -94,8 +94,8 @@ def main():
         simulate(cell, R, r0, out=buf, stream=stream)
         return accumulate(buf, cell.rho, stream=stream)
 
-    for s in range(args.warmup):
-        step(1_000_000 + s)
+    for s in range(args.warmup):          # warmup runs replicate indices after the timed ones
+        step(args.steps + s)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

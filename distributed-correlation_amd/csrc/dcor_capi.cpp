@@ -9,6 +9,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -235,6 +236,38 @@ int make_subg(int64_t n, double eps1, double eps2, double eta1, double eta2, dou
   return DCOR_OK;
 }
 
+// Per-device scratch arena for the one-pass sign kernel (grid * n * 4 B); owned by the
+// library, grown on demand outside any kernel, released by dcor_shutdown().
+struct Arena { void* p = nullptr; size_t bytes = 0; };
+Arena g_arena[64];
+
+int arena_get(size_t bytes, void** out) {
+  int dev = 0;
+  HIPCHK(hipGetDevice(&dev));
+  if (dev < 0 || dev >= 64) return fail(DCOR_EINVAL, "device id out of range");
+  Arena& a = g_arena[dev];
+  if (a.bytes < bytes) {
+    if (a.p) { HIPCHK(hipDeviceSynchronize()); HIPCHK(hipFree(a.p)); a.p = nullptr; a.bytes = 0; }
+    if (hipMalloc(&a.p, bytes) != hipSuccess) {
+      (void)hipGetLastError();
+      a.p = nullptr;
+      return fail(DCOR_ENOMEM, "scratch arena: cannot allocate %zu bytes", bytes);
+    }
+    a.bytes = bytes;
+  }
+  *out = a.p;
+  return DCOR_OK;
+}
+
+// Monotone code map of clip(v): base + [0, 2R) -> [0, levels).  Only affects speed (how many
+// samples tie a threshold's code), never results.
+void code_map(double center, double R, double levels, double* base, double* inv) {
+  if (!(R > 0) || !std::isfinite(R)) R = 1.0;
+  if (!std::isfinite(center)) center = 0.0;
+  *base = center - R;
+  *inv = levels / (2.0 * R);
+}
+
 }  // namespace
 
 // ===================================================================== ABI
@@ -319,7 +352,38 @@ int dcor_sim_launch(const dcor_cell* cell, int64_t rep_begin, int64_t rep_count,
     if (int st = make_sign(c.n, c.eps1, c.eps2, c.alpha, c.normalise, c.ci_mode, c.nsim, false, k)) return st;
     k.g = g; k.rep_begin = rep_begin;
     k.k0 = (uint32_t)c.seed; k.k1 = (uint32_t)(c.seed >> 32);
-    rc = launch_sign_fused(k, rep_count, d_out, stream);
+    // code windows centred on the DGP's location (speed only)
+    double cx = 0.0, cy = 0.0, rx = 1.0, ry = 1.0;
+    if (c.dgp == DCOR_DGP_GAUSSIAN) {
+      cx = r_min(r_max(c.mu[0], -k.L), k.L); cy = r_min(r_max(c.mu[1], -k.L), k.L);
+      rx = 2.0 * std::sqrt(g.a00 * g.a00 + g.a01 * g.a01);
+      ry = 2.0 * std::sqrt(g.a10 * g.a10 + g.a11 * g.a11);
+    } else if (c.dgp == DCOR_DGP_BERNOULLI) {
+      cx = cy = 0.5; rx = ry = 1.0;
+    } else {
+      cx = cy = 0.0; rx = ry = 2.0;
+    }
+    code_map(cx, rx, 65536.0, &k.cbase_x, &k.cinv_x);
+    code_map(cy, ry, 32768.0, &k.cbase_y, &k.cinv_y);
+    const char* var = std::getenv("DCOR_SIGN_KERNEL");
+    const bool regen = (var && std::strcmp(var, "regen") == 0) || !c.normalise;
+    if (regen || rep_count == 0) {
+      rc = launch_sign_fused(k, rep_count, d_out, stream);
+    } else {
+      // scratch budget: >= 1 GiB and >= 2048 replicates' codes, <= 8 GiB
+      const size_t per_rep = (size_t)c.n * sizeof(uint32_t) + 4 * sizeof(double);
+      size_t budget = (size_t)1 << 30;
+      if (budget < 2048 * per_rep) budget = 2048 * per_rep;
+      if (budget > ((size_t)8 << 30)) budget = (size_t)8 << 30;
+      int64_t chunk = (int64_t)(budget / per_rep);
+      if (chunk < 1) chunk = 1;
+      if (chunk > rep_count) chunk = rep_count;
+      void* scratch = nullptr;
+      const size_t codes_bytes = ((size_t)chunk * (size_t)c.n * sizeof(uint32_t) + 255) / 256 * 256;
+      if (int st = arena_get(codes_bytes + (size_t)chunk * 4 * sizeof(double), &scratch)) return st;
+      rc = launch_sign_fused_codes(k, rep_count, chunk, (uint32_t*)scratch,
+                                   (double*)((char*)scratch + codes_bytes), d_out, stream);
+    }
   } else if (c.family == DCOR_FAMILY_SUBG) {
     SubgConst k;
     if (int st = make_subg(c.n, c.eps1, c.eps2, c.eta1, c.eta2, c.alpha, 0, NAN, NAN, NAN, NAN,
@@ -625,6 +689,13 @@ int dcor_dp_sd(const double* x, int64_t n, double lo, double hi, double eps1, do
                               bo.as<double>(), nullptr);
   if (rc) return hip_fail((hipError_t)rc, "dp_sd launch");
   HIPCHK(hipMemcpy(out, bo.p, sizeof(double) * 2, hipMemcpyDeviceToHost));
+  return DCOR_OK;
+}
+
+int dcor_shutdown(void) {
+  for (auto& a : g_arena) {
+    if (a.p) { (void)hipFree(a.p); a.p = nullptr; a.bytes = 0; }
+  }
   return DCOR_OK;
 }
 

@@ -1,0 +1,95 @@
+// dcor_common.h -- device helpers shared by the fused and pre-materialised kernels:
+// R-exact sign of a standardised value, mixquant order statistic from loaded draws, and
+// the NI / INT epilogues of both estimator families (cited R lines inline).
+#pragma once
+#include "dcor_device.h"
+#include "dcor_engine.h"
+
+namespace dcor {
+
+// sign((a - mu)/sd) exactly as R computes it (sd > 0): the quotient has the sign of
+// the numerator unless it underflows, which needs |a - mu| < sd * 2^-1000.
+__device__ __forceinline__ int sgn_std(double a, double mu, double sd, bool& bad) {
+  const double d = a - mu;
+  if (fabs(d) >= sd * 0x1p-1000) return (d > 0) - (d < 0);
+  const double q = d / sd;
+  bad |= (q != q);
+  return (q > 0) - (q < 0);
+}
+__device__ __forceinline__ int sgn_raw(double a, bool& bad) {
+  bad |= (a != a);
+  return (a > 0) - (a < 0);
+}
+
+__device__ __forceinline__ double mixquant_loaded(const MixConst& mx, double c, const double* z,
+                                                  const double* l, double* keys, int* nan_cnt) {
+  if (threadIdx.x == 0) *nan_cnt = 0;
+  __syncthreads();
+  int nn = 0;
+  for (int i = threadIdx.x; i < mx.nsim; i += DCOR_BLOCK) {
+    double v = z[i] + c * l[i];
+    if (v != v) { v = __longlong_as_double(0x7ff0000000000000LL); ++nn; }
+    keys[i] = v;
+  }
+  if (nn) atomicAdd(nan_cnt, nn);
+  __syncthreads();
+  return lds_select(keys, mx.nsim, mx.P, mx.pos, nan_cnt);
+}
+
+#define MIX_MAX 2048
+
+// ------------------------------------------------- sign-family epilogues
+struct SignStd { double muNx, sdNx, muNy, sdNy, muIx, sdIx, muIy, sdIy; };
+
+__device__ __forceinline__ void priv_std_from_sums(const SignConst& c, const double v[4],
+                                                   const double lap[8], SignStd& s) {
+  // vert-cor.R:335-344 with mean(xc) = sum/n (R: LD mean, agrees to rounding)
+  const double mx = v[0] / c.nd, m2x = v[1] / c.nd, my = v[2] / c.nd, m2y = v[3] / c.nd;
+  s.muNx = mx + c.s_mu_x * lap[0];
+  s.sdNx = sqrt(rmax((m2x + c.s_m2_x * lap[1]) - s.muNx * s.muNx, 1e-12));
+  s.muNy = my + c.s_mu_y * lap[2];
+  s.sdNy = sqrt(rmax((m2y + c.s_m2_y * lap[3]) - s.muNy * s.muNy, 1e-12));
+  s.muIx = mx + c.s_mu_x * lap[4];
+  s.sdIx = sqrt(rmax((m2x + c.s_m2_x * lap[5]) - s.muIx * s.muIx, 1e-12));
+  s.muIy = my + c.s_mu_y * lap[6];
+  s.sdIy = sqrt(rmax((m2y + c.s_m2_y * lap[7]) - s.muIy * s.muIy, 1e-12));
+}
+
+__device__ __forceinline__ void ni_sign_result(const SignConst& c, DD sT, DD sT2, bool bad,
+                                               double* o) {
+  // vert-cor.R:233-254
+  const double sumT = sT.hi + sT.lo;
+  const double eta = c.inv_k * sumT;
+  const double S = sqrt(dd_var(sT, sT2, c.kd));
+  o[0] = sin(M_PI * eta / 2.0);
+  o[1] = sin(M_PI / 2.0 * rmax(eta - c.crit * S / c.sqrt_k, -1.0));
+  o[2] = sin(M_PI / 2.0 * rmin(eta + c.crit * S / c.sqrt_k, 1.0));
+  if (bad) o[0] = o[1] = o[2] = dnan();
+}
+
+// vert-cor.R:186-194, 281-313.  Returns (rho, eta, se_eta) and the mixquant c*.
+__device__ __forceinline__ void int_sign_point(const SignConst& c, long long core, double lapz,
+                                               double& rho, double& eta, double& se,
+                                               double& cstar) {
+  const double Z = c.scale_Z * lapz;
+  const double eta0 = c.coefZ * (double)core + Z;
+  rho = sin(M_PI * eta0 / 2.0);
+  eta = 1.0 - acos(rho) * 2.0 / M_PI;
+  const double h = 1.0 - acos(rho) * 2.0 / M_PI;
+  const double s2 = 1.0 - c.q2 * (h * h);
+  se = 1.0 / sqrt(c.nd) * sqrt(s2) * c.ratio;
+  cstar = 2.0 / (sqrt(c.nd * s2) * c.eps_r);
+}
+
+__device__ __forceinline__ void ni_subg_result(const SubgConst& c, DD sP, DD sT, DD sT2,
+                                               double* o) {
+  // ver-cor-subG.R:51-59
+  const double rho = c.m_over_k * (sP.hi + sP.lo);
+  const double se = sqrt(dd_var(sT, sT2, c.kd)) / c.sqrt_k;
+  o[0] = rho;
+  o[1] = rmax(rho - c.crit * se, -1.0);
+  o[2] = rmin(rho + c.crit * se, 1.0);
+}
+
+
+}  // namespace dcor

@@ -21,12 +21,13 @@ struct U4 { uint32_t w0, w1, w2, w3; };
 
 __device__ __forceinline__ U4 philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
                                      uint32_t k0, uint32_t k1) {
+  // 32x32->64 products map to one v_mad_u64_u32 each (hi and lo together).
 #pragma unroll
   for (int r = 0; r < 10; ++r) {
-    const uint32_t hi0 = __umulhi(0xD2511F53u, c0), lo0 = 0xD2511F53u * c0;
-    const uint32_t hi1 = __umulhi(0xCD9E8D57u, c2), lo1 = 0xCD9E8D57u * c2;
-    const uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
-    c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c0;
+    const uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
+    const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0, n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+    c0 = n0; c1 = (uint32_t)p1; c2 = n2; c3 = (uint32_t)p0;
     k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
   }
   return U4{c0, c1, c2, c3};
@@ -37,10 +38,11 @@ __device__ __forceinline__ U4 draw(uint32_t idx, uint32_t rep, uint32_t site, ui
   return philox(idx, rep, site, 0u, k0, k1);
 }
 
-// (2x+1) * 2^-53 with x the top 52 bits of (a, b): in (0, 1), exact.
+// (2x+1) * 2^-53 with x the top 52 bits of (a, b): in (0, 1), exact.  Built from bits:
+// as_double(1.x) - (1 - 2^-53) is exact (Sterbenz), one v_add_f64.
 __device__ __forceinline__ double u53(uint32_t a, uint32_t b) {
-  const uint64_t x = ((uint64_t)a << 20) | (uint64_t)(b >> 12);
-  return (double)(2 * x + 1) * 0x1p-53;
+  const uint64_t bits = 0x3FF0000000000000ull | ((uint64_t)a << 20) | (uint64_t)(b >> 12);
+  return __longlong_as_double((long long)bits) - (1.0 - 0x1p-53);
 }
 
 // fdlibm-style log for positive normal x (same code as oracle/orc_log).

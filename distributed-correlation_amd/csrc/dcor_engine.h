@@ -38,6 +38,7 @@ struct SignConst {
   double inv_k, crit, sqrt_k;
   double pflip;                               // exp(eps_s)/(exp(eps_s)+1)
   double scale_Z, coefZ, q2, ratio, inv_sqrt_n, eps_r, w_laplace;
+  double cbase_x, cinv_x, cbase_y, cinv_y;    // monotone code maps of clip(x), clip(y)
 };
 
 // Sub-G family: correlation_NI_subG + ci_INT_subG (ver-cor-subG.R:25-108).
@@ -80,6 +81,10 @@ struct PrematSubgConst {
 
 // Kernel launchers (dcor_kernels.hip).  Return hipError_t as int.
 int launch_sign_fused(const SignConst& c, int64_t reps, dcor_rep_out* out, void* stream);
+// One-pass sign algorithm: pass-1 / pass-2 kernels over replicate chunks of `chunk`;
+// scratch = chunk * n * 4 B of codes, sums = chunk * 4 doubles.
+int launch_sign_fused_codes(const SignConst& c, int64_t reps, int64_t chunk, uint32_t* scratch,
+                            double* sums, dcor_rep_out* out, void* stream);
 int launch_subg_fused(const SubgConst& c, int64_t reps, dcor_rep_out* out, void* stream);
 int launch_premat_sign(const PrematSignConst& c, int64_t reps, dcor_rep_out* out, void* stream);
 int launch_premat_subg(const PrematSubgConst& c, int64_t reps, dcor_rep_out* out, void* stream);

@@ -1,0 +1,537 @@
+// dcor_fused.hip -- fused Monte-Carlo kernels (the hot path): Philox DGP -> clip ->
+// reduce -> Laplace -> NI + INT estimate + CI, one 256-thread workgroup per replicate.
+//
+// Nothing of a replicate's input is materialised in HBM except, for the one-pass sign
+// kernel, a 4-byte code per sample (k_sign_fused_codes).  The DGP is a template parameter
+// so the sample loops are straight-line code.  fp64 throughout (R `double`).
+#include <hip/hip_runtime.h>
+
+#include "dcor_common.h"
+
+namespace dcor {
+
+// ------------------------------------------------------------- generators
+// Sample i of a replicate from the draw-site contract of include/dcor.h.
+template <int DGP> struct Dgp;
+
+template <> struct Dgp<DCOR_DGP_GAUSSIAN> {  // MASS::mvrnorm (vert-cor.R:389-394)
+  static __device__ __forceinline__ void one(const DgpConst& g, uint32_t i, uint32_t rep,
+                                             uint32_t k0, uint32_t k1, double& x, double& y) {
+    const U4 w = draw(i, rep, DCOR_SITE_DGP_A, k0, k1);
+    double z1, z2;
+    normal_pair(w, &z1, &z2);
+    x = g.mu0 + (g.a00 * z1 + g.a01 * z2);
+    y = g.mu1 + (g.a10 * z1 + g.a11 * z2);
+  }
+  static __device__ __forceinline__ void quad(const DgpConst& g, uint32_t i0, uint32_t rep,
+                                              uint32_t k0, uint32_t k1, double* x, double* y) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) one(g, i0 + q, rep, k0, k1, x[q], y[q]);
+  }
+  static __device__ __forceinline__ double lap(uint32_t i, uint32_t rep, uint32_t k0, uint32_t k1) {
+    const U4 v = draw(i, rep, DCOR_SITE_DGP_B, k0, k1);
+    return unit_laplace(u53(v.w2, v.w3));
+  }
+};
+
+template <> struct Dgp<DCOR_DGP_BERNOULLI> {  // gen_bernoulli (vert-cor.R:78-98), 2 samples/block
+  static __device__ __forceinline__ void from_words(const DgpConst& g, uint32_t wa, uint32_t wb,
+                                                    double& x, double& y) {
+    const double u = (double)wa * 0x1p-32, v = (double)wb * 0x1p-32;
+    x = (u < 0.5) ? 1.0 : 0.0;
+    y = (x == 0.0) ? (v < g.thr0 ? 1.0 : 0.0) : (v < g.thr1 ? 1.0 : 0.0);
+  }
+  static __device__ __forceinline__ void one(const DgpConst& g, uint32_t i, uint32_t rep,
+                                             uint32_t k0, uint32_t k1, double& x, double& y) {
+    const U4 w = draw(i >> 1, rep, DCOR_SITE_DGP_A, k0, k1);
+    if (i & 1) from_words(g, w.w2, w.w3, x, y); else from_words(g, w.w0, w.w1, x, y);
+  }
+  static __device__ __forceinline__ void quad(const DgpConst& g, uint32_t i0, uint32_t rep,
+                                              uint32_t k0, uint32_t k1, double* x, double* y) {
+    const U4 a = draw(i0 >> 1, rep, DCOR_SITE_DGP_A, k0, k1);
+    const U4 b = draw((i0 >> 1) + 1, rep, DCOR_SITE_DGP_A, k0, k1);
+    from_words(g, a.w0, a.w1, x[0], y[0]);
+    from_words(g, a.w2, a.w3, x[1], y[1]);
+    from_words(g, b.w0, b.w1, x[2], y[2]);
+    from_words(g, b.w2, b.w3, x[3], y[3]);
+  }
+  static __device__ __forceinline__ double lap(uint32_t i, uint32_t rep, uint32_t k0, uint32_t k1) {
+    const U4 v = draw(i, rep, DCOR_SITE_DGP_B, k0, k1);
+    return unit_laplace(u53(v.w2, v.w3));
+  }
+};
+
+template <> struct Dgp<DCOR_DGP_BOUNDED_FACTOR> {  // gen_bounded_factor (ver-cor-subG.R:141-154)
+  static __device__ __forceinline__ void one_lap(const DgpConst& g, uint32_t i, uint32_t rep,
+                                                 uint32_t k0, uint32_t k1, double& x, double& y,
+                                                 double* lap) {
+    const U4 w = draw(i, rep, DCOR_SITE_DGP_A, k0, k1);
+    const U4 v = draw(i, rep, DCOR_SITE_DGP_B, k0, k1);
+    const double U = -g.cU + g.cU2 * u53(w.w0, w.w1);
+    x = U + (-g.cE + g.cE2 * u53(w.w2, w.w3));
+    y = U + (-g.cE + g.cE2 * u53(v.w0, v.w1));
+    if (lap) *lap = unit_laplace(u53(v.w2, v.w3));
+  }
+  static __device__ __forceinline__ void one(const DgpConst& g, uint32_t i, uint32_t rep,
+                                             uint32_t k0, uint32_t k1, double& x, double& y) {
+    one_lap(g, i, rep, k0, k1, x, y, nullptr);
+  }
+  static __device__ __forceinline__ void quad(const DgpConst& g, uint32_t i0, uint32_t rep,
+                                              uint32_t k0, uint32_t k1, double* x, double* y) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) one(g, i0 + q, rep, k0, k1, x[q], y[q]);
+  }
+};
+
+// Sub-G needs the sample and its local Laplace (DGP_B words 2,3).
+template <int DGP>
+__device__ __forceinline__ void sample_lap(const DgpConst& g, uint32_t i, uint32_t rep, uint32_t k0,
+                                           uint32_t k1, double& x, double& y, double& l) {
+  if constexpr (DGP == DCOR_DGP_BOUNDED_FACTOR) {
+    Dgp<DGP>::one_lap(g, i, rep, k0, k1, x, y, &l);
+  } else {
+    Dgp<DGP>::one(g, i, rep, k0, k1, x, y);
+    l = Dgp<DGP>::lap(i, rep, k0, k1);
+  }
+}
+
+__device__ __forceinline__ uint32_t word(const U4& w, uint32_t q) {
+  return q == 0 ? w.w0 : (q == 1 ? w.w1 : (q == 2 ? w.w2 : w.w3));
+}
+
+struct FlipGen {  // sign-family INT flips, 4 per Philox block (SITE_FLIP), cached per block
+  uint32_t cidx;
+  U4 cw;
+  __device__ __forceinline__ int get(uint32_t i, uint32_t rep, uint32_t k0, uint32_t k1,
+                                     double p) {
+    const uint32_t bi = i >> 2;
+    if (bi != cidx) { cw = draw(bi, rep, DCOR_SITE_FLIP, k0, k1); cidx = bi; }
+    return ((double)word(cw, i & 3) * 0x1p-32 < p) ? 1 : -1;  // 2*S - 1 (vert-cor.R:175-179)
+  }
+};
+
+// mixquant inside the workgroup: keys = z + c*l from Philox, then the order statistic.
+__device__ __forceinline__ double mixquant_fused(const MixConst& mx, double c, uint32_t rep,
+                                                 uint32_t k0, uint32_t k1, double* keys,
+                                                 int* nan_cnt) {
+  if (threadIdx.x == 0) *nan_cnt = 0;
+  __syncthreads();
+  int nn = 0;
+  for (int b = threadIdx.x; 2 * b < mx.nsim; b += DCOR_BLOCK) {
+    const U4 wz = draw((uint32_t)b, rep, DCOR_SITE_MIX_Z, k0, k1);
+    const U4 wl = draw((uint32_t)b, rep, DCOR_SITE_MIX_L, k0, k1);
+    double z0, z1;
+    normal_pair(wz, &z0, &z1);
+    double v0 = z0 + c * unit_laplace(u53(wl.w0, wl.w1));
+    if (v0 != v0) { v0 = __longlong_as_double(0x7ff0000000000000LL); ++nn; }
+    keys[2 * b] = v0;
+    if (2 * b + 1 < mx.nsim) {
+      double v1 = z1 + c * unit_laplace(u53(wl.w2, wl.w3));
+      if (v1 != v1) { v1 = __longlong_as_double(0x7ff0000000000000LL); ++nn; }
+      keys[2 * b + 1] = v1;
+    }
+  }
+  if (nn) atomicAdd(nan_cnt, nn);
+  __syncthreads();
+  return lds_select(keys, mx.nsim, mx.P, mx.pos, nan_cnt);
+}
+
+__device__ __forceinline__ void scalar_laplace(uint32_t rep, uint32_t k0, uint32_t k1, double* lap) {
+  if (threadIdx.x < 5) {  // SITE_SCALAR blocks 0..4: NI mu/m2 X, NI mu/m2 Y, INT ..., Z
+    const U4 w = draw((uint32_t)threadIdx.x, rep, DCOR_SITE_SCALAR, k0, k1);
+    lap[2 * threadIdx.x] = unit_laplace(u53(w.w0, w.w1));
+    lap[2 * threadIdx.x + 1] = unit_laplace(u53(w.w2, w.w3));
+  }
+}
+
+// INT epilogue + CI write shared by the sign kernels (vert-cor.R:281-313).
+__device__ __forceinline__ void sign_finish(const SignConst& c, uint32_t rep, DD sT, DD sT2,
+                                            long long core, bool any_ni, bool any_int,
+                                            const double* lap, double* keys, int* nan_cnt,
+                                            dcor_rep_out* dst) {
+  double o[6];
+  ni_sign_result(c, sT, sT2, any_ni, o);
+  double rho, eta, se, cstar;
+  int_sign_point(c, core, lap[8], rho, eta, se, cstar);
+  double w;
+  if (c.mode_normal)
+    w = mixquant_fused(c.mix, cstar, rep, c.k0, c.k1, keys, nan_cnt) * se;
+  else
+    w = c.w_laplace;
+  o[3] = rho;
+  o[4] = sin(M_PI / 2.0 * rmax(eta - w, -1.0));
+  o[5] = sin(M_PI / 2.0 * rmin(eta + w, 1.0));
+  if (any_int) o[3] = o[4] = o[5] = dnan();
+  if (threadIdx.x == 0) *dst = dcor_rep_out{o[0], o[1], o[2], o[3], o[4], o[5]};
+}
+
+// ======================================== fused sign family, one pass (hot) ===
+// Pass 1 generates each sample once: the DP-mean sums of clip(x), clip(y) (vert-cor.R:
+// 328-340) and a 4-byte record per sample in a per-workgroup slab -- a monotone 16-bit
+// code of clip(x), a 15-bit code of clip(y) and the INT flip bit.  q(v) = clamp(floor(
+// (v - base) * inv)) is monotone non-decreasing, so q(xc) != q(mu) proves sign(xc - mu);
+// pass 2 decides every sign from codes and regenerates only samples whose code ties a
+// threshold's code.  Results equal the two-pass algorithm's exactly.  Each thread
+// generates groups of 4 consecutive samples (one flip block per group, 16-B slab stores).
+// Two launches per replicate chunk (pass 1, pass 2); scratch = chunk * n * 4 B.
+__device__ __forceinline__ uint32_t code16(double v, double base, double inv, double top) {
+  double t = (v - base) * inv;
+  t = fmin(fmax(t, 0.0), top);  // NaN -> 0 (a NaN sample makes mu NaN: flagged)
+  return (uint32_t)t;
+}
+__device__ __forceinline__ int sgnq(uint32_t q, uint32_t qm) { return (q > qm) - (q < qm); }
+
+template <int DGP>
+__device__ __forceinline__ void exact_signs(const SignConst& c, const SignStd& s, uint32_t i,
+                                            uint32_t rep, int& nx, int& ny, int& ix, int& iy,
+                                            bool& bad_ni, bool& bad_int) {
+  double x, y;
+  Dgp<DGP>::one(c.g, i, rep, c.k0, c.k1, x, y);
+  const double xc = rclip(x, c.L), yc = rclip(y, c.L);
+  nx = sgn_std(xc, s.muNx, s.sdNx, bad_ni);
+  ny = sgn_std(yc, s.muNy, s.sdNy, bad_ni);
+  ix = sgn_std(xc, s.muIx, s.sdIx, bad_int);
+  iy = sgn_std(yc, s.muIy, s.sdIy, bad_int);
+}
+
+// Pass 1: replicate r of the chunk -> slab r (n records) and its 4 clipped sums.
+template <int DGP>
+__global__ __launch_bounds__(DCOR_BLOCK) void k_sign_pass1(SignConst c,
+                                                           uint32_t* __restrict__ scratch,
+                                                           double* __restrict__ sums) {
+  __shared__ double red[16 * DCOR_WAVES];
+  const int tid = threadIdx.x;
+  const uint32_t rep = (uint32_t)(c.rep_begin + blockIdx.x);
+  uint32_t* slab = scratch + (size_t)blockIdx.x * (size_t)c.n;
+  double v[4] = {0.0, 0.0, 0.0, 0.0};
+  const int64_t ngrp = (c.n + 3) / 4;
+  for (int64_t g4 = tid; g4 < ngrp; g4 += DCOR_BLOCK) {
+    const uint32_t i0 = (uint32_t)(4 * g4);
+    const U4 fw = draw((uint32_t)g4, rep, DCOR_SITE_FLIP, c.k0, c.k1);
+    double x[4], y[4];
+    Dgp<DGP>::quad(c.g, i0, rep, c.k0, c.k1, x, y);
+    uint32_t rec[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const double xc = rclip(x[q], c.L), yc = rclip(y[q], c.L);
+      if ((int64_t)(i0 + q) < c.n) { v[0] += xc; v[1] += xc * xc; v[2] += yc; v[3] += yc * yc; }
+      const uint32_t qx = code16(xc, c.cbase_x, c.cinv_x, 65535.0);
+      const uint32_t qy = code16(yc, c.cbase_y, c.cinv_y, 32767.0);
+      const uint32_t f = ((double)word(fw, q) * 0x1p-32 < c.pflip) ? 1u : 0u;
+      rec[q] = qx | (qy << 16) | (f << 31);
+    }
+    if ((int64_t)i0 + 3 < c.n) {
+      *reinterpret_cast<uint4*>(slab + i0) = make_uint4(rec[0], rec[1], rec[2], rec[3]);
+    } else {
+      for (int q = 0; q < 4; ++q) if ((int64_t)(i0 + q) < c.n) slab[i0 + q] = rec[q];
+    }
+  }
+  block_sum<4>(v, red);
+  if (tid < 4) sums[4 * (size_t)blockIdx.x + tid] = v[tid];
+}
+
+// Pass 2: signs from the codes (exact regeneration on a code tie), batch counts, NI
+// Laplace, INT flip sum, epilogue.
+template <int DGP>
+__global__ __launch_bounds__(DCOR_BLOCK) void k_sign_pass2(SignConst c,
+                                                           const uint32_t* __restrict__ scratch,
+                                                           const double* __restrict__ sums,
+                                                           dcor_rep_out* out) {
+  __shared__ double red[16 * DCOR_WAVES];
+  __shared__ long long redi[DCOR_WAVES];
+  __shared__ double lap[10];
+  __shared__ double keys[MIX_MAX];
+  __shared__ int nan_cnt;
+  const int tid = threadIdx.x;
+  const uint32_t rep = (uint32_t)(c.rep_begin + blockIdx.x);
+  const uint32_t* slab = scratch + (size_t)blockIdx.x * (size_t)c.n;
+  scalar_laplace(rep, c.k0, c.k1, lap);
+  __syncthreads();
+  SignStd s;
+  {
+    double v[4], l8[8];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) v[q] = sums[4 * (size_t)blockIdx.x + q];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) l8[q] = lap[q];
+    priv_std_from_sums(c, v, l8, s);
+  }
+  const bool thr_nan = (s.muNx != s.muNx) || (s.muNy != s.muNy) || (s.muIx != s.muIx) ||
+                       (s.muIy != s.muIy) || (s.sdNx != s.sdNx) || (s.sdNy != s.sdNy) ||
+                       (s.sdIx != s.sdIx) || (s.sdIy != s.sdIy);
+  // sign(d/sd) == sign(d) needs sd < 2^900 (no underflow of the quotient); else exact path.
+  const bool force_exact = !(s.sdNx < 0x1p900 && s.sdNy < 0x1p900 && s.sdIx < 0x1p900 &&
+                             s.sdIy < 0x1p900);
+  const uint32_t qNx = code16(s.muNx, c.cbase_x, c.cinv_x, 65535.0);
+  const uint32_t qIx = code16(s.muIx, c.cbase_x, c.cinv_x, 65535.0);
+  const uint32_t qNy = code16(s.muNy, c.cbase_y, c.cinv_y, 32767.0);
+  const uint32_t qIy = code16(s.muIy, c.cbase_y, c.cinv_y, 32767.0);
+  bool bad_ni = thr_nan, bad_int = thr_nan;
+  DD sT{0.0, 0.0}, sT2{0.0, 0.0};
+  long long core = 0;
+  auto decide = [&](int64_t i, uint32_t w, int& nx, int& ny, int& ix, int& iy, int& f,
+                    bool& bni) {
+    const uint32_t qx = w & 0xffffu, qy = (w >> 16) & 0x7fffu;
+    f = (w >> 31) ? 1 : -1;
+    if (force_exact || qx == qNx || qx == qIx || qy == qNy || qy == qIy) {
+      exact_signs<DGP>(c, s, (uint32_t)i, rep, nx, ny, ix, iy, bni, bad_int);
+    } else {
+      nx = sgnq(qx, qNx); ny = sgnq(qy, qNy);
+      ix = sgnq(qx, qIx); iy = sgnq(qy, qIy);
+    }
+  };
+  const bool vec4 = (c.m % 4) == 0;
+  for (int64_t j = tid; j < c.k; j += DCOR_BLOCK) {
+    int cx = 0, cy = 0, cc = 0;
+    const int64_t i0 = j * c.m;
+    if (vec4) {
+      for (int r = 0; r < c.m; r += 4) {
+        const uint4 w4 = *reinterpret_cast<const uint4*>(slab + i0 + r);
+        const U4 ws{w4.x, w4.y, w4.z, w4.w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          int nx, ny, ix, iy, f;
+          decide(i0 + r + q, word(ws, q), nx, ny, ix, iy, f, bad_ni);
+          cx += nx; cy += ny; cc += f * ix * iy;
+        }
+      }
+    } else {
+      for (int r = 0; r < c.m; ++r) {
+        int nx, ny, ix, iy, f;
+        decide(i0 + r, slab[i0 + r], nx, ny, ix, iy, f, bad_ni);
+        cx += nx; cy += ny; cc += f * ix * iy;
+      }
+    }
+    core += cc;
+    const U4 w = draw((uint32_t)j, rep, DCOR_SITE_NI_LAP, c.k0, c.k1);   // vert-cor.R:230-231
+    const double xt = (double)cx / c.md + c.bx * unit_laplace(u53(w.w0, w.w1));
+    const double yt = (double)cy / c.md + c.by * unit_laplace(u53(w.w2, w.w3));
+    const double T = c.md * xt * yt;                                     // vert-cor.R:233
+    dd_acc(sT, T);
+    dd_acc(sT2, T * T);
+  }
+  for (int64_t i = c.k * c.m + tid; i < c.n; i += DCOR_BLOCK) {  // tail: INT only
+    int nx, ny, ix, iy, f;
+    bool ignore = false;  // NI never reads the tail
+    decide(i, slab[i], nx, ny, ix, iy, f, ignore);
+    core += f * ix * iy;
+  }
+  DD d2[2] = {sT, sT2};
+  block_sum_dd<2>(d2, red);
+  core = block_sum_i(core, redi);
+  const long long nbad = block_sum_i((bad_ni ? 1LL : 0LL) + (bad_int ? (1LL << 20) : 0LL), redi);
+  sign_finish(c, rep, d2[0], d2[1], core, (nbad & 0xFFFFF) != 0, (nbad >> 20) != 0, lap, keys,
+              &nan_cnt, out + blockIdx.x);
+}
+
+// ============================= fused sign family, regenerate (two-pass, A/B) ===
+// The direct two-pass algorithm: pass 2 regenerates every sample.  Used for
+// normalise = FALSE (signs against 0: pass 1 is skipped, so it is one pass) and as the
+// A/B reference for k_sign_fused_codes (DCOR_SIGN_KERNEL=regen).
+template <int DGP>
+__global__ __launch_bounds__(DCOR_BLOCK) void k_sign_fused(SignConst c, dcor_rep_out* out) {
+  __shared__ double red[16 * DCOR_WAVES];
+  __shared__ long long redi[DCOR_WAVES];
+  __shared__ double lap[10];
+  __shared__ double keys[MIX_MAX];
+  __shared__ int nan_cnt;
+  const uint32_t rep = (uint32_t)(c.rep_begin + blockIdx.x);
+  const int tid = threadIdx.x;
+  scalar_laplace(rep, c.k0, c.k1, lap);
+  double v[4] = {0.0, 0.0, 0.0, 0.0};
+  if (c.normalise) {
+    for (int64_t g4 = tid; 4 * g4 < c.n; g4 += DCOR_BLOCK) {
+      double x[4], y[4];
+      Dgp<DGP>::quad(c.g, (uint32_t)(4 * g4), rep, c.k0, c.k1, x, y);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        if (4 * g4 + q < c.n) {
+          const double xc = rclip(x[q], c.L), yc = rclip(y[q], c.L);
+          v[0] += xc; v[1] += xc * xc; v[2] += yc; v[3] += yc * yc;
+        }
+      }
+    }
+  }
+  block_sum<4>(v, red);
+  SignStd s;
+  {
+    double l8[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) l8[q] = lap[q];
+    priv_std_from_sums(c, v, l8, s);
+  }
+  FlipGen fl;
+  fl.cidx = 0xffffffffu;
+  bool bad_ni = false, bad_int = false;
+  DD sT{0.0, 0.0}, sT2{0.0, 0.0};
+  long long core = 0;
+  auto signs = [&](uint32_t i, int& nx, int& ny, int& ix, int& iy, bool& bni) {
+    double x, y;
+    Dgp<DGP>::one(c.g, i, rep, c.k0, c.k1, x, y);
+    if (c.normalise) {
+      const double xc = rclip(x, c.L), yc = rclip(y, c.L);
+      nx = sgn_std(xc, s.muNx, s.sdNx, bni);
+      ny = sgn_std(yc, s.muNy, s.sdNy, bni);
+      ix = sgn_std(xc, s.muIx, s.sdIx, bad_int);
+      iy = sgn_std(yc, s.muIy, s.sdIy, bad_int);
+    } else {
+      bool b = false;
+      nx = ix = sgn_raw(x, b);
+      ny = iy = sgn_raw(y, b);
+      bni |= b;
+      bad_int |= b;
+    }
+  };
+  for (int64_t j = tid; j < c.k; j += DCOR_BLOCK) {
+    int cx = 0, cy = 0;
+    const int64_t i0 = j * c.m;
+    for (int r = 0; r < c.m; ++r) {
+      const uint32_t i = (uint32_t)(i0 + r);
+      int nx, ny, ix, iy;
+      signs(i, nx, ny, ix, iy, bad_ni);
+      cx += nx; cy += ny;
+      core += fl.get(i, rep, c.k0, c.k1, c.pflip) * ix * iy;
+    }
+    const U4 w = draw((uint32_t)j, rep, DCOR_SITE_NI_LAP, c.k0, c.k1);
+    const double xt = (double)cx / c.md + c.bx * unit_laplace(u53(w.w0, w.w1));
+    const double yt = (double)cy / c.md + c.by * unit_laplace(u53(w.w2, w.w3));
+    const double T = c.md * xt * yt;
+    dd_acc(sT, T);
+    dd_acc(sT2, T * T);
+  }
+  for (int64_t i = c.k * c.m + tid; i < c.n; i += DCOR_BLOCK) {
+    int nx, ny, ix, iy;
+    bool ignore = false;
+    signs((uint32_t)i, nx, ny, ix, iy, ignore);
+    core += fl.get((uint32_t)i, rep, c.k0, c.k1, c.pflip) * ix * iy;
+  }
+  DD d2[2] = {sT, sT2};
+  block_sum_dd<2>(d2, red);
+  core = block_sum_i(core, redi);
+  const long long nbad = block_sum_i((bad_ni ? 1LL : 0LL) + (bad_int ? (1LL << 20) : 0LL), redi);
+  sign_finish(c, rep, d2[0], d2[1], core, (nbad & 0xFFFFF) != 0, (nbad >> 20) != 0, lap, keys,
+              &nan_cnt, out + blockIdx.x);
+}
+
+// ===================================================== fused sub-G family ===
+// correlation_NI_subG + ci_INT_subG (ver-cor-subG.R:25-108): single pass (the clip
+// thresholds are data-independent).  Each thread owns whole contiguous batches.
+template <int DGP>
+__global__ __launch_bounds__(DCOR_BLOCK) void k_subg_fused(SubgConst c, dcor_rep_out* out) {
+  __shared__ double red[16 * DCOR_WAVES];
+  __shared__ double lapz;
+  __shared__ double keys[MIX_MAX];
+  __shared__ int nan_cnt;
+  const uint32_t rep = (uint32_t)(c.rep_begin + blockIdx.x);
+  const int tid = threadIdx.x;
+  if (tid == 0) {
+    const U4 w = draw(4u, rep, DCOR_SITE_SCALAR, c.k0, c.k1);
+    lapz = unit_laplace(u53(w.w0, w.w1));
+  }
+  DD sP{0, 0}, sT{0, 0}, sT2{0, 0}, sU{0, 0}, sU2{0, 0};
+  auto int_term = [&](double x, double y, double l) {
+    const double S = c.sender_is_X ? x : y, O = c.sender_is_X ? y : x;
+    const double Uc = rclip((rclip(S, c.ls) + c.bs * l) * O, c.lr);   // ver-cor-subG.R:88-90
+    dd_acc(sU, Uc);
+    dd_acc(sU2, Uc * Uc);
+  };
+  for (int64_t j = tid; j < c.k; j += DCOR_BLOCK) {
+    double sx = 0.0, sy = 0.0;
+    const int64_t i0 = j * c.m;
+    for (int r = 0; r < c.m; ++r) {
+      double x, y, l;
+      sample_lap<DGP>(c.g, (uint32_t)(i0 + r), rep, c.k0, c.k1, x, y, l);
+      sx += rclip(x, c.l1);                                              // :33
+      sy += rclip(y, c.l2);                                              // :34
+      int_term(x, y, l);
+    }
+    const U4 w = draw((uint32_t)j, rep, DCOR_SITE_NI_LAP, c.k0, c.k1);
+    const double xt = sx / c.md + c.bx * unit_laplace(u53(w.w0, w.w1)); // :48
+    const double yt = sy / c.md + c.by * unit_laplace(u53(w.w2, w.w3)); // :49
+    dd_acc(sP, xt * yt);
+    const double T = c.md * xt * yt;                                     // :55
+    dd_acc(sT, T);
+    dd_acc(sT2, T * T);
+  }
+  for (int64_t i = c.k * c.m + tid; i < c.n; i += DCOR_BLOCK) {
+    double x, y, l;
+    sample_lap<DGP>(c.g, (uint32_t)i, rep, c.k0, c.k1, x, y, l);
+    int_term(x, y, l);
+  }
+  DD d5[5] = {sP, sT, sT2, sU, sU2};
+  block_sum_dd<5>(d5, red);
+  double o[6];
+  ni_subg_result(c, d5[0], d5[1], d5[2], o);
+  const DD mU = dd_div_d(d5[3], c.nd);
+  const double rho = (mU.hi + mU.lo) + c.s_central * lapz;             // :91
+  const double sd = sqrt(dd_var(d5[3], d5[4], c.nd));
+  const double se_norm = sqrt(sd * sd + c.sn2x2);                      // :99
+  const double cstar = 2.0 / (c.sqrt_n * sd * c.eps_r);                // :100
+  const double q = mixquant_fused(c.mix, cstar, rep, c.k0, c.k1, keys, &nan_cnt);
+  const double width = q * se_norm / c.sqrt_n;                         // :101
+  o[3] = rho;
+  o[4] = rmax(rho - width, -1.0);
+  o[5] = rmin(rho + width, 1.0);
+  if (tid == 0) out[blockIdx.x] = dcor_rep_out{o[0], o[1], o[2], o[3], o[4], o[5]};
+}
+
+// ============================================================ launchers ===
+static inline int last_err() { return (int)hipGetLastError(); }
+
+template <int DGP>
+static int launch_sign_t(const SignConst& c, int64_t reps, dcor_rep_out* out, void* stream) {
+  hipLaunchKernelGGL(k_sign_fused<DGP>, dim3((unsigned)reps), dim3(DCOR_BLOCK), 0,
+                     (hipStream_t)stream, c, out);
+  return last_err();
+}
+
+int launch_sign_fused(const SignConst& c, int64_t reps, dcor_rep_out* out, void* stream) {
+  if (reps <= 0) return 0;
+  switch (c.g.dgp) {
+    case DCOR_DGP_GAUSSIAN: return launch_sign_t<DCOR_DGP_GAUSSIAN>(c, reps, out, stream);
+    case DCOR_DGP_BERNOULLI: return launch_sign_t<DCOR_DGP_BERNOULLI>(c, reps, out, stream);
+    default: return launch_sign_t<DCOR_DGP_BOUNDED_FACTOR>(c, reps, out, stream);
+  }
+}
+
+template <int DGP>
+static int launch_codes_t(SignConst c, int64_t reps, int64_t chunk, uint32_t* scratch,
+                          double* sums, dcor_rep_out* out, void* stream) {
+  const int64_t rep0 = c.rep_begin;
+  for (int64_t r = 0; r < reps; r += chunk) {
+    const int64_t nr = (reps - r < chunk) ? reps - r : chunk;
+    c.rep_begin = rep0 + r;
+    hipLaunchKernelGGL(k_sign_pass1<DGP>, dim3((unsigned)nr), dim3(DCOR_BLOCK), 0,
+                       (hipStream_t)stream, c, scratch, sums);
+    hipLaunchKernelGGL(k_sign_pass2<DGP>, dim3((unsigned)nr), dim3(DCOR_BLOCK), 0,
+                       (hipStream_t)stream, c, scratch, sums, out + r);
+    if (int e = last_err()) return e;
+  }
+  return 0;
+}
+
+int launch_sign_fused_codes(const SignConst& c, int64_t reps, int64_t chunk, uint32_t* scratch,
+                            double* sums, dcor_rep_out* out, void* stream) {
+  if (reps <= 0) return 0;
+  switch (c.g.dgp) {
+    case DCOR_DGP_GAUSSIAN: return launch_codes_t<DCOR_DGP_GAUSSIAN>(c, reps, chunk, scratch, sums, out, stream);
+    case DCOR_DGP_BERNOULLI: return launch_codes_t<DCOR_DGP_BERNOULLI>(c, reps, chunk, scratch, sums, out, stream);
+    default: return launch_codes_t<DCOR_DGP_BOUNDED_FACTOR>(c, reps, chunk, scratch, sums, out, stream);
+  }
+}
+
+int launch_subg_fused(const SubgConst& c, int64_t reps, dcor_rep_out* out, void* stream) {
+  if (reps <= 0) return 0;
+  const dim3 g((unsigned)reps), b(DCOR_BLOCK);
+  switch (c.g.dgp) {
+    case DCOR_DGP_GAUSSIAN:
+      hipLaunchKernelGGL(k_subg_fused<DCOR_DGP_GAUSSIAN>, g, b, 0, (hipStream_t)stream, c, out); break;
+    case DCOR_DGP_BERNOULLI:
+      hipLaunchKernelGGL(k_subg_fused<DCOR_DGP_BERNOULLI>, g, b, 0, (hipStream_t)stream, c, out); break;
+    default:
+      hipLaunchKernelGGL(k_subg_fused<DCOR_DGP_BOUNDED_FACTOR>, g, b, 0, (hipStream_t)stream, c, out);
+  }
+  return last_err();
+}
+
+}  // namespace dcor

@@ -1,0 +1,176 @@
+/*
+ * dcor_r.c -- R `.Call` shim over include/dcor.h (the drop-in binding of the reference's
+ * R surface).  Built by R CMD SHLIB against libdcor.so on a machine with R:
+ *
+ *   R CMD SHLIB -o dcor_r.so dcor_r.c -I../../include -L../dcor -ldcor -Wl,-rpath,$(realpath ../dcor)
+ *
+ * R is absent from the build image, so this file is not compiled there;
+ * the same entry points are exercised through ctypes by tests/ (dcor/_lib.py).
+ * Contract: inputs are borrowed REAL()/INTEGER() views; outputs are allocated here with
+ * allocVector; C resources are released BEFORE Rf_error (R errors longjmp).
+ */
+#include <R.h>
+#include <Rinternals.h>
+#include <string.h>
+
+#include "dcor.h"
+
+static void dcor_stop(int st) {
+  char msg[512];
+  dcor_last_error(msg, sizeof msg);
+  Rf_error("dcor: %s (status %d)", msg, st);
+}
+
+static double num(SEXP x) { return Rf_asReal(x); }
+static const double* dptr_or_null(SEXP x) { return Rf_isNull(x) ? NULL : REAL(x); }
+
+static SEXP triple(const double o[3]) {
+  SEXP r = PROTECT(allocVector(REALSXP, 3));
+  memcpy(REAL(r), o, 3 * sizeof(double));
+  UNPROTECT(1);
+  return r;
+}
+
+SEXP dcor_R_lambda_n(SEXP n, SEXP eta) { return ScalarReal(dcor_lambda_n(num(n), num(eta))); }
+
+SEXP dcor_R_lambda_INT_n(SEXP n, SEXP eta_s, SEXP eta_r, SEXP eps_s) {
+  SEXP r = PROTECT(allocVector(REALSXP, 2));
+  dcor_lambda_int_n(num(n), num(eta_s), num(eta_r), num(eps_s), REAL(r));
+  UNPROTECT(1);
+  return r;
+}
+
+SEXP dcor_R_mixquant(SEXP z, SEXP l, SEXP c, SEXP p) {
+  double o;
+  const int st = dcor_mixquant(REAL(z), REAL(l), XLENGTH(z), num(c), num(p), &o);
+  if (st) dcor_stop(st);
+  return ScalarReal(o);
+}
+
+SEXP dcor_R_priv_standardize(SEXP v, SEXP eps, SEXP L, SEXP lap) {
+  SEXP r = PROTECT(allocVector(REALSXP, XLENGTH(v)));
+  const int st = dcor_priv_standardize(REAL(v), XLENGTH(v), num(eps), num(L), REAL(lap), REAL(r));
+  UNPROTECT(1);
+  if (st) dcor_stop(st);
+  return r;
+}
+
+SEXP dcor_R_dp_sd(SEXP x, SEXP lo, SEXP hi, SEXP e1, SEXP e2, SEXP lap) {
+  double o[2];
+  const int st = dcor_dp_sd(REAL(x), XLENGTH(x), num(lo), num(hi), num(e1), num(e2), REAL(lap), o);
+  if (st) dcor_stop(st);
+  SEXP r = PROTECT(allocVector(REALSXP, 2));
+  REAL(r)[0] = o[0];
+  REAL(r)[1] = o[1];
+  UNPROTECT(1);
+  return r;
+}
+
+SEXP dcor_R_ci_NI_signbatch(SEXP X, SEXP Y, SEXP e1, SEXP e2, SEXP alpha, SEXP normalise,
+                            SEXP lap_sc, SEXP lap_x, SEXP lap_y) {
+  double o[3];
+  const int st = dcor_ci_ni_signbatch(REAL(X), REAL(Y), XLENGTH(X), num(e1), num(e2), num(alpha),
+                                      Rf_asLogical(normalise), dptr_or_null(lap_sc), REAL(lap_x),
+                                      REAL(lap_y), o);
+  if (st) dcor_stop(st);
+  return triple(o);
+}
+
+SEXP dcor_R_ci_INT_signflip(SEXP X, SEXP Y, SEXP e1, SEXP e2, SEXP alpha, SEXP mode,
+                            SEXP normalise, SEXP lap_sc, SEXP flips, SEXP lap_z, SEXP mz, SEXP ml) {
+  const R_xlen_t n = XLENGTH(X);
+  unsigned char* fl = (unsigned char*)R_alloc(n, 1); /* R-managed: freed on longjmp */
+  for (R_xlen_t i = 0; i < n; ++i) fl[i] = (unsigned char)(INTEGER(flips)[i] != 0);
+  double o[3];
+  const int st = dcor_ci_int_signflip(REAL(X), REAL(Y), n, num(e1), num(e2), num(alpha),
+                                      Rf_asInteger(mode), Rf_asLogical(normalise),
+                                      dptr_or_null(lap_sc), fl, num(lap_z), REAL(mz), REAL(ml),
+                                      XLENGTH(mz), o);
+  if (st) dcor_stop(st);
+  return triple(o);
+}
+
+SEXP dcor_R_correlation_NI_subG(SEXP X, SEXP Y, SEXP e1, SEXP e2, SEXP eta1, SEXP eta2,
+                                SEXP alpha, SEXP hrs, SEXP lam_x, SEXP lam_y, SEXP perm,
+                                SEXP lap_x, SEXP lap_y) {
+  double o[3];
+  const int st = dcor_correlation_ni_subg(
+      REAL(X), REAL(Y), XLENGTH(X), num(e1), num(e2), num(eta1), num(eta2), num(alpha),
+      Rf_asLogical(hrs), num(lam_x), num(lam_y), Rf_isNull(perm) ? NULL : INTEGER(perm),
+      REAL(lap_x), REAL(lap_y), o);
+  if (st) dcor_stop(st);
+  return triple(o);
+}
+
+SEXP dcor_R_ci_INT_subG(SEXP X, SEXP Y, SEXP e1, SEXP e2, SEXP eta1, SEXP eta2, SEXP alpha,
+                        SEXP hrs, SEXP lam_s, SEXP lam_o, SEXP lam_r, SEXP delta, SEXP lap_local,
+                        SEXP lap_central, SEXP mz, SEXP ml) {
+  double o[3];
+  const int st = dcor_ci_int_subg(REAL(X), REAL(Y), XLENGTH(X), num(e1), num(e2), num(eta1),
+                                  num(eta2), num(alpha), Rf_asLogical(hrs), num(lam_s),
+                                  num(lam_o), num(lam_r), num(delta), REAL(lap_local),
+                                  num(lap_central), REAL(mz), REAL(ml), XLENGTH(mz), o);
+  if (st) dcor_stop(st);
+  return triple(o);
+}
+
+/* One grid on the current device: cells given as parallel vectors (one element per cell). */
+SEXP dcor_R_grid_run(SEXP family, SEXP dgp, SEXP n, SEXP rho, SEXP eps1, SEXP eps2, SEXP alpha,
+                     SEXP mu1, SEXP mu2, SEXP s1, SEXP s2, SEXP normalise, SEXP mode, SEXP seed,
+                     SEXP B, SEXP want_detail) {
+  const int nc = LENGTH(n);
+  const long long b = (long long)Rf_asReal(B);
+  dcor_cell* cells = (dcor_cell*)R_alloc(nc, sizeof(dcor_cell));
+  for (int i = 0; i < nc; ++i) {
+    memset(&cells[i], 0, sizeof(dcor_cell));
+    cells[i].family = INTEGER(family)[i];
+    cells[i].dgp = INTEGER(dgp)[i];
+    cells[i].n = (int64_t)REAL(n)[i];
+    cells[i].rho = REAL(rho)[i];
+    cells[i].eps1 = REAL(eps1)[i];
+    cells[i].eps2 = REAL(eps2)[i];
+    cells[i].alpha = REAL(alpha)[i];
+    cells[i].mu[0] = REAL(mu1)[i]; cells[i].mu[1] = REAL(mu2)[i];
+    cells[i].sigma[0] = REAL(s1)[i]; cells[i].sigma[1] = REAL(s2)[i];
+    cells[i].eta1 = cells[i].eta2 = 1.0;
+    cells[i].normalise = LOGICAL(normalise)[i];
+    cells[i].ci_mode = INTEGER(mode)[i];
+    cells[i].nsim = 1000;
+    cells[i].seed = (uint64_t)REAL(seed)[i];
+  }
+  SEXP acc = PROTECT(allocVector(RAWSXP, (R_xlen_t)nc * 2 * sizeof(dcor_accum)));
+  SEXP det = PROTECT(Rf_asLogical(want_detail) ? allocVector(REALSXP, (R_xlen_t)nc * b * 6)
+                                               : allocVector(REALSXP, 0));
+  const int st = dcor_grid_run(cells, nc, b, (dcor_accum*)RAW(acc),
+                               XLENGTH(det) ? (dcor_rep_out*)REAL(det) : NULL);
+  if (st) { UNPROTECT(2); dcor_stop(st); }
+  /* summaries: [cell][method][mse, bias, var, coverage, ci_length] */
+  SEXP sm = PROTECT(allocVector(REALSXP, (R_xlen_t)nc * 2 * 5));
+  for (int i = 0; i < nc; ++i)
+    for (int m = 0; m < 2; ++m)
+      dcor_accum_finalize((dcor_accum*)RAW(acc) + 2 * i + m, cells[i].rho,
+                          (dcor_summary*)(REAL(sm) + (2 * i + m) * 5));
+  SEXP out = PROTECT(allocVector(VECSXP, 2));
+  SET_VECTOR_ELT(out, 0, sm);
+  SET_VECTOR_ELT(out, 1, det);
+  UNPROTECT(4);
+  return out;
+}
+
+static const R_CallMethodDef calls[] = {
+    {"dcor_R_lambda_n", (DL_FUNC)&dcor_R_lambda_n, 2},
+    {"dcor_R_lambda_INT_n", (DL_FUNC)&dcor_R_lambda_INT_n, 4},
+    {"dcor_R_mixquant", (DL_FUNC)&dcor_R_mixquant, 4},
+    {"dcor_R_priv_standardize", (DL_FUNC)&dcor_R_priv_standardize, 4},
+    {"dcor_R_dp_sd", (DL_FUNC)&dcor_R_dp_sd, 6},
+    {"dcor_R_ci_NI_signbatch", (DL_FUNC)&dcor_R_ci_NI_signbatch, 9},
+    {"dcor_R_ci_INT_signflip", (DL_FUNC)&dcor_R_ci_INT_signflip, 12},
+    {"dcor_R_correlation_NI_subG", (DL_FUNC)&dcor_R_correlation_NI_subG, 13},
+    {"dcor_R_ci_INT_subG", (DL_FUNC)&dcor_R_ci_INT_subG, 16},
+    {"dcor_R_grid_run", (DL_FUNC)&dcor_R_grid_run, 16},
+    {NULL, NULL, 0}};
+
+void R_init_dcor_r(DllInfo* dll) {
+  R_registerRoutines(dll, NULL, calls, NULL, NULL);
+  R_useDynamicSymbols(dll, FALSE);
+}

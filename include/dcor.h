@@ -89,6 +89,9 @@ const char* dcor_version(void);
 int dcor_last_error(char* buf, size_t len);
 /* Number of visible HIP devices (0 on a host without GPU; never fails). */
 int dcor_device_count(void);
+/* Release the library-owned per-device scratch arenas (the one-pass sign kernel keeps a
+ * grid x n x 4 B slab of per-sample codes).  Safe to call at any time from the host. */
+int dcor_shutdown(void);
 
 /* ---- calibration scalars (host closed forms) ----------------------------- */
 /* lambda_n, ver-cor-subG.R:1 (= real-data-sims.R:109). */
