@@ -143,7 +143,8 @@ def main():
                        "parallelism": f"replicate-shard x{world}"},
             "roofline": {"bound": "valu_fp64", "achieved": achieved, "peak": FP64_PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": achieved / FP64_PEAK_TFLOPS, "traffic": None,
-                         "kernel": "k_sign_fused", "kernel_ms_avg": kern_ms,
+                         "kernel": "k_sign_pass1 + k_sign_pass2 (one simulate() call)",
+                         "kernel_ms_avg": kern_ms,
                          "work_units_per_rep": W,
                          "note": "achieved = R * W_rep(SURVEY §8d pinned weights) * 2 / kernel time"},
             "summary": {"coverage_NI": summ["NI"]["coverage"], "coverage_INT": summ["INT"]["coverage"],

@@ -4,16 +4,14 @@ set -o pipefail
 export TMPDIR=/tmp
 O=gpurun_out
 mkdir -p $O
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -4 $O/pytest_gpu.log
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 timeout -k 10 300 python -u bench.py > $O/bench.log 2>&1 || exit $?
 tail -1 $O/bench.log
-DCOR_SIGN_KERNEL=regen timeout -k 10 300 python -u bench.py --steps 10 --no-cpu-baseline > $O/bench_regen.log 2>&1 || exit $?
-tail -1 $O/bench_regen.log
-timeout -k 10 60 rocprofv3 -L > $O/rocprof_counters.txt 2>&1
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_trace -o run -- python bench.py --steps 10 --warmup 2 --no-cpu-baseline > $O/prof_trace.log 2>&1 || exit $?
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/prof_fetch -o run -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline > $O/prof_fetch.log 2>&1 || exit $?
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/prof_write -o run -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline > $O/prof_write.log 2>&1 || exit $?
-timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE --output-format csv -d $O/prof_sq -o run -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline > $O/prof_sq.log 2>&1 || exit $?
+timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY SQ_WAIT_ANY GRBM_GUI_ACTIVE --output-format csv -d $O/prof_sq -o run -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline > $O/prof_sq.log 2>&1 || exit $?
+timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_INSTS_VALU_CVT SQ_INSTS_SALU --output-format csv -d $O/prof_mix -o run -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline > $O/prof_mix.log 2>&1 || exit $?
 echo done
