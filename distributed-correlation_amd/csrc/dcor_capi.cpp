@@ -67,6 +67,14 @@ int upload(DevBuf& b, const T* h, size_t count) {
   return DCOR_OK;
 }
 
+// T with (double)w * 2^-32 < p  <=>  w < T for every uint32 w: T = ceil(p * 2^32) clamped
+// to [0, 2^32] (p * 2^32 is exact).
+uint64_t u32_threshold(double p) {
+  if (!(p > 0)) return 0;
+  const double t = std::ceil(p * 4294967296.0);
+  return t >= 4294967296.0 ? (uint64_t)4294967296ull : (uint64_t)t;
+}
+
 // MixConst for sort(x)[ceiling(p*nsim)], p = 1 - alpha/2.
 int make_mix(int64_t nsim, double alpha, MixConst& mx) {
   if (nsim < 1 || nsim > 2048) return fail(DCOR_EINVAL, "nsim must be in [1, 2048] (got %lld)", (long long)nsim);
@@ -113,6 +121,7 @@ int make_dgp(const dcor_cell& c, DgpConst& g) {
     if (!(std::fabs(c.rho) <= 1)) return fail(DCOR_EINVAL, "gen_bernoulli: |rho| <= 1 required (vert-cor.R:79)");
     const double p11 = 0.25 + c.rho / 4, p10 = 0.25 - c.rho / 4, p01 = p10;  // vert-cor.R:80-83
     g.thr0 = p01 / 0.5; g.thr1 = p11 / 0.5;
+    g.T0 = u32_threshold(g.thr0); g.T1 = u32_threshold(g.thr1);
   } else if (c.dgp == DCOR_DGP_BOUNDED_FACTOR) {
     if (!(c.rho >= 0 && c.rho <= 1)) return fail(DCOR_EINVAL, "gen_bounded_factor: rho in [0,1] required");
     g.cU = std::sqrt(3.0 * c.rho); g.cE = std::sqrt(3.0 * (1.0 - c.rho));  // ver-cor-subG.R:148-149
@@ -161,6 +170,7 @@ int make_sign(int64_t n, double eps1, double eps2, double alpha, int normalise, 
   const double eps_s = c.sender_is_X ? eps1 : eps2, eps_r = c.sender_is_X ? eps2 : eps1;
   const double es = std::exp(eps_s);
   c.pflip = es / (es + 1.0);                                             // :174
+  c.flipT = u32_threshold(c.pflip);
   c.scale_Z = 2.0 * (es + 1.0) / (nd * (es - 1.0) * eps_r);              // :186-187
   c.coefZ = (es + 1.0) / (nd * (es - 1.0));                              // :190-191
   const double q = (es - 1.0) / (es + 1.0);

@@ -19,14 +19,22 @@ namespace dcor {
 // ------------------------------------------------------------------ Philox
 struct U4 { uint32_t w0, w1, w2, w3; };
 
+// a ^ b ^ k in one gfx950 v_bitop3_b32 (truth table 0x96); k is wave-uniform (SGPR).
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t k) {
+  uint32_t r;
+  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "s"(k));
+  return r;
+}
+
 __device__ __forceinline__ U4 philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
                                      uint32_t k0, uint32_t k1) {
-  // 32x32->64 products map to one v_mad_u64_u32 each (hi and lo together).
+  // 32x32->64 products map to one v_mad_u64_u32 each (hi and lo together); the two
+  // xors of each output word are one v_bitop3_b32.
 #pragma unroll
   for (int r = 0; r < 10; ++r) {
     const uint64_t p0 = (uint64_t)0xD2511F53u * c0;
     const uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
-    const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0, n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+    const uint32_t n0 = xor3((uint32_t)(p1 >> 32), c1, k0), n2 = xor3((uint32_t)(p0 >> 32), c3, k1);
     c0 = n0; c1 = (uint32_t)p1; c2 = n2; c3 = (uint32_t)p0;
     k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
   }
@@ -106,10 +114,26 @@ __device__ __forceinline__ double unit_laplace(double u) {
   return (up > 0) ? -g : g;
 }
 
+// Correctly rounded sqrt for positive normal x >= 2^-767 (LLVM's own f64 sqrt lowering
+// without its tiny-input scaling and 0/inf class fix-ups): rsq + two Goldschmidt steps +
+// two fma residual corrections.  Bit-identical to IEEE sqrt on that range (the draws tests
+// compare against the CPU's sqrt).  Box-Muller's -2 log(u) >= 2.2e-16 always.
+__device__ __forceinline__ double sqrt_pos(double x) {
+  const double y = __builtin_amdgcn_rsq(x);
+  double g = x * y, h = 0.5 * y;
+  const double r = fma(-h, g, 0.5);
+  g = fma(g, r, g);
+  h = fma(h, r, h);
+  double d = fma(-g, g, x);
+  g = fma(d, h, g);
+  d = fma(-g, g, x);
+  return fma(d, h, g);
+}
+
 __device__ __forceinline__ void normal_pair(const U4& w, double* z1, double* z2) {
   const double u1 = u53(w.w0, w.w1);
   const double u2 = u53(w.w2, w.w3);
-  const double r = sqrt(-2.0 * dlog(u1));
+  const double r = sqrt_pos(-2.0 * dlog(u1));
   double s, c;
   dsincospi(2.0 * u2, &s, &c);
   *z1 = r * c;
@@ -122,6 +146,8 @@ __device__ __forceinline__ double rclip(double x, double L) {  // pmax(pmin(x, L
   const double t = (x < L) ? x : L;
   return (t > -L) ? t : -L;
 }
+// Same clip for inputs known not to be NaN (generated samples): one v_min + one v_max.
+__device__ __forceinline__ double rclip_fin(double x, double L) { return fmax(fmin(x, L), -L); }
 __device__ __forceinline__ double rclip_lohi(double x, double lo, double hi) {  // pmin(pmax(x,lo),hi)
   if (x != x) return x;
   const double t = (x > lo) ? x : lo;

@@ -16,6 +16,7 @@ struct DgpConst {
   int32_t pad;
   double mu0, mu1, a00, a01, a10, a11;  // Gaussian: X = mu + A z  (MASS::mvrnorm)
   double thr0, thr1;                    // Bernoulli: p01/0.5, p11/0.5
+  uint64_t T0, T1;                      // ceil(thr*2^32): u32*2^-32 < thr  <=>  u32 < T
   double cU, cU2, cE, cE2;              // bounded factor: -c + (c - -c) * u
 };
 
@@ -37,6 +38,7 @@ struct SignConst {
   double bx, by;                              // 2/(m*eps1), 2/(m*eps2)
   double inv_k, crit, sqrt_k;
   double pflip;                               // exp(eps_s)/(exp(eps_s)+1)
+  uint64_t flipT;                             // ceil(pflip*2^32): flip <=> u32 < flipT
   double scale_Z, coefZ, q2, ratio, inv_sqrt_n, eps_r, w_laplace;
   double cbase_x, cinv_x, cbase_y, cinv_y;    // monotone code maps of clip(x), clip(y)
 };

@@ -35,11 +35,12 @@ template <> struct Dgp<DCOR_DGP_GAUSSIAN> {  // MASS::mvrnorm (vert-cor.R:389-39
 };
 
 template <> struct Dgp<DCOR_DGP_BERNOULLI> {  // gen_bernoulli (vert-cor.R:78-98), 2 samples/block
+  // u = wa*2^-32 < 0.5 <=> wa < 2^31; v < thr <=> wb < ceil(thr*2^32) (exact).
   static __device__ __forceinline__ void from_words(const DgpConst& g, uint32_t wa, uint32_t wb,
                                                     double& x, double& y) {
-    const double u = (double)wa * 0x1p-32, v = (double)wb * 0x1p-32;
-    x = (u < 0.5) ? 1.0 : 0.0;
-    y = (x == 0.0) ? (v < g.thr0 ? 1.0 : 0.0) : (v < g.thr1 ? 1.0 : 0.0);
+    const bool xb = wa < 0x80000000u;
+    x = xb ? 1.0 : 0.0;
+    y = ((uint64_t)wb < (xb ? g.T1 : g.T0)) ? 1.0 : 0.0;
   }
   static __device__ __forceinline__ void one(const DgpConst& g, uint32_t i, uint32_t rep,
                                              uint32_t k0, uint32_t k1, double& x, double& y) {
@@ -103,10 +104,10 @@ struct FlipGen {  // sign-family INT flips, 4 per Philox block (SITE_FLIP), cach
   uint32_t cidx;
   U4 cw;
   __device__ __forceinline__ int get(uint32_t i, uint32_t rep, uint32_t k0, uint32_t k1,
-                                     double p) {
+                                     uint64_t p) {
     const uint32_t bi = i >> 2;
     if (bi != cidx) { cw = draw(bi, rep, DCOR_SITE_FLIP, k0, k1); cidx = bi; }
-    return ((double)word(cw, i & 3) * 0x1p-32 < p) ? 1 : -1;  // 2*S - 1 (vert-cor.R:175-179)
+    return ((uint64_t)word(cw, i & 3) < p) ? 1 : -1;  // 2*S - 1 (vert-cor.R:175-179)
   }
 };
 
@@ -187,7 +188,7 @@ __device__ __forceinline__ void exact_signs(const SignConst& c, const SignStd& s
                                             bool& bad_ni, bool& bad_int) {
   double x, y;
   Dgp<DGP>::one(c.g, i, rep, c.k0, c.k1, x, y);
-  const double xc = rclip(x, c.L), yc = rclip(y, c.L);
+  const double xc = rclip_fin(x, c.L), yc = rclip_fin(y, c.L);
   nx = sgn_std(xc, s.muNx, s.sdNx, bad_ni);
   ny = sgn_std(yc, s.muNy, s.sdNy, bad_ni);
   ix = sgn_std(xc, s.muIx, s.sdIx, bad_int);
@@ -213,11 +214,11 @@ __global__ __launch_bounds__(DCOR_BLOCK) void k_sign_pass1(SignConst c,
     uint32_t rec[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const double xc = rclip(x[q], c.L), yc = rclip(y[q], c.L);
+      const double xc = rclip_fin(x[q], c.L), yc = rclip_fin(y[q], c.L);
       if ((int64_t)(i0 + q) < c.n) { v[0] += xc; v[1] += xc * xc; v[2] += yc; v[3] += yc * yc; }
       const uint32_t qx = code16(xc, c.cbase_x, c.cinv_x, 65535.0);
       const uint32_t qy = code16(yc, c.cbase_y, c.cinv_y, 32767.0);
-      const uint32_t f = ((double)word(fw, q) * 0x1p-32 < c.pflip) ? 1u : 0u;
+      const uint32_t f = ((uint64_t)word(fw, q) < c.flipT) ? 1u : 0u;
       rec[q] = qx | (qy << 16) | (f << 31);
     }
     if ((int64_t)i0 + 3 < c.n) {
@@ -346,7 +347,7 @@ __global__ __launch_bounds__(DCOR_BLOCK) void k_sign_fused(SignConst c, dcor_rep
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         if (4 * g4 + q < c.n) {
-          const double xc = rclip(x[q], c.L), yc = rclip(y[q], c.L);
+          const double xc = rclip_fin(x[q], c.L), yc = rclip_fin(y[q], c.L);
           v[0] += xc; v[1] += xc * xc; v[2] += yc; v[3] += yc * yc;
         }
       }
@@ -369,7 +370,7 @@ __global__ __launch_bounds__(DCOR_BLOCK) void k_sign_fused(SignConst c, dcor_rep
     double x, y;
     Dgp<DGP>::one(c.g, i, rep, c.k0, c.k1, x, y);
     if (c.normalise) {
-      const double xc = rclip(x, c.L), yc = rclip(y, c.L);
+      const double xc = rclip_fin(x, c.L), yc = rclip_fin(y, c.L);
       nx = sgn_std(xc, s.muNx, s.sdNx, bni);
       ny = sgn_std(yc, s.muNy, s.sdNy, bni);
       ix = sgn_std(xc, s.muIx, s.sdIx, bad_int);
@@ -390,7 +391,7 @@ __global__ __launch_bounds__(DCOR_BLOCK) void k_sign_fused(SignConst c, dcor_rep
       int nx, ny, ix, iy;
       signs(i, nx, ny, ix, iy, bad_ni);
       cx += nx; cy += ny;
-      core += fl.get(i, rep, c.k0, c.k1, c.pflip) * ix * iy;
+      core += fl.get(i, rep, c.k0, c.k1, c.flipT) * ix * iy;
     }
     const U4 w = draw((uint32_t)j, rep, DCOR_SITE_NI_LAP, c.k0, c.k1);
     const double xt = (double)cx / c.md + c.bx * unit_laplace(u53(w.w0, w.w1));
@@ -403,7 +404,7 @@ __global__ __launch_bounds__(DCOR_BLOCK) void k_sign_fused(SignConst c, dcor_rep
     int nx, ny, ix, iy;
     bool ignore = false;
     signs((uint32_t)i, nx, ny, ix, iy, ignore);
-    core += fl.get((uint32_t)i, rep, c.k0, c.k1, c.pflip) * ix * iy;
+    core += fl.get((uint32_t)i, rep, c.k0, c.k1, c.flipT) * ix * iy;
   }
   DD d2[2] = {sT, sT2};
   block_sum_dd<2>(d2, red);
@@ -431,7 +432,7 @@ __global__ __launch_bounds__(DCOR_BLOCK) void k_subg_fused(SubgConst c, dcor_rep
   DD sP{0, 0}, sT{0, 0}, sT2{0, 0}, sU{0, 0}, sU2{0, 0};
   auto int_term = [&](double x, double y, double l) {
     const double S = c.sender_is_X ? x : y, O = c.sender_is_X ? y : x;
-    const double Uc = rclip((rclip(S, c.ls) + c.bs * l) * O, c.lr);   // ver-cor-subG.R:88-90
+    const double Uc = rclip_fin((rclip_fin(S, c.ls) + c.bs * l) * O, c.lr);  // ver-cor-subG.R:88-90
     dd_acc(sU, Uc);
     dd_acc(sU2, Uc * Uc);
   };
@@ -441,8 +442,8 @@ __global__ __launch_bounds__(DCOR_BLOCK) void k_subg_fused(SubgConst c, dcor_rep
     for (int r = 0; r < c.m; ++r) {
       double x, y, l;
       sample_lap<DGP>(c.g, (uint32_t)(i0 + r), rep, c.k0, c.k1, x, y, l);
-      sx += rclip(x, c.l1);                                              // :33
-      sy += rclip(y, c.l2);                                              // :34
+      sx += rclip_fin(x, c.l1);                                          // :33
+      sy += rclip_fin(y, c.l2);                                          // :34
       int_term(x, y, l);
     }
     const U4 w = draw((uint32_t)j, rep, DCOR_SITE_NI_LAP, c.k0, c.k1);
