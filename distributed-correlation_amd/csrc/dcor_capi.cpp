@@ -381,7 +381,7 @@ int dcor_sim_launch(const dcor_cell* cell, int64_t rep_begin, int64_t rep_count,
       rc = launch_sign_fused(k, rep_count, d_out, stream);
     } else {
       // scratch budget: >= 1 GiB and >= 2048 replicates' codes, <= 8 GiB
-      const size_t per_rep = (size_t)c.n * sizeof(uint32_t) + 4 * sizeof(double);
+      const size_t per_rep = (size_t)c.n * sizeof(uint32_t) + 4 * sizeof(double) + 48;
       size_t budget = (size_t)1 << 30;
       if (budget < 2048 * per_rep) budget = 2048 * per_rep;
       if (budget > ((size_t)8 << 30)) budget = (size_t)8 << 30;
@@ -390,7 +390,7 @@ int dcor_sim_launch(const dcor_cell* cell, int64_t rep_begin, int64_t rep_count,
       if (chunk > rep_count) chunk = rep_count;
       void* scratch = nullptr;
       const size_t codes_bytes = ((size_t)chunk * (size_t)c.n * sizeof(uint32_t) + 255) / 256 * 256;
-      if (int st = arena_get(codes_bytes + (size_t)chunk * 4 * sizeof(double), &scratch)) return st;
+      if (int st = arena_get(codes_bytes + (size_t)chunk * (4 * sizeof(double) + 48), &scratch)) return st;
       rc = launch_sign_fused_codes(k, rep_count, chunk, (uint32_t*)scratch,
                                    (double*)((char*)scratch + codes_bytes), d_out, stream);
     }

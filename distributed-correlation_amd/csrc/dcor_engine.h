@@ -84,7 +84,8 @@ struct PrematSubgConst {
 // Kernel launchers (dcor_kernels.hip).  Return hipError_t as int.
 int launch_sign_fused(const SignConst& c, int64_t reps, dcor_rep_out* out, void* stream);
 // One-pass sign algorithm: pass-1 / pass-2 kernels over replicate chunks of `chunk`;
-// scratch = chunk * n * 4 B of codes, sums = chunk * 4 doubles.
+// scratch = chunk * n * 4 B of codes; sums = chunk * 4 doubles followed by chunk
+// SignPartial records (48 B).
 int launch_sign_fused_codes(const SignConst& c, int64_t reps, int64_t chunk, uint32_t* scratch,
                             double* sums, dcor_rep_out* out, void* stream);
 int launch_subg_fused(const SubgConst& c, int64_t reps, dcor_rep_out* out, void* stream);

@@ -231,18 +231,23 @@ __global__ __launch_bounds__(DCOR_BLOCK) void k_sign_pass1(SignConst c,
   if (tid < 4) sums[4 * (size_t)blockIdx.x + tid] = v[tid];
 }
 
+// Per-replicate partial results handed from pass 2 to the epilogue.
+struct SignPartial {
+  double sT[2], sT2[2];  // double-double sum of T_j and T_j^2 (vert-cor.R:233-239)
+  long long core;        // sum of (2S-1) sign(X) sign(Y) (vert-cor.R:178-183)
+  long long flags;       // bit 0: NI saw NaN, bit 1: INT saw NaN
+};
+
 // Pass 2: signs from the codes (exact regeneration on a code tie), batch counts, NI
-// Laplace, INT flip sum, epilogue.
+// Laplace, T sums and the INT flip sum.  Lean: the mixquant/CI epilogue is its own kernel.
 template <int DGP>
 __global__ __launch_bounds__(DCOR_BLOCK) void k_sign_pass2(SignConst c,
                                                            const uint32_t* __restrict__ scratch,
                                                            const double* __restrict__ sums,
-                                                           dcor_rep_out* out) {
+                                                           SignPartial* __restrict__ part) {
   __shared__ double red[16 * DCOR_WAVES];
   __shared__ long long redi[DCOR_WAVES];
   __shared__ double lap[10];
-  __shared__ double keys[MIX_MAX];
-  __shared__ int nan_cnt;
   const int tid = threadIdx.x;
   const uint32_t rep = (uint32_t)(c.rep_begin + blockIdx.x);
   const uint32_t* slab = scratch + (size_t)blockIdx.x * (size_t)c.n;
@@ -270,59 +275,111 @@ __global__ __launch_bounds__(DCOR_BLOCK) void k_sign_pass2(SignConst c,
   bool bad_ni = thr_nan, bad_int = thr_nan;
   DD sT{0.0, 0.0}, sT2{0.0, 0.0};
   long long core = 0;
-  auto decide = [&](int64_t i, uint32_t w, int& nx, int& ny, int& ix, int& iy, int& f,
-                    bool& bni) {
+  // Fast path: signs from codes (branch-free).  A sample whose code ties a threshold's
+  // code is flagged and fixed up afterwards by exact regeneration (rolled loop, rare).
+  auto fast = [&](uint32_t w, int& cx, int& cy, int& cc) -> bool {
     const uint32_t qx = w & 0xffffu, qy = (w >> 16) & 0x7fffu;
-    f = (w >> 31) ? 1 : -1;
-    if (force_exact || qx == qNx || qx == qIx || qy == qNy || qy == qIy) {
-      exact_signs<DGP>(c, s, (uint32_t)i, rep, nx, ny, ix, iy, bni, bad_int);
-    } else {
-      nx = sgnq(qx, qNx); ny = sgnq(qy, qNy);
-      ix = sgnq(qx, qIx); iy = sgnq(qy, qIy);
-    }
+    const int f = (w >> 31) ? 1 : -1;
+    cx += sgnq(qx, qNx);
+    cy += sgnq(qy, qNy);
+    cc += f * sgnq(qx, qIx) * sgnq(qy, qIy);
+    return force_exact || qx == qNx || qx == qIx || qy == qNy || qy == qIy;
   };
-  const bool vec4 = (c.m % 4) == 0;
-  for (int64_t j = tid; j < c.k; j += DCOR_BLOCK) {
-    int cx = 0, cy = 0, cc = 0;
-    const int64_t i0 = j * c.m;
-    if (vec4) {
-      for (int r = 0; r < c.m; r += 4) {
-        const uint4 w4 = *reinterpret_cast<const uint4*>(slab + i0 + r);
-        const U4 ws{w4.x, w4.y, w4.z, w4.w};
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          int nx, ny, ix, iy, f;
-          decide(i0 + r + q, word(ws, q), nx, ny, ix, iy, f, bad_ni);
-          cx += nx; cy += ny; cc += f * ix * iy;
-        }
-      }
-    } else {
-      for (int r = 0; r < c.m; ++r) {
-        int nx, ny, ix, iy, f;
-        decide(i0 + r, slab[i0 + r], nx, ny, ix, iy, f, bad_ni);
-        cx += nx; cy += ny; cc += f * ix * iy;
-      }
-    }
-    core += cc;
+  auto fixup = [&](int64_t i, uint32_t w, int& cx, int& cy, int& cc, bool& bni) {
+    const uint32_t qx = w & 0xffffu, qy = (w >> 16) & 0x7fffu;
+    const int f = (w >> 31) ? 1 : -1;
+    int nx, ny, ix, iy;
+    exact_signs<DGP>(c, s, (uint32_t)i, rep, nx, ny, ix, iy, bni, bad_int);
+    cx += nx - sgnq(qx, qNx);
+    cy += ny - sgnq(qy, qNy);
+    cc += f * (ix * iy - sgnq(qx, qIx) * sgnq(qy, qIy));
+  };
+  auto batch_T = [&](int64_t j, int cx, int cy) {
     const U4 w = draw((uint32_t)j, rep, DCOR_SITE_NI_LAP, c.k0, c.k1);   // vert-cor.R:230-231
     const double xt = (double)cx / c.md + c.bx * unit_laplace(u53(w.w0, w.w1));
     const double yt = (double)cy / c.md + c.by * unit_laplace(u53(w.w2, w.w3));
     const double T = c.md * xt * yt;                                     // vert-cor.R:233
     dd_acc(sT, T);
     dd_acc(sT2, T * T);
+  };
+  if (c.m == 8) {
+    // headline geometry: one thread = one batch = two 16-B loads; the next batch's loads
+    // are issued before the current batch is decided (two batches in flight per thread).
+    int64_t j = tid;
+    uint4 a0 = make_uint4(0, 0, 0, 0), a1 = a0;
+    if (j < c.k) {
+      a0 = *reinterpret_cast<const uint4*>(slab + 8 * j);
+      a1 = *reinterpret_cast<const uint4*>(slab + 8 * j + 4);
+    }
+    for (; j < c.k; j += DCOR_BLOCK) {
+      const int64_t jn = j + DCOR_BLOCK;
+      const U4 w0{a0.x, a0.y, a0.z, a0.w}, w1{a1.x, a1.y, a1.z, a1.w};
+      if (jn < c.k) {
+        a0 = *reinterpret_cast<const uint4*>(slab + 8 * jn);
+        a1 = *reinterpret_cast<const uint4*>(slab + 8 * jn + 4);
+      }
+      int cx = 0, cy = 0, cc = 0;
+      uint32_t tie = 0;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) tie |= (fast(word(q < 4 ? w0 : w1, q & 3), cx, cy, cc) ? 1u : 0u) << q;
+      if (tie) {
+#pragma unroll 1
+        for (int q = 0; q < 8; ++q)
+          if ((tie >> q) & 1u) fixup(8 * j + q, word(q < 4 ? w0 : w1, q & 3), cx, cy, cc, bad_ni);
+      }
+      core += cc;
+      batch_T(j, cx, cy);
+    }
+  } else {
+    for (int64_t j = tid; j < c.k; j += DCOR_BLOCK) {
+      int cx = 0, cy = 0, cc = 0;
+      const int64_t i0 = j * c.m;
+      bool any = false;
+      for (int r = 0; r < c.m; ++r) any |= fast(slab[i0 + r], cx, cy, cc);
+      if (any) {
+        for (int r = 0; r < c.m; ++r) {
+          const uint32_t w = slab[i0 + r];
+          int dx = 0, dy = 0, dc = 0;
+          if (fast(w, dx, dy, dc)) fixup(i0 + r, w, cx, cy, cc, bad_ni);
+        }
+      }
+      core += cc;
+      batch_T(j, cx, cy);
+    }
   }
   for (int64_t i = c.k * c.m + tid; i < c.n; i += DCOR_BLOCK) {  // tail: INT only
-    int nx, ny, ix, iy, f;
+    int dx = 0, dy = 0, cc = 0;
     bool ignore = false;  // NI never reads the tail
-    decide(i, slab[i], nx, ny, ix, iy, f, ignore);
-    core += f * ix * iy;
+    const uint32_t w = slab[i];
+    if (fast(w, dx, dy, cc)) fixup(i, w, dx, dy, cc, ignore);
+    core += cc;
   }
   DD d2[2] = {sT, sT2};
   block_sum_dd<2>(d2, red);
   core = block_sum_i(core, redi);
   const long long nbad = block_sum_i((bad_ni ? 1LL : 0LL) + (bad_int ? (1LL << 20) : 0LL), redi);
-  sign_finish(c, rep, d2[0], d2[1], core, (nbad & 0xFFFFF) != 0, (nbad >> 20) != 0, lap, keys,
-              &nan_cnt, out + blockIdx.x);
+  if (tid == 0) {
+    SignPartial p;
+    p.sT[0] = d2[0].hi; p.sT[1] = d2[0].lo; p.sT2[0] = d2[1].hi; p.sT2[1] = d2[1].lo;
+    p.core = core;
+    p.flags = ((nbad & 0xFFFFF) ? 1 : 0) | ((nbad >> 20) ? 2 : 0);
+    part[blockIdx.x] = p;
+  }
+}
+
+// Epilogue: NI estimate/CI, INT estimate, mixquant, INT CI (vert-cor.R:233-254, 186-194, 281-313).
+__global__ __launch_bounds__(DCOR_BLOCK) void k_sign_epilogue(SignConst c,
+                                                              const SignPartial* __restrict__ part,
+                                                              dcor_rep_out* out) {
+  __shared__ double lap[10];
+  __shared__ double keys[MIX_MAX];
+  __shared__ int nan_cnt;
+  const uint32_t rep = (uint32_t)(c.rep_begin + blockIdx.x);
+  scalar_laplace(rep, c.k0, c.k1, lap);
+  __syncthreads();
+  const SignPartial p = part[blockIdx.x];
+  sign_finish(c, rep, DD{p.sT[0], p.sT[1]}, DD{p.sT2[0], p.sT2[1]}, p.core, (p.flags & 1) != 0,
+              (p.flags & 2) != 0, lap, keys, &nan_cnt, out + blockIdx.x);
 }
 
 // ============================= fused sign family, regenerate (two-pass, A/B) ===
@@ -499,13 +556,16 @@ template <int DGP>
 static int launch_codes_t(SignConst c, int64_t reps, int64_t chunk, uint32_t* scratch,
                           double* sums, dcor_rep_out* out, void* stream) {
   const int64_t rep0 = c.rep_begin;
+  SignPartial* part = reinterpret_cast<SignPartial*>(sums + 4 * chunk);
   for (int64_t r = 0; r < reps; r += chunk) {
     const int64_t nr = (reps - r < chunk) ? reps - r : chunk;
     c.rep_begin = rep0 + r;
     hipLaunchKernelGGL(k_sign_pass1<DGP>, dim3((unsigned)nr), dim3(DCOR_BLOCK), 0,
                        (hipStream_t)stream, c, scratch, sums);
     hipLaunchKernelGGL(k_sign_pass2<DGP>, dim3((unsigned)nr), dim3(DCOR_BLOCK), 0,
-                       (hipStream_t)stream, c, scratch, sums, out + r);
+                       (hipStream_t)stream, c, scratch, sums, part);
+    hipLaunchKernelGGL(k_sign_epilogue, dim3((unsigned)nr), dim3(DCOR_BLOCK), 0,
+                       (hipStream_t)stream, c, part, out + r);
     if (int e = last_err()) return e;
   }
   return 0;
