@@ -1,0 +1,202 @@
+"""bench_configs.py -- the BASELINE.json configs beyond the headline (one JSON line each).
+
+C1  vert-cor.R sign family n=1000 rho=.5 eps=(1,1), 1000 reps: GPU vs CPU oracle (1 and nproc-1 threads)
+C2  Bernoulli sign-family grid n=1e4, 8 rho x 3 eps, 1e4 reps/cell (fused kernels)
+C3  Gaussian + mixquant grid n=1e6, 8 rho x 3 eps (1e5 reps/cell in the config; --c3-reps here)
+C4  legacy paper sweep: {sign: gaussian, bernoulli; sub-G: gaussian, bounded factor} x rho {0,.3,.8}
+    x 5 eps pairs x n {200..3200, 1e4, 1e5, 1e6}, B=1000
+C5  HRS BMI-vs-Age pre-materialised streaming (synthetic stand-in panel n=19,433, eps=2): noise
+    generated on device into HBM, then the streaming kernel is timed -> replicates/s and HBM GB/s
+S   sub-G fused, bounded factor, n=1e5, rho=.5, eps=(1,1)
+Run on one GPU: python bench_configs.py [--only C2,C5] > profiles/rNN_configs.jsonl
+"""
+import argparse
+import ctypes as C
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "distributed-correlation_amd"))
+sys.path.insert(0, ROOT)
+
+W_SAMPLE = {"gaussian": 260, "bernoulli": 120, "bounded_factor": 292}
+FP64_PEAK_UNITS = 3.93e13
+HBM_PEAK = 8.0e12
+
+
+def timed(fn, reps=3):
+    import torch
+    fn()
+    torch.cuda.synchronize()
+    best = 1e30
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        fn()
+        torch.cuda.synchronize()
+        best = min(best, time.perf_counter() - t0)
+    return best
+
+
+def grid_units(cells, B):
+    from dcor.api import batch_geometry
+    tot = 0.0
+    for c in cells:
+        try:
+            k, m = batch_geometry(c.n, c.eps1, c.eps2, "subG" if c.family == "subG" else "sign")
+        except Exception:
+            k = 0
+        tot += B * (W_SAMPLE[c.dgp] * c.n + 183 * k + 2.0e5)
+    return tot
+
+
+def run_grid_gpu(cells, B, chunk=1 << 15):
+    import torch
+    from dcor.sim import simulate, accumulate
+    buf = torch.empty((min(B, chunk), 6), dtype=torch.float64, device="cuda")
+    acc = []
+    for c in cells:
+        for r0 in range(0, B, chunk):
+            nr = min(chunk, B - r0)
+            simulate(c, nr, r0, out=buf)
+            acc.append(accumulate(buf[:nr], c.rho))
+    return acc
+
+
+def line(name, **kw):
+    kw["config"] = name
+    print(json.dumps(kw), flush=True)
+
+
+def c1():
+    from dcor.sim import CellSpec, simulate
+    from oracle.oracle import sim_reps
+    cell = CellSpec(n=1000, rho=0.5, eps1=1.0, eps2=1.0, mu=(0.5, 0.5), sigma=(2.0, 2.0), seed=1_000_073)
+    B = 1000
+    t = timed(lambda: simulate(cell, B))
+    t0 = time.perf_counter()
+    sim_reps(cell.to_c(), 0, B, threads=1)
+    t1 = time.perf_counter() - t0
+    nthr = max(1, min(os.cpu_count() or 1, 16) - 1)
+    t0 = time.perf_counter()
+    sim_reps(cell.to_c(), 0, B, threads=nthr)
+    tn = time.perf_counter() - t0
+    line("C1", reps=B, gpu_s=t, gpu_reps_per_s=B / t, cpu_1thread_s=t1, cpu_1thread_reps_per_s=B / t1,
+         cpu_threads=nthr, cpu_nthread_s=tn, cpu_nthread_reps_per_s=B / tn,
+         note="CPU = oracle fused restatement (C); R's interpreted loop would be slower")
+
+
+def c2():
+    from dcor.sim import expand_grid
+    cells = expand_grid([10_000], [0, 0.15, 0.3, 0.4, 0.5, 0.65, 0.8, 0.9],
+                        [(0.5, 0.5), (1.0, 1.0), (1.5, 0.5)], family="sign", dgp="bernoulli")
+    B = 10_000
+    t = timed(lambda: run_grid_gpu(cells, B), reps=2)
+    u = grid_units(cells, B)
+    line("C2", cells=len(cells), reps_per_cell=B, seconds=t, reps_per_s=len(cells) * B / t,
+         roofline_frac=u / t / FP64_PEAK_UNITS)
+
+
+def c3(reps):
+    from dcor.sim import expand_grid
+    cells = expand_grid([1_000_000], [0, 0.15, 0.3, 0.4, 0.5, 0.65, 0.8, 0.9],
+                        [(0.5, 0.5), (1.0, 1.0), (1.5, 0.5)], family="sign", dgp="gaussian",
+                        mu=(0.5, 0.5), sigma=(2.0, 2.0))
+    t = timed(lambda: run_grid_gpu(cells, reps), reps=1)
+    u = grid_units(cells, reps)
+    rps = len(cells) * reps / t
+    line("C3", cells=len(cells), reps_per_cell=reps, seconds=t, reps_per_s=rps,
+         roofline_frac=u / t / FP64_PEAK_UNITS,
+         projected_full_config_seconds_1gpu=len(cells) * 1e5 / rps,
+         projected_full_config_seconds_8gpu=len(cells) * 1e5 / rps / 8)
+
+
+def c4(B):
+    from dcor.sim import paper_grid
+    cells = paper_grid(n_grid=(200, 400, 800, 1600, 3200, 10_000, 100_000, 1_000_000))
+    ok = []
+    for c in cells:  # sign family needs k >= 1 (vert-cor.R:209): skip (n, eps) pairs where it fails
+        m = math.ceil(8 / (c.eps1 * c.eps2))
+        if c.family == "sign" and c.n // m < 1:
+            continue
+        ok.append(c)
+    t = timed(lambda: run_grid_gpu(ok, B), reps=1)
+    u = grid_units(ok, B)
+    line("C4", cells=len(ok), cells_skipped_k_lt_1=len(cells) - len(ok), reps_per_cell=B, seconds=t,
+         reps_per_s=len(ok) * B / t, roofline_frac=u / t / FP64_PEAK_UNITS)
+
+
+def c5(R):
+    import numpy as np
+    import torch
+    from dcor import _lib
+    n, eps = 19433, 2.0
+    k, m = 9716, 2
+    nsim = 2000
+    g = np.random.default_rng(2)
+    age = np.clip(g.normal(0.0, 1.0, n), -2.22, 2.22)         # synthetic stand-in (HRS not shipped)
+    bmi = -0.19 * age + math.sqrt(1 - 0.19 ** 2) * g.normal(0.0, 1.0, n)
+    X = torch.as_tensor(age, device="cuda")
+    Y = torch.as_tensor(bmi, device="cuda")
+    perm = torch.empty((R, k * m), dtype=torch.int32, device="cuda")
+    lx = torch.empty((R, k), dtype=torch.float64, device="cuda")
+    ly = torch.empty((R, k), dtype=torch.float64, device="cuda")
+    ll = torch.empty((R, n), dtype=torch.float64, device="cuda")
+    lc = torch.empty((R,), dtype=torch.float64, device="cuda")
+    mz = torch.empty((R, nsim), dtype=torch.float64, device="cuda")
+    ml = torch.empty((R, nsim), dtype=torch.float64, device="cuda")
+    seed = 231
+    P = lambda t: C.c_void_p(t.data_ptr())
+    _lib.check(_lib.lib.dcor_perm_launch(seed, _lib.SITE_PERM, 0, R, n, k * m, P(perm), None))
+    _lib.check(_lib.lib.dcor_draws_launch(0, seed, 11, 0, R, k, P(lx), None))
+    _lib.check(_lib.lib.dcor_draws_launch(0, seed, 12, 0, R, k, P(ly), None))
+    _lib.check(_lib.lib.dcor_draws_launch(0, seed, 13, 0, R, n, P(ll), None))
+    _lib.check(_lib.lib.dcor_draws_launch(0, seed, 14, 0, 1, R, P(lc), None))
+    _lib.check(_lib.lib.dcor_draws_launch(1, seed, 15, 0, R, nsim, P(mz), None))
+    _lib.check(_lib.lib.dcor_draws_launch(0, seed, 16, 0, R, nsim, P(ml), None))
+    out = torch.empty((R, 6), dtype=torch.float64, device="cuda")
+    d = _lib.PrematSubg(n=n, reps=R, eps1=eps, eps2=eps, eta1=1.0, eta2=1.0, alpha=0.05, hrs=1,
+                        lam_x=2.22, lam_y=2.60, lam_s=2.22, lam_o=2.60, lam_r=math.nan,
+                        delta=math.nan, nsim=nsim, X=X.data_ptr(), Y=Y.data_ptr(), xy_stride=0,
+                        perm=perm.data_ptr(), lap_ni_x=lx.data_ptr(), lap_ni_y=ly.data_ptr(),
+                        lap_local=ll.data_ptr(), lap_central=lc.data_ptr(), mix_z=mz.data_ptr(),
+                        mix_l=ml.data_ptr())
+    t = timed(lambda: _lib.check(_lib.lib.dcor_premat_subg_launch(C.byref(d), P(out), None)), reps=5)
+    per_rep = 4 * k * m + 16 * k + 8 * n + 8 + 16 * nsim
+    line("C5", reps=R, seconds=t, reps_per_s=R / t, algorithmic_bytes_per_rep=per_rep,
+         hbm_gbps=per_rep * R / t / 1e9, hbm_frac=per_rep * R / t / HBM_PEAK,
+         note="synthetic stand-in panel (n=19,433, clipped std-normal age_z, corr -0.19); "
+              "noise pre-generated on device (dcor_draws_launch / dcor_perm_launch); timed = streaming kernel only")
+
+
+def subg():
+    from dcor.sim import CellSpec, simulate
+    cell = CellSpec(n=100_000, rho=0.5, eps1=1.0, eps2=1.0, family="subG", dgp="bounded_factor", seed=5)
+    R = 4096
+    t = timed(lambda: simulate(cell, R))
+    u = R * (292 * cell.n + 183 * 12500 + 2e5)
+    line("S", reps=R, seconds=t, reps_per_s=R / t, roofline_frac=u / t / FP64_PEAK_UNITS)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--only", default="C1,C2,C3,C4,C5,S")
+    ap.add_argument("--c3-reps", type=int, default=2000)
+    ap.add_argument("--c4-B", type=int, default=1000)
+    ap.add_argument("--c5-R", type=int, default=4096)
+    a = ap.parse_args()
+    import torch
+    torch.cuda.set_device(0)
+    which = a.only.split(",")
+    if "C1" in which: c1()
+    if "C2" in which: c2()
+    if "C3" in which: c3(a.c3_reps)
+    if "C4" in which: c4(a.c4_B)
+    if "C5" in which: c5(a.c5_R)
+    if "S" in which: subg()
+
+
+if __name__ == "__main__":
+    main()

@@ -513,7 +513,23 @@ int dcor_premat_subg_launch(const dcor_premat_subg* d, dcor_rep_out* d_out, void
   if (int st = need_device()) return st;
   PrematSubgConst p;
   if (int st = premat_subg_const(d, p)) return st;
-  const int rc = launch_premat_subg(p, d->reps, d_out, stream);
+  // stream-ordered scratch for the stream -> epilogue partials: safe under concurrent
+  // launches on different streams.
+  // HRS over one shared panel: the packed clipped panel (2 x n x 16 B) follows the partials.
+  const bool pack = p.hrs && p.perm && p.xy_stride == 0 && p.s.m == 2;
+  const size_t part_b = ((size_t)d->reps * 80 + 255) & ~(size_t)255;
+  const size_t bytes = part_b + (pack ? (size_t)p.s.n * 32 : 0);
+  void* part = nullptr;
+  if (hipMallocAsync(&part, bytes, (hipStream_t)stream) != hipSuccess) {
+    (void)hipGetLastError();
+    return fail(DCOR_ENOMEM, "premat sub-G: cannot allocate %zu scratch bytes", bytes);
+  }
+  if (pack) {
+    p.xyc = (const double2*)((char*)part + part_b);
+    p.soc = p.xyc + p.s.n;
+  }
+  const int rc = launch_premat_subg(p, d->reps, part, d_out, stream);
+  (void)hipFreeAsync(part, (hipStream_t)stream);
   if (rc) return hip_fail((hipError_t)rc, "premat_subg launch");
   return DCOR_OK;
 }
@@ -615,7 +631,9 @@ static int run_premat_subg_1(const double* X, const double* Y, int64_t n, double
   p.perm = perm ? bp.as<int32_t>() : nullptr;
   p.lap_ni_x = blx.as<double>(); p.lap_ni_y = bly.as<double>(); p.lap_local = bll.as<double>();
   p.lap_central = bc.as<double>(); p.mix_z = bmz.as<double>(); p.mix_l = bml.as<double>();
-  const int rc = launch_premat_subg(p, 1, bout.as<dcor_rep_out>(), nullptr);
+  DevBuf bpart;
+  HIPCHK(bpart.alloc(80));
+  const int rc = launch_premat_subg(p, 1, bpart.p, bout.as<dcor_rep_out>(), nullptr);
   if (rc) return hip_fail((hipError_t)rc, "premat_subg launch");
   HIPCHK(hipMemcpy(res, bout.p, sizeof(dcor_rep_out), hipMemcpyDeviceToHost));
   return DCOR_OK;
@@ -702,10 +720,24 @@ int dcor_dp_sd(const double* x, int64_t n, double lo, double hi, double eps1, do
   return DCOR_OK;
 }
 
+int dcor_perm_launch(uint64_t seed, int site, int64_t rep_begin, int64_t reps, int64_t n,
+                     int64_t count, int32_t* d_out, void* stream) {
+  if (n < 1 || n > 0x7fffffffLL || count < 0 || count > n || reps < 0 || reps > 65535 ||
+      (reps * count > 0 && !d_out))
+    return fail(DCOR_EINVAL, "bad perm arguments (need 0 <= count <= n < 2^31, reps <= 65535)");
+  if (rep_begin < 0 || rep_begin + reps > 0xffffffffLL) return fail(DCOR_EINVAL, "rep range");
+  if (int st = need_device()) return st;
+  const int rc = launch_perm((uint32_t)seed, (uint32_t)(seed >> 32), (uint32_t)site, rep_begin,
+                             reps, n, count, d_out, stream);
+  if (rc) return hip_fail((hipError_t)rc, "perm launch");
+  return DCOR_OK;
+}
+
 int dcor_shutdown(void) {
   for (auto& a : g_arena) {
     if (a.p) { (void)hipFree(a.p); a.p = nullptr; a.bytes = 0; }
   }
+
   return DCOR_OK;
 }
 

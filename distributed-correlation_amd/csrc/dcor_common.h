@@ -22,18 +22,24 @@ __device__ __forceinline__ int sgn_raw(double a, bool& bad) {
 }
 
 __device__ __forceinline__ double mixquant_loaded(const MixConst& mx, double c, const double* z,
-                                                  const double* l, double* keys, int* nan_cnt) {
-  if (threadIdx.x == 0) *nan_cnt = 0;
+                                                  const double* l, SelScratch* sc) {
+  if (threadIdx.x == 0) sc->nan_cnt = 0;
   __syncthreads();
+  unsigned long long key[SEL_VPT];
   int nn = 0;
-  for (int i = threadIdx.x; i < mx.nsim; i += DCOR_BLOCK) {
-    double v = z[i] + c * l[i];
-    if (v != v) { v = __longlong_as_double(0x7ff0000000000000LL); ++nn; }
-    keys[i] = v;
+#pragma unroll
+  for (int s = 0; s < SEL_VPT; ++s) {
+    const int i = threadIdx.x + s * DCOR_BLOCK;
+    key[s] = ~0ull;
+    if (i < mx.nsim) {
+      const double v = z[i] + c * l[i];
+      nn += (v != v);
+      key[s] = sel_key(v);
+    }
   }
-  if (nn) atomicAdd(nan_cnt, nn);
+  if (nn) atomicAdd(&sc->nan_cnt, nn);
   __syncthreads();
-  return lds_select(keys, mx.nsim, mx.P, mx.pos, nan_cnt);
+  return reg_select(key, mx.pos, mx.nsim - sc->nan_cnt, sc);
 }
 
 #define MIX_MAX 2048

@@ -79,6 +79,10 @@ struct PrematSubgConst {
   const int32_t* perm;
   const double* lap_ni_x; const double* lap_ni_y; const double* lap_local;
   const double* lap_central; const double* mix_z; const double* mix_l;
+  // HRS with a shared panel (xy_stride 0): clipped panel packed once per launch,
+  // xyc[i] = (clip(X_i, l1), clip(Y_i, l2)) for the NI gathers, soc[i] = (clip(S_i, ls),
+  // clip(O_i, lo)) for the INT stream.  nullptr: read X / Y directly.
+  const double2* xyc; const double2* soc;
 };
 
 // Kernel launchers (dcor_kernels.hip).  Return hipError_t as int.
@@ -90,7 +94,9 @@ int launch_sign_fused_codes(const SignConst& c, int64_t reps, int64_t chunk, uin
                             double* sums, dcor_rep_out* out, void* stream);
 int launch_subg_fused(const SubgConst& c, int64_t reps, dcor_rep_out* out, void* stream);
 int launch_premat_sign(const PrematSignConst& c, int64_t reps, dcor_rep_out* out, void* stream);
-int launch_premat_subg(const PrematSubgConst& c, int64_t reps, dcor_rep_out* out, void* stream);
+// part: reps * 80 B scratch (stream -> epilogue partial sums).
+int launch_premat_subg(const PrematSubgConst& c, int64_t reps, void* part, dcor_rep_out* out,
+                       void* stream);
 int launch_accumulate(const dcor_rep_out* d_out, int64_t count, double rho, dcor_accum* acc,
                       void* stream);
 int launch_mixquant(const double* z, const double* l, int32_t nsim, double c, int32_t pos,
@@ -99,6 +105,8 @@ int launch_priv_standardize(const double* v, int64_t n, double L, double s_mu, d
                             const double* lap2, double* out, void* stream);
 int launch_draws(int kind, uint32_t k0, uint32_t k1, uint32_t site, int64_t rep_begin,
                  int64_t reps, int64_t count, double* out, void* stream);
+int launch_perm(uint32_t k0, uint32_t k1, uint32_t site, int64_t rep_begin, int64_t reps,
+                int64_t n, int64_t count, int32_t* out, void* stream);
 int launch_dp_sd(const double* x, int64_t n, double lo, double hi, double s_mu, double s_m2,
                  const double* lap2, double* out2, void* stream);
 

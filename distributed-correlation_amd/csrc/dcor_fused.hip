@@ -113,28 +113,33 @@ struct FlipGen {  // sign-family INT flips, 4 per Philox block (SITE_FLIP), cach
 
 // mixquant inside the workgroup: keys = z + c*l from Philox, then the order statistic.
 __device__ __forceinline__ double mixquant_fused(const MixConst& mx, double c, uint32_t rep,
-                                                 uint32_t k0, uint32_t k1, double* keys,
-                                                 int* nan_cnt) {
-  if (threadIdx.x == 0) *nan_cnt = 0;
+                                                 uint32_t k0, uint32_t k1, SelScratch* sc) {
+  if (threadIdx.x == 0) sc->nan_cnt = 0;
   __syncthreads();
+  unsigned long long key[SEL_VPT];
   int nn = 0;
-  for (int b = threadIdx.x; 2 * b < mx.nsim; b += DCOR_BLOCK) {
-    const U4 wz = draw((uint32_t)b, rep, DCOR_SITE_MIX_Z, k0, k1);
-    const U4 wl = draw((uint32_t)b, rep, DCOR_SITE_MIX_L, k0, k1);
-    double z0, z1;
-    normal_pair(wz, &z0, &z1);
-    double v0 = z0 + c * unit_laplace(u53(wl.w0, wl.w1));
-    if (v0 != v0) { v0 = __longlong_as_double(0x7ff0000000000000LL); ++nn; }
-    keys[2 * b] = v0;
-    if (2 * b + 1 < mx.nsim) {
-      double v1 = z1 + c * unit_laplace(u53(wl.w2, wl.w3));
-      if (v1 != v1) { v1 = __longlong_as_double(0x7ff0000000000000LL); ++nn; }
-      keys[2 * b + 1] = v1;
+#pragma unroll
+  for (int s = 0; s < SEL_VPT / 2; ++s) {
+    const int b = threadIdx.x + s * DCOR_BLOCK;  // Philox block b -> elements 2b, 2b+1
+    key[2 * s] = key[2 * s + 1] = ~0ull;
+    if (2 * b < mx.nsim) {
+      const U4 wz = draw((uint32_t)b, rep, DCOR_SITE_MIX_Z, k0, k1);
+      const U4 wl = draw((uint32_t)b, rep, DCOR_SITE_MIX_L, k0, k1);
+      double z0, z1;
+      normal_pair(wz, &z0, &z1);
+      const double v0 = z0 + c * unit_laplace(u53(wl.w0, wl.w1));
+      nn += (v0 != v0);
+      key[2 * s] = sel_key(v0);
+      if (2 * b + 1 < mx.nsim) {
+        const double v1 = z1 + c * unit_laplace(u53(wl.w2, wl.w3));
+        nn += (v1 != v1);
+        key[2 * s + 1] = sel_key(v1);
+      }
     }
   }
-  if (nn) atomicAdd(nan_cnt, nn);
+  if (nn) atomicAdd(&sc->nan_cnt, nn);
   __syncthreads();
-  return lds_select(keys, mx.nsim, mx.P, mx.pos, nan_cnt);
+  return reg_select(key, mx.pos, mx.nsim - sc->nan_cnt, sc);
 }
 
 __device__ __forceinline__ void scalar_laplace(uint32_t rep, uint32_t k0, uint32_t k1, double* lap) {
@@ -148,7 +153,7 @@ __device__ __forceinline__ void scalar_laplace(uint32_t rep, uint32_t k0, uint32
 // INT epilogue + CI write shared by the sign kernels (vert-cor.R:281-313).
 __device__ __forceinline__ void sign_finish(const SignConst& c, uint32_t rep, DD sT, DD sT2,
                                             long long core, bool any_ni, bool any_int,
-                                            const double* lap, double* keys, int* nan_cnt,
+                                            const double* lap, SelScratch* sel,
                                             dcor_rep_out* dst) {
   double o[6];
   ni_sign_result(c, sT, sT2, any_ni, o);
@@ -156,7 +161,7 @@ __device__ __forceinline__ void sign_finish(const SignConst& c, uint32_t rep, DD
   int_sign_point(c, core, lap[8], rho, eta, se, cstar);
   double w;
   if (c.mode_normal)
-    w = mixquant_fused(c.mix, cstar, rep, c.k0, c.k1, keys, nan_cnt) * se;
+    w = mixquant_fused(c.mix, cstar, rep, c.k0, c.k1, sel) * se;
   else
     w = c.w_laplace;
   o[3] = rho;
@@ -372,14 +377,13 @@ __global__ __launch_bounds__(DCOR_BLOCK) void k_sign_epilogue(SignConst c,
                                                               const SignPartial* __restrict__ part,
                                                               dcor_rep_out* out) {
   __shared__ double lap[10];
-  __shared__ double keys[MIX_MAX];
-  __shared__ int nan_cnt;
+  __shared__ SelScratch sel;
   const uint32_t rep = (uint32_t)(c.rep_begin + blockIdx.x);
   scalar_laplace(rep, c.k0, c.k1, lap);
   __syncthreads();
   const SignPartial p = part[blockIdx.x];
   sign_finish(c, rep, DD{p.sT[0], p.sT[1]}, DD{p.sT2[0], p.sT2[1]}, p.core, (p.flags & 1) != 0,
-              (p.flags & 2) != 0, lap, keys, &nan_cnt, out + blockIdx.x);
+              (p.flags & 2) != 0, lap, &sel, out + blockIdx.x);
 }
 
 // ============================= fused sign family, regenerate (two-pass, A/B) ===
@@ -391,8 +395,7 @@ __global__ __launch_bounds__(DCOR_BLOCK) void k_sign_fused(SignConst c, dcor_rep
   __shared__ double red[16 * DCOR_WAVES];
   __shared__ long long redi[DCOR_WAVES];
   __shared__ double lap[10];
-  __shared__ double keys[MIX_MAX];
-  __shared__ int nan_cnt;
+  __shared__ SelScratch sel;
   const uint32_t rep = (uint32_t)(c.rep_begin + blockIdx.x);
   const int tid = threadIdx.x;
   scalar_laplace(rep, c.k0, c.k1, lap);
@@ -467,8 +470,8 @@ __global__ __launch_bounds__(DCOR_BLOCK) void k_sign_fused(SignConst c, dcor_rep
   block_sum_dd<2>(d2, red);
   core = block_sum_i(core, redi);
   const long long nbad = block_sum_i((bad_ni ? 1LL : 0LL) + (bad_int ? (1LL << 20) : 0LL), redi);
-  sign_finish(c, rep, d2[0], d2[1], core, (nbad & 0xFFFFF) != 0, (nbad >> 20) != 0, lap, keys,
-              &nan_cnt, out + blockIdx.x);
+  sign_finish(c, rep, d2[0], d2[1], core, (nbad & 0xFFFFF) != 0, (nbad >> 20) != 0, lap, &sel,
+              out + blockIdx.x);
 }
 
 // ===================================================== fused sub-G family ===
@@ -478,8 +481,7 @@ template <int DGP>
 __global__ __launch_bounds__(DCOR_BLOCK) void k_subg_fused(SubgConst c, dcor_rep_out* out) {
   __shared__ double red[16 * DCOR_WAVES];
   __shared__ double lapz;
-  __shared__ double keys[MIX_MAX];
-  __shared__ int nan_cnt;
+  __shared__ SelScratch sel;
   const uint32_t rep = (uint32_t)(c.rep_begin + blockIdx.x);
   const int tid = threadIdx.x;
   if (tid == 0) {
@@ -525,7 +527,7 @@ __global__ __launch_bounds__(DCOR_BLOCK) void k_subg_fused(SubgConst c, dcor_rep
   const double sd = sqrt(dd_var(d5[3], d5[4], c.nd));
   const double se_norm = sqrt(sd * sd + c.sn2x2);                      // :99
   const double cstar = 2.0 / (c.sqrt_n * sd * c.eps_r);                // :100
-  const double q = mixquant_fused(c.mix, cstar, rep, c.k0, c.k1, keys, &nan_cnt);
+  const double q = mixquant_fused(c.mix, cstar, rep, c.k0, c.k1, &sel);
   const double width = q * se_norm / c.sqrt_n;                         // :101
   o[3] = rho;
   o[4] = rmax(rho - width, -1.0);

@@ -12,8 +12,7 @@ namespace dcor {
 __global__ __launch_bounds__(DCOR_BLOCK) void k_premat_sign(PrematSignConst p, dcor_rep_out* out) {
   __shared__ double red[16 * DCOR_WAVES];
   __shared__ long long redi[DCOR_WAVES];
-  __shared__ double keys[MIX_MAX];
-  __shared__ int nan_cnt;
+  __shared__ SelScratch sel;
   const SignConst& c = p.s;
   const int64_t rep = blockIdx.x;
   const int tid = threadIdx.x;
@@ -108,7 +107,7 @@ __global__ __launch_bounds__(DCOR_BLOCK) void k_premat_sign(PrematSignConst p, d
   double w;
   if (c.mode_normal)
     w = mixquant_loaded(c.mix, cstar, p.mix_z + rep * c.mix.nsim, p.mix_l + rep * c.mix.nsim,
-                        keys, &nan_cnt) * se;
+                        &sel) * se;
   else
     w = c.w_laplace;
   o[3] = rho;
@@ -122,66 +121,191 @@ __global__ __launch_bounds__(DCOR_BLOCK) void k_premat_sign(PrematSignConst p, d
 }
 
 // ================================================== pre-materialised sub-G ===
-__global__ __launch_bounds__(DCOR_BLOCK) void k_premat_subg(PrematSubgConst p, dcor_rep_out* out) {
+// Streaming kernel (one workgroup per replicate): NI batch means + INT clipped products,
+// compensated partial sums -> SubgPartial.  The mixquant / CI epilogue is a second kernel,
+// so the streaming kernel carries no sort scratch and keeps many loads in flight (each
+// thread issues UNR iterations' loads before using them).
+struct SubgPartial { double s[10]; };  // sP, sT, sT2, sU, sU2 as (hi, lo)
+
+#define SUBG_UNR 4
+
+// Pack the shared HRS panel once per launch (same clips as the per-rep path, so the
+// results are identical): halves the NI gather transactions (one 16-B line access per
+// sample instead of two 8-B ones) and removes the per-rep clip work.
+__global__ __launch_bounds__(DCOR_BLOCK) void k_premat_xy_pack(PrematSubgConst p,
+                                                               double2* __restrict__ xyc,
+                                                               double2* __restrict__ soc) {
+  const SubgConst& c = p.s;
+  const int64_t i = (int64_t)blockIdx.x * DCOR_BLOCK + threadIdx.x;
+  if (i >= c.n) return;
+  const double x = p.X[i], y = p.Y[i];
+  const double sv = c.sender_is_X ? x : y, ov = c.sender_is_X ? y : x;
+  xyc[i] = make_double2(rclip(x, c.l1), rclip(y, c.l2));
+  soc[i] = make_double2(rclip(sv, c.ls), rclip(ov, p.lo_));
+}
+
+__global__ __launch_bounds__(DCOR_BLOCK) void k_premat_subg_stream(PrematSubgConst p,
+                                                                   SubgPartial* __restrict__ part) {
   __shared__ double red[16 * DCOR_WAVES];
-  __shared__ double keys[MIX_MAX];
-  __shared__ int nan_cnt;
   const SubgConst& c = p.s;
   const int64_t rep = blockIdx.x;
   const int tid = threadIdx.x;
-  const double* X = p.X + rep * p.xy_stride;
-  const double* Y = p.Y + rep * p.xy_stride;
-  const double* S = c.sender_is_X ? X : Y;
-  const double* O = c.sender_is_X ? Y : X;
-  const double* lx = p.lap_ni_x + rep * c.k;
-  const double* ly = p.lap_ni_y + rep * c.k;
-  const double* ll = p.lap_local + rep * c.n;
+  const double* __restrict__ X = p.X + rep * p.xy_stride;
+  const double* __restrict__ Y = p.Y + rep * p.xy_stride;
+  const double* __restrict__ S = c.sender_is_X ? X : Y;
+  const double* __restrict__ O = c.sender_is_X ? Y : X;
+  const double* __restrict__ lx = p.lap_ni_x + rep * c.k;
+  const double* __restrict__ ly = p.lap_ni_y + rep * c.k;
+  const double* __restrict__ ll = p.lap_local + rep * c.n;
   DD sP{0, 0}, sT{0, 0}, sT2{0, 0}, sU{0, 0}, sU2{0, 0};
-  auto int_term = [&](int64_t i) {
-    const double ov = p.hrs ? rclip(O[i], p.lo_) : O[i];
-    const double Uc = rclip((rclip(S[i], c.ls) + c.bs * ll[i]) * ov, c.lr);
-    dd_acc(sU, Uc);
-    dd_acc(sU2, Uc * Uc);
+  auto int_term = [&](double sv, double ov0, double l) {   // ver-cor-subG.R:88-90; rds:222-232
+    const double ov = p.hrs ? rclip(ov0, p.lo_) : ov0;
+    const double Uc = rclip((rclip(sv, c.ls) + c.bs * l) * ov, c.lr);
+    ks_acc(sU, Uc);
+    ks_acc(sU2, Uc * Uc);
   };
-  auto batch_term = [&](int64_t j, DD bx, DD by) {
+  auto batch_term = [&](double lxj, double lyj, DD bx, DD by) {  // ver-cor-subG.R:44-55
     const DD xb = dd_div_d(bx, c.md), yb = dd_div_d(by, c.md);
-    const double xt = (xb.hi + xb.lo) + c.bx * lx[j];
-    const double yt = (yb.hi + yb.lo) + c.by * ly[j];
-    dd_acc(sP, xt * yt);
+    const double xt = (xb.hi + xb.lo) + c.bx * lxj;
+    const double yt = (yb.hi + yb.lo) + c.by * lyj;
+    ks_acc(sP, xt * yt);
     const double T = c.md * xt * yt;
-    dd_acc(sT, T);
-    dd_acc(sT2, T * T);
+    ks_acc(sT, T);
+    ks_acc(sT2, T * T);
   };
-  if (p.perm == nullptr) {
+  if (p.xyc != nullptr && c.m == 2) {
+    // HRS, shared packed panel (real-data-sims.R:131, 222-232).
+    const double2* __restrict__ so = p.soc;
+    const double2* __restrict__ xy = p.xyc;
+    const int64_t step = (int64_t)DCOR_BLOCK * SUBG_UNR;
+    auto uterm = [&](double2 v, double l) {
+      const double Uc = rclip((v.x + c.bs * l) * v.y, c.lr);
+      ks_acc(sU, Uc);
+      ks_acc(sU2, Uc * Uc);
+    };
+    int64_t i = tid;
+    for (; i + (SUBG_UNR - 1) * DCOR_BLOCK < c.n; i += step) {
+      double l[SUBG_UNR];
+      double2 v[SUBG_UNR];
+#pragma unroll
+      for (int u = 0; u < SUBG_UNR; ++u) { l[u] = ll[i + u * DCOR_BLOCK]; v[u] = so[i + u * DCOR_BLOCK]; }
+#pragma unroll
+      for (int u = 0; u < SUBG_UNR; ++u) uterm(v[u], l[u]);
+    }
+    for (; i < c.n; i += DCOR_BLOCK) uterm(so[i], ll[i]);
+    const int32_t* __restrict__ pm = p.perm + rep * (c.k * c.m);
+    int64_t j = tid;
+    for (; j + (SUBG_UNR - 1) * DCOR_BLOCK < c.k; j += step) {
+      int2 pr[SUBG_UNR];
+      double ax[SUBG_UNR], ay[SUBG_UNR];
+#pragma unroll
+      for (int u = 0; u < SUBG_UNR; ++u) {
+        const int64_t jj = j + u * DCOR_BLOCK;
+        pr[u] = *reinterpret_cast<const int2*>(pm + 2 * jj);
+        ax[u] = lx[jj]; ay[u] = ly[jj];
+      }
+#pragma unroll
+      for (int u = 0; u < SUBG_UNR; ++u) {
+        const double2 a = xy[pr[u].x], b = xy[pr[u].y];
+        batch_term(ax[u], ay[u], two_sum(a.x, b.x), two_sum(a.y, b.y));
+      }
+    }
+    for (; j < c.k; j += DCOR_BLOCK) {
+      const double2 a = xy[pm[2 * j]], b = xy[pm[2 * j + 1]];
+      batch_term(lx[j], ly[j], two_sum(a.x, b.x), two_sum(a.y, b.y));
+    }
+  } else if (p.perm == nullptr) {
     // contiguous batches: each element read once by its batch owner (NI + INT)
     for (int64_t j = tid; j < c.k; j += DCOR_BLOCK) {
       DD bx{0, 0}, by{0, 0};
       const int64_t i0 = j * c.m;
       for (int r = 0; r < c.m; ++r) {
         const int64_t i = i0 + r;
-        dd_acc(bx, rclip(X[i], c.l1));
-        dd_acc(by, rclip(Y[i], c.l2));
-        int_term(i);
+        const double xv = X[i], yv = Y[i];
+        dd_acc(bx, rclip(xv, c.l1));
+        dd_acc(by, rclip(yv, c.l2));
+        int_term(c.sender_is_X ? xv : yv, c.sender_is_X ? yv : xv, ll[i]);
       }
-      batch_term(j, bx, by);
+      batch_term(lx[j], ly[j], bx, by);
     }
-    for (int64_t i = c.k * c.m + tid; i < c.n; i += DCOR_BLOCK) int_term(i);
+    for (int64_t i = c.k * c.m + tid; i < c.n; i += DCOR_BLOCK) int_term(S[i], O[i], ll[i]);
   } else {
-    // HRS: random batches idx = sample.int(n, k*m) (real-data-sims.R:131)
-    const int32_t* pm = p.perm + rep * (c.k * c.m);
-    for (int64_t i = tid; i < c.n; i += DCOR_BLOCK) int_term(i);
-    for (int64_t j = tid; j < c.k; j += DCOR_BLOCK) {
-      DD bx{0, 0}, by{0, 0};
-      for (int r = 0; r < c.m; ++r) {
-        const int64_t i = pm[j * c.m + r];
-        dd_acc(bx, rclip(X[i], c.l1));
-        dd_acc(by, rclip(Y[i], c.l2));
+    // HRS: random batches idx = sample.int(n, k*m) (real-data-sims.R:131).
+    // INT over all n: UNR coalesced loads in flight per thread.
+    const int64_t step = (int64_t)DCOR_BLOCK * SUBG_UNR;
+    int64_t i = tid;
+    for (; i + (SUBG_UNR - 1) * DCOR_BLOCK < c.n; i += step) {
+      double l[SUBG_UNR], sv[SUBG_UNR], ov[SUBG_UNR];
+#pragma unroll
+      for (int u = 0; u < SUBG_UNR; ++u) {
+        l[u] = ll[i + u * DCOR_BLOCK];
+        sv[u] = S[i + u * DCOR_BLOCK];
+        ov[u] = O[i + u * DCOR_BLOCK];
       }
-      batch_term(j, bx, by);
+#pragma unroll
+      for (int u = 0; u < SUBG_UNR; ++u) int_term(sv[u], ov[u], l[u]);
+    }
+    for (; i < c.n; i += DCOR_BLOCK) int_term(S[i], O[i], ll[i]);
+    // NI over batches: perm rows gathered from the (cache-resident) panel.
+    const int32_t* __restrict__ pm = p.perm + rep * (c.k * c.m);
+    if (c.m == 2) {
+      int64_t j = tid;
+      for (; j + (SUBG_UNR - 1) * DCOR_BLOCK < c.k; j += step) {
+        int32_t i0[SUBG_UNR], i1[SUBG_UNR];
+        double ax[SUBG_UNR], ay[SUBG_UNR];
+#pragma unroll
+        for (int u = 0; u < SUBG_UNR; ++u) {
+          const int64_t jj = j + u * DCOR_BLOCK;
+          const int2 pr = *reinterpret_cast<const int2*>(pm + 2 * jj);
+          i0[u] = pr.x; i1[u] = pr.y;
+          ax[u] = lx[jj]; ay[u] = ly[jj];
+        }
+#pragma unroll
+        for (int u = 0; u < SUBG_UNR; ++u) {
+          const DD bx = two_sum(rclip(X[i0[u]], c.l1), rclip(X[i1[u]], c.l1));
+          const DD by = two_sum(rclip(Y[i0[u]], c.l2), rclip(Y[i1[u]], c.l2));
+          batch_term(ax[u], ay[u], bx, by);
+        }
+      }
+      for (; j < c.k; j += DCOR_BLOCK) {
+        const DD bx = two_sum(rclip(X[pm[2 * j]], c.l1), rclip(X[pm[2 * j + 1]], c.l1));
+        const DD by = two_sum(rclip(Y[pm[2 * j]], c.l2), rclip(Y[pm[2 * j + 1]], c.l2));
+        batch_term(lx[j], ly[j], bx, by);
+      }
+    } else {
+      for (int64_t j = tid; j < c.k; j += DCOR_BLOCK) {
+        DD bx{0, 0}, by{0, 0};
+        for (int r = 0; r < c.m; ++r) {
+          const int64_t ii = pm[j * c.m + r];
+          dd_acc(bx, rclip(X[ii], c.l1));
+          dd_acc(by, rclip(Y[ii], c.l2));
+        }
+        batch_term(lx[j], ly[j], bx, by);
+      }
     }
   }
   DD d5[5] = {sP, sT, sT2, sU, sU2};
   block_sum_dd<5>(d5, red);
+  if (tid == 0) {
+    SubgPartial q;
+#pragma unroll
+    for (int v = 0; v < 5; ++v) { q.s[2 * v] = d5[v].hi; q.s[2 * v + 1] = d5[v].lo; }
+    part[rep] = q;
+  }
+}
+
+// Epilogue: NI result, INT estimate, mixquant, INT CI (ver-cor-subG.R:51-59, 91-103;
+// real-data-sims.R:233-243).
+__global__ __launch_bounds__(DCOR_BLOCK) void k_premat_subg_epilogue(PrematSubgConst p,
+                                                                     const SubgPartial* __restrict__ part,
+                                                                     dcor_rep_out* out) {
+  __shared__ SelScratch sel;
+  const SubgConst& c = p.s;
+  const int64_t rep = blockIdx.x;
+  const SubgPartial q = part[rep];
+  DD d5[5];
+#pragma unroll
+  for (int v = 0; v < 5; ++v) d5[v] = two_sum(q.s[2 * v], q.s[2 * v + 1]);
   double o[6];
   ni_subg_result(c, d5[0], d5[1], d5[2], o);
   const DD mU = dd_div_d(d5[3], c.nd);
@@ -191,24 +315,21 @@ __global__ __launch_bounds__(DCOR_BLOCK) void k_premat_subg(PrematSubgConst p, d
   if (!p.hrs) {
     const double se_norm = sqrt(sd * sd + c.sn2x2);
     const double cstar = 2.0 / (c.sqrt_n * sd * c.eps_r);
-    const double q = mixquant_loaded(c.mix, cstar, p.mix_z + rep * c.mix.nsim,
-                                     p.mix_l + rep * c.mix.nsim, keys, &nan_cnt);
-    width = q * se_norm / c.sqrt_n;
+    const double qq = mixquant_loaded(c.mix, cstar, p.mix_z + rep * c.mix.nsim,
+                                      p.mix_l + rep * c.mix.nsim, &sel);
+    width = qq * se_norm / c.sqrt_n;
   } else if (sd == 0.0) {
     width = p.crit_sqrt2_s;
   } else {
     const double cstar = (2.0 * c.lr) / (c.sqrt_n * sd * c.eps_r);
-    const double q = mixquant_loaded(c.mix, cstar, p.mix_z + rep * c.mix.nsim,
-                                     p.mix_l + rep * c.mix.nsim, keys, &nan_cnt);
-    width = q * (sd / c.sqrt_n);
+    const double qq = mixquant_loaded(c.mix, cstar, p.mix_z + rep * c.mix.nsim,
+                                      p.mix_l + rep * c.mix.nsim, &sel);
+    width = qq * (sd / c.sqrt_n);
   }
   o[3] = rho;
   o[4] = rmax(rho - width, -1.0);
   o[5] = rmin(rho + width, 1.0);
-  if (tid == 0) {
-    dcor_rep_out r{o[0], o[1], o[2], o[3], o[4], o[5]};
-    out[rep] = r;
-  }
+  if (threadIdx.x == 0) out[rep] = dcor_rep_out{o[0], o[1], o[2], o[3], o[4], o[5]};
 }
 
 // ======================================================== accumulation ===
@@ -261,9 +382,8 @@ __global__ __launch_bounds__(DCOR_BLOCK) void k_accumulate(const dcor_rep_out* r
 // ================================================== single-call helpers ===
 __global__ __launch_bounds__(DCOR_BLOCK) void k_mixquant(const double* z, const double* l,
                                                          MixConst mx, double c, double* out) {
-  __shared__ double keys[MIX_MAX];
-  __shared__ int nan_cnt;
-  const double q = mixquant_loaded(mx, c, z, l, keys, &nan_cnt);
+  __shared__ SelScratch sel;
+  const double q = mixquant_loaded(mx, c, z, l, &sel);
   if (threadIdx.x == 0) *out = q;
 }
 
@@ -336,6 +456,44 @@ __global__ __launch_bounds__(DCOR_BLOCK) void k_draws(int kind, uint32_t k0, uin
   }
 }
 
+// ========================================================== permutation ===
+// Keyed pseudo-random permutation of [0, n): a 4-round balanced Feistel network on
+// 2b >= ceil(log2 n) bits, cycle-walked into [0, n).  out[r][t] = P_r(t), t < count, is
+// a random ordered subset of size `count` -- the role of sample.int(n, k*m)
+// (real-data-sims.R:131) for the HRS random batches.  Round keys: Philox block
+// (0, rep, site, 0).  Restated in oracle/ (orc_perm) for bit-exact tests.
+__device__ __forceinline__ uint32_t feistel_f(uint32_t r, uint32_t k, uint32_t mask) {
+  uint32_t t = (r + k) * 0xCC9E2D51u;
+  t ^= t >> 15;
+  t *= 0x1B873593u;
+  t ^= t >> 13;
+  return t & mask;
+}
+
+__device__ __forceinline__ uint32_t feistel_perm(uint32_t x, uint32_t n, int b, const U4& kk) {
+  const uint32_t mask = (1u << b) - 1u;
+  do {
+    uint32_t L = x >> b, R = x & mask;
+    uint32_t t;
+    t = L ^ feistel_f(R, kk.w0, mask); L = R; R = t;
+    t = L ^ feistel_f(R, kk.w1, mask); L = R; R = t;
+    t = L ^ feistel_f(R, kk.w2, mask); L = R; R = t;
+    t = L ^ feistel_f(R, kk.w3, mask); L = R; R = t;
+    x = (L << b) | R;
+  } while (x >= n);
+  return x;
+}
+
+__global__ __launch_bounds__(DCOR_BLOCK) void k_perm(uint32_t k0, uint32_t k1, uint32_t site,
+                                                     int64_t rep_begin, uint32_t n, int b,
+                                                     int64_t count, int32_t* out) {
+  const int64_t r = blockIdx.y;
+  const U4 kk = draw(0u, (uint32_t)(rep_begin + r), site, k0, k1);
+  for (int64_t t = (int64_t)blockIdx.x * DCOR_BLOCK + threadIdx.x; t < count;
+       t += (int64_t)gridDim.x * DCOR_BLOCK)
+    out[r * count + t] = (int32_t)feistel_perm((uint32_t)t, n, b, kk);
+}
+
 // ============================================================ launchers ===
 static inline int last_err() { return (int)hipGetLastError(); }
 
@@ -345,10 +503,17 @@ int launch_premat_sign(const PrematSignConst& c, int64_t reps, dcor_rep_out* out
                      (hipStream_t)stream, c, out);
   return last_err();
 }
-int launch_premat_subg(const PrematSubgConst& c, int64_t reps, dcor_rep_out* out, void* stream) {
+int launch_premat_subg(const PrematSubgConst& c, int64_t reps, void* part, dcor_rep_out* out,
+                       void* stream) {
   if (reps <= 0) return 0;
-  hipLaunchKernelGGL(k_premat_subg, dim3((unsigned)reps), dim3(DCOR_BLOCK), 0,
-                     (hipStream_t)stream, c, out);
+  if (c.xyc != nullptr)
+    hipLaunchKernelGGL(k_premat_xy_pack, dim3((unsigned)((c.s.n + DCOR_BLOCK - 1) / DCOR_BLOCK)),
+                       dim3(DCOR_BLOCK), 0, (hipStream_t)stream, c, (double2*)c.xyc,
+                       (double2*)c.soc);
+  hipLaunchKernelGGL(k_premat_subg_stream, dim3((unsigned)reps), dim3(DCOR_BLOCK), 0,
+                     (hipStream_t)stream, c, (SubgPartial*)part);
+  hipLaunchKernelGGL(k_premat_subg_epilogue, dim3((unsigned)reps), dim3(DCOR_BLOCK), 0,
+                     (hipStream_t)stream, c, (const SubgPartial*)part, out);
   return last_err();
 }
 int launch_accumulate(const dcor_rep_out* d_out, int64_t count, double rho, dcor_accum* acc,
@@ -381,6 +546,18 @@ int launch_draws(int kind, uint32_t k0, uint32_t k1, uint32_t site, int64_t rep_
   if (gx > 4096) gx = 4096;
   hipLaunchKernelGGL(k_draws, dim3((unsigned)gx, (unsigned)reps), dim3(DCOR_BLOCK), 0,
                      (hipStream_t)stream, kind, k0, k1, site, rep_begin, count, out);
+  return last_err();
+}
+int launch_perm(uint32_t k0, uint32_t k1, uint32_t site, int64_t rep_begin, int64_t reps,
+                int64_t n, int64_t count, int32_t* out, void* stream) {
+  if (reps <= 0 || count <= 0) return 0;
+  int bits = 1;
+  while ((1ll << bits) < n) ++bits;
+  const int b = (bits + 1) / 2;
+  int64_t gx = (count + DCOR_BLOCK - 1) / DCOR_BLOCK;
+  if (gx > 4096) gx = 4096;
+  hipLaunchKernelGGL(k_perm, dim3((unsigned)gx, (unsigned)reps), dim3(DCOR_BLOCK), 0,
+                     (hipStream_t)stream, k0, k1, site, rep_begin, (uint32_t)n, b, count, out);
   return last_err();
 }
 int launch_dp_sd(const double* x, int64_t n, double lo, double hi, double s_mu, double s_m2,

@@ -16,7 +16,7 @@ DCOR_OK, DCOR_EINVAL, DCOR_EKLT1, DCOR_EHIP, DCOR_ENOMEM, DCOR_ENODEV = 0, 1, 2,
 FAMILY_SIGN, FAMILY_SUBG = 0, 1
 DGP_GAUSSIAN, DGP_BERNOULLI, DGP_BOUNDED_FACTOR = 0, 1, 2
 MODE_AUTO, MODE_NORMAL, MODE_LAPLACE = 0, 1, 2
-SITE_DGP_A, SITE_DGP_B, SITE_FLIP, SITE_NI_LAP, SITE_SCALAR, SITE_MIX_Z, SITE_MIX_L = 1, 2, 3, 4, 5, 6, 7
+SITE_DGP_A, SITE_DGP_B, SITE_FLIP, SITE_NI_LAP, SITE_SCALAR, SITE_MIX_Z, SITE_MIX_L, SITE_PERM = 1, 2, 3, 4, 5, 6, 7, 8
 
 _MODES = {"auto": MODE_AUTO, "normal": MODE_NORMAL, "laplace": MODE_LAPLACE}
 
@@ -124,6 +124,8 @@ SIGNATURES = {
     "dcor_priv_standardize": (C.c_int, [_D, C.c_int64, C.c_double, C.c_double, _D, _D]),
     "dcor_draws_launch": (C.c_int, [C.c_int, C.c_uint64, C.c_int, C.c_int64, C.c_int64, C.c_int64,
                                     _P, _P]),
+    "dcor_perm_launch": (C.c_int, [C.c_uint64, C.c_int, C.c_int64, C.c_int64, C.c_int64, C.c_int64,
+                                   _P, _P]),
     "dcor_dp_sd": (C.c_int, [_D, C.c_int64, C.c_double, C.c_double, C.c_double, C.c_double, _D, _D]),
 }
 

@@ -90,7 +90,9 @@ int dcor_last_error(char* buf, size_t len);
 /* Number of visible HIP devices (0 on a host without GPU; never fails). */
 int dcor_device_count(void);
 /* Release the library-owned per-device scratch arenas (the one-pass sign kernel keeps a
- * grid x n x 4 B slab of per-sample codes).  Safe to call at any time from the host. */
+ * chunk x n x 4 B slab of per-sample codes, reused by every dcor_sim_launch on that
+ * device: launches on different streams of one device must be ordered by the caller).
+ * Safe to call at any time from the host. */
 int dcor_shutdown(void);
 
 /* ---- calibration scalars (host closed forms) ----------------------------- */
@@ -216,6 +218,13 @@ int dcor_dp_sd(const double* x, int64_t n, double lo, double hi, double eps1, do
 int dcor_draws_launch(int kind, uint64_t seed, int site, int64_t rep_begin, int64_t reps,
                       int64_t count, double* d_out, void* stream);
 
+/* On-device keyed random batches for the HRS NI estimator: d_out[r][t] = P_r(t), t < count,
+ * where P_r is a pseudo-random permutation of [0, n) (4-round Feistel, cycle-walked, keyed by
+ * Philox block (0, rep_begin + r, site, 0)) -- the role of sample.int(n, k*m) 0-based
+ * (real-data-sims.R:131).  d_out: [reps][count] int32. */
+int dcor_perm_launch(uint64_t seed, int site, int64_t rep_begin, int64_t reps, int64_t n,
+                     int64_t count, int32_t* d_out, void* stream);
+
 /* Draw-site contract of the fused engine (DESIGN.md "RNG"): Philox4x32-10 with
  * key = (seed lo32, seed hi32), counter = (index, rep, site, 0). */
 enum {
@@ -225,7 +234,8 @@ enum {
   DCOR_SITE_NI_LAP = 4,  /* batch j: Laplace X (w0,w1), Y (w2,w3)                  */
   DCOR_SITE_SCALAR = 5,  /* blocks 0..4: NI mu/m2 X, NI mu/m2 Y, INT mu/m2 X, INT mu/m2 Y, Z */
   DCOR_SITE_MIX_Z = 6,   /* mixquant normals, 2 per block                         */
-  DCOR_SITE_MIX_L = 7    /* mixquant unit Laplace, 2 per block                    */
+  DCOR_SITE_MIX_L = 7,   /* mixquant unit Laplace, 2 per block                    */
+  DCOR_SITE_PERM = 8     /* HRS random-batch permutation keys (dcor_perm_launch)  */
 };
 
 #ifdef __cplusplus

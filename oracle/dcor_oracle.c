@@ -711,3 +711,35 @@ int orc_sim_reps(const void* cell, int64_t r0, int64_t r1, int threads, double* 
   }
   return st;
 }
+
+/* ---------------------------------------------- keyed permutation (HRS) --- */
+static uint32_t orc_feistel_f(uint32_t r, uint32_t k, uint32_t mask) {
+  uint32_t t = (r + k) * 0xCC9E2D51u;
+  t ^= t >> 15;
+  t *= 0x1B873593u;
+  t ^= t >> 13;
+  return t & mask;
+}
+
+void orc_perm(uint64_t seed, int site, int64_t rep, int64_t n, int64_t count, int32_t* out) {
+  /* 4-round balanced Feistel on 2b >= ceil(log2 n) bits, cycle-walked into [0, n). */
+  int bits = 1;
+  while ((1ll << bits) < n) ++bits;
+  const int b = (bits + 1) / 2;
+  const uint32_t mask = (1u << b) - 1u;
+  uint32_t kk[4];
+  blk(seed, 0u, (uint32_t)rep, (uint32_t)site, kk);
+  for (int64_t t = 0; t < count; ++t) {
+    uint32_t x = (uint32_t)t;
+    do {
+      uint32_t L = x >> b, R = x & mask;
+      for (int q = 0; q < 4; ++q) {
+        const uint32_t nt = L ^ orc_feistel_f(R, kk[q], mask);
+        L = R;
+        R = nt;
+      }
+      x = (L << b) | R;
+    } while (x >= (uint32_t)n);
+    out[t] = (int32_t)x;
+  }
+}

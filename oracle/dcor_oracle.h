@@ -123,6 +123,9 @@ int orc_sim_reps(const void* cell, int64_t r0, int64_t r1, int threads, double* 
 void orc_gen_normals(uint64_t seed, int64_t rep, int site, int64_t count, double* z);
 void orc_gen_laplace(uint64_t seed, int64_t rep, int site, int64_t count, double* l);
 
+/* Keyed pseudo-random permutation of [0, n) (the engine's dcor_perm_launch). */
+void orc_perm(uint64_t seed, int site, int64_t rep, int64_t n, int64_t count, int32_t* out);
+
 #ifdef __cplusplus
 }
 #endif

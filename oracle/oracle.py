@@ -61,6 +61,7 @@ _sigs = {
     "orc_sim_reps": (C.c_int, [C.c_void_p, C.c_int64, C.c_int64, C.c_int, _D]),
     "orc_gen_normals": (None, [C.c_uint64, C.c_int64, C.c_int, C.c_int64, _D]),
     "orc_gen_laplace": (None, [C.c_uint64, C.c_int64, C.c_int, C.c_int64, _D]),
+    "orc_perm": (None, [C.c_uint64, C.c_int, C.c_int64, C.c_int64, C.c_int64, _I32]),
 }
 for _n, (_r, _a) in _sigs.items():
     _f = getattr(lib, _n)
@@ -210,4 +211,10 @@ def sim_reps(cell_struct, r0, r1, threads=1):
                           out.ctypes.data_as(_D))
     if st:
         raise RuntimeError(f"oracle status {st}")
+    return out
+
+
+def perm(seed, site, rep, n, count):
+    out = np.zeros(count, dtype=np.int32)
+    lib.orc_perm(seed, site, rep, n, count, out.ctypes.data_as(_I32))
     return out

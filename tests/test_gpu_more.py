@@ -290,3 +290,19 @@ def test_mc_coverage_vs_independent_restatement(dc):
         p = (p1 * B + p2 * Bn) / (B + Bn)
         z = (p1 - p2) / math.sqrt(p * (1 - p) * (1 / B + 1 / Bn))
         assert abs(z) < 4.5, (j, p1, p2, z)
+
+
+def test_perm_bitexact_and_valid(dc, orc):
+    """dcor_perm_launch (HRS random batches) equals the oracle's restatement and is an
+    ordered sample without replacement."""
+    import torch
+    from dcor import _lib
+    n, count, reps = 19433, 19432, 3
+    out = torch.empty((reps, count), dtype=torch.int32, device="cuda")
+    _lib.check(_lib.lib.dcor_perm_launch(322, _lib.SITE_PERM, 7, reps, n, count,
+                                         C.c_void_p(out.data_ptr()), None))
+    got = out.cpu().numpy()
+    for r in range(reps):
+        ref = orc.perm(322, _lib.SITE_PERM, 7 + r, n, count)
+        assert np.array_equal(got[r], ref)
+        assert len(np.unique(got[r])) == count and got[r].min() >= 0 and got[r].max() < n
