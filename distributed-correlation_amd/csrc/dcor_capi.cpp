@@ -377,7 +377,20 @@ int dcor_sim_launch(const dcor_cell* cell, int64_t rep_begin, int64_t rep_count,
     code_map(cy, ry, 32768.0, &k.cbase_y, &k.cinv_y);
     const char* var = std::getenv("DCOR_SIGN_KERNEL");
     const bool regen = (var && std::strcmp(var, "regen") == 0) || !c.normalise;
-    if (regen || rep_count == 0) {
+    if (c.dgp == DCOR_DGP_BERNOULLI && !(var && std::strcmp(var, "regen") == 0) && rep_count > 0) {
+      // two-valued samples: bit-plane kernel (normalise = TRUE or FALSE)
+      const size_t per_rep = (size_t)3 * 4 * (size_t)((c.n + 255) / 256) * sizeof(uint64_t) + 64;
+      size_t budget = (size_t)1 << 30;
+      if (budget < 2048 * per_rep) budget = 2048 * per_rep;
+      int64_t chunk = (int64_t)(budget / per_rep);
+      if (chunk < 1) chunk = 1;
+      if (chunk > rep_count) chunk = rep_count;
+      const size_t plane_bytes = ((size_t)chunk * (per_rep - 64) + 255) / 256 * 256;
+      void* scratch = nullptr;
+      if (int st = arena_get(plane_bytes + (size_t)chunk * 64, &scratch)) return st;
+      rc = launch_sign_bern(k, rep_count, chunk, (uint64_t*)scratch,
+                            (SignPartial*)((char*)scratch + plane_bytes), d_out, stream);
+    } else if (regen || rep_count == 0) {
       rc = launch_sign_fused(k, rep_count, d_out, stream);
     } else {
       // scratch budget: >= 1 GiB and >= 2048 replicates' codes, <= 8 GiB

@@ -90,6 +90,11 @@ int launch_sign_fused(const SignConst& c, int64_t reps, dcor_rep_out* out, void*
 // One-pass sign algorithm: pass-1 / pass-2 kernels over replicate chunks of `chunk`;
 // scratch = chunk * n * 4 B of codes; sums = chunk * 4 doubles followed by chunk
 // SignPartial records (48 B).
+// Bernoulli sign family (bit planes): scratch = chunk * 3 * 4*ceil(n/256) u64, part = chunk
+// SignPartial records (48 B each).
+struct SignPartial;
+int launch_sign_bern(SignConst c, int64_t reps, int64_t chunk, uint64_t* scratch,
+                     SignPartial* part, dcor_rep_out* out, void* stream);
 int launch_sign_fused_codes(const SignConst& c, int64_t reps, int64_t chunk, uint32_t* scratch,
                             double* sums, dcor_rep_out* out, void* stream);
 int launch_subg_fused(const SubgConst& c, int64_t reps, dcor_rep_out* out, void* stream);

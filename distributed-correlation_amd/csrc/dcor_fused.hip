@@ -386,6 +386,176 @@ __global__ __launch_bounds__(DCOR_BLOCK) void k_sign_epilogue(SignConst c,
               (p.flags & 2) != 0, lap, &sel, out + blockIdx.x);
 }
 
+// ================================ Bernoulli sign family: bit planes (hot, exact) ===
+// gen_bernoulli (vert-cor.R:78-98) yields X, Y in {0, 1}, so clip(X) takes two values and
+// every sign is one of two per threshold: s0 = sign((clip(0) - mu)/sd), s1 = sign((clip(1)
+// - mu)/sd) (vert-cor.R:343-347), evaluated once per replicate with the exact rule.  The
+// replicate reduces to counts: pass A generates each sample once into three bit planes
+// (X, Y, flip) in a per-replicate slab (0.375 B/sample) and popcounts the INT combination
+// totals; pass B gives each NI batch its popcounts (vert-cor.R:226-229).  Results equal
+// the per-sample algorithm's exactly.  One kernel per replicate chunk, then the epilogue.
+// Plane word w covers samples [64w, 64w + 64); a wave's 256-sample chunk is 4 words, built
+// from 12 ballots (lane l holds samples 4l..4l+3) by a 4-way bit interleave on the SALU.
+__device__ __forceinline__ uint64_t part1by3(uint64_t x) {
+  x &= 0xFFFFull;
+  x = (x ^ (x << 24)) & 0x000000FF000000FFull;
+  x = (x ^ (x << 12)) & 0x000F000F000F000Full;
+  x = (x ^ (x << 6)) & 0x0303030303030303ull;
+  x = (x ^ (x << 3)) & 0x1111111111111111ull;
+  return x;
+}
+__device__ __forceinline__ uint64_t interleave4(const uint64_t (&b)[4], int q) {
+  const int sh = 16 * q;
+  return part1by3(b[0] >> sh) | (part1by3(b[1] >> sh) << 1) | (part1by3(b[2] >> sh) << 2) |
+         (part1by3(b[3] >> sh) << 3);
+}
+
+__global__ __launch_bounds__(DCOR_BLOCK) void k_sign_bern(SignConst c, uint64_t* __restrict__ scratch,
+                                                          SignPartial* __restrict__ part) {
+  __shared__ double red[16 * DCOR_WAVES];
+  __shared__ long long redi[8 * DCOR_WAVES];
+  __shared__ double lap[10];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const uint32_t rep = (uint32_t)(c.rep_begin + blockIdx.x);
+  const int64_t nw = 4 * ((c.n + 255) / 256);  // plane words per replicate
+  uint64_t* planes = scratch + (size_t)blockIdx.x * 3 * (size_t)nw;
+  scalar_laplace(rep, c.k0, c.k1, lap);
+  // ---- pass A: generate, ballot into plane words, count (wave-uniform counters)
+  long long n1x = 0, n1y = 0, n11 = 0, fx = 0, fy = 0, f11 = 0, ft = 0;
+  const int64_t ngrp = (c.n + 3) / 4;
+  const int64_t ngrp_pad = (ngrp + DCOR_BLOCK - 1) / DCOR_BLOCK * DCOR_BLOCK;
+  for (int64_t g4 = tid; g4 < ngrp_pad; g4 += DCOR_BLOCK) {  // whole waves stay converged
+    uint32_t xb = 0, yb = 0, fb = 0;
+    if (g4 < ngrp) {
+      const uint32_t i0 = (uint32_t)(4 * g4);
+      const U4 a = draw(i0 >> 1, rep, DCOR_SITE_DGP_A, c.k0, c.k1);
+      const U4 b = draw((i0 >> 1) + 1, rep, DCOR_SITE_DGP_A, c.k0, c.k1);
+      const U4 fw = draw((uint32_t)g4, rep, DCOR_SITE_FLIP, c.k0, c.k1);
+      const uint32_t wa[4] = {a.w0, a.w2, b.w0, b.w2}, wb[4] = {a.w1, a.w3, b.w1, b.w3};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        if ((int64_t)i0 + q < c.n) {
+          const bool x1 = wa[q] < 0x80000000u;  // Dgp<BERNOULLI>::from_words
+          const bool y1 = (uint64_t)wb[q] < (x1 ? c.g.T1 : c.g.T0);
+          xb |= (uint32_t)x1 << q;
+          yb |= (uint32_t)y1 << q;
+          fb |= (uint32_t)((uint64_t)word(fw, q) < c.flipT) << q;
+        }
+      }
+    }
+    uint64_t BX[4], BY[4], BF[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      BX[q] = __ballot((xb >> q) & 1u);
+      BY[q] = __ballot((yb >> q) & 1u);
+      BF[q] = __ballot((fb >> q) & 1u);
+      n1x += __popcll(BX[q]);
+      n1y += __popcll(BY[q]);
+      n11 += __popcll(BX[q] & BY[q]);
+      fx += __popcll(BF[q] & BX[q]);
+      fy += __popcll(BF[q] & BY[q]);
+      f11 += __popcll(BF[q] & BX[q] & BY[q]);
+      ft += __popcll(BF[q]);
+    }
+    const int64_t w0 = (g4 - lane) / 16;  // first plane word of this wave's chunk
+    if (lane < 12 && w0 < nw) {
+      const int q = lane & 3, pl = lane >> 2;
+      const uint64_t v = pl == 0 ? interleave4(BX, q) : (pl == 1 ? interleave4(BY, q) : interleave4(BF, q));
+      planes[(size_t)pl * nw + w0 + q] = v;
+    }
+  }
+  // block totals (one lane per wave contributes its wave-uniform counters)
+  long long cnt[7] = {n1x, n1y, n11, fx, fy, f11, ft};
+  if (lane == 0) {
+#pragma unroll
+    for (int q = 0; q < 7; ++q) redi[8 * (tid >> 6) + q] = cnt[q];
+  }
+  __syncthreads();  // also orders the plane stores before pass B (workgroup scope)
+#pragma unroll
+  for (int q = 0; q < 7; ++q) {
+    long long t = 0;
+#pragma unroll
+    for (int w = 0; w < DCOR_WAVES; ++w) t += redi[8 * w + q];
+    cnt[q] = t;
+  }
+  const long long N1x = cnt[0], N1y = cnt[1], N11 = cnt[2], Fx = cnt[3], Fy = cnt[4],
+                  F11 = cnt[5], Ft = cnt[6];
+  // ---- thresholds (vert-cor.R:322-348) and the two signs per threshold
+  const double c0 = rclip_fin(0.0, c.L), c1 = rclip_fin(1.0, c.L);
+  bool bad_ni = false, bad_int = false;
+  int sN0x, sN1x, sN0y, sN1y, sI0x, sI1x, sI0y, sI1y;
+  bool bN0x = false, bN1x = false, bN0y = false, bN1y = false;
+  bool bI0x = false, bI1x = false, bI0y = false, bI1y = false;
+  if (c.normalise) {
+    const double nd = c.nd;
+    const double n0x = nd - (double)N1x, n0y = nd - (double)N1y;
+    double v[4];
+    v[0] = (double)N1x * c1 + n0x * c0;
+    v[1] = (double)N1x * (c1 * c1) + n0x * (c0 * c0);
+    v[2] = (double)N1y * c1 + n0y * c0;
+    v[3] = (double)N1y * (c1 * c1) + n0y * (c0 * c0);
+    double l8[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) l8[q] = lap[q];
+    SignStd st;
+    priv_std_from_sums(c, v, l8, st);
+    const bool thr_nan = (st.muNx != st.muNx) || (st.muNy != st.muNy) || (st.muIx != st.muIx) ||
+                         (st.muIy != st.muIy) || (st.sdNx != st.sdNx) || (st.sdNy != st.sdNy) ||
+                         (st.sdIx != st.sdIx) || (st.sdIy != st.sdIy);
+    bad_ni = bad_int = thr_nan;
+    sN0x = sgn_std(c0, st.muNx, st.sdNx, bN0x); sN1x = sgn_std(c1, st.muNx, st.sdNx, bN1x);
+    sN0y = sgn_std(c0, st.muNy, st.sdNy, bN0y); sN1y = sgn_std(c1, st.muNy, st.sdNy, bN1y);
+    sI0x = sgn_std(c0, st.muIx, st.sdIx, bI0x); sI1x = sgn_std(c1, st.muIx, st.sdIx, bI1x);
+    sI0y = sgn_std(c0, st.muIy, st.sdIy, bI0y); sI1y = sgn_std(c1, st.muIy, st.sdIy, bI1y);
+  } else {  // signs of the raw values (vert-cor.R:172-173, 226-227)
+    sN0x = sN0y = sI0x = sI0y = 0;
+    sN1x = sN1y = sI1x = sI1y = 1;
+  }
+  // INT: sum of (2S-1) sign(X) sign(Y) from the combination counts (vert-cor.R:175-183)
+  const long long N10 = N1x - N11, N01 = N1y - N11, N00 = (long long)c.n - N1x - N1y + N11;
+  const long long F10 = Fx - F11, F01 = Fy - F11, F00 = Ft - Fx - Fy + F11;
+  const long long core = (long long)(sI1x * sI1y) * (2 * F11 - N11) +
+                         (long long)(sI1x * sI0y) * (2 * F10 - N10) +
+                         (long long)(sI0x * sI1y) * (2 * F01 - N01) +
+                         (long long)(sI0x * sI0y) * (2 * F00 - N00);
+  bad_int |= (bI1x && N1x > 0) || (bI0x && N1x < c.n) || (bI1y && N1y > 0) || (bI0y && N1y < c.n);
+  // ---- pass B: NI batches from plane popcounts (vert-cor.R:226-239)
+  const uint64_t* PX = planes;
+  const uint64_t* PY = planes + nw;
+  DD sT{0.0, 0.0}, sT2{0.0, 0.0};
+  for (int64_t j = tid; j < c.k; j += DCOR_BLOCK) {
+    const int64_t a = j * c.m, b = a + c.m;
+    const int64_t wa = a >> 6, wb = (b - 1) >> 6;
+    int cx1 = 0, cy1 = 0;
+    for (int64_t w = wa; w <= wb; ++w) {
+      uint64_t mask = ~0ull;
+      if (w == wa) mask &= ~0ull << (a & 63);
+      if (w == wb) mask &= ~0ull >> (63 - ((b - 1) & 63));
+      cx1 += __popcll(PX[w] & mask);
+      cy1 += __popcll(PY[w] & mask);
+    }
+    const int cx0 = c.m - cx1, cy0 = c.m - cy1;
+    bad_ni |= (bN1x && cx1) || (bN0x && cx0) || (bN1y && cy1) || (bN0y && cy0);
+    const int cx = sN1x * cx1 + sN0x * cx0, cy = sN1y * cy1 + sN0y * cy0;
+    const U4 w = draw((uint32_t)j, rep, DCOR_SITE_NI_LAP, c.k0, c.k1);   // vert-cor.R:230-231
+    const double xt = (double)cx / c.md + c.bx * unit_laplace(u53(w.w0, w.w1));
+    const double yt = (double)cy / c.md + c.by * unit_laplace(u53(w.w2, w.w3));
+    const double T = c.md * xt * yt;                                     // vert-cor.R:233
+    dd_acc(sT, T);
+    dd_acc(sT2, T * T);
+  }
+  DD d2[2] = {sT, sT2};
+  block_sum_dd<2>(d2, red);
+  const long long nbad = block_sum_i(bad_ni ? 1LL : 0LL, redi);
+  if (tid == 0) {
+    SignPartial p;
+    p.sT[0] = d2[0].hi; p.sT[1] = d2[0].lo; p.sT2[0] = d2[1].hi; p.sT2[1] = d2[1].lo;
+    p.core = core;
+    p.flags = (nbad ? 1 : 0) | (bad_int ? 2 : 0);
+    part[blockIdx.x] = p;
+  }
+}
+
 // ============================= fused sign family, regenerate (two-pass, A/B) ===
 // The direct two-pass algorithm: pass 2 regenerates every sample.  Used for
 // normalise = FALSE (signs against 0: pass 1 is skipped, so it is one pass) and as the
@@ -581,6 +751,22 @@ int launch_sign_fused_codes(const SignConst& c, int64_t reps, int64_t chunk, uin
     case DCOR_DGP_BERNOULLI: return launch_codes_t<DCOR_DGP_BERNOULLI>(c, reps, chunk, scratch, sums, out, stream);
     default: return launch_codes_t<DCOR_DGP_BOUNDED_FACTOR>(c, reps, chunk, scratch, sums, out, stream);
   }
+}
+
+int launch_sign_bern(SignConst c, int64_t reps, int64_t chunk, uint64_t* scratch,
+                     SignPartial* part, dcor_rep_out* out, void* stream) {
+  if (reps <= 0) return 0;
+  const int64_t rep0 = c.rep_begin;
+  for (int64_t r = 0; r < reps; r += chunk) {
+    const int64_t nr = (reps - r < chunk) ? reps - r : chunk;
+    c.rep_begin = rep0 + r;
+    hipLaunchKernelGGL(k_sign_bern, dim3((unsigned)nr), dim3(DCOR_BLOCK), 0, (hipStream_t)stream,
+                       c, scratch, part);
+    hipLaunchKernelGGL(k_sign_epilogue, dim3((unsigned)nr), dim3(DCOR_BLOCK), 0,
+                       (hipStream_t)stream, c, part, out + r);
+    if (int e = last_err()) return e;
+  }
+  return 0;
 }
 
 int launch_subg_fused(const SubgConst& c, int64_t reps, dcor_rep_out* out, void* stream) {

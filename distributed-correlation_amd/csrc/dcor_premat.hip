@@ -334,48 +334,85 @@ __global__ __launch_bounds__(DCOR_BLOCK) void k_premat_subg_epilogue(PrematSubgC
 
 // ======================================================== accumulation ===
 // Deterministic per-method summary of `count` records (one workgroup).
+// Stage 1: block b folds records [b*per, min((b+1)*per, count)) of both methods into a
+// partial accumulator pair part[2b], part[2b+1].  Stage 2 merges the partials in block
+// order (deterministic for a given count).
+__device__ __forceinline__ void acc_record(double est, double lo, double hi, double rho, DD* s,
+                                           long long* cnt) {
+  const bool nae = (est != est), nal = (lo != lo), nah = (hi != hi);
+  if (nae) ++cnt[2]; else {
+    ks_acc(s[0], est);
+    ks_acc(s[1], est * est);
+    const double e = est - rho;
+    ks_acc(s[2], e * e);
+  }
+  if (nal || nah) ++cnt[3]; else {
+    ks_acc(s[3], hi - lo);
+    ks_acc(s[4], lo);
+    ks_acc(s[5], hi);
+  }
+  // R: rho >= lo && rho <= hi with NA three-valued logic
+  const int a = nal ? 2 : (rho >= lo ? 1 : 0);
+  const int bq = nah ? 2 : (rho <= hi ? 1 : 0);
+  int cv;
+  if (a == 0) cv = 0; else if (a == 1) cv = bq; else cv = (bq == 0) ? 0 : 2;
+  if (cv == 1) ++cnt[0]; else if (cv == 2) ++cnt[1];
+}
+
+__device__ __forceinline__ void acc_write(dcor_accum* dst, int64_t n, const DD* s, const long long* t) {
+  dcor_accum a;
+  a.n = n; a.n_cover = t[0]; a.n_cover_na = t[1]; a.n_na_est = t[2]; a.n_na_ci = t[3];
+  a.reserved[0] = a.reserved[1] = a.reserved[2] = 0;
+  a.est[0] = s[0].hi; a.est[1] = s[0].lo; a.est2[0] = s[1].hi; a.est2[1] = s[1].lo;
+  a.se2[0] = s[2].hi; a.se2[1] = s[2].lo; a.len[0] = s[3].hi; a.len[1] = s[3].lo;
+  a.lo[0] = s[4].hi; a.lo[1] = s[4].lo; a.hi[0] = s[5].hi; a.hi[1] = s[5].lo;
+  *dst = a;
+}
+
 __global__ __launch_bounds__(DCOR_BLOCK) void k_accumulate(const dcor_rep_out* rec, int64_t count,
-                                                           double rho, dcor_accum* acc) {
+                                                           int64_t per, double rho,
+                                                           dcor_accum* part) {
   __shared__ double red[16 * DCOR_WAVES];
   __shared__ long long redi[DCOR_WAVES];
+  const int64_t b0 = (int64_t)blockIdx.x * per;
+  const int64_t b1 = (b0 + per < count) ? b0 + per : count;
   for (int meth = 0; meth < 2; ++meth) {
     DD s[6] = {{0, 0}, {0, 0}, {0, 0}, {0, 0}, {0, 0}, {0, 0}};
     long long cnt[4] = {0, 0, 0, 0};  // cover, cover_na, na_est, na_ci
-    for (int64_t b = threadIdx.x; b < count; b += DCOR_BLOCK) {
+    for (int64_t b = b0 + threadIdx.x; b < b1; b += DCOR_BLOCK) {
       const double* r = &rec[b].ni_hat + 3 * meth;
-      const double est = r[0], lo = r[1], hi = r[2];
-      const bool nae = (est != est), nal = (lo != lo), nah = (hi != hi);
-      if (nae) ++cnt[2]; else {
-        dd_acc(s[0], est);
-        dd_acc(s[1], est * est);
-        const double e = est - rho;
-        dd_acc(s[2], e * e);
-      }
-      if (nal || nah) ++cnt[3]; else {
-        dd_acc(s[3], hi - lo);
-        dd_acc(s[4], lo);
-        dd_acc(s[5], hi);
-      }
-      // R: rho >= lo && rho <= hi with NA three-valued logic
-      const int a = nal ? 2 : (rho >= lo ? 1 : 0);
-      const int bq = nah ? 2 : (rho <= hi ? 1 : 0);
-      int cv;
-      if (a == 0) cv = 0; else if (a == 1) cv = bq; else cv = (bq == 0) ? 0 : 2;
-      if (cv == 1) ++cnt[0]; else if (cv == 2) ++cnt[1];
+      acc_record(r[0], r[1], r[2], rho, s, cnt);
     }
     block_sum_dd<6>(s, red);
     long long tot[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) tot[q] = block_sum_i(cnt[q], redi);
-    if (threadIdx.x == 0) {
-      dcor_accum a;
-      a.n = count; a.n_cover = tot[0]; a.n_cover_na = tot[1]; a.n_na_est = tot[2]; a.n_na_ci = tot[3];
-      a.reserved[0] = a.reserved[1] = a.reserved[2] = 0;
-      a.est[0] = s[0].hi; a.est[1] = s[0].lo; a.est2[0] = s[1].hi; a.est2[1] = s[1].lo;
-      a.se2[0] = s[2].hi; a.se2[1] = s[2].lo; a.len[0] = s[3].hi; a.len[1] = s[3].lo;
-      a.lo[0] = s[4].hi; a.lo[1] = s[4].lo; a.hi[0] = s[5].hi; a.hi[1] = s[5].lo;
-      acc[meth] = a;
+    if (threadIdx.x == 0) acc_write(part + 2 * blockIdx.x + meth, b1 > b0 ? b1 - b0 : 0, s, tot);
+  }
+}
+
+__global__ __launch_bounds__(DCOR_BLOCK) void k_accumulate_merge(const dcor_accum* part, int nb,
+                                                                 int64_t count, dcor_accum* acc) {
+  __shared__ double red[16 * DCOR_WAVES];
+  __shared__ long long redi[DCOR_WAVES];
+  for (int meth = 0; meth < 2; ++meth) {
+    DD s[6] = {{0, 0}, {0, 0}, {0, 0}, {0, 0}, {0, 0}, {0, 0}};
+    long long cnt[4] = {0, 0, 0, 0};
+    for (int b = threadIdx.x; b < nb; b += DCOR_BLOCK) {
+      const dcor_accum& a = part[2 * b + meth];
+      s[0] = dd_add(s[0], DD{a.est[0], a.est[1]});
+      s[1] = dd_add(s[1], DD{a.est2[0], a.est2[1]});
+      s[2] = dd_add(s[2], DD{a.se2[0], a.se2[1]});
+      s[3] = dd_add(s[3], DD{a.len[0], a.len[1]});
+      s[4] = dd_add(s[4], DD{a.lo[0], a.lo[1]});
+      s[5] = dd_add(s[5], DD{a.hi[0], a.hi[1]});
+      cnt[0] += a.n_cover; cnt[1] += a.n_cover_na; cnt[2] += a.n_na_est; cnt[3] += a.n_na_ci;
     }
+    block_sum_dd<6>(s, red);
+    long long tot[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) tot[q] = block_sum_i(cnt[q], redi);
+    if (threadIdx.x == 0) acc_write(acc + meth, count, s, tot);
   }
 }
 
@@ -518,9 +555,26 @@ int launch_premat_subg(const PrematSubgConst& c, int64_t reps, void* part, dcor_
 }
 int launch_accumulate(const dcor_rep_out* d_out, int64_t count, double rho, dcor_accum* acc,
                       void* stream) {
-  hipLaunchKernelGGL(k_accumulate, dim3(1), dim3(DCOR_BLOCK), 0, (hipStream_t)stream, d_out,
-                     count, rho, acc);
-  return last_err();
+  // ~2048 records per block, at most 512 blocks; 1 block writes acc directly.
+  int64_t nb = (count + 2047) / 2048;
+  if (nb < 1) nb = 1;
+  if (nb > 512) nb = 512;
+  const int64_t per = (count + nb - 1) / nb > 0 ? (count + nb - 1) / nb : 1;
+  if (nb == 1) {
+    hipLaunchKernelGGL(k_accumulate, dim3(1), dim3(DCOR_BLOCK), 0, (hipStream_t)stream, d_out,
+                       count, per, rho, acc);
+    return last_err();
+  }
+  dcor_accum* part = nullptr;
+  hipError_t e = hipMallocAsync((void**)&part, (size_t)nb * 2 * sizeof(dcor_accum), (hipStream_t)stream);
+  if (e != hipSuccess) return (int)e;
+  hipLaunchKernelGGL(k_accumulate, dim3((unsigned)nb), dim3(DCOR_BLOCK), 0, (hipStream_t)stream,
+                     d_out, count, per, rho, part);
+  hipLaunchKernelGGL(k_accumulate_merge, dim3(1), dim3(DCOR_BLOCK), 0, (hipStream_t)stream, part,
+                     (int)nb, count, acc);
+  const int rc = last_err();
+  (void)hipFreeAsync(part, (hipStream_t)stream);
+  return rc;
 }
 int launch_mixquant(const double* z, const double* l, int32_t nsim, double c, int32_t pos,
                     double* out, void* stream) {

@@ -125,6 +125,42 @@ def test_fused_vs_oracle(dc, orc, spec):
     assert_close(got, ref, what=f"fused {spec}")
 
 
+# Bernoulli sign cells run the bit-plane kernel: batch sizes m = 1, 2, 8, 11, 32, 128,
+# n off the 256-sample chunk grid, normalise = FALSE, the Laplace CI mode.
+BERN_CELLS = [
+    dict(n=1000, rho=0.5, eps1=4.0, eps2=4.0),     # m = 1
+    dict(n=777, rho=0.9, eps1=2.0, eps2=2.0),      # m = 2
+    dict(n=2049, rho=0.0, eps1=1.0, eps2=1.0),     # m = 8, tail
+    dict(n=3001, rho=0.65, eps1=1.5, eps2=0.5),    # m = 11
+    dict(n=1500, rho=0.3, eps1=0.5, eps2=0.5),     # m = 32
+    dict(n=1300, rho=0.8, eps1=0.25, eps2=0.25),   # m = 128, k < 256
+    dict(n=999, rho=0.4, eps1=1.0, eps2=1.0, normalise=False),
+    dict(n=1200, rho=0.15, eps1=1.0, eps2=1.0, ci_mode="laplace"),
+]
+
+
+@pytest.mark.parametrize("spec", BERN_CELLS)
+def test_bernoulli_planes_vs_oracle(dc, orc, spec):
+    from dcor.sim import CellSpec, simulate
+    cell = CellSpec(seed=2_000_003 + spec["n"], family="sign", dgp="bernoulli", **spec)
+    got = simulate(cell, 20, rep_begin=5).cpu().numpy()
+    ref = orc.sim_reps(cell.to_c(), 5, 25)
+    assert_close(got, ref, what=f"bernoulli planes {spec}")
+
+
+@pytest.mark.parametrize("eps", [(1.0, 1.0), (1.5, 0.5), (0.5, 0.5)])
+def test_bernoulli_planes_vs_regen(dc, eps, monkeypatch):
+    """Bit-plane kernel == per-sample regenerate kernel, bit for bit (clip(1) = 1 makes
+    the DP-mean sums integers in both)."""
+    from dcor.sim import CellSpec, simulate
+    cell = CellSpec(n=30_011, rho=0.5, eps1=eps[0], eps2=eps[1], family="sign", dgp="bernoulli",
+                    seed=77)
+    a = simulate(cell, 64).cpu().numpy()
+    monkeypatch.setenv("DCOR_SIGN_KERNEL", "regen")
+    b = simulate(cell, 64).cpu().numpy()
+    assert np.array_equal(a, b, equal_nan=True)
+
+
 def test_fused_split_invariance(dc):
     """Per-replicate results do not depend on how the replicate range is split."""
     from dcor.sim import headline_cell, simulate
