@@ -54,6 +54,20 @@ def cpu_baseline(cell, seconds: float = 12.0):
                       "one core per cell)"}
 
 
+def pmc_traffic(path=os.path.join(ROOT, "profiles", "r01_headline_summary.json")):
+    """HBM bytes per simulate() call from the committed rocprofv3 PMC passes (FETCH_SIZE x2
+    for gfx950's half-count of wide reads, + WRITE_SIZE; scripts/summarize_prof.py), summed
+    over the sign kernels of one call.  None if the profile is absent."""
+    try:
+        ks = json.load(open(path))["kernels"]
+        calls = ks["dcor::k_accumulate"]["calls"]
+        tot = sum((v["hbm_read_bytes_corrected"] + v["hbm_write_bytes"]) * v["calls"]
+                  for name, v in ks.items() if "k_sign_" in name)
+        return tot / calls
+    except (OSError, KeyError, ValueError, ZeroDivisionError):
+        return None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -142,7 +156,8 @@ def main():
                        "n": cell.n, "m": m, "k": k, "replicates_per_gpu_per_step": R,
                        "parallelism": f"replicate-shard x{world}"},
             "roofline": {"bound": "valu_fp64", "achieved": achieved, "peak": FP64_PEAK_TFLOPS,
-                         "unit": "TFLOP/s", "frac": achieved / FP64_PEAK_TFLOPS, "traffic": None,
+                         "unit": "TFLOP/s", "frac": achieved / FP64_PEAK_TFLOPS, "traffic": pmc_traffic(),
+                         "traffic_unit": "B per simulate() call (rocprofv3 PMC, profiles/r01_headline_summary.json)",
                          "kernel": "k_sign_pass1 + k_sign_pass2 (one simulate() call)",
                          "kernel_ms_avg": kern_ms,
                          "work_units_per_rep": W,

@@ -164,8 +164,10 @@ def c5(R):
                         lap_local=ll.data_ptr(), lap_central=lc.data_ptr(), mix_z=mz.data_ptr(),
                         mix_l=ml.data_ptr())
     t = timed(lambda: _lib.check(_lib.lib.dcor_premat_subg_launch(C.byref(d), P(out), None)), reps=5)
-    per_rep = 4 * k * m + 16 * k + 8 * n + 8 + 16 * nsim
+    per_rep = 8 * n + 4 * k * m + 16 * k + 8 * nsim    # SURVEY §8d pinned: 404,648 B
+    read_rep = 8 * n + 4 * k * m + 16 * k + 8 + 16 * nsim  # bytes the ABI actually reads (z, l apart)
     line("C5", reps=R, seconds=t, reps_per_s=R / t, algorithmic_bytes_per_rep=per_rep,
+         input_bytes_per_rep=read_rep,
          hbm_gbps=per_rep * R / t / 1e9, hbm_frac=per_rep * R / t / HBM_PEAK,
          note="synthetic stand-in panel (n=19,433, clipped std-normal age_z, corr -0.19); "
               "noise pre-generated on device (dcor_draws_launch / dcor_perm_launch); timed = streaming kernel only")

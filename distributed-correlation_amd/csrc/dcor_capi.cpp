@@ -250,6 +250,23 @@ int make_subg(int64_t n, double eps1, double eps2, double eta1, double eta2, dou
 // library, grown on demand outside any kernel, released by dcor_shutdown().
 struct Arena { void* p = nullptr; size_t bytes = 0; };
 Arena g_arena[64];
+// per-device auxiliary stream + fork/join events of the two-stream chunk pipeline
+struct Pipe { hipStream_t s = nullptr; hipEvent_t fork = nullptr, join = nullptr; };
+Pipe g_pipe[64];
+
+int pipe_get(Pipe** out) {
+  int dev = 0;
+  HIPCHK(hipGetDevice(&dev));
+  if (dev < 0 || dev >= 64) return fail(DCOR_EINVAL, "device id out of range");
+  Pipe& p = g_pipe[dev];
+  if (!p.s) {
+    HIPCHK(hipStreamCreateWithFlags(&p.s, hipStreamNonBlocking));
+    HIPCHK(hipEventCreateWithFlags(&p.fork, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&p.join, hipEventDisableTiming));
+  }
+  *out = &p;
+  return DCOR_OK;
+}
 
 int arena_get(size_t bytes, void** out) {
   int dev = 0;
@@ -393,19 +410,36 @@ int dcor_sim_launch(const dcor_cell* cell, int64_t rep_begin, int64_t rep_count,
     } else if (regen || rep_count == 0) {
       rc = launch_sign_fused(k, rep_count, d_out, stream);
     } else {
-      // scratch budget: >= 1 GiB and >= 2048 replicates' codes, <= 8 GiB
-      const size_t per_rep = (size_t)c.n * sizeof(uint32_t) + 4 * sizeof(double) + 48;
+      // two slabs (two-stream chunk pipeline), each within a budget of >= 1 GiB and
+      // >= 2048 replicates' codes, <= 8 GiB; equal chunks (no small tail launch)
+      const size_t per_rep = (size_t)c.n * sizeof(uint32_t);
       size_t budget = (size_t)1 << 30;
       if (budget < 2048 * per_rep) budget = 2048 * per_rep;
       if (budget > ((size_t)8 << 30)) budget = (size_t)8 << 30;
-      int64_t chunk = (int64_t)(budget / per_rep);
-      if (chunk < 1) chunk = 1;
-      if (chunk > rep_count) chunk = rep_count;
+      int64_t maxchunk = (int64_t)(budget / per_rep);
+      if (maxchunk < 1) maxchunk = 1;
+      const int64_t nch = (rep_count + maxchunk - 1) / maxchunk;
+      const int64_t chunk = (rep_count + nch - 1) / nch;
+      const size_t slab_b = ((size_t)chunk * per_rep + 255) / 256 * 256;
+      const size_t sums_b = ((size_t)chunk * (4 * sizeof(double) + 48) + 255) / 256 * 256;
+      const int nbuf = nch > 1 ? 2 : 1;
       void* scratch = nullptr;
-      const size_t codes_bytes = ((size_t)chunk * (size_t)c.n * sizeof(uint32_t) + 255) / 256 * 256;
-      if (int st = arena_get(codes_bytes + (size_t)chunk * (4 * sizeof(double) + 48), &scratch)) return st;
-      rc = launch_sign_fused_codes(k, rep_count, chunk, (uint32_t*)scratch,
-                                   (double*)((char*)scratch + codes_bytes), d_out, stream);
+      if (int st = arena_get(nbuf * (slab_b + sums_b), &scratch)) return st;
+      CodesBufs bf;
+      char* base = (char*)scratch;
+      for (int b = 0; b < 2; ++b) {
+        const int bb = b < nbuf ? b : 0;
+        bf.slab[b] = (uint32_t*)(base + bb * slab_b);
+        bf.sums[b] = (double*)(base + nbuf * slab_b + bb * sums_b);
+      }
+      bf.aux = bf.ev_fork = bf.ev_join = nullptr;
+      const char* pv = std::getenv("DCOR_SIGN_PIPELINE");
+      if (nbuf == 2 && !(pv && std::strcmp(pv, "0") == 0)) {
+        Pipe* pp = nullptr;
+        if (int st = pipe_get(&pp)) return st;
+        bf.aux = pp->s; bf.ev_fork = pp->fork; bf.ev_join = pp->join;
+      }
+      rc = launch_sign_fused_codes(k, rep_count, chunk, bf, d_out, stream);
     }
   } else if (c.family == DCOR_FAMILY_SUBG) {
     SubgConst k;
@@ -749,6 +783,15 @@ int dcor_perm_launch(uint64_t seed, int site, int64_t rep_begin, int64_t reps, i
 int dcor_shutdown(void) {
   for (auto& a : g_arena) {
     if (a.p) { (void)hipFree(a.p); a.p = nullptr; a.bytes = 0; }
+  }
+  for (auto& p : g_pipe) {
+    if (p.s) {
+      (void)hipStreamSynchronize(p.s);
+      (void)hipStreamDestroy(p.s);
+      (void)hipEventDestroy(p.fork);
+      (void)hipEventDestroy(p.join);
+      p = Pipe();
+    }
   }
 
   return DCOR_OK;

@@ -95,8 +95,18 @@ int launch_sign_fused(const SignConst& c, int64_t reps, dcor_rep_out* out, void*
 struct SignPartial;
 int launch_sign_bern(SignConst c, int64_t reps, int64_t chunk, uint64_t* scratch,
                      SignPartial* part, dcor_rep_out* out, void* stream);
-int launch_sign_fused_codes(const SignConst& c, int64_t reps, int64_t chunk, uint32_t* scratch,
-                            double* sums, dcor_rep_out* out, void* stream);
+// One-pass sign engine buffers: two slabs (chunk * n * 4 B) and two sums/partials areas
+// (chunk * 80 B), an auxiliary stream and two events (fork / join) for the two-stream
+// chunk pipeline; aux == nullptr runs every chunk on the caller's stream.
+struct CodesBufs {
+  uint32_t* slab[2];
+  double* sums[2];
+  void* aux;
+  void* ev_fork;
+  void* ev_join;
+};
+int launch_sign_fused_codes(const SignConst& c, int64_t reps, int64_t chunk, const CodesBufs& bf,
+                            dcor_rep_out* out, void* stream);
 int launch_subg_fused(const SubgConst& c, int64_t reps, dcor_rep_out* out, void* stream);
 int launch_premat_sign(const PrematSignConst& c, int64_t reps, dcor_rep_out* out, void* stream);
 // part: reps * 80 B scratch (stream -> epilogue partial sums).

@@ -724,32 +724,47 @@ int launch_sign_fused(const SignConst& c, int64_t reps, dcor_rep_out* out, void*
   }
 }
 
+// Replicate chunks alternate between the caller's stream and an auxiliary stream, each
+// with its own slab, so pass 2 (memory-latency bound) of one chunk runs beside pass 1
+// (VALU bound) of the next.
 template <int DGP>
-static int launch_codes_t(SignConst c, int64_t reps, int64_t chunk, uint32_t* scratch,
-                          double* sums, dcor_rep_out* out, void* stream) {
+static int launch_codes_t(SignConst c, int64_t reps, int64_t chunk, const CodesBufs& bf,
+                          dcor_rep_out* out, void* stream) {
   const int64_t rep0 = c.rep_begin;
-  SignPartial* part = reinterpret_cast<SignPartial*>(sums + 4 * chunk);
-  for (int64_t r = 0; r < reps; r += chunk) {
+  hipStream_t st[2] = {(hipStream_t)stream, (hipStream_t)bf.aux};
+  const bool two = reps > chunk && bf.aux != nullptr;
+  if (two) {
+    if (hipEventRecord((hipEvent_t)bf.ev_fork, st[0]) != hipSuccess) return last_err();
+    if (hipStreamWaitEvent(st[1], (hipEvent_t)bf.ev_fork, 0) != hipSuccess) return last_err();
+  }
+  int64_t t = 0;
+  for (int64_t r = 0; r < reps; r += chunk, ++t) {
     const int64_t nr = (reps - r < chunk) ? reps - r : chunk;
+    const int b = two ? (int)(t & 1) : 0;
     c.rep_begin = rep0 + r;
-    hipLaunchKernelGGL(k_sign_pass1<DGP>, dim3((unsigned)nr), dim3(DCOR_BLOCK), 0,
-                       (hipStream_t)stream, c, scratch, sums);
-    hipLaunchKernelGGL(k_sign_pass2<DGP>, dim3((unsigned)nr), dim3(DCOR_BLOCK), 0,
-                       (hipStream_t)stream, c, scratch, sums, part);
-    hipLaunchKernelGGL(k_sign_epilogue, dim3((unsigned)nr), dim3(DCOR_BLOCK), 0,
-                       (hipStream_t)stream, c, part, out + r);
+    SignPartial* part = reinterpret_cast<SignPartial*>(bf.sums[b] + 4 * chunk);
+    hipLaunchKernelGGL(k_sign_pass1<DGP>, dim3((unsigned)nr), dim3(DCOR_BLOCK), 0, st[b], c,
+                       bf.slab[b], bf.sums[b]);
+    hipLaunchKernelGGL(k_sign_pass2<DGP>, dim3((unsigned)nr), dim3(DCOR_BLOCK), 0, st[b], c,
+                       bf.slab[b], bf.sums[b], part);
+    hipLaunchKernelGGL(k_sign_epilogue, dim3((unsigned)nr), dim3(DCOR_BLOCK), 0, st[b], c, part,
+                       out + r);
     if (int e = last_err()) return e;
+  }
+  if (two) {
+    if (hipEventRecord((hipEvent_t)bf.ev_join, st[1]) != hipSuccess) return last_err();
+    if (hipStreamWaitEvent(st[0], (hipEvent_t)bf.ev_join, 0) != hipSuccess) return last_err();
   }
   return 0;
 }
 
-int launch_sign_fused_codes(const SignConst& c, int64_t reps, int64_t chunk, uint32_t* scratch,
-                            double* sums, dcor_rep_out* out, void* stream) {
+int launch_sign_fused_codes(const SignConst& c, int64_t reps, int64_t chunk, const CodesBufs& bf,
+                            dcor_rep_out* out, void* stream) {
   if (reps <= 0) return 0;
   switch (c.g.dgp) {
-    case DCOR_DGP_GAUSSIAN: return launch_codes_t<DCOR_DGP_GAUSSIAN>(c, reps, chunk, scratch, sums, out, stream);
-    case DCOR_DGP_BERNOULLI: return launch_codes_t<DCOR_DGP_BERNOULLI>(c, reps, chunk, scratch, sums, out, stream);
-    default: return launch_codes_t<DCOR_DGP_BOUNDED_FACTOR>(c, reps, chunk, scratch, sums, out, stream);
+    case DCOR_DGP_GAUSSIAN: return launch_codes_t<DCOR_DGP_GAUSSIAN>(c, reps, chunk, bf, out, stream);
+    case DCOR_DGP_BERNOULLI: return launch_codes_t<DCOR_DGP_BERNOULLI>(c, reps, chunk, bf, out, stream);
+    default: return launch_codes_t<DCOR_DGP_BOUNDED_FACTOR>(c, reps, chunk, bf, out, stream);
   }
 }
 
