@@ -128,7 +128,10 @@ def c4(B):
          reps_per_s=len(ok) * B / t, roofline_frac=u / t / FP64_PEAK_UNITS)
 
 
-def c5(R):
+def c5(R, panel="coded"):
+    """panel 'coded': generic stand-in of the HRS kind (whole-year ages, one-decimal BMIs,
+    dcor.hrs.standin_panel, DP-standardised as real-data-sims.R:273-287): the dictionary-coded
+    LDS kernel.  panel 'continuous': every value distinct: the L2-gather kernel."""
     import numpy as np
     import torch
     from dcor import _lib
@@ -136,8 +139,16 @@ def c5(R):
     k, m = 9716, 2
     nsim = 2000
     g = np.random.default_rng(2)
-    age = np.clip(g.normal(0.0, 1.0, n), -2.22, 2.22)         # synthetic stand-in (HRS not shipped)
-    bmi = -0.19 * age + math.sqrt(1 - 0.19 ** 2) * g.normal(0.0, 1.0, n)
+    lam = (2.22, 2.60)
+    if panel == "coded":
+        from dcor import hrs
+        age_raw, bmi_raw = hrs.standin_panel(n, -0.3)
+        z = hrs.standardize_panel(age_raw, bmi_raw, lap=np.zeros(4))
+        age, bmi = z["age_z"], z["bmi_z"]
+        lam = (z["lambda_age_z"], z["lambda_bmi_z"])
+    else:
+        age = np.clip(g.normal(0.0, 1.0, n), -2.22, 2.22)     # synthetic stand-in (HRS not shipped)
+        bmi = -0.19 * age + math.sqrt(1 - 0.19 ** 2) * g.normal(0.0, 1.0, n)
     X = torch.as_tensor(age, device="cuda")
     Y = torch.as_tensor(bmi, device="cuda")
     perm = torch.empty((R, k * m), dtype=torch.int32, device="cuda")
@@ -158,19 +169,28 @@ def c5(R):
     _lib.check(_lib.lib.dcor_draws_launch(0, seed, 16, 0, R, nsim, P(ml), None))
     out = torch.empty((R, 6), dtype=torch.float64, device="cuda")
     d = _lib.PrematSubg(n=n, reps=R, eps1=eps, eps2=eps, eta1=1.0, eta2=1.0, alpha=0.05, hrs=1,
-                        lam_x=2.22, lam_y=2.60, lam_s=2.22, lam_o=2.60, lam_r=math.nan,
+                        lam_x=lam[0], lam_y=lam[1], lam_s=lam[0], lam_o=lam[1], lam_r=math.nan,
                         delta=math.nan, nsim=nsim, X=X.data_ptr(), Y=Y.data_ptr(), xy_stride=0,
                         perm=perm.data_ptr(), lap_ni_x=lx.data_ptr(), lap_ni_y=ly.data_ptr(),
                         lap_local=ll.data_ptr(), lap_central=lc.data_ptr(), mix_z=mz.data_ptr(),
                         mix_l=ml.data_ptr())
-    t = timed(lambda: _lib.check(_lib.lib.dcor_premat_subg_launch(C.byref(d), P(out), None)), reps=5)
+    pn = C.c_void_p()      # the panel is encoded once for the whole sweep (dcor_panel_create)
+    _lib.check(_lib.lib.dcor_panel_create(P(X), P(Y), n, None, C.byref(pn)))
+    t = timed(lambda: _lib.check(_lib.lib.dcor_premat_subg_panel_launch(C.byref(d), pn, P(out), None)),
+              reps=5)
     per_rep = 8 * n + 4 * k * m + 16 * k + 8 * nsim    # SURVEY §8d pinned: 404,648 B
     read_rep = 8 * n + 4 * k * m + 16 * k + 8 + 16 * nsim  # bytes the ABI actually reads (z, l apart)
-    line("C5", reps=R, seconds=t, reps_per_s=R / t, algorithmic_bytes_per_rep=per_rep,
-         input_bytes_per_rep=read_rep,
+    ok = C.c_int(-1)
+    _lib.check(_lib.lib.dcor_panel_coded(pn, C.byref(ok)))
+    _lib.check(_lib.lib.dcor_panel_destroy(pn))
+    line("C5" if panel == "coded" else "C5-continuous", reps=R, seconds=t, reps_per_s=R / t,
+         algorithmic_bytes_per_rep=per_rep, input_bytes_per_rep=read_rep,
          hbm_gbps=per_rep * R / t / 1e9, hbm_frac=per_rep * R / t / HBM_PEAK,
-         note="synthetic stand-in panel (n=19,433, clipped std-normal age_z, corr -0.19); "
-              "noise pre-generated on device (dcor_draws_launch / dcor_perm_launch); timed = streaming kernel only")
+         input_gbps=read_rep * R / t / 1e9, panel=panel,
+         kernel="dictionary-coded LDS panel" if ok.value else "L2-gather packed panel",
+         note="synthetic stand-in panel; noise pre-generated on device (dcor_draws_launch / "
+              "dcor_perm_launch); timed = one dcor_premat_subg_panel_launch (stream + epilogue) over a panel "
+              "encoded once by dcor_panel_create")
 
 
 def subg():
@@ -184,10 +204,10 @@ def subg():
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--only", default="C1,C2,C3,C4,C5,S")
+    ap.add_argument("--only", default="C1,C2,C3,C4,C5,C5c,S")
     ap.add_argument("--c3-reps", type=int, default=2000)
     ap.add_argument("--c4-B", type=int, default=1000)
-    ap.add_argument("--c5-R", type=int, default=4096)
+    ap.add_argument("--c5-R", type=int, default=8192)
     a = ap.parse_args()
     import torch
     torch.cuda.set_device(0)
@@ -197,6 +217,7 @@ def main():
     if "C3" in which: c3(a.c3_reps)
     if "C4" in which: c4(a.c4_B)
     if "C5" in which: c5(a.c5_R)
+    if "C5c" in which: c5(a.c5_R, panel="continuous")
     if "S" in which: subg()
 
 

@@ -552,7 +552,86 @@ static int premat_subg_const(const dcor_premat_subg* d, PrematSubgConst& p) {
   return DCOR_OK;
 }
 
+}  // extern "C" (reopened below)
+
+struct dcor_panel {
+  const double* X;
+  const double* Y;
+  int64_t n;
+  void* buf;          // codes (n u16, 256-B padded) | 512 dictionary doubles | ok flag
+  size_t codes_b;
+  void* stream;
+  int coded;          // host copy of the device flag (read once at create)
+  uint16_t* codes() const { return (uint16_t*)buf; }
+  double* dict() const { return (double*)((char*)buf + codes_b); }
+  int* ok() const { return (int*)((char*)buf + codes_b + 512 * sizeof(double)); }
+};
+
+static int premat_subg_run(const dcor_premat_subg* d, const dcor_panel* panel, dcor_rep_out* d_out,
+                           void* stream);
+
+extern "C" {
+
+int dcor_panel_create(const double* d_X, const double* d_Y, int64_t n, void* stream,
+                      dcor_panel** out) {
+  if (!d_X || !d_Y || !out || n < 1) return fail(DCOR_EINVAL, "panel_create: bad arguments");
+  if (int st = need_device()) return st;
+  *out = nullptr;
+  dcor_panel* pn = new dcor_panel();
+  pn->X = d_X; pn->Y = d_Y; pn->n = n; pn->stream = stream;
+  pn->codes_b = ((size_t)n * 2 + 255) & ~(size_t)255;
+  if (hipMalloc(&pn->buf, pn->codes_b + 512 * sizeof(double) + 256) != hipSuccess) {
+    (void)hipGetLastError();
+    delete pn;
+    return fail(DCOR_ENOMEM, "panel_create: cannot allocate the coded panel");
+  }
+  int rc = 0;
+  if (n <= DCOR_DICT_NMAX && premat_dict_lds_bytes(n) <= 150 * 1024)
+    rc = launch_panel_dict(d_X, d_Y, n, pn->codes(), pn->dict(), pn->ok(), stream);
+  else
+    rc = (int)hipMemsetAsync(pn->ok(), 0, sizeof(int), (hipStream_t)stream);
+  if (!rc) rc = (int)hipMemcpyAsync(&pn->coded, pn->ok(), sizeof(int), hipMemcpyDeviceToHost,
+                                     (hipStream_t)stream);
+  if (!rc) rc = (int)hipStreamSynchronize((hipStream_t)stream);
+  if (rc) {
+    (void)hipFree(pn->buf);
+    delete pn;
+    return hip_fail((hipError_t)rc, "panel_create");
+  }
+  *out = pn;
+  return DCOR_OK;
+}
+
+int dcor_panel_coded(const dcor_panel* pn, int* coded) {
+  if (!pn || !coded) return fail(DCOR_EINVAL, "panel_coded: null argument");
+  *coded = pn->coded;
+  return DCOR_OK;
+}
+
+int dcor_panel_destroy(dcor_panel* pn) {
+  if (!pn) return DCOR_OK;
+  (void)hipStreamSynchronize((hipStream_t)pn->stream);
+  const hipError_t e = hipFree(pn->buf);
+  delete pn;
+  return e == hipSuccess ? DCOR_OK : hip_fail(e, "panel_destroy");
+}
+
+int dcor_premat_subg_panel_launch(const dcor_premat_subg* d, const dcor_panel* panel,
+                                  dcor_rep_out* d_out, void* stream) {
+  if (!panel) return fail(DCOR_EINVAL, "premat_subg_panel: null panel");
+  if (!d || d->X != panel->X || d->Y != panel->Y || d->xy_stride != 0 || d->n != panel->n)
+    return fail(DCOR_EINVAL, "premat_subg_panel: X, Y, n must be the panel's and xy_stride 0");
+  return premat_subg_run(d, panel, d_out, stream);
+}
+
 int dcor_premat_subg_launch(const dcor_premat_subg* d, dcor_rep_out* d_out, void* stream) {
+  return premat_subg_run(d, nullptr, d_out, stream);
+}
+
+}  // extern "C" (reopened below)
+
+static int premat_subg_run(const dcor_premat_subg* d, const dcor_panel* panel, dcor_rep_out* d_out,
+                           void* stream) {
   if (!d || !d_out || d->reps < 0) return fail(DCOR_EINVAL, "null argument");
   if (!d->X || !d->Y || !d->lap_ni_x || !d->lap_ni_y || !d->lap_local || !d->lap_central ||
       !d->mix_z || !d->mix_l)
@@ -563,9 +642,18 @@ int dcor_premat_subg_launch(const dcor_premat_subg* d, dcor_rep_out* d_out, void
   // stream-ordered scratch for the stream -> epilogue partials: safe under concurrent
   // launches on different streams.
   // HRS over one shared panel: the packed clipped panel (2 x n x 16 B) follows the partials.
-  const bool pack = p.hrs && p.perm && p.xy_stride == 0 && p.s.m == 2;
+  // a prepared panel's path is known on the host: launch only the kernel that does the work
+  const bool pack = p.hrs && p.perm && p.xy_stride == 0 && p.s.m == 2 &&
+                    !(panel != nullptr && panel->coded);
+  // Shared panel + random batches: try the dictionary-coded LDS kernel first (the device
+  // decides; the packed L2-gather kernel is the fallback).
+  const bool dict = p.perm && p.xy_stride == 0 && p.s.n <= DCOR_DICT_NMAX &&
+                    premat_dict_lds_bytes(p.s.n) <= 150 * 1024 && panel == nullptr;
   const size_t part_b = ((size_t)d->reps * 80 + 255) & ~(size_t)255;
-  const size_t bytes = part_b + (pack ? (size_t)p.s.n * 32 : 0);
+  const size_t pack_b = pack ? (size_t)p.s.n * 32 : 0;
+  const size_t codes_b = dict ? (((size_t)p.s.n * 2 + 255) & ~(size_t)255) : 0;
+  const size_t dict_b = dict ? 2 * 256 * sizeof(double) + 256 : 0;
+  const size_t bytes = part_b + pack_b + codes_b + dict_b;
   void* part = nullptr;
   if (hipMallocAsync(&part, bytes, (hipStream_t)stream) != hipSuccess) {
     (void)hipGetLastError();
@@ -575,9 +663,38 @@ int dcor_premat_subg_launch(const dcor_premat_subg* d, dcor_rep_out* d_out, void
     p.xyc = (const double2*)((char*)part + part_b);
     p.soc = p.xyc + p.s.n;
   }
+  if (dict) {
+    char* q = (char*)part + part_b + pack_b;
+    p.dict_codes = (uint16_t*)q;
+    p.dict_vals = (double*)(q + codes_b);
+    p.dict_ok = (int*)(q + codes_b + 2 * 256 * sizeof(double));
+  } else if (panel != nullptr && p.perm && panel->coded) {
+    p.dict_codes = panel->codes();
+    p.dict_vals = panel->dict();
+    p.dict_ok = panel->ok();
+    p.dict_built = 2;  // built and known coded: no L2-gather launch
+  }
   const int rc = launch_premat_subg(p, d->reps, part, d_out, stream);
   (void)hipFreeAsync(part, (hipStream_t)stream);
   if (rc) return hip_fail((hipError_t)rc, "premat_subg launch");
+  return DCOR_OK;
+}
+
+extern "C" {
+
+int dcor_panel_dict_probe(const double* d_X, const double* d_Y, int64_t n, int* ok) {
+  if (!d_X || !d_Y || !ok || n < 1) return fail(DCOR_EINVAL, "panel_dict_probe: bad arguments");
+  if (int st = need_device()) return st;
+  *ok = 0;
+  if (n > DCOR_DICT_NMAX) return DCOR_OK;
+  DevBuf buf;
+  const size_t codes_b = ((size_t)n * 2 + 255) & ~(size_t)255;
+  HIPCHK(buf.alloc(codes_b + 512 * sizeof(double) + 256));
+  char* q = (char*)buf.p;
+  int* d_ok = (int*)(q + codes_b + 512 * sizeof(double));
+  const int rc = launch_panel_dict(d_X, d_Y, n, (uint16_t*)q, (double*)(q + codes_b), d_ok, nullptr);
+  if (rc) return hip_fail((hipError_t)rc, "panel_dict launch");
+  HIPCHK(hipMemcpy(ok, d_ok, sizeof(int), hipMemcpyDeviceToHost));
   return DCOR_OK;
 }
 

@@ -25,21 +25,20 @@ __device__ __forceinline__ double mixquant_loaded(const MixConst& mx, double c, 
                                                   const double* l, SelScratch* sc) {
   if (threadIdx.x == 0) sc->nan_cnt = 0;
   __syncthreads();
-  unsigned long long key[SEL_VPT];
+  double val[SEL_VPT];
   int nn = 0;
 #pragma unroll
   for (int s = 0; s < SEL_VPT; ++s) {
     const int i = threadIdx.x + s * DCOR_BLOCK;
-    key[s] = ~0ull;
+    val[s] = dnan();
     if (i < mx.nsim) {
-      const double v = z[i] + c * l[i];
-      nn += (v != v);
-      key[s] = sel_key(v);
+      val[s] = z[i] + c * l[i];
+      nn += (val[s] != val[s]);
     }
   }
   if (nn) atomicAdd(&sc->nan_cnt, nn);
   __syncthreads();
-  return reg_select(key, mx.pos, mx.nsim - sc->nan_cnt, sc);
+  return value_select(val, mx.pos, mx.nsim - sc->nan_cnt, sc);
 }
 
 #define MIX_MAX 2048

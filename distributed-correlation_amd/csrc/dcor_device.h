@@ -311,12 +311,16 @@ __device__ __forceinline__ long long block_sum_i(long long v, long long* scratch
 // prefix, a block scan to find the digit holding rank pos, stop when that bin holds
 // one key.  No sort, no key array in LDS: ~3 passes for 2000 keys.
 #define SEL_VPT 8  // MIX_MAX / DCOR_BLOCK
+#define SEL_CAND 256  // candidates ranked directly by value_select
 struct SelScratch {
   uint32_t hist[256];
   uint32_t wtot[DCOR_WAVES];
   uint32_t sel[3];
   int nan_cnt;
+  int ncand;
   unsigned long long key;
+  double mm[2 * DCOR_WAVES];
+  double cand[SEL_CAND];
 };
 
 __device__ __forceinline__ unsigned long long sel_key(double v) {
@@ -373,6 +377,100 @@ __device__ __forceinline__ double reg_select(const unsigned long long (&key)[SEL
   }
   __syncthreads();
   return sel_unkey(prefix);
+}
+
+// Order statistic by value binning: sort(valid v)[pos] for v held SEL_VPT per thread (NaN =
+// absent / NA, counted in `valid` by the caller).  Keys map to 256 bins by the monotone
+// non-decreasing b(v) = min(floor((v - min) * 256 / (max - min)), 255), so the bin where the
+// cumulative count crosses pos holds the answer; its few keys (~nsim/100 for mixquant draws)
+// are ranked directly.  One histogram pass with little atomic contention instead of the radix
+// passes (whose top digit piles every key of a narrow range into one or two bins).  Falls
+// back to reg_select for non-finite ranges or a crowded bin.  All threads call.
+__device__ __forceinline__ double value_select(const double (&v)[SEL_VPT], int pos, int valid,
+                                               SelScratch* sc) {
+  if (pos < 0 || pos >= valid) return dnan();  // uniform
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  double lo = __longlong_as_double(0x7FF0000000000000LL), hi = -lo;
+#pragma unroll
+  for (int s = 0; s < SEL_VPT; ++s)
+    if (v[s] == v[s]) { lo = fmin(lo, v[s]); hi = fmax(hi, v[s]); }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    lo = fmin(lo, __shfl_xor(lo, o, 64));
+    hi = fmax(hi, __shfl_xor(hi, o, 64));
+  }
+  if (lane == 0) { sc->mm[wv] = lo; sc->mm[DCOR_WAVES + wv] = hi; }
+  sc->hist[tid] = 0;
+  if (tid == 0) sc->ncand = 0;
+  __syncthreads();
+#pragma unroll
+  for (int w = 0; w < DCOR_WAVES; ++w) { lo = fmin(lo, sc->mm[w]); hi = fmax(hi, sc->mm[DCOR_WAVES + w]); }
+  if (!(hi > lo)) {                      // every valid key equal (pos < valid >= 1)
+    __syncthreads();
+    return lo;
+  }
+  const double scale = 256.0 / (hi - lo);
+  if (!(scale > 0.0) || !(scale < __longlong_as_double(0x7FF0000000000000LL)) ||
+      !((hi - lo) < __longlong_as_double(0x7FF0000000000000LL))) {
+    __syncthreads();
+    unsigned long long key[SEL_VPT];
+#pragma unroll
+    for (int s = 0; s < SEL_VPT; ++s) key[s] = sel_key(v[s]);
+    return reg_select(key, pos, valid, sc);
+  }
+  int bin[SEL_VPT];
+#pragma unroll
+  for (int s = 0; s < SEL_VPT; ++s) {
+    bin[s] = -1;
+    if (v[s] == v[s]) {
+      const double t = (v[s] - lo) * scale;
+      bin[s] = t < 255.0 ? (int)t : 255;
+      atomicAdd(&sc->hist[bin[s]], 1u);
+    }
+  }
+  __syncthreads();
+  const uint32_t h = sc->hist[tid];
+  uint32_t inc = h;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t t = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += t;
+  }
+  if (lane == 63) sc->wtot[wv] = inc;
+  __syncthreads();
+  uint32_t base = 0;
+#pragma unroll
+  for (int w = 0; w < DCOR_WAVES; ++w) base += (w < wv) ? sc->wtot[w] : 0u;
+  const uint32_t ex = base + inc - h;
+  const uint32_t k = (uint32_t)pos;
+  if (h != 0 && k >= ex && k < ex + h) { sc->sel[0] = (uint32_t)tid; sc->sel[1] = k - ex; sc->sel[2] = h; }
+  __syncthreads();
+  const int b = (int)sc->sel[0];
+  const uint32_t kk = sc->sel[1], cnt = sc->sel[2];
+  if (cnt > SEL_CAND) {  // crowded bin: radix select over all keys (uniform branch)
+    __syncthreads();
+    unsigned long long key[SEL_VPT];
+#pragma unroll
+    for (int s = 0; s < SEL_VPT; ++s) key[s] = sel_key(v[s]);
+    return reg_select(key, pos, valid, sc);
+  }
+#pragma unroll
+  for (int s = 0; s < SEL_VPT; ++s)
+    if (bin[s] == b) sc->cand[atomicAdd(&sc->ncand, 1)] = v[s];
+  __syncthreads();
+  if ((uint32_t)tid < cnt) {  // rank = #smaller + #equal at a lower slot (ties broken by slot)
+    const double x = sc->cand[tid];
+    uint32_t r = 0;
+    for (uint32_t j = 0; j < cnt; ++j) {
+      const double y = sc->cand[j];
+      r += (y < x) || (y == x && j < (uint32_t)tid);
+    }
+    if (r == kk) sc->mm[0] = x;
+  }
+  __syncthreads();
+  const double res = sc->mm[0];
+  __syncthreads();
+  return res;
 }
 
 }  // namespace dcor

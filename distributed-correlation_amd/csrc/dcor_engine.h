@@ -72,7 +72,7 @@ struct PrematSignConst {
 // Pre-materialised sub-G (simulation or HRS variant).
 struct PrematSubgConst {
   SubgConst s;
-  int32_t hrs, pad;
+  int32_t hrs, dict_built;  // dict_built: 1 coded panel built (dcor_panel), 2 built and known coded
   double lo_;                        // HRS: lambda_other (clip of the non-sender)
   double crit_sqrt2_s;               // HRS: qnorm*sqrt(2)*(2*lr/(n*eps_r))  (sd==0 branch)
   const double* X; const double* Y; int64_t xy_stride;
@@ -83,7 +83,16 @@ struct PrematSubgConst {
   // xyc[i] = (clip(X_i, l1), clip(Y_i, l2)) for the NI gathers, soc[i] = (clip(S_i, ls),
   // clip(O_i, lo)) for the INT stream.  nullptr: read X / Y directly.
   const double2* xyc; const double2* soc;
+  // Shared panel, random batches, n <= DCOR_DICT_NMAX: dictionary-coded panel built on device
+  // per launch (k_panel_dict).  dict_ok is set by the device: 1 -> the coded kernel runs,
+  // 0 (more than 256 distinct values in a column, or a NaN) -> the L2-gather kernel runs.
+  uint16_t* dict_codes; double* dict_vals; int* dict_ok;
 };
+#define DCOR_DICT_NMAX 65536
+size_t premat_dict_lds_bytes(int64_t n);
+// codes: n u16 (16-B padded), dict: 512 doubles, ok: 1 int (device).
+int launch_panel_dict(const double* X, const double* Y, int64_t n, uint16_t* codes, double* dict,
+                      int* ok, void* stream);
 
 // Kernel launchers (dcor_kernels.hip).  Return hipError_t as int.
 int launch_sign_fused(const SignConst& c, int64_t reps, dcor_rep_out* out, void* stream);

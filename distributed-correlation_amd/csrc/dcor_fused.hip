@@ -116,30 +116,28 @@ __device__ __forceinline__ double mixquant_fused(const MixConst& mx, double c, u
                                                  uint32_t k0, uint32_t k1, SelScratch* sc) {
   if (threadIdx.x == 0) sc->nan_cnt = 0;
   __syncthreads();
-  unsigned long long key[SEL_VPT];
+  double val[SEL_VPT];
   int nn = 0;
 #pragma unroll
   for (int s = 0; s < SEL_VPT / 2; ++s) {
     const int b = threadIdx.x + s * DCOR_BLOCK;  // Philox block b -> elements 2b, 2b+1
-    key[2 * s] = key[2 * s + 1] = ~0ull;
+    val[2 * s] = val[2 * s + 1] = dnan();
     if (2 * b < mx.nsim) {
       const U4 wz = draw((uint32_t)b, rep, DCOR_SITE_MIX_Z, k0, k1);
       const U4 wl = draw((uint32_t)b, rep, DCOR_SITE_MIX_L, k0, k1);
       double z0, z1;
       normal_pair(wz, &z0, &z1);
-      const double v0 = z0 + c * unit_laplace(u53(wl.w0, wl.w1));
-      nn += (v0 != v0);
-      key[2 * s] = sel_key(v0);
+      val[2 * s] = z0 + c * unit_laplace(u53(wl.w0, wl.w1));
+      nn += (val[2 * s] != val[2 * s]);
       if (2 * b + 1 < mx.nsim) {
-        const double v1 = z1 + c * unit_laplace(u53(wl.w2, wl.w3));
-        nn += (v1 != v1);
-        key[2 * s + 1] = sel_key(v1);
+        val[2 * s + 1] = z1 + c * unit_laplace(u53(wl.w2, wl.w3));
+        nn += (val[2 * s + 1] != val[2 * s + 1]);
       }
     }
   }
   if (nn) atomicAdd(&sc->nan_cnt, nn);
   __syncthreads();
-  return reg_select(key, mx.pos, mx.nsim - sc->nan_cnt, sc);
+  return value_select(val, mx.pos, mx.nsim - sc->nan_cnt, sc);
 }
 
 __device__ __forceinline__ void scalar_laplace(uint32_t rep, uint32_t k0, uint32_t k1, double* lap) {

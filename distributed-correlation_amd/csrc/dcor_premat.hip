@@ -145,8 +145,10 @@ __global__ __launch_bounds__(DCOR_BLOCK) void k_premat_xy_pack(PrematSubgConst p
 }
 
 __global__ __launch_bounds__(DCOR_BLOCK) void k_premat_subg_stream(PrematSubgConst p,
+                                                                   const int* __restrict__ dict_ok,
                                                                    SubgPartial* __restrict__ part) {
   __shared__ double red[16 * DCOR_WAVES];
+  if (dict_ok != nullptr && *dict_ok) return;  // the dictionary-coded kernel owns this launch
   const SubgConst& c = p.s;
   const int64_t rep = blockIdx.x;
   const int tid = threadIdx.x;
@@ -168,6 +170,16 @@ __global__ __launch_bounds__(DCOR_BLOCK) void k_premat_subg_stream(PrematSubgCon
     const DD xb = dd_div_d(bx, c.md), yb = dd_div_d(by, c.md);
     const double xt = (xb.hi + xb.lo) + c.bx * lxj;
     const double yt = (yb.hi + yb.lo) + c.by * lyj;
+    ks_acc(sP, xt * yt);
+    const double T = c.md * xt * yt;
+    ks_acc(sT, T);
+    ks_acc(sT2, T * T);
+  };
+  // m = 2: the batch mean of two values is fl(a + b) / 2 exactly (scaling by 1/2 is exact),
+  // which is what the double-double batch mean rounds to.
+  auto pair_term = [&](double xa, double xb, double ya, double yb, double lxj, double lyj) {
+    const double xt = (xa + xb) * 0.5 + c.bx * lxj;
+    const double yt = (ya + yb) * 0.5 + c.by * lyj;
     ks_acc(sP, xt * yt);
     const double T = c.md * xt * yt;
     ks_acc(sT, T);
@@ -207,12 +219,12 @@ __global__ __launch_bounds__(DCOR_BLOCK) void k_premat_subg_stream(PrematSubgCon
 #pragma unroll
       for (int u = 0; u < SUBG_UNR; ++u) {
         const double2 a = xy[pr[u].x], b = xy[pr[u].y];
-        batch_term(ax[u], ay[u], two_sum(a.x, b.x), two_sum(a.y, b.y));
+        pair_term(a.x, b.x, a.y, b.y, ax[u], ay[u]);
       }
     }
     for (; j < c.k; j += DCOR_BLOCK) {
       const double2 a = xy[pm[2 * j]], b = xy[pm[2 * j + 1]];
-      batch_term(lx[j], ly[j], two_sum(a.x, b.x), two_sum(a.y, b.y));
+      pair_term(a.x, b.x, a.y, b.y, lx[j], ly[j]);
     }
   } else if (p.perm == nullptr) {
     // contiguous batches: each element read once by its batch owner (NI + INT)
@@ -294,18 +306,13 @@ __global__ __launch_bounds__(DCOR_BLOCK) void k_premat_subg_stream(PrematSubgCon
   }
 }
 
-// Epilogue: NI result, INT estimate, mixquant, INT CI (ver-cor-subG.R:51-59, 91-103;
-// real-data-sims.R:233-243).
-__global__ __launch_bounds__(DCOR_BLOCK) void k_premat_subg_epilogue(PrematSubgConst p,
-                                                                     const SubgPartial* __restrict__ part,
-                                                                     dcor_rep_out* out) {
-  __shared__ SelScratch sel;
+
+// NI result, INT estimate, mixquant, INT CI of replicate `rep` from its five workgroup sums
+// (ver-cor-subG.R:51-59, 91-103; real-data-sims.R:233-243).  All threads call.
+__device__ __forceinline__ void premat_subg_finish(const PrematSubgConst& p, int64_t rep,
+                                                   const DD (&d5)[5], SelScratch* sel,
+                                                   dcor_rep_out* out) {
   const SubgConst& c = p.s;
-  const int64_t rep = blockIdx.x;
-  const SubgPartial q = part[rep];
-  DD d5[5];
-#pragma unroll
-  for (int v = 0; v < 5; ++v) d5[v] = two_sum(q.s[2 * v], q.s[2 * v + 1]);
   double o[6];
   ni_subg_result(c, d5[0], d5[1], d5[2], o);
   const DD mU = dd_div_d(d5[3], c.nd);
@@ -316,20 +323,252 @@ __global__ __launch_bounds__(DCOR_BLOCK) void k_premat_subg_epilogue(PrematSubgC
     const double se_norm = sqrt(sd * sd + c.sn2x2);
     const double cstar = 2.0 / (c.sqrt_n * sd * c.eps_r);
     const double qq = mixquant_loaded(c.mix, cstar, p.mix_z + rep * c.mix.nsim,
-                                      p.mix_l + rep * c.mix.nsim, &sel);
+                                      p.mix_l + rep * c.mix.nsim, sel);
     width = qq * se_norm / c.sqrt_n;
   } else if (sd == 0.0) {
     width = p.crit_sqrt2_s;
   } else {
     const double cstar = (2.0 * c.lr) / (c.sqrt_n * sd * c.eps_r);
     const double qq = mixquant_loaded(c.mix, cstar, p.mix_z + rep * c.mix.nsim,
-                                      p.mix_l + rep * c.mix.nsim, &sel);
+                                      p.mix_l + rep * c.mix.nsim, sel);
     width = qq * (sd / c.sqrt_n);
   }
   o[3] = rho;
   o[4] = rmax(rho - width, -1.0);
   o[5] = rmin(rho + width, 1.0);
   if (threadIdx.x == 0) out[rep] = dcor_rep_out{o[0], o[1], o[2], o[3], o[4], o[5]};
+}
+
+// Epilogue of the streaming kernels that hand their sums over through SubgPartial.
+__global__ __launch_bounds__(DCOR_BLOCK) void k_premat_subg_epilogue(PrematSubgConst p,
+                                                                     const SubgPartial* __restrict__ part,
+                                                                     dcor_rep_out* out) {
+  __shared__ SelScratch sel;
+  const int64_t rep = blockIdx.x;
+  const SubgPartial q = part[rep];
+  DD d5[5];
+#pragma unroll
+  for (int v = 0; v < 5; ++v) d5[v] = two_sum(q.s[2 * v], q.s[2 * v + 1]);
+  premat_subg_finish(p, rep, d5, &sel, out);
+}
+
+// ------------------------------------------- dictionary-coded shared panel (HRS) ---
+// Survey panels take few distinct values (HRS wave 2: 46 clipped ages, 201 clipped BMIs), so
+// the shared panel is stored as one byte-pair code per sample plus two value dictionaries:
+// 2 B per sample instead of 16 B, small enough to sit in LDS.  Every random NI batch gather
+// and every INT panel read then hits LDS, and only the per-replicate noise / permutation
+// streams touch HBM.  The values are the panel's own doubles, so results are unchanged.
+// k_panel_dict builds the dictionaries with an LDS hash table (one workgroup); if a column
+// has more than 256 distinct values (or a NaN), it clears *ok and the L2-gather kernel runs.
+#define DICT_SLOTS 1024
+#define DICT_MAX 256
+#define DICT_THREADS 1024
+__device__ __forceinline__ uint32_t dict_hash(unsigned long long key) {
+  return (uint32_t)((key * 0x9E3779B97F4A7C15ull) >> 54);  // 10 bits
+}
+
+__global__ __launch_bounds__(DICT_THREADS) void k_panel_dict(const double* __restrict__ X,
+                                                           const double* __restrict__ Y, int64_t n,
+                                                           uint16_t* __restrict__ codes,
+                                                           double* __restrict__ dict, int* ok) {
+  __shared__ unsigned long long tab[2][DICT_SLOTS];
+  __shared__ int16_t sid[2][DICT_SLOTS];
+  __shared__ int cnt[2], bad, wtot[2][DICT_THREADS / 64];
+  const unsigned long long EMPTY = ~0ull;  // a NaN pattern: NaN inputs are rejected anyway
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  for (int s = tid; s < DICT_SLOTS; s += DICT_THREADS) { tab[0][s] = EMPTY; tab[1][s] = EMPTY; }
+  if (tid == 0) { cnt[0] = cnt[1] = 0; bad = 0; }
+  __syncthreads();
+  for (int64_t i0 = tid; i0 < n; i0 += 4 * DICT_THREADS) {
+    double xv[4], yv[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t i = i0 + u * DICT_THREADS;
+      xv[u] = i < n ? X[i] : 0.0;
+      yv[u] = i < n ? Y[i] : 0.0;
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int cpt = q & 1, u = q >> 1;
+      if (i0 + u * DICT_THREADS >= n) break;
+      if (*(volatile int*)&bad) break;
+      const double v = cpt == 0 ? xv[u] : yv[u];
+      if (v != v) { bad = 1; break; }
+      const unsigned long long key = (unsigned long long)__double_as_longlong(v);
+      uint32_t h = dict_hash(key);
+      // Plain reads find a present key without an atomic (most samples repeat a value); the
+      // CAS only runs on an empty slot.  The table is at most 1/4 full (256 of 1024).
+      for (int probe = 0; probe < DICT_SLOTS; ++probe) {
+        unsigned long long cur = *(volatile unsigned long long*)&tab[cpt][h];
+        if (cur == EMPTY) {
+          cur = atomicCAS(&tab[cpt][h], EMPTY, key);
+          if (cur == EMPTY) {
+            if (atomicAdd(&cnt[cpt], 1) >= DICT_MAX) bad = 1;
+            break;
+          }
+        }
+        if (cur == key) break;
+        if (*(volatile int*)&bad) break;
+        h = (h + 1) & (DICT_SLOTS - 1);
+      }
+    }
+  }
+  __syncthreads();
+  if (bad) {
+    if (tid == 0) *ok = 0;
+    return;
+  }
+  // dense ids in slot order: wave ballot ranks + a scan over the 16 wave totals
+  for (int cpt = 0; cpt < 2; ++cpt) {
+    const bool occ = tab[cpt][tid] != EMPTY;
+    const unsigned long long b = __ballot(occ);
+    const int below = __popcll(b & ((1ull << lane) - 1ull));
+    if (lane == 0) wtot[cpt][wv] = __popcll(b);
+    __syncthreads();
+    int base = 0;
+    for (int w = 0; w < wv; ++w) base += wtot[cpt][w];
+    if (occ) {
+      sid[cpt][tid] = (int16_t)(base + below);
+      dict[cpt * DICT_MAX + base + below] = __longlong_as_double((long long)tab[cpt][tid]);
+    }
+  }
+  if (tid < DICT_MAX) {  // unused entries are defined (never referenced by a code)
+    if (tid >= cnt[0]) dict[tid] = 0.0;
+    if (tid >= cnt[1]) dict[DICT_MAX + tid] = 0.0;
+  }
+  __syncthreads();
+  for (int64_t i0 = tid; i0 < n; i0 += 4 * DICT_THREADS) {
+    double xv[4], yv[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t i = i0 + u * DICT_THREADS;
+      xv[u] = i < n ? X[i] : 0.0;
+      yv[u] = i < n ? Y[i] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t i = i0 + u * DICT_THREADS;
+      if (i >= n) break;
+      uint32_t id[2];
+#pragma unroll
+      for (int cpt = 0; cpt < 2; ++cpt) {
+        const unsigned long long key = (unsigned long long)__double_as_longlong(cpt == 0 ? xv[u] : yv[u]);
+        uint32_t h = dict_hash(key);
+        while (tab[cpt][h] != key) h = (h + 1) & (DICT_SLOTS - 1);  // present by construction
+        id[cpt] = (uint32_t)sid[cpt][h];
+      }
+      codes[i] = (uint16_t)(id[0] | (id[1] << 8));
+    }
+  }
+  if (tid == 0) *ok = 1;
+}
+
+// Streaming kernel over the dictionary-coded panel: persistent workgroups (the coded panel is
+// loaded into LDS once per workgroup), replicates grid-strided.  Dynamic LDS layout: four
+// clipped dictionaries dX, dY (NI clips), dS, dO (INT sender / other clips), the reduction
+// scratch, then the n codes.
+__global__ __launch_bounds__(DCOR_BLOCK) void k_premat_subg_dict(PrematSubgConst p,
+                                                                 const uint16_t* __restrict__ codes_g,
+                                                                 const double* __restrict__ dict_g,
+                                                                 const int* __restrict__ dict_ok,
+                                                                 int64_t reps,
+                                                                 SubgPartial* __restrict__ part) {
+  extern __shared__ double dsm[];
+  if (*dict_ok == 0) return;  // the L2-gather kernel owns this launch
+  const SubgConst& c = p.s;
+  const int tid = threadIdx.x;
+  double* dX = dsm;
+  double* dY = dsm + DICT_MAX;
+  double* dS = dsm + 2 * DICT_MAX;
+  double* dO = dsm + 3 * DICT_MAX;
+  double* red = dsm + 4 * DICT_MAX;
+  uint16_t* cod = reinterpret_cast<uint16_t*>(dsm + 4 * DICT_MAX + 16 * DCOR_WAVES);
+  {
+    const double x = dict_g[tid], y = dict_g[DICT_MAX + tid];  // DCOR_BLOCK == DICT_MAX
+    dX[tid] = rclip(x, c.l1);                                   // real-data-sims.R:126-127
+    dY[tid] = rclip(y, c.l2);
+    const double sv = c.sender_is_X ? x : y, ov = c.sender_is_X ? y : x;
+    dS[tid] = rclip(sv, c.ls);                                  // real-data-sims.R:222-227
+    dO[tid] = p.hrs ? rclip(ov, p.lo_) : ov;
+    const int64_t nv = (c.n * 2 + 15) / 16;                      // 16-B words of codes
+    const uint4* src = reinterpret_cast<const uint4*>(codes_g);
+    uint4* dst = reinterpret_cast<uint4*>(cod);
+    for (int64_t w = tid; w < nv; w += DCOR_BLOCK) dst[w] = src[w];
+  }
+  __syncthreads();
+#define DUNR 8  // loads in flight per thread: ~48 KB per CU at 3 workgroups / CU
+  const int64_t step = (int64_t)DCOR_BLOCK * DUNR;
+  for (int64_t rep = blockIdx.x; rep < reps; rep += gridDim.x) {
+    const double* __restrict__ lx = p.lap_ni_x + rep * c.k;
+    const double* __restrict__ ly = p.lap_ni_y + rep * c.k;
+    const double* __restrict__ ll = p.lap_local + rep * c.n;
+    const int32_t* __restrict__ pm = p.perm + rep * (c.k * c.m);
+    DD sP{0, 0}, sT{0, 0}, sT2{0, 0}, sU{0, 0}, sU2{0, 0};
+    auto uterm = [&](uint32_t cd, double l) {  // ver-cor-subG.R:88-90; real-data-sims.R:222-232
+      const double Uc = rclip((dS[cd & 255u] + c.bs * l) * dO[cd >> 8], c.lr);
+      ks_acc(sU, Uc);
+      ks_acc(sU2, Uc * Uc);
+    };
+    int64_t i = tid;
+    for (; i + (DUNR - 1) * DCOR_BLOCK < c.n; i += step) {
+      double l[DUNR];
+#pragma unroll
+      for (int u = 0; u < DUNR; ++u) l[u] = ll[i + u * DCOR_BLOCK];
+#pragma unroll
+      for (int u = 0; u < DUNR; ++u) uterm(cod[i + u * DCOR_BLOCK], l[u]);
+    }
+    for (; i < c.n; i += DCOR_BLOCK) uterm(cod[i], ll[i]);
+    if (c.m == 2) {  // real-data-sims.R:131-137 with the exact two-value batch mean
+      int64_t j = tid;
+      auto pair = [&](int2 pr, double lxj, double lyj) {
+        const uint32_t a = cod[pr.x], b = cod[pr.y];
+        const double xt = (dX[a & 255u] + dX[b & 255u]) * 0.5 + c.bx * lxj;
+        const double yt = (dY[a >> 8] + dY[b >> 8]) * 0.5 + c.by * lyj;
+        ks_acc(sP, xt * yt);
+        const double T = c.md * xt * yt;
+        ks_acc(sT, T);
+        ks_acc(sT2, T * T);
+      };
+      for (; j + (DUNR - 1) * DCOR_BLOCK < c.k; j += step) {
+        int2 pr[DUNR];
+        double ax[DUNR], ay[DUNR];
+#pragma unroll
+        for (int u = 0; u < DUNR; ++u) {
+          const int64_t jj = j + u * DCOR_BLOCK;
+          pr[u] = *reinterpret_cast<const int2*>(pm + 2 * jj);
+          ax[u] = lx[jj]; ay[u] = ly[jj];
+        }
+#pragma unroll
+        for (int u = 0; u < DUNR; ++u) pair(pr[u], ax[u], ay[u]);
+      }
+      for (; j < c.k; j += DCOR_BLOCK)
+        pair(*reinterpret_cast<const int2*>(pm + 2 * j), lx[j], ly[j]);
+    } else {
+      for (int64_t j = tid; j < c.k; j += DCOR_BLOCK) {
+        DD bx{0, 0}, by{0, 0};
+        for (int r = 0; r < c.m; ++r) {
+          const uint32_t a = cod[pm[j * c.m + r]];
+          dd_acc(bx, dX[a & 255u]);
+          dd_acc(by, dY[a >> 8]);
+        }
+        const DD xb = dd_div_d(bx, c.md), yb = dd_div_d(by, c.md);
+        const double xt = (xb.hi + xb.lo) + c.bx * lx[j];
+        const double yt = (yb.hi + yb.lo) + c.by * ly[j];
+        ks_acc(sP, xt * yt);
+        const double T = c.md * xt * yt;
+        ks_acc(sT, T);
+        ks_acc(sT2, T * T);
+      }
+    }
+    DD d5[5] = {sP, sT, sT2, sU, sU2};
+    block_sum_dd<5>(d5, red);
+    if (tid == 0) {
+      SubgPartial q;
+#pragma unroll
+      for (int v = 0; v < 5; ++v) { q.s[2 * v] = d5[v].hi; q.s[2 * v + 1] = d5[v].lo; }
+      part[rep] = q;
+    }
+  }
 }
 
 // ======================================================== accumulation ===
@@ -540,15 +779,53 @@ int launch_premat_sign(const PrematSignConst& c, int64_t reps, dcor_rep_out* out
                      (hipStream_t)stream, c, out);
   return last_err();
 }
+int launch_panel_dict(const double* X, const double* Y, int64_t n, uint16_t* codes, double* dict,
+                      int* ok, void* stream) {
+  hipLaunchKernelGGL(k_panel_dict, dim3(1), dim3(DICT_THREADS), 0, (hipStream_t)stream, X, Y, n,
+                     codes, dict, ok);
+  return last_err();
+}
+
+size_t premat_dict_lds_bytes(int64_t n) {
+  return (size_t)(4 * DICT_MAX + 16 * DCOR_WAVES) * sizeof(double) + (size_t)((n * 2 + 15) / 16) * 16;
+}
+
 int launch_premat_subg(const PrematSubgConst& c, int64_t reps, void* part, dcor_rep_out* out,
                        void* stream) {
   if (reps <= 0) return 0;
+  if (c.dict_codes != nullptr) {
+    static_assert(DCOR_BLOCK == DICT_MAX, "dictionary fill assumes one entry per thread");
+    if (!c.dict_built)
+      hipLaunchKernelGGL(k_panel_dict, dim3(1), dim3(DICT_THREADS), 0, (hipStream_t)stream, c.X,
+                         c.Y, c.s.n, c.dict_codes, c.dict_vals, c.dict_ok);
+    const size_t lds = premat_dict_lds_bytes(c.s.n);
+    static bool attr_set = false;
+    if (!attr_set) {
+      if (hipFuncSetAttribute((const void*)k_premat_subg_dict,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024) != hipSuccess)
+        return last_err();
+      attr_set = true;
+    }
+    int dev = 0, cus = 0, per_cu = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return last_err();
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      return last_err();
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_premat_subg_dict, DCOR_BLOCK, lds) !=
+        hipSuccess)
+      return last_err();
+    if (per_cu < 1) per_cu = 1;
+    const int64_t grid = reps < (int64_t)cus * per_cu ? reps : (int64_t)cus * per_cu;
+    hipLaunchKernelGGL(k_premat_subg_dict, dim3((unsigned)grid), dim3(DCOR_BLOCK), lds,
+                       (hipStream_t)stream, c, c.dict_codes, c.dict_vals, c.dict_ok, reps,
+                       (SubgPartial*)part);
+  }
   if (c.xyc != nullptr)
     hipLaunchKernelGGL(k_premat_xy_pack, dim3((unsigned)((c.s.n + DCOR_BLOCK - 1) / DCOR_BLOCK)),
                        dim3(DCOR_BLOCK), 0, (hipStream_t)stream, c, (double2*)c.xyc,
                        (double2*)c.soc);
-  hipLaunchKernelGGL(k_premat_subg_stream, dim3((unsigned)reps), dim3(DCOR_BLOCK), 0,
-                     (hipStream_t)stream, c, (SubgPartial*)part);
+  if (c.dict_built != 2)  // 2: a prepared panel known to be coded (dcor_panel)
+    hipLaunchKernelGGL(k_premat_subg_stream, dim3((unsigned)reps), dim3(DCOR_BLOCK), 0,
+                       (hipStream_t)stream, c, (const int*)c.dict_ok, (SubgPartial*)part);
   hipLaunchKernelGGL(k_premat_subg_epilogue, dim3((unsigned)reps), dim3(DCOR_BLOCK), 0,
                      (hipStream_t)stream, c, (const SubgPartial*)part, out);
   return last_err();

@@ -108,6 +108,11 @@ SIGNATURES = {
     "dcor_grid_run": (C.c_int, [C.POINTER(Cell), C.c_int, C.c_int64, C.POINTER(Accum), C.POINTER(RepOut)]),
     "dcor_premat_sign_launch": (C.c_int, [C.POINTER(PrematSign), _P, _P]),
     "dcor_premat_subg_launch": (C.c_int, [C.POINTER(PrematSubg), _P, _P]),
+    "dcor_panel_dict_probe": (C.c_int, [_P, _P, C.c_int64, C.POINTER(C.c_int)]),
+    "dcor_panel_create": (C.c_int, [_P, _P, C.c_int64, _P, C.POINTER(C.c_void_p)]),
+    "dcor_panel_coded": (C.c_int, [_P, C.POINTER(C.c_int)]),
+    "dcor_panel_destroy": (C.c_int, [_P]),
+    "dcor_premat_subg_panel_launch": (C.c_int, [C.POINTER(PrematSubg), _P, _P, _P]),
     "dcor_batch_geometry": (C.c_int, [C.c_int64, C.c_double, C.c_double, C.c_int, C.c_int, _I64]),
     "dcor_ci_ni_signbatch": (C.c_int, [_D, _D, C.c_int64, C.c_double, C.c_double, C.c_double,
                                        C.c_int, _D, _D, _D, _D]),

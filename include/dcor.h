@@ -171,6 +171,28 @@ typedef struct dcor_premat_subg {
   const double* mix_l;      /* [reps][nsim]                                       */
 } dcor_premat_subg;
 
+/* Whether a shared panel (DEVICE pointers) is dictionary-codable: *ok = 1 iff n <= 65536 and
+ * both columns hold at most 256 distinct doubles and no NaN.  dcor_premat_subg_launch with a
+ * shared panel (xy_stride 0) and random batches (perm) then runs the LDS-resident coded kernel;
+ * otherwise the L2-gather kernel.  Synchronous; results never depend on the path. */
+int dcor_panel_dict_probe(const double* d_X, const double* d_Y, int64_t n, int* ok);
+
+/* A shared (X, Y) panel prepared once for many pre-materialised sub-G launches: the HRS panel
+ * of real-data-sims.R, reused by every replicate of the eps sweep (real-data-sims.R:345-404).
+ * Create encodes the panel on `stream` and waits for it (dictionary codes when codable, see
+ * the probe above);
+ * the device arrays d_X, d_Y must stay valid and unchanged until destroy. */
+typedef struct dcor_panel dcor_panel;
+int dcor_panel_create(const double* d_X, const double* d_Y, int64_t n, void* stream,
+                      dcor_panel** out);
+/* *coded = 1 if the panel is dictionary-coded (create synchronises once to learn it). */
+int dcor_panel_coded(const dcor_panel* panel, int* coded);
+int dcor_panel_destroy(dcor_panel* panel);
+/* dcor_premat_subg_launch over a prepared panel: d->X, d->Y must be the panel's arrays,
+ * d->xy_stride 0, d->n the panel's n.  Skips the per-launch encoding. */
+int dcor_premat_subg_panel_launch(const dcor_premat_subg* d, const dcor_panel* panel,
+                                  dcor_rep_out* d_out, void* stream);
+
 int dcor_premat_sign_launch(const dcor_premat_sign* d, dcor_rep_out* d_out, void* stream);
 int dcor_premat_subg_launch(const dcor_premat_subg* d, dcor_rep_out* d_out, void* stream);
 

@@ -108,15 +108,41 @@ def test_premat_sign_batch_device(dc, orc):
         assert_close(got[r], np.concatenate([ni, it]), what=f"rep {r}")
 
 
-def test_premat_subg_hrs_shared_panel(dc, orc):
-    """HRS mode: one shared (X, Y) panel (stride 0), per-replicate perms and noise."""
+def _hrs_panel(kind, n, g):
+    """Shared HRS-like panels: 'continuous' (every value distinct: L2-gather kernel), 'coded'
+    (integer ages, one-decimal BMI like the real wave-2 panel: dictionary-coded LDS kernel),
+    'd256' / 'd257' (exactly 256 / 257 distinct values in X: the dictionary boundary)."""
+    if kind == "continuous":
+        age = np.clip(g.normal(0.0, 1.0, n), -2.2, 2.2)
+        bmi = -0.19 * age + math.sqrt(1 - 0.19 ** 2) * g.normal(0.0, 1.0, n)
+        return age, bmi
+    if kind == "coded":
+        a = np.clip(np.round(g.normal(65.0, 10.0, n)), 23, 103)
+        b = np.round(np.clip(g.normal(27.0, 5.0, n) - 0.05 * (a - 65.0), 12.6, 92.2), 1)
+        a = (np.clip(a, 45, 90) - 66.1) / 9.7     # standardize_dp (real-data-sims.R:87-90)
+        b = (np.clip(b, 15, 35) - 26.9) / 4.6
+        return a, b
+    d = 256 if kind == "d256" else 257
+    vals = np.linspace(-2.0, 2.0, d)
+    a = vals[np.arange(n) % d]
+    g.shuffle(a)
+    b = np.round(g.normal(0.0, 1.0, n), 1)
+    return a, b
+
+
+@pytest.mark.parametrize("kind,n,eps", [("continuous", 19433, 2.0), ("coded", 19433, 2.0),
+                                        ("coded", 19433, 0.5), ("coded", 1001, 2.0),
+                                        ("d256", 5000, 2.0), ("d257", 5000, 2.0),
+                                        ("continuous", 3000, 0.5)])
+def test_premat_subg_hrs_shared_panel(dc, orc, kind, n, eps):
+    """HRS mode: one shared (X, Y) panel (stride 0), per-replicate perms and noise; the
+    dictionary-coded kernel (few distinct values) and the L2-gather fallback."""
     import torch
     from dcor import _lib
-    R, n, eps = 5, 19433, 2.0
+    R = 5
     g = np.random.default_rng(7)
-    age = np.clip(g.normal(0.0, 1.0, n), -2.2, 2.2)
-    bmi = -0.19 * age + math.sqrt(1 - 0.19 ** 2) * g.normal(0.0, 1.0, n)
-    k, m = 9716, 2
+    age, bmi = _hrs_panel(kind, n, g)
+    k, m = dc.api.batch_geometry(n, eps, eps, "subG", hrs=True)
     perms = np.stack([g.permutation(n)[: k * m] for _ in range(R)]).astype(np.int32)
     lx, ly = unit_laplace(g, (R, k)), unit_laplace(g, (R, k))
     ll, lc = unit_laplace(g, (R, n)), unit_laplace(g, R)
@@ -129,16 +155,31 @@ def test_premat_subg_hrs_shared_panel(dc, orc):
                         perm=T["perm"].data_ptr(), lap_ni_x=T["lx"].data_ptr(), lap_ni_y=T["ly"].data_ptr(),
                         lap_local=T["ll"].data_ptr(), lap_central=T["lc"].data_ptr(),
                         mix_z=T["mz"].data_ptr(), mix_l=T["ml"].data_ptr())
+    ok = C.c_int(-1)
+    _lib.check(_lib.lib.dcor_panel_dict_probe(C.c_void_p(T["X"].data_ptr()), C.c_void_p(T["Y"].data_ptr()),
+                                              n, C.byref(ok)))
+    assert ok.value == (1 if kind in ("coded", "d256") else 0), (kind, ok.value)
     out = torch.empty((R, 6), dtype=torch.float64, device="cuda")
     _lib.check(_lib.lib.dcor_premat_subg_launch(C.byref(d), C.c_void_p(out.data_ptr()), None))
     got = out.cpu().numpy()
+    # the prepared-panel entry (encoding hoisted out of the launch) gives identical bits
+    pn = C.c_void_p()
+    _lib.check(_lib.lib.dcor_panel_create(C.c_void_p(T["X"].data_ptr()), C.c_void_p(T["Y"].data_ptr()),
+                                          n, None, C.byref(pn)))
+    coded = C.c_int(-1)
+    _lib.check(_lib.lib.dcor_panel_coded(pn, C.byref(coded)))
+    assert coded.value == ok.value
+    out2 = torch.full((R, 6), -7.0, dtype=torch.float64, device="cuda")
+    _lib.check(_lib.lib.dcor_premat_subg_panel_launch(C.byref(d), pn, C.c_void_p(out2.data_ptr()), None))
+    _lib.check(_lib.lib.dcor_panel_destroy(pn))
+    np.testing.assert_array_equal(out2.cpu().numpy().view(np.int64), got.view(np.int64))
     for r in range(R):
         st, ni, km = orc.ni_subg(age, bmi, eps, eps, hrs=1, lam_x=2.22, lam_y=2.60, perm=perms[r],
                                  lap_x=lx[r], lap_y=ly[r])
         assert list(km) == [k, m]
         st, it, _ = orc.int_subg(age, bmi, eps, eps, hrs=1, lam_s=2.22, lam_o=2.60, lap_local=ll[r],
                                  lap_central=lc[r], mix_z=mz[r], mix_l=ml[r])
-        assert_close(got[r], np.concatenate([ni, it]), what=f"hrs rep {r}")
+        assert_close(got[r], np.concatenate([ni, it]), what=f"hrs {kind} rep {r}")
 
 
 # ------------------------------------------------------------ edge semantics
