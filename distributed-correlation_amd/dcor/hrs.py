@@ -7,9 +7,9 @@ The reference loads `hrs_long_panel.rds`, keeps wave 2 complete cases of (agey_e
 panel (real-data-sims.R:290-323), then sweeps eps over seq(.25, 2.5, .1) with R = 200
 replicates each (real-data-sims.R:345-448).
 
-`load_panel(path)` reads the RDS with the engine's own C++ reader (libdcor.so: gzip + R XDR
-serialisation, no R).  The repository ships no HRS microdata and nothing computed from them
-(HRS terms of use).  `standin_panel(n, rho)` is a generic synthetic panel of the same kind
+Ingesting the HRS panel itself waits for a data-licensing decision by the
+project owner, so the repository ships no HRS microdata, nothing computed from them, and no
+reader for them.  `standin_panel(n, rho)` is a generic synthetic panel of the same kind
 (whole-year ages, one-decimal BMIs): each column is centred on its clip interval
 (real-data-sims.R:260-261) with sd = interval width / 4; n and rho are the caller's.
 """
@@ -38,13 +38,6 @@ def standin_panel(n: int, rho: float, seed: int = 2):
     age = np.round(0.5 * (AGE_LO + AGE_HI) + 0.25 * (AGE_HI - AGE_LO) * za)
     bmi = np.round(0.5 * (BMI_LO + BMI_HI) + 0.25 * (BMI_HI - BMI_LO) * zb, 1)
     return age, bmi
-
-
-def load_panel(path: str, wave: str = "2"):
-    """readRDS + filter(wave == "2") + transmute(age = agey_e, bmi) + drop_na
-    (real-data-sims.R:13, 38-41) through the engine's RDS reader."""
-    from . import rds
-    return rds.hrs_wave(path, wave)
 
 
 def standardize_panel(age, bmi, lap=None, rng=None):
