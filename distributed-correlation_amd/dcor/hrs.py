@@ -54,3 +54,100 @@ def standardize_panel(age, bmi, lap=None, rng=None):
             "age_priv": age_priv, "bmi_priv": bmi_priv,
             "lambda_age_z": api.lambda_from_priv(AGE_LO, AGE_HI, age_priv),
             "lambda_bmi_z": api.lambda_from_priv(BMI_LO, BMI_HI, bmi_priv)}
+
+
+# ------------------------------------------------------------ replicate sweep (a19 / C5)
+# On-device unit-noise streams of one HRS replicate (dcor_draws_launch / dcor_perm_launch
+# sites).  The reference reseeds per run with set.seed(10 + 37 rep + 1000 idx) (NI) and
+# set.seed(20 + 41 rep + 1000 idx) (INT) (real-data-sims.R:404, 423); here the per-eps seed
+# is the Philox key and the replicate index is the counter, so replicates are independent
+# streams and any split over launches or GPUs reproduces them exactly.
+SITE_NI_LAP_X, SITE_NI_LAP_Y, SITE_INT_LOCAL, SITE_INT_CENTRAL, SITE_MIX_Z, SITE_MIX_L = 11, 12, 13, 14, 15, 16
+DRAW_LAPLACE, DRAW_NORMAL = 0, 1
+
+
+def hrs_replicates(age_z, bmi_z, lam_age, lam_bmi, eps, reps, seed_ni=NI_SEED, seed_int=INT_SEED,
+                   nsim=2000, rep_begin=0, chunk=8192, alpha=0.05, keep_noise=False):
+    """`reps` NI + INT replicates of the HRS estimators on one standardised panel at one eps:
+    correlation_NI_subG(lambda_X = lam_age, lambda_Y = lam_bmi) and ci_INT_subG(AGE sends,
+    lambda_receiver_from_noise, delta_clip = 1/n) (real-data-sims.R:357-400).  The panel is
+    encoded once (dcor_panel_create); noise is generated in HBM per chunk and streamed by the
+    pre-materialised kernel.  Returns float64 [reps, 6] (ni_hat, ni_lo, ni_hi, int_hat, int_lo,
+    int_hi) and, with keep_noise, the host copies of every noise array."""
+    import ctypes as C
+
+    import torch
+
+    from . import _lib, api
+    X = torch.as_tensor(np.ascontiguousarray(age_z, dtype=np.float64), device="cuda")
+    Y = torch.as_tensor(np.ascontiguousarray(bmi_z, dtype=np.float64), device="cuda")
+    n = int(X.shape[0])
+    k, m = api.batch_geometry(n, eps, eps, "subG", hrs=True)
+    delta = 1.0 / n
+    lam_r = api.lambda_receiver_from_noise(lam_age, lam_bmi, eps, delta)
+    P = lambda t: C.c_void_p(t.data_ptr())
+    stream = torch.cuda.current_stream()
+    sp = C.c_void_p(stream.cuda_stream)
+    pn = C.c_void_p()
+    _lib.check(_lib.lib.dcor_panel_create(P(X), P(Y), n, sp, C.byref(pn)))
+    cr = min(chunk, max(1, reps))
+    f64 = dict(dtype=torch.float64, device="cuda")
+    perm = torch.empty((cr, k * m), dtype=torch.int32, device="cuda")
+    lx, ly = torch.empty((cr, k), **f64), torch.empty((cr, k), **f64)
+    ll, lc = torch.empty((cr, n), **f64), torch.empty((cr,), **f64)
+    mz, ml = torch.empty((cr, nsim), **f64), torch.empty((cr, nsim), **f64)
+    out = torch.empty((reps, 6), **f64)
+    noise = {key: [] for key in ("perm", "lap_x", "lap_y", "lap_local", "lap_central", "mix_z", "mix_l")}
+    try:
+        for r0 in range(0, reps, cr):
+            nr = min(cr, reps - r0)
+            rb = rep_begin + r0
+            chk = _lib.check
+            chk(_lib.lib.dcor_perm_launch(seed_ni, _lib.SITE_PERM, rb, nr, n, k * m, P(perm), sp))
+            chk(_lib.lib.dcor_draws_launch(DRAW_LAPLACE, seed_ni, SITE_NI_LAP_X, rb, nr, k, P(lx), sp))
+            chk(_lib.lib.dcor_draws_launch(DRAW_LAPLACE, seed_ni, SITE_NI_LAP_Y, rb, nr, k, P(ly), sp))
+            chk(_lib.lib.dcor_draws_launch(DRAW_LAPLACE, seed_int, SITE_INT_LOCAL, rb, nr, n, P(ll), sp))
+            chk(_lib.lib.dcor_draws_launch(DRAW_LAPLACE, seed_int, SITE_INT_CENTRAL, rb, nr, 1, P(lc), sp))
+            chk(_lib.lib.dcor_draws_launch(DRAW_NORMAL, seed_int, SITE_MIX_Z, rb, nr, nsim, P(mz), sp))
+            chk(_lib.lib.dcor_draws_launch(DRAW_LAPLACE, seed_int, SITE_MIX_L, rb, nr, nsim, P(ml), sp))
+            d = _lib.PrematSubg(n=n, reps=nr, eps1=eps, eps2=eps, eta1=1.0, eta2=1.0, alpha=alpha, hrs=1,
+                                lam_x=lam_age, lam_y=lam_bmi, lam_s=lam_age, lam_o=lam_bmi, lam_r=lam_r,
+                                delta=delta, nsim=nsim, X=X.data_ptr(), Y=Y.data_ptr(), xy_stride=0,
+                                perm=perm.data_ptr(), lap_ni_x=lx.data_ptr(), lap_ni_y=ly.data_ptr(),
+                                lap_local=ll.data_ptr(), lap_central=lc.data_ptr(), mix_z=mz.data_ptr(),
+                                mix_l=ml.data_ptr())
+            chk(_lib.lib.dcor_premat_subg_panel_launch(C.byref(d), pn, P(out[r0:]), sp))
+            if keep_noise:
+                for key, t in (("perm", perm), ("lap_x", lx), ("lap_y", ly), ("lap_local", ll),
+                               ("lap_central", lc), ("mix_z", mz), ("mix_l", ml)):
+                    noise[key].append(t[:nr].cpu().numpy().copy())
+        res = out.cpu().numpy()
+    finally:
+        _lib.lib.dcor_panel_destroy(pn)
+    if keep_noise:
+        return res, {key: np.concatenate(v) for key, v in noise.items()}, {"k": k, "m": m, "lam_r": lam_r,
+                                                                           "delta": delta}
+    return res
+
+
+def _summ(method, eps, hat, lo, hi) -> dict:
+    """real-data-sims.R:408-418 / 427-437: means and type-7 quantiles (NA propagates)."""
+    def q(v, p):
+        return float("nan") if np.isnan(v).any() else float(np.quantile(v, p))
+    return {"method": method, "eps_corr": eps, "rho_hat_mean": float(np.mean(hat)),
+            "ci_low_mean": float(np.mean(lo)), "ci_high_mean": float(np.mean(hi)),
+            "ci_low_q10": q(lo, 0.10), "ci_high_q90": q(hi, 0.90)}
+
+
+def eps_sweep(age_z, bmi_z, lam_age, lam_bmi, eps_grid=EPS_GRID, reps=R_PER_EPS, nsim=2000):
+    """The replicate sweep of real-data-sims.R:345-448: for every eps in seq(.25, 2.5, .1),
+    `reps` NI and INT runs (Philox keys 10 + 1000 idx and 20 + 1000 idx, idx 1-based as
+    which(eps_grid == eps)) and the per-eps summaries ni_mean / int_mean."""
+    runs, ni_mean, int_mean = [], [], []
+    for idx, eps in enumerate(eps_grid, start=1):
+        res = hrs_replicates(age_z, bmi_z, lam_age, lam_bmi, eps, reps, seed_ni=10 + 1000 * idx,
+                             seed_int=20 + 1000 * idx, nsim=nsim)
+        runs.append(res)
+        ni_mean.append(_summ("NI", eps, res[:, 0], res[:, 1], res[:, 2]))
+        int_mean.append(_summ("INT", eps, res[:, 3], res[:, 4], res[:, 5]))
+    return {"eps": list(eps_grid), "runs": np.stack(runs), "ni_mean": ni_mean, "int_mean": int_mean}

@@ -1,0 +1,79 @@
+"""GPU tests of the HRS replicate driver (real-data-sims.R:345-448, BASELINE config C5) on a
+generic stand-in panel: on-device noise streams bit-exact against the oracle's Philox
+restatement, every replicate against the oracle estimators, chunk-split invariance, and the
+eps sweep summaries."""
+import math
+
+import numpy as np
+import pytest
+
+from helpers import assert_close
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def panel():
+    import torch
+    assert torch.cuda.is_available()
+    from dcor import hrs
+    age, bmi = hrs.standin_panel(2501, -0.3, seed=5)
+    return hrs.standardize_panel(age, bmi, lap=np.array([0.3, -0.2, 0.1, 0.4]))
+
+
+@pytest.mark.parametrize("eps", [2.0, 0.5])
+def test_hrs_replicates_match_oracle(panel, eps):
+    from dcor import hrs
+    from oracle import oracle as orc
+    z = panel
+    n = len(z["age_z"])
+    R, rb = 5, 3
+    res, noise, geo = hrs.hrs_replicates(z["age_z"], z["bmi_z"], z["lambda_age_z"], z["lambda_bmi_z"], eps,
+                                         R, seed_ni=1010, seed_int=1020, rep_begin=rb, chunk=2,
+                                         keep_noise=True)
+    k, m = geo["k"], geo["m"]
+    for r in range(R):
+        rep = rb + r
+        np.testing.assert_array_equal(noise["perm"][r], orc.perm(1010, 8, rep, n, k * m))
+        for key, seed, site, cnt in (("lap_x", 1010, hrs.SITE_NI_LAP_X, k), ("lap_y", 1010, hrs.SITE_NI_LAP_Y, k),
+                                     ("lap_local", 1020, hrs.SITE_INT_LOCAL, n),
+                                     ("mix_l", 1020, hrs.SITE_MIX_L, 2000)):
+            np.testing.assert_array_equal(noise[key][r], orc.gen_laplace(seed, rep, site, cnt), err_msg=key)
+        np.testing.assert_array_equal(noise["mix_z"][r], orc.gen_normals(1020, rep, hrs.SITE_MIX_Z, 2000))
+        assert noise["lap_central"][r] == orc.gen_laplace(1020, rep, hrs.SITE_INT_CENTRAL, 1)[0]
+        st, ni, km = orc.ni_subg(z["age_z"], z["bmi_z"], eps, eps, hrs=1, lam_x=z["lambda_age_z"],
+                                 lam_y=z["lambda_bmi_z"], perm=noise["perm"][r], lap_x=noise["lap_x"][r],
+                                 lap_y=noise["lap_y"][r])
+        assert st == 0 and list(km) == [k, m]
+        st, it, _ = orc.int_subg(z["age_z"], z["bmi_z"], eps, eps, hrs=1, lam_s=z["lambda_age_z"],
+                                 lam_o=z["lambda_bmi_z"], lam_r=geo["lam_r"], delta=geo["delta"],
+                                 lap_local=noise["lap_local"][r], lap_central=noise["lap_central"][r],
+                                 mix_z=noise["mix_z"][r], mix_l=noise["mix_l"][r])
+        assert st == 0
+        assert_close(res[r], np.concatenate([ni, it]), what=f"hrs eps={eps} rep {rep}")
+
+
+def test_hrs_replicates_split_invariant(panel):
+    from dcor import hrs
+    z = panel
+    args = (z["age_z"], z["bmi_z"], z["lambda_age_z"], z["lambda_bmi_z"], 1.05)
+    whole = hrs.hrs_replicates(*args, 9, chunk=9)
+    parts = np.concatenate([hrs.hrs_replicates(*args, 4, chunk=3),
+                            hrs.hrs_replicates(*args, 5, rep_begin=4, chunk=5)])
+    np.testing.assert_array_equal(whole.view(np.int64), parts.view(np.int64))
+
+
+def test_eps_sweep_summaries(panel):
+    from dcor import hrs
+    z = panel
+    out = hrs.eps_sweep(z["age_z"], z["bmi_z"], z["lambda_age_z"], z["lambda_bmi_z"], eps_grid=(0.25, 2.45),
+                        reps=4)
+    assert out["runs"].shape == (2, 4, 6)
+    for s, runs in zip(out["ni_mean"], out["runs"]):
+        assert s["method"] == "NI"
+        assert math.isclose(s["rho_hat_mean"], float(np.mean(runs[:, 0])), rel_tol=0, abs_tol=0)
+        assert math.isclose(s["ci_low_q10"], float(np.quantile(runs[:, 1], 0.1)), rel_tol=0, abs_tol=0)
+    for s, runs in zip(out["int_mean"], out["runs"]):
+        assert s["method"] == "INT" and s["ci_low_mean"] <= s["ci_high_mean"]  # rho_hat is not clipped
+        assert math.isclose(s["ci_high_q90"], float(np.quantile(runs[:, 5], 0.9)), rel_tol=0, abs_tol=0)
+    assert [round(e, 2) for e in hrs.EPS_GRID][:3] == [0.25, 0.35, 0.45] and len(hrs.EPS_GRID) == 23
