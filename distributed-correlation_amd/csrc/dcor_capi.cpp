@@ -126,6 +126,14 @@ int make_dgp(const dcor_cell& c, DgpConst& g) {
     if (!(c.rho >= 0 && c.rho <= 1)) return fail(DCOR_EINVAL, "gen_bounded_factor: rho in [0,1] required");
     g.cU = std::sqrt(3.0 * c.rho); g.cE = std::sqrt(3.0 * (1.0 - c.rho));  // ver-cor-subG.R:148-149
     g.cU2 = g.cU - -g.cU; g.cE2 = g.cE - -g.cE;
+  } else if (c.dgp == DCOR_DGP_MIX_GAUSSIAN) {
+    if (!(c.mix_pi >= 0 && c.mix_pi <= 1)) return fail(DCOR_EINVAL, "gen_mix_gaussian: pi_mix in [0,1] required");
+    mvrnorm_factor(c.mix_sigma0, c.rho, g.xa[0]);   // ver-cor-subG.R:119-122
+    mvrnorm_factor(c.mix_sigma1, c.rho, g.xa[1]);
+    g.xmu[0][0] = c.mix_mu0[0]; g.xmu[0][1] = c.mix_mu0[1];
+    g.xmu[1][0] = c.mix_mu1[0]; g.xmu[1][1] = c.mix_mu1[1];
+    const double t = std::ceil(c.mix_pi * 16777216.0);  // exact: pi * 2^24
+    g.T24 = t >= 16777216.0 ? 16777216u : (uint32_t)t;
   } else {
     return fail(DCOR_EINVAL, "unknown dgp %d", c.dgp);
   }
@@ -387,6 +395,8 @@ int dcor_sim_launch(const dcor_cell* cell, int64_t rep_begin, int64_t rep_count,
       ry = 2.0 * std::sqrt(g.a10 * g.a10 + g.a11 * g.a11);
     } else if (c.dgp == DCOR_DGP_BERNOULLI) {
       cx = cy = 0.5; rx = ry = 1.0;
+    } else if (c.dgp == DCOR_DGP_MIX_GAUSSIAN) {
+      cx = cy = 0.0; rx = ry = 1.0;       // clipped to [-1, 1]
     } else {
       cx = cy = 0.0; rx = ry = 2.0;
     }

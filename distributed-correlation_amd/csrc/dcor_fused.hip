@@ -84,6 +84,36 @@ template <> struct Dgp<DCOR_DGP_BOUNDED_FACTOR> {  // gen_bounded_factor (ver-co
   }
 };
 
+template <> struct Dgp<DCOR_DGP_MIX_GAUSSIAN> {  // gen_mix_gaussian (ver-cor-subG.R:113-133)
+  // One DGP_A block: Box-Muller from the top 52 bits of (w0,w1), (w2,w3); the component label
+  // from the 24 bits Box-Muller leaves unused (low 12 of w1 and of w3): u24 < ceil(pi 2^24)
+  // (exact for pi = .5, the R default; |bias| < 2^-24 otherwise).  Row shuffling
+  // (sample.int, :131) leaves the law of an iid mixture sample unchanged, so samples are
+  // drawn iid.  pmax(pmin(., 1), -1) last (:132).
+  static __device__ __forceinline__ void one(const DgpConst& g, uint32_t i, uint32_t rep,
+                                             uint32_t k0, uint32_t k1, double& x, double& y) {
+    const U4 w = draw(i, rep, DCOR_SITE_DGP_A, k0, k1);
+    double z1, z2;
+    normal_pair(w, &z1, &z2);
+    const uint32_t u24 = ((w.w1 & 0xFFFu) << 12) | (w.w3 & 0xFFFu);
+    const int c = u24 < g.T24 ? 1 : 0;   // label ~ rbinom(1, pi_mix): 1 -> component 1
+    const double mx = c ? g.xmu[1][0] : g.xmu[0][0], my = c ? g.xmu[1][1] : g.xmu[0][1];
+    const double a00 = c ? g.xa[1][0] : g.xa[0][0], a01 = c ? g.xa[1][1] : g.xa[0][1];
+    const double a10 = c ? g.xa[1][2] : g.xa[0][2], a11 = c ? g.xa[1][3] : g.xa[0][3];
+    x = rclip_fin(mx + (a00 * z1 + a01 * z2), 1.0);
+    y = rclip_fin(my + (a10 * z1 + a11 * z2), 1.0);
+  }
+  static __device__ __forceinline__ void quad(const DgpConst& g, uint32_t i0, uint32_t rep,
+                                              uint32_t k0, uint32_t k1, double* x, double* y) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) one(g, i0 + q, rep, k0, k1, x[q], y[q]);
+  }
+  static __device__ __forceinline__ double lap(uint32_t i, uint32_t rep, uint32_t k0, uint32_t k1) {
+    const U4 v = draw(i, rep, DCOR_SITE_DGP_B, k0, k1);
+    return unit_laplace(u53(v.w2, v.w3));
+  }
+};
+
 // Sub-G needs the sample and its local Laplace (DGP_B words 2,3).
 template <int DGP>
 __device__ __forceinline__ void sample_lap(const DgpConst& g, uint32_t i, uint32_t rep, uint32_t k0,
@@ -718,6 +748,7 @@ int launch_sign_fused(const SignConst& c, int64_t reps, dcor_rep_out* out, void*
   switch (c.g.dgp) {
     case DCOR_DGP_GAUSSIAN: return launch_sign_t<DCOR_DGP_GAUSSIAN>(c, reps, out, stream);
     case DCOR_DGP_BERNOULLI: return launch_sign_t<DCOR_DGP_BERNOULLI>(c, reps, out, stream);
+    case DCOR_DGP_MIX_GAUSSIAN: return launch_sign_t<DCOR_DGP_MIX_GAUSSIAN>(c, reps, out, stream);
     default: return launch_sign_t<DCOR_DGP_BOUNDED_FACTOR>(c, reps, out, stream);
   }
 }
@@ -762,6 +793,7 @@ int launch_sign_fused_codes(const SignConst& c, int64_t reps, int64_t chunk, con
   switch (c.g.dgp) {
     case DCOR_DGP_GAUSSIAN: return launch_codes_t<DCOR_DGP_GAUSSIAN>(c, reps, chunk, bf, out, stream);
     case DCOR_DGP_BERNOULLI: return launch_codes_t<DCOR_DGP_BERNOULLI>(c, reps, chunk, bf, out, stream);
+    case DCOR_DGP_MIX_GAUSSIAN: return launch_codes_t<DCOR_DGP_MIX_GAUSSIAN>(c, reps, chunk, bf, out, stream);
     default: return launch_codes_t<DCOR_DGP_BOUNDED_FACTOR>(c, reps, chunk, bf, out, stream);
   }
 }
@@ -790,6 +822,8 @@ int launch_subg_fused(const SubgConst& c, int64_t reps, dcor_rep_out* out, void*
       hipLaunchKernelGGL(k_subg_fused<DCOR_DGP_GAUSSIAN>, g, b, 0, (hipStream_t)stream, c, out); break;
     case DCOR_DGP_BERNOULLI:
       hipLaunchKernelGGL(k_subg_fused<DCOR_DGP_BERNOULLI>, g, b, 0, (hipStream_t)stream, c, out); break;
+    case DCOR_DGP_MIX_GAUSSIAN:
+      hipLaunchKernelGGL(k_subg_fused<DCOR_DGP_MIX_GAUSSIAN>, g, b, 0, (hipStream_t)stream, c, out); break;
     default:
       hipLaunchKernelGGL(k_subg_fused<DCOR_DGP_BOUNDED_FACTOR>, g, b, 0, (hipStream_t)stream, c, out);
   }

@@ -14,7 +14,7 @@ LIB_PATH = os.path.join(_HERE, "libdcor.so")
 
 DCOR_OK, DCOR_EINVAL, DCOR_EKLT1, DCOR_EHIP, DCOR_ENOMEM, DCOR_ENODEV = 0, 1, 2, 3, 4, 5
 FAMILY_SIGN, FAMILY_SUBG = 0, 1
-DGP_GAUSSIAN, DGP_BERNOULLI, DGP_BOUNDED_FACTOR = 0, 1, 2
+DGP_GAUSSIAN, DGP_BERNOULLI, DGP_BOUNDED_FACTOR, DGP_MIX_GAUSSIAN = 0, 1, 2, 3
 MODE_AUTO, MODE_NORMAL, MODE_LAPLACE = 0, 1, 2
 SITE_DGP_A, SITE_DGP_B, SITE_FLIP, SITE_NI_LAP, SITE_SCALAR, SITE_MIX_Z, SITE_MIX_L, SITE_PERM = 1, 2, 3, 4, 5, 6, 7, 8
 
@@ -41,6 +41,8 @@ class Cell(C.Structure):
         ("eta1", C.c_double), ("eta2", C.c_double),
         ("normalise", C.c_int32), ("ci_mode", C.c_int32), ("nsim", C.c_int64),
         ("seed", C.c_uint64),
+        ("mix_mu0", C.c_double * 2), ("mix_sigma0", C.c_double * 2),
+        ("mix_mu1", C.c_double * 2), ("mix_sigma1", C.c_double * 2), ("mix_pi", C.c_double),
     ]
 
 

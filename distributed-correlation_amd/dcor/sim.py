@@ -31,7 +31,7 @@ class CellSpec:
     eps1: float
     eps2: float
     family: str = "sign"            # "sign" (vert-cor.R) or "subG" (ver-cor-subG.R)
-    dgp: str = "gaussian"           # "gaussian" | "bernoulli" | "bounded_factor"
+    dgp: str = "gaussian"           # "gaussian" | "bernoulli" | "bounded_factor" | "mix_gaussian"
     alpha: float = 0.05
     mu: Sequence[float] = (0.0, 0.0)
     sigma: Sequence[float] = (1.0, 1.0)
@@ -41,12 +41,19 @@ class CellSpec:
     ci_mode: str = "auto"
     nsim: int = 1000
     seed: int = 2025
+    # gen_mix_gaussian arguments (ver-cor-subG.R:113-116 defaults)
+    mix_mu0: Sequence[float] = (0.0, 0.0)
+    mix_sigma0: Sequence[float] = (1.0, 1.0)
+    mix_mu1: Sequence[float] = (3.0, 3.0)
+    mix_sigma1: Sequence[float] = (2.0, 0.5)
+    pi_mix: float = 0.5
 
     def to_c(self) -> _lib.Cell:
         c = _lib.Cell()
         c.family = _lib.FAMILY_SUBG if self.family == "subG" else _lib.FAMILY_SIGN
         c.dgp = {"gaussian": _lib.DGP_GAUSSIAN, "bernoulli": _lib.DGP_BERNOULLI,
-                 "bounded_factor": _lib.DGP_BOUNDED_FACTOR}[self.dgp]
+                 "bounded_factor": _lib.DGP_BOUNDED_FACTOR,
+                 "mix_gaussian": _lib.DGP_MIX_GAUSSIAN}[self.dgp]
         c.n = int(self.n)
         c.rho, c.eps1, c.eps2, c.alpha = float(self.rho), float(self.eps1), float(self.eps2), float(self.alpha)
         c.mu[0], c.mu[1] = float(self.mu[0]), float(self.mu[1])
@@ -56,6 +63,10 @@ class CellSpec:
         c.ci_mode = _lib.mode_code(self.ci_mode)
         c.nsim = int(self.nsim)
         c.seed = int(self.seed) & 0xFFFFFFFFFFFFFFFF
+        for name, v in (("mix_mu0", self.mix_mu0), ("mix_sigma0", self.mix_sigma0),
+                        ("mix_mu1", self.mix_mu1), ("mix_sigma1", self.mix_sigma1)):
+            getattr(c, name)[0], getattr(c, name)[1] = float(v[0]), float(v[1])
+        c.mix_pi = float(self.pi_mix)
         return c
 
 
@@ -168,9 +179,13 @@ def run_sim_one_subG(n, rho, eps1, eps2, dgp_fun="bounded_factor", dgp_args=None
                      alpha=0.05, use_subG=True, ci_mode="auto", seed=2025) -> dict:
     """run_sim_one of ver-cor-subG.R:159-222.  use_subG=FALSE routes to the sign family."""
     args = dict(dgp_args or {})
+    mix = {}
+    if dgp_fun == "mix_gaussian":  # gen_mix_gaussian(mu0, sigma0, mu1, sigma1, pi_mix)
+        mix = {k2: args[k1] for k1, k2 in (("mu0", "mix_mu0"), ("sigma0", "mix_sigma0"), ("mu1", "mix_mu1"),
+                                           ("sigma1", "mix_sigma1"), ("pi_mix", "pi_mix")) if k1 in args}
     cell = CellSpec(n=n, rho=rho, eps1=eps1, eps2=eps2, family="subG" if use_subG else "sign",
                     dgp=dgp_fun, alpha=alpha, ci_mode=ci_mode, seed=seed,
-                    mu=args.get("mu", (0.0, 0.0)), sigma=args.get("sigma", (1.0, 1.0)))
+                    mu=args.get("mu", (0.0, 0.0)), sigma=args.get("sigma", (1.0, 1.0)), **mix)
     return run_cell(cell, B)
 
 

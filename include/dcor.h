@@ -39,7 +39,8 @@ extern "C" {
 #define DCOR_ENODEV 5  /* no gfx950 device visible                                     */
 
 enum { DCOR_FAMILY_SIGN = 0, DCOR_FAMILY_SUBG = 1 };
-enum { DCOR_DGP_GAUSSIAN = 0, DCOR_DGP_BERNOULLI = 1, DCOR_DGP_BOUNDED_FACTOR = 2 };
+enum { DCOR_DGP_GAUSSIAN = 0, DCOR_DGP_BERNOULLI = 1, DCOR_DGP_BOUNDED_FACTOR = 2,
+       DCOR_DGP_MIX_GAUSSIAN = 3 /* gen_mix_gaussian, ver-cor-subG.R:113-133 */ };
 enum { DCOR_MODE_AUTO = 0, DCOR_MODE_NORMAL = 1, DCOR_MODE_LAPLACE = 2 };
 
 /* One (distribution, rho, eps, n) grid cell.  Replaces one row of
@@ -57,6 +58,11 @@ typedef struct dcor_cell {
   int32_t ci_mode;        /* DCOR_MODE_*, vert-cor.R:294-296                           */
   int64_t nsim;           /* mixquant draws (1000; 2000 in real-data-sims.R:161)       */
   uint64_t seed;          /* per-cell seed (R: 1e6 + i, vert-cor.R:552): Philox key    */
+  /* DCOR_DGP_MIX_GAUSSIAN (ver-cor-subG.R:113-116; R defaults mu0 (0,0), sigma0 (1,1),
+   * mu1 (3,3), sigma1 (2,.5), pi_mix .5): label ~ Bern(pi_mix), (X, Y) ~ mvrnorm of that
+   * component with correlation rho, then pmax(pmin(., 1), -1). */
+  double mix_mu0[2], mix_sigma0[2], mix_mu1[2], mix_sigma1[2];
+  double mix_pi;
 } dcor_cell;
 
 /* Per-replicate result: the six numbers of one row of run_sim_one's `detail`

@@ -578,8 +578,13 @@ void orc_gen_laplace(uint64_t seed, int64_t rep, int site, int64_t count, double
 /* ------------------------------------------- fused replicate restatement - */
 static void gen_xy(const dcor_cell* c, int64_t rep, double* X, double* Y, double* lap_local) {
   const int64_t n = c->n;
-  double A[4];
+  double A[4], XA[2][4];
   if (c->dgp == DCOR_DGP_GAUSSIAN) orc_mvrnorm_factor(c->mu, c->sigma, c->rho, A);
+  if (c->dgp == DCOR_DGP_MIX_GAUSSIAN) {  /* ver-cor-subG.R:119-122 */
+    orc_mvrnorm_factor(c->mix_mu0, c->mix_sigma0, c->rho, XA[0]);
+    orc_mvrnorm_factor(c->mix_mu1, c->mix_sigma1, c->rho, XA[1]);
+  }
+  const double T24 = ceil(c->mix_pi * 16777216.0);
   const double cU = sqrt(3.0 * c->rho), cE = sqrt(3.0 * (1.0 - c->rho));
   const double p11 = 0.25 + c->rho / 4, p10 = 0.25 - c->rho / 4, p01 = p10;
   for (int64_t i = 0; i < n; ++i) {
@@ -590,6 +595,20 @@ static void gen_xy(const dcor_cell* c, int64_t rep, double* X, double* Y, double
       orc_normal_pair(w, &z1, &z2);
       X[i] = c->mu[0] + (A[0] * z1 + A[1] * z2);
       Y[i] = c->mu[1] + (A[2] * z1 + A[3] * z2);
+    } else if (c->dgp == DCOR_DGP_MIX_GAUSSIAN) {
+      /* gen_mix_gaussian (ver-cor-subG.R:113-133): label = rbinom(1, pi_mix) from the 24
+       * bits the normal pair leaves unused, u24 < ceil(pi * 2^24); component mvrnorm;
+       * rows iid (the sample.int shuffle keeps the iid-mixture law); clip to [-1, 1]. */
+      blk(c->seed, (uint32_t)i, (uint32_t)rep, DCOR_SITE_DGP_A, w);
+      double z1, z2;
+      orc_normal_pair(w, &z1, &z2);
+      const uint32_t u24 = ((w[1] & 0xFFFu) << 12) | (w[3] & 0xFFFu);
+      const int lab = (double)u24 < T24;
+      const double* mu = lab ? c->mix_mu1 : c->mix_mu0;
+      const double* a = XA[lab];
+      const double x = mu[0] + (a[0] * z1 + a[1] * z2), y = mu[1] + (a[2] * z1 + a[3] * z2);
+      X[i] = fmax(fmin(x, 1.0), -1.0);
+      Y[i] = fmax(fmin(y, 1.0), -1.0);
     } else if (c->dgp == DCOR_DGP_BERNOULLI) {
       blk(c->seed, (uint32_t)(i >> 1), (uint32_t)rep, DCOR_SITE_DGP_A, w);
       const int b = 2 * (int)(i & 1);
@@ -612,6 +631,11 @@ static void gen_xy(const dcor_cell* c, int64_t rep, double* X, double* Y, double
       lap_local[i] = orc_unit_laplace(orc_u53(w2[2], w2[3]));
     }
   }
+}
+
+/* The DGP draws of replicate `rep` of a cell (test hook for the DGP laws). */
+void orc_gen_xy(const void* cellp, int64_t rep, double* X, double* Y) {
+  gen_xy((const dcor_cell*)cellp, rep, X, Y, NULL);
 }
 
 int orc_sim_rep(const void* cellp, int64_t rep, double out[6]) {

@@ -92,6 +92,9 @@ double orc_lambda_from_priv(double lo, double hi, double mean, double sd);
 double orc_lambda_receiver_from_noise(double lam_s, double lam_o, double eps_s, double delta);
 
 /* ---- DGPs from explicit uniforms / normals -------------------------------- */
+/* X, Y of replicate `rep` of a dcor_cell from the fused engine's draw streams. */
+void orc_gen_xy(const void* cellp, int64_t rep, double* X, double* Y);
+
 /* MASS::mvrnorm, 2-d (vert-cor.R:389-394): X = mu + A z, A = V diag(sqrt(ev)). */
 void orc_mvrnorm_factor(const double mu[2], const double sigma[2], double rho, double A[4]);
 void orc_mvrnorm_apply(const double* z1, const double* z2, int64_t n, const double mu[2],

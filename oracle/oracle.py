@@ -49,6 +49,7 @@ _sigs = {
     "orc_lambda_from_priv": (C.c_double, [C.c_double] * 4),
     "orc_lambda_receiver_from_noise": (C.c_double, [C.c_double] * 4),
     "orc_mvrnorm_factor": (None, [_D, _D, C.c_double, _D]),
+    "orc_gen_xy": (None, [C.c_void_p, C.c_int64, _D, _D]),
     "orc_mvrnorm_apply": (None, [_D, _D, C.c_int64, _D, _D, _D, _D]),
     "orc_gen_bernoulli": (None, [_D, _D, C.c_int64, C.c_double, _D, _D]),
     "orc_gen_bounded_factor": (None, [_D, _D, _D, C.c_int64, C.c_double, _D, _D]),
@@ -218,3 +219,12 @@ def perm(seed, site, rep, n, count):
     out = np.zeros(count, dtype=np.int32)
     lib.orc_perm(seed, site, rep, n, count, out.ctypes.data_as(_I32))
     return out
+
+
+def gen_xy(cell_struct, rep):
+    """DGP draws (X, Y) of replicate `rep` of a dcor_cell (ctypes struct)."""
+    X = np.zeros(cell_struct.n)
+    Y = np.zeros(cell_struct.n)
+    lib.orc_gen_xy(C.cast(C.pointer(cell_struct), C.c_void_p), rep, X.ctypes.data_as(_D),
+                   Y.ctypes.data_as(_D))
+    return X, Y

@@ -113,6 +113,11 @@ FUSED_CELLS = [
     dict(n=2500, rho=0.3, eps1=0.5, eps2=0.5, family="subG", dgp="gaussian"),
     dict(n=1600, rho=0.8, eps1=1.0, eps2=1.0, family="sign", dgp="gaussian", ci_mode="laplace"),
     dict(n=1000, rho=0.4, eps1=1.0, eps2=1.0, family="sign", dgp="gaussian", normalise=False),
+    # gen_mix_gaussian (ver-cor-subG.R:113-133): R defaults, and a non-dyadic pi_mix
+    dict(n=5500, rho=0.6, eps1=5.0, eps2=1.0, family="subG", dgp="mix_gaussian"),
+    dict(n=3001, rho=0.4, eps1=1.0, eps2=1.0, family="sign", dgp="mix_gaussian", pi_mix=0.3,
+         mix_mu1=(0.5, -0.5), mix_sigma1=(0.7, 1.3)),
+    dict(n=2000, rho=0.2, eps1=1.0, eps2=1.0, family="sign", dgp="mix_gaussian", normalise=False),
 ]
 
 

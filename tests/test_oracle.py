@@ -291,3 +291,29 @@ def test_fused_oracle_statistics():
     cov_int = np.mean((out[:, 4] <= 0.5) & (0.5 <= out[:, 5]))
     assert 0.85 < cov_ni <= 1.0 and 0.85 < cov_int <= 1.0
     assert abs(np.mean(out[:, 0]) - 0.5) < 0.1 and abs(np.mean(out[:, 3]) - 0.5) < 0.1
+
+
+def test_mix_gaussian_dgp_law():
+    """gen_mix_gaussian (ver-cor-subG.R:113-133) in the oracle's draw streams: the label rate,
+    the clipped marginal means and the clip masses match the mixture's closed forms."""
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "distributed-correlation_amd"))
+    from scipy import stats
+    from dcor.sim import CellSpec
+    n = 400_000
+    for pi, mu1, s1 in ((0.5, (3.0, 3.0), (2.0, 0.5)), (0.3, (0.5, -0.5), (0.7, 1.3))):
+        cell = CellSpec(n=n, rho=0.4, eps1=1.0, eps2=1.0, family="subG", dgp="mix_gaussian", pi_mix=pi,
+                        mix_mu1=mu1, mix_sigma1=s1, seed=99)
+        X, Y = O.gen_xy(cell.to_c(), 7)
+        assert X.min() >= -1.0 and X.max() <= 1.0 and Y.min() >= -1.0 and Y.max() <= 1.0
+        for v, j in ((X, 0), (Y, 1)):
+            comps = [(1 - pi, 0.0, 1.0), (pi, mu1[j], s1[j])]
+            def clipped_mean(m, s):   # E[clip(N(m, s^2), -1, 1)]
+                a, b = (-1 - m) / s, (1 - m) / s
+                return (-stats.norm.cdf(a) + stats.norm.sf(b)
+                        + m * (stats.norm.cdf(b) - stats.norm.cdf(a)) - s * (stats.norm.pdf(b) - stats.norm.pdf(a)))
+            mean = sum(w * clipped_mean(m, s) for w, m, s in comps)
+            top = sum(w * stats.norm.sf((1 - m) / s) for w, m, s in comps)
+            assert abs(v.mean() - mean) < 5e-3, (pi, j, v.mean(), mean)
+            assert abs(np.mean(v == 1.0) - top) < 4e-3, (pi, j)
