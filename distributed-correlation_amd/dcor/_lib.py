@@ -142,6 +142,13 @@ def _load() -> C.CDLL:
         raise ImportError(
             f"{LIB_PATH} is missing: build the gfx950 engine first "
             "(python -c 'import __graft_entry__ as g; g.build()'); there is no CPU fallback")
+    # One HIP runtime per process: torch (the device-memory / stream plumbing) ships its own
+    # libamdhip64; loading it before libdcor.so makes the engine bind to that same runtime
+    # whichever of `import dcor` / `import torch` the caller writes first.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     lib = C.CDLL(LIB_PATH)
     for name, (res, args) in SIGNATURES.items():
         f = getattr(lib, name)
