@@ -110,19 +110,25 @@ dp_sd <- function(x, lo, hi, eps1, eps2) {
 }
 
 ## Fused grid: run_sim_one over many cells in one .Call (replaces mclapply).
-## family: "sign" (vert-cor.R) or "subG" (ver-cor-subG.R); dgp: "gaussian"/"bernoulli"/"bounded_factor".
+## family: "sign" (vert-cor.R) or "subG" (ver-cor-subG.R);
+## dgp: "gaussian"/"bernoulli"/"bounded_factor"/"mix_gaussian" (gen_mix_gaussian, whose
+## arguments come in `mix`, defaults as ver-cor-subG.R:113-116).
 dcor_grid <- function(design, B = 250, alpha = 0.05, mu = c(0, 0), sigma = c(1, 1),
                       family = "sign", dgp = "gaussian", ci_mode = "auto", normalise = TRUE,
-                      detail = FALSE) {
+                      detail = FALSE,
+                      mix = list(mu0 = c(0, 0), sigma0 = c(1, 1), mu1 = c(3, 3),
+                                 sigma1 = c(2, 0.5), pi_mix = 0.5)) {
   nc <- nrow(design)
   fam <- rep(match(family, c("sign", "subG")) - 1L, length.out = nc)
-  dg <- rep(match(dgp, c("gaussian", "bernoulli", "bounded_factor")) - 1L, length.out = nc)
+  dg <- rep(match(dgp, c("gaussian", "bernoulli", "bounded_factor", "mix_gaussian")) - 1L,
+            length.out = nc)
+  mixv <- as.double(c(mix$mu0, mix$sigma0, mix$mu1, mix$sigma1, mix$pi_mix))
   r <- .Call("dcor_R_grid_run", fam, dg, as.double(design$n), as.double(design$rho),
              as.double(design$eps1), as.double(design$eps2), rep(as.double(alpha), nc),
              rep(mu[1], nc), rep(mu[2], nc), rep(sigma[1], nc), rep(sigma[2], nc),
              rep(as.logical(normalise), nc),
              rep(match(ci_mode, c("auto", "normal", "laplace")) - 1L, nc),
-             as.double(1e6 + seq_len(nc)), as.double(B), as.logical(detail))
+             as.double(1e6 + seq_len(nc)), as.double(B), as.logical(detail), mixv)
   s <- matrix(r[[1]], ncol = 5, byrow = TRUE,
               dimnames = list(NULL, c("mse", "bias", "var", "coverage", "ci_length")))
   summ <- data.frame(design[rep(seq_len(nc), each = 2), , drop = FALSE],

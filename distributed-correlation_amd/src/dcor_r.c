@@ -117,7 +117,10 @@ SEXP dcor_R_ci_INT_subG(SEXP X, SEXP Y, SEXP e1, SEXP e2, SEXP eta1, SEXP eta2, 
 /* One grid on the current device: cells given as parallel vectors (one element per cell). */
 SEXP dcor_R_grid_run(SEXP family, SEXP dgp, SEXP n, SEXP rho, SEXP eps1, SEXP eps2, SEXP alpha,
                      SEXP mu1, SEXP mu2, SEXP s1, SEXP s2, SEXP normalise, SEXP mode, SEXP seed,
-                     SEXP B, SEXP want_detail) {
+                     SEXP B, SEXP want_detail, SEXP mix) {
+  /* mix: gen_mix_gaussian's mu0[2], sigma0[2], mu1[2], sigma1[2], pi_mix (ver-cor-subG.R:113-116) */
+  if (XLENGTH(mix) != 9) Rf_error("dcor_grid: mix must hold 9 numbers");
+  const double* mx = REAL(mix);
   const int nc = LENGTH(n);
   const long long b = (long long)Rf_asReal(B);
   dcor_cell* cells = (dcor_cell*)R_alloc(nc, sizeof(dcor_cell));
@@ -137,6 +140,11 @@ SEXP dcor_R_grid_run(SEXP family, SEXP dgp, SEXP n, SEXP rho, SEXP eps1, SEXP ep
     cells[i].ci_mode = INTEGER(mode)[i];
     cells[i].nsim = 1000;
     cells[i].seed = (uint64_t)REAL(seed)[i];
+    cells[i].mix_mu0[0] = mx[0]; cells[i].mix_mu0[1] = mx[1];
+    cells[i].mix_sigma0[0] = mx[2]; cells[i].mix_sigma0[1] = mx[3];
+    cells[i].mix_mu1[0] = mx[4]; cells[i].mix_mu1[1] = mx[5];
+    cells[i].mix_sigma1[0] = mx[6]; cells[i].mix_sigma1[1] = mx[7];
+    cells[i].mix_pi = mx[8];
   }
   SEXP acc = PROTECT(allocVector(RAWSXP, (R_xlen_t)nc * 2 * sizeof(dcor_accum)));
   SEXP det = PROTECT(Rf_asLogical(want_detail) ? allocVector(REALSXP, (R_xlen_t)nc * b * 6)
@@ -167,7 +175,7 @@ static const R_CallMethodDef calls[] = {
     {"dcor_R_ci_INT_signflip", (DL_FUNC)&dcor_R_ci_INT_signflip, 12},
     {"dcor_R_correlation_NI_subG", (DL_FUNC)&dcor_R_correlation_NI_subG, 13},
     {"dcor_R_ci_INT_subG", (DL_FUNC)&dcor_R_ci_INT_subG, 16},
-    {"dcor_R_grid_run", (DL_FUNC)&dcor_R_grid_run, 16},
+    {"dcor_R_grid_run", (DL_FUNC)&dcor_R_grid_run, 17},
     {NULL, NULL, 0}};
 
 void R_init_dcor_r(DllInfo* dll) {
