@@ -179,6 +179,10 @@ int make_sign(int64_t n, double eps1, double eps2, double alpha, int normalise, 
   const double es = std::exp(eps_s);
   c.pflip = es / (es + 1.0);                                             // :174
   c.flipT = u32_threshold(c.pflip);
+  {
+    const double t = std::ceil(c.pflip * 16777216.0);  // exact scaling
+    c.flipT24 = t >= 16777216.0 ? 16777216u : (t > 0 ? (uint32_t)t : 0u);
+  }
   c.scale_Z = 2.0 * (es + 1.0) / (nd * (es - 1.0) * eps_r);              // :186-187
   c.coefZ = (es + 1.0) / (nd * (es - 1.0));                              // :190-191
   const double q = (es - 1.0) / (es + 1.0);

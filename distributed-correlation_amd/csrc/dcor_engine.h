@@ -41,6 +41,7 @@ struct SignConst {
   double inv_k, crit, sqrt_k;
   double pflip;                               // exp(eps_s)/(exp(eps_s)+1)
   uint64_t flipT;                             // ceil(pflip*2^32): flip <=> u32 < flipT
+  uint32_t flipT24, pad3;                     // ceil(pflip*2^24): Gaussian DGP spare-bit flips
   double scale_Z, coefZ, q2, ratio, inv_sqrt_n, eps_r, w_laplace;
   double cbase_x, cinv_x, cbase_y, cinv_y;    // monotone code maps of clip(x), clip(y)
 };

@@ -15,13 +15,29 @@ namespace dcor {
 template <int DGP> struct Dgp;
 
 template <> struct Dgp<DCOR_DGP_GAUSSIAN> {  // MASS::mvrnorm (vert-cor.R:389-394)
-  static __device__ __forceinline__ void one(const DgpConst& g, uint32_t i, uint32_t rep,
-                                             uint32_t k0, uint32_t k1, double& x, double& y) {
+  // The sample's 24 bits Box-Muller leaves unused (low 12 of w1 and of w3) carry the sign
+  // family's INT flip for this DGP (spare_flip): u24 < ceil(p 2^24) (vert-cor.R:175).
+  static constexpr bool spare_flip = true;
+  static __device__ __forceinline__ void one_u24(const DgpConst& g, uint32_t i, uint32_t rep,
+                                                 uint32_t k0, uint32_t k1, double& x, double& y,
+                                                 uint32_t& u24) {
     const U4 w = draw(i, rep, DCOR_SITE_DGP_A, k0, k1);
     double z1, z2;
     normal_pair(w, &z1, &z2);
     x = g.mu0 + (g.a00 * z1 + g.a01 * z2);
     y = g.mu1 + (g.a10 * z1 + g.a11 * z2);
+    u24 = ((w.w1 & 0xFFFu) << 12) | (w.w3 & 0xFFFu);
+  }
+  static __device__ __forceinline__ void one(const DgpConst& g, uint32_t i, uint32_t rep,
+                                             uint32_t k0, uint32_t k1, double& x, double& y) {
+    uint32_t u24;
+    one_u24(g, i, rep, k0, k1, x, y, u24);
+  }
+  static __device__ __forceinline__ void quad_u24(const DgpConst& g, uint32_t i0, uint32_t rep,
+                                                  uint32_t k0, uint32_t k1, double* x, double* y,
+                                                  uint32_t* u24) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) one_u24(g, i0 + q, rep, k0, k1, x[q], y[q], u24[q]);
   }
   static __device__ __forceinline__ void quad(const DgpConst& g, uint32_t i0, uint32_t rep,
                                               uint32_t k0, uint32_t k1, double* x, double* y) {
@@ -35,6 +51,7 @@ template <> struct Dgp<DCOR_DGP_GAUSSIAN> {  // MASS::mvrnorm (vert-cor.R:389-39
 };
 
 template <> struct Dgp<DCOR_DGP_BERNOULLI> {  // gen_bernoulli (vert-cor.R:78-98), 2 samples/block
+  static constexpr bool spare_flip = false;  // INT flips from the FLIP site
   // u = wa*2^-32 < 0.5 <=> wa < 2^31; v < thr <=> wb < ceil(thr*2^32) (exact).
   static __device__ __forceinline__ void from_words(const DgpConst& g, uint32_t wa, uint32_t wb,
                                                     double& x, double& y) {
@@ -63,6 +80,7 @@ template <> struct Dgp<DCOR_DGP_BERNOULLI> {  // gen_bernoulli (vert-cor.R:78-98
 };
 
 template <> struct Dgp<DCOR_DGP_BOUNDED_FACTOR> {  // gen_bounded_factor (ver-cor-subG.R:141-154)
+  static constexpr bool spare_flip = false;  // INT flips from the FLIP site
   static __device__ __forceinline__ void one_lap(const DgpConst& g, uint32_t i, uint32_t rep,
                                                  uint32_t k0, uint32_t k1, double& x, double& y,
                                                  double* lap) {
@@ -85,6 +103,7 @@ template <> struct Dgp<DCOR_DGP_BOUNDED_FACTOR> {  // gen_bounded_factor (ver-co
 };
 
 template <> struct Dgp<DCOR_DGP_MIX_GAUSSIAN> {  // gen_mix_gaussian (ver-cor-subG.R:113-133)
+  static constexpr bool spare_flip = false;  // INT flips from the FLIP site
   // One DGP_A block: Box-Muller from the top 52 bits of (w0,w1), (w2,w3); the component label
   // from the 24 bits Box-Muller leaves unused (low 12 of w1 and of w3): u24 < ceil(pi 2^24)
   // (exact for pi = .5, the R default; |bias| < 2^-24 otherwise).  Row shuffling
@@ -241,9 +260,19 @@ __global__ __launch_bounds__(DCOR_BLOCK) void k_sign_pass1(SignConst c,
   const int64_t ngrp = (c.n + 3) / 4;
   for (int64_t g4 = tid; g4 < ngrp; g4 += DCOR_BLOCK) {
     const uint32_t i0 = (uint32_t)(4 * g4);
-    const U4 fw = draw((uint32_t)g4, rep, DCOR_SITE_FLIP, c.k0, c.k1);
     double x[4], y[4];
-    Dgp<DGP>::quad(c.g, i0, rep, c.k0, c.k1, x, y);
+    uint32_t fl[4];  // INT flip bits (vert-cor.R:175)
+    if constexpr (Dgp<DGP>::spare_flip) {
+      uint32_t u24[4];
+      Dgp<DGP>::quad_u24(c.g, i0, rep, c.k0, c.k1, x, y, u24);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) fl[q] = u24[q] < c.flipT24 ? 1u : 0u;
+    } else {
+      const U4 fw = draw((uint32_t)g4, rep, DCOR_SITE_FLIP, c.k0, c.k1);
+      Dgp<DGP>::quad(c.g, i0, rep, c.k0, c.k1, x, y);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) fl[q] = ((uint64_t)word(fw, q) < c.flipT) ? 1u : 0u;
+    }
     uint32_t rec[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
@@ -251,7 +280,7 @@ __global__ __launch_bounds__(DCOR_BLOCK) void k_sign_pass1(SignConst c,
       if ((int64_t)(i0 + q) < c.n) { v[0] += xc; v[1] += xc * xc; v[2] += yc; v[3] += yc * yc; }
       const uint32_t qx = code16(xc, c.cbase_x, c.cinv_x, 65535.0);
       const uint32_t qy = code16(yc, c.cbase_y, c.cinv_y, 32767.0);
-      const uint32_t f = ((uint64_t)word(fw, q) < c.flipT) ? 1u : 0u;
+      const uint32_t f = fl[q];
       rec[q] = qx | (qy << 16) | (f << 31);
     }
     if ((int64_t)i0 + 3 < c.n) {
@@ -624,9 +653,16 @@ __global__ __launch_bounds__(DCOR_BLOCK) void k_sign_fused(SignConst c, dcor_rep
   bool bad_ni = false, bad_int = false;
   DD sT{0.0, 0.0}, sT2{0.0, 0.0};
   long long core = 0;
-  auto signs = [&](uint32_t i, int& nx, int& ny, int& ix, int& iy, bool& bni) {
+  auto signs = [&](uint32_t i, int& nx, int& ny, int& ix, int& iy, bool& bni, int& flip) {
     double x, y;
-    Dgp<DGP>::one(c.g, i, rep, c.k0, c.k1, x, y);
+    if constexpr (Dgp<DGP>::spare_flip) {
+      uint32_t u24;
+      Dgp<DGP>::one_u24(c.g, i, rep, c.k0, c.k1, x, y, u24);
+      flip = u24 < c.flipT24 ? 1 : -1;
+    } else {
+      Dgp<DGP>::one(c.g, i, rep, c.k0, c.k1, x, y);
+      flip = fl.get(i, rep, c.k0, c.k1, c.flipT);
+    }
     if (c.normalise) {
       const double xc = rclip_fin(x, c.L), yc = rclip_fin(y, c.L);
       nx = sgn_std(xc, s.muNx, s.sdNx, bni);
@@ -646,10 +682,10 @@ __global__ __launch_bounds__(DCOR_BLOCK) void k_sign_fused(SignConst c, dcor_rep
     const int64_t i0 = j * c.m;
     for (int r = 0; r < c.m; ++r) {
       const uint32_t i = (uint32_t)(i0 + r);
-      int nx, ny, ix, iy;
-      signs(i, nx, ny, ix, iy, bad_ni);
+      int nx, ny, ix, iy, flip;
+      signs(i, nx, ny, ix, iy, bad_ni, flip);
       cx += nx; cy += ny;
-      core += fl.get(i, rep, c.k0, c.k1, c.flipT) * ix * iy;
+      core += flip * ix * iy;
     }
     const U4 w = draw((uint32_t)j, rep, DCOR_SITE_NI_LAP, c.k0, c.k1);
     const double xt = (double)cx / c.md + c.bx * unit_laplace(u53(w.w0, w.w1));
@@ -659,10 +695,10 @@ __global__ __launch_bounds__(DCOR_BLOCK) void k_sign_fused(SignConst c, dcor_rep
     dd_acc(sT2, T * T);
   }
   for (int64_t i = c.k * c.m + tid; i < c.n; i += DCOR_BLOCK) {
-    int nx, ny, ix, iy;
+    int nx, ny, ix, iy, flip;
     bool ignore = false;
-    signs((uint32_t)i, nx, ny, ix, iy, ignore);
-    core += fl.get((uint32_t)i, rep, c.k0, c.k1, c.flipT) * ix * iy;
+    signs((uint32_t)i, nx, ny, ix, iy, ignore, flip);
+    core += flip * ix * iy;
   }
   DD d2[2] = {sT, sT2};
   block_sum_dd<2>(d2, red);

@@ -682,8 +682,15 @@ int orc_sim_rep(const void* cellp, int64_t rep, double out[6]) {
       uint8_t* fl = (uint8_t*)malloc((size_t)n);
       for (int64_t i = 0; i < n; ++i) {
         uint32_t w[4];
-        blk(c->seed, (uint32_t)(i >> 2), (uint32_t)rep, DCOR_SITE_FLIP, w);
-        fl[i] = ((double)w[i & 3] * 0x1p-32 < p) ? 1 : 0;
+        if (c->dgp == DCOR_DGP_GAUSSIAN) {
+          /* the 24 bits of sample i's normal-pair block that Box-Muller leaves unused */
+          blk(c->seed, (uint32_t)i, (uint32_t)rep, DCOR_SITE_DGP_A, w);
+          const uint32_t u24 = ((w[1] & 0xFFFu) << 12) | (w[3] & 0xFFFu);
+          fl[i] = ((double)u24 * 0x1p-24 < p) ? 1 : 0;
+        } else {
+          blk(c->seed, (uint32_t)(i >> 2), (uint32_t)rep, DCOR_SITE_FLIP, w);
+          fl[i] = ((double)w[i & 3] * 0x1p-32 < p) ? 1 : 0;
+        }
       }
       int md;
       st = orc_ci_int_signflip(X, Y, n, c->eps1, c->eps2, c->alpha, c->ci_mode, c->normalise,
