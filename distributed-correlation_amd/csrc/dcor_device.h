@@ -11,6 +11,9 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#define DCOR_TABLE_ATTR __device__
+#include "dcor_tables.h"
+
 #define DCOR_BLOCK 256
 #define DCOR_WAVES (DCOR_BLOCK / 64)
 
@@ -53,59 +56,39 @@ __device__ __forceinline__ double u53(uint32_t a, uint32_t b) {
   return __longlong_as_double((long long)bits) - (1.0 - 0x1p-53);
 }
 
-// fdlibm-style log for positive normal x (same code as oracle/orc_log).
+// Division-free log for positive normal x (same code as oracle/orc_log): x = 2^k z with
+// z in [0.6875, 1.375), r = fma(z, 1/c, -1) against a 128-entry table, log x = k ln2 +
+// log c + log1p(r) with a degree-8 polynomial (|r| < 2^-7).  ~14 fp64 ops; <= 2.7 ulp.
 __device__ __forceinline__ double dlog(double x) {
-  const double ln2_hi = 6.93147180369123816490e-01, ln2_lo = 1.90821492927058770002e-10,
-               Lg1 = 6.666666666666735130e-01, Lg2 = 3.999999999940941908e-01,
-               Lg3 = 2.857142874366239149e-01, Lg4 = 2.222219843214978396e-01,
-               Lg5 = 1.818357216161805012e-01, Lg6 = 1.531383769920937332e-01,
-               Lg7 = 1.479819860511658591e-01;
-  const uint64_t bits = __double_as_longlong(x);
-  int32_t hx = (int32_t)(bits >> 32);
-  const uint32_t lx = (uint32_t)bits;
-  int32_t k = ((hx >> 20) & 0x7ff) - 1023;
-  hx &= 0x000fffff;
-  const int32_t i = (hx + 0x95f64) & 0x100000;
-  hx |= (i ^ 0x3ff00000);
-  k += (i >> 20);
-  const double mnt = __longlong_as_double((long long)(((uint64_t)(uint32_t)hx << 32) | lx));
-  const double f = mnt - 1.0;
-  const double s = f / (2.0 + f);
-  const double dk = (double)k;
-  const double z = s * s, w = z * z;
-  const double t1 = w * fma(w, fma(w, Lg6, Lg4), Lg2);
-  const double t2 = z * fma(w, fma(w, fma(w, Lg7, Lg5), Lg3), Lg1);
-  const double R = t2 + t1;
-  const double hfsq = 0.5 * f * f;
-  return dk * ln2_hi - ((hfsq - (s * (hfsq + R) + dk * ln2_lo)) - f);
+  const uint64_t ix = (uint64_t)__double_as_longlong(x);
+  const uint64_t tmp = ix - 0x3fe6000000000000ull;
+  const int i = (int)((tmp >> 45) & 127u);
+  const int64_t k = (int64_t)tmp >> 52;
+  const double z = __longlong_as_double((long long)(ix - (tmp & (0xfffull << 52))));
+  const double invc = dcor_log_tab[i][0], logc = dcor_log_tab[i][1];
+  const double r = fma(z, invc, -1.0), kd = (double)k, r2 = r * r;
+  double p = fma(r, DCOR_LOG1P_C8, DCOR_LOG1P_C7);
+  p = fma(r, p, DCOR_LOG1P_C6);
+  p = fma(r, p, DCOR_LOG1P_C5);
+  p = fma(r, p, DCOR_LOG1P_C4);
+  p = fma(r, p, DCOR_LOG1P_C3);
+  p = fma(r, p, DCOR_LOG1P_C2);
+  const double w = fma(kd, DCOR_LN2_HI, logc), lo = fma(kd, DCOR_LN2_LO, r2 * p);
+  return w + (r + lo);
 }
 
-// sin(pi t), cos(pi t) for t with 2t exactly representable (same as oracle/orc_sincospi).
+// sin(pi t), cos(pi t) for t in [0, 2] (same code as oracle/orc_sincospi): j = rint(64 t),
+// d = (64 t - j) pi / 64 (|d| <= pi/128), angle addition with the 129-entry table of
+// sin / cos(pi j / 64) and degree-7 / 8 polynomials in d.  ~19 fp64 ops.
 __device__ __forceinline__ void dsincospi(double t, double* sp, double* cp) {
-  const double S1 = -1.66666666666666324348e-01, S2 = 8.33333333332248946124e-03,
-               S3 = -1.98412698298579493134e-04, S4 = 2.75573137070700676789e-06,
-               S5 = -2.50507602534068634195e-08, S6 = 1.58969099521155010221e-10,
-               C1 = 4.16666666666666019037e-02, C2 = -1.38888888888741095749e-03,
-               C3 = 2.48015872894767294178e-05, C4 = -2.75573143513906633035e-07,
-               C5 = 2.08757232129817482790e-09, C6 = -1.13596475577881948265e-11,
-               PIO2_HI = 1.57079632679489655800e+00, PIO2_LO = 6.12323399573676603587e-17;
-  const double t2 = 2.0 * t;
-  const double j = rint(t2);
-  const double r = t2 - j;
-  const double x = fma(r, PIO2_HI, r * PIO2_LO);
-  const double z = x * x;
-  const double v = z * x;
-  const double rs = fma(z, fma(z, fma(z, S6, S5), S4), S3);
-  const double sn = x + v * fma(z, fma(z, rs, S2), S1);
-  const double rc = z * fma(z, fma(z, fma(z, fma(z, fma(z, C6, C5), C4), C3), C2), C1);
-  const double hz = 0.5 * z;
-  const double wc = 1.0 - hz;
-  const double cs = wc + (((1.0 - wc) - hz) + z * rc);
-  const int q = ((int)j) & 3;
-  const double a = (q & 1) ? cs : sn;   // |sin| source
-  const double b = (q & 1) ? sn : cs;   // |cos| source
-  *sp = (q & 2) ? -a : a;
-  *cp = ((q + 1) & 2) ? -b : b;
+  const double t64 = t * 64.0, jd = rint(t64), r = t64 - jd;
+  const int j = (int)jd;
+  const double d = fma(r, DCOR_PI64_HI, r * DCOR_PI64_LO), z = d * d;
+  const double sd = fma(d * z, fma(z, fma(z, DCOR_SIN_S7, DCOR_SIN_S5), DCOR_SIN_S3), d);
+  const double cm1 = z * fma(z, fma(z, fma(z, DCOR_COS_C8, DCOR_COS_C6), DCOR_COS_C4), DCOR_COS_C2);
+  const double S = dcor_sincospi_tab[j][0], C = dcor_sincospi_tab[j][1];
+  *sp = fma(S, cm1, fma(C, sd, S));
+  *cp = fma(C, cm1, fma(-S, sd, C));
 }
 
 __device__ __forceinline__ double unit_laplace(double u) {
