@@ -162,6 +162,11 @@ int make_sign(int64_t n, double eps1, double eps2, double alpha, int normalise, 
   if (md > 0x7fffffff) return fail(DCOR_EINVAL, "batch size m too large");
   c.n = n; c.m = (int32_t)md; c.k = kd >= 1 ? (int64_t)kd : 0;
   c.nd = nd; c.md = md; c.kd = kd;
+  {
+    int e = 0;
+    c.md_pow2 = (std::frexp(md, &e) == 0.5) ? 1 : 0;  // md = 2^(e-1): count / md == count * 2^(1-e)
+    c.inv_md = c.md_pow2 ? std::ldexp(1.0, 1 - e) : 0.0;
+  }
   c.normalise = normalise ? 1 : 0;
   const double L = std::sqrt(2.0 * std::log(nd));                        // :212
   c.L = L;
@@ -406,6 +411,8 @@ int dcor_sim_launch(const dcor_cell* cell, int64_t rep_begin, int64_t rep_count,
     }
     code_map(cx, rx, 65536.0, &k.cbase_x, &k.cinv_x);
     code_map(cy, ry, 32768.0, &k.cbase_y, &k.cinv_y);
+    k.cinv_xf = (float)k.cinv_x; k.cnb_xf = (float)(-k.cbase_x * k.cinv_x);
+    k.cinv_yf = (float)k.cinv_y; k.cnb_yf = (float)(-k.cbase_y * k.cinv_y);
     const char* var = std::getenv("DCOR_SIGN_KERNEL");
     const bool regen = (var && std::strcmp(var, "regen") == 0) || !c.normalise;
     if (c.dgp == DCOR_DGP_BERNOULLI && !(var && std::strcmp(var, "regen") == 0) && rep_count > 0) {

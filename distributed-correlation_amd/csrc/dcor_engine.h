@@ -41,9 +41,12 @@ struct SignConst {
   double inv_k, crit, sqrt_k;
   double pflip;                               // exp(eps_s)/(exp(eps_s)+1)
   uint64_t flipT;                             // ceil(pflip*2^32): flip <=> u32 < flipT
-  uint32_t flipT24, pad3;                     // ceil(pflip*2^24): Gaussian DGP spare-bit flips
+  uint32_t flipT24;                           // ceil(pflip*2^24): Gaussian DGP spare-bit flips
+  int32_t md_pow2;                            // m is a power of two: count / m == count * inv_md
+  double inv_md;
   double scale_Z, coefZ, q2, ratio, inv_sqrt_n, eps_r, w_laplace;
   double cbase_x, cinv_x, cbase_y, cinv_y;    // monotone code maps of clip(x), clip(y)
+  float cinv_xf, cnb_xf, cinv_yf, cnb_yf;     // the same maps in fp32: q = fma(v, inv, -base*inv)
 };
 
 // Sub-G family: correlation_NI_subG + ci_INT_subG (ver-cor-subG.R:25-108).

@@ -227,12 +227,19 @@ __device__ __forceinline__ void sign_finish(const SignConst& c, uint32_t rep, DD
 // threshold's code.  Results equal the two-pass algorithm's exactly.  Each thread
 // generates groups of 4 consecutive samples (one flip block per group, 16-B slab stores).
 // Two launches per replicate chunk (pass 1, pass 2); scratch = chunk * n * 4 B.
-__device__ __forceinline__ uint32_t code16(double v, double base, double inv, double top) {
-  double t = (v - base) * inv;
-  t = fmin(fmax(t, 0.0), top);  // NaN -> 0 (a NaN sample makes mu NaN: flagged)
-  return (uint32_t)t;
+// q(v) = clamp(fma(float(v), inv, -base*inv), 0, top) in fp32: every step (round to float,
+// fma with inv > 0, clamp, truncation) is monotone non-decreasing, which is all the sign
+// decision needs; the 2^15-2^16 code levels sit far above fp32 resolution.
+__device__ __forceinline__ uint32_t code16(double v, float inv, float nb, float top) {
+  const float t = fmaf((float)v, inv, nb);
+  return (uint32_t)__builtin_amdgcn_fmed3f(t, 0.0f, top);  // NaN -> 0 (a NaN mu is flagged)
 }
 __device__ __forceinline__ int sgnq(uint32_t q, uint32_t qm) { return (q > qm) - (q < qm); }
+// sign(q - qm) for 16-bit codes as one subtract + one v_med3_i32 (clamp to [-1, 1]).
+__device__ __forceinline__ int sgnd(uint32_t q, uint32_t qm) {
+  const int d = (int)q - (int)qm;
+  return min(max(d, -1), 1);
+}
 
 template <int DGP>
 __device__ __forceinline__ void exact_signs(const SignConst& c, const SignStd& s, uint32_t i,
@@ -278,8 +285,8 @@ __global__ __launch_bounds__(DCOR_BLOCK) void k_sign_pass1(SignConst c,
     for (int q = 0; q < 4; ++q) {
       const double xc = rclip_fin(x[q], c.L), yc = rclip_fin(y[q], c.L);
       if ((int64_t)(i0 + q) < c.n) { v[0] += xc; v[1] += xc * xc; v[2] += yc; v[3] += yc * yc; }
-      const uint32_t qx = code16(xc, c.cbase_x, c.cinv_x, 65535.0);
-      const uint32_t qy = code16(yc, c.cbase_y, c.cinv_y, 32767.0);
+      const uint32_t qx = code16(xc, c.cinv_xf, c.cnb_xf, 65535.0f);
+      const uint32_t qy = code16(yc, c.cinv_yf, c.cnb_yf, 32767.0f);
       const uint32_t f = fl[q];
       rec[q] = qx | (qy << 16) | (f << 31);
     }
@@ -330,22 +337,26 @@ __global__ __launch_bounds__(DCOR_BLOCK) void k_sign_pass2(SignConst c,
   // sign(d/sd) == sign(d) needs sd < 2^900 (no underflow of the quotient); else exact path.
   const bool force_exact = !(s.sdNx < 0x1p900 && s.sdNy < 0x1p900 && s.sdIx < 0x1p900 &&
                              s.sdIy < 0x1p900);
-  const uint32_t qNx = code16(s.muNx, c.cbase_x, c.cinv_x, 65535.0);
-  const uint32_t qIx = code16(s.muIx, c.cbase_x, c.cinv_x, 65535.0);
-  const uint32_t qNy = code16(s.muNy, c.cbase_y, c.cinv_y, 32767.0);
-  const uint32_t qIy = code16(s.muIy, c.cbase_y, c.cinv_y, 32767.0);
+  const uint32_t qNx = code16(s.muNx, c.cinv_xf, c.cnb_xf, 65535.0f);
+  const uint32_t qIx = code16(s.muIx, c.cinv_xf, c.cnb_xf, 65535.0f);
+  const uint32_t qNy = code16(s.muNy, c.cinv_yf, c.cnb_yf, 32767.0f);
+  const uint32_t qIy = code16(s.muIy, c.cinv_yf, c.cnb_yf, 32767.0f);
   bool bad_ni = thr_nan, bad_int = thr_nan;
   DD sT{0.0, 0.0}, sT2{0.0, 0.0};
   long long core = 0;
   // Fast path: signs from codes (branch-free).  A sample whose code ties a threshold's
   // code is flagged and fixed up afterwards by exact regeneration (rolled loop, rare).
+  // sign(xc - mu) from codes: sgnd in {-1, 0, 1}; 0 is a tie (the code cannot decide).
+  // Bit 0 of a sign is set iff it is nonzero, so the AND of the four flags a tie.
   auto fast = [&](uint32_t w, int& cx, int& cy, int& cc) -> bool {
     const uint32_t qx = w & 0xffffu, qy = (w >> 16) & 0x7fffu;
-    const int f = (w >> 31) ? 1 : -1;
-    cx += sgnq(qx, qNx);
-    cy += sgnq(qy, qNy);
-    cc += f * sgnq(qx, qIx) * sgnq(qy, qIy);
-    return force_exact || qx == qNx || qx == qIx || qy == qNy || qy == qIy;
+    const int sNx = sgnd(qx, qNx), sNy = sgnd(qy, qNy), sIx = sgnd(qx, qIx), sIy = sgnd(qy, qIy);
+    cx += sNx;
+    cy += sNy;
+    const int p = __mul24(sIx, sIy);
+    const int m = (int)(w >> 31) - 1;  // 0 for flip S = 1, -1 for S = 0: (2S - 1) p
+    cc += (p ^ m) - m;
+    return ((sNx & sNy & sIx & sIy) & 1) == 0;
   };
   auto fixup = [&](int64_t i, uint32_t w, int& cx, int& cy, int& cc, bool& bni) {
     const uint32_t qx = w & 0xffffu, qy = (w >> 16) & 0x7fffu;
@@ -358,8 +369,12 @@ __global__ __launch_bounds__(DCOR_BLOCK) void k_sign_pass2(SignConst c,
   };
   auto batch_T = [&](int64_t j, int cx, int cy) {
     const U4 w = draw((uint32_t)j, rep, DCOR_SITE_NI_LAP, c.k0, c.k1);   // vert-cor.R:230-231
-    const double xt = (double)cx / c.md + c.bx * unit_laplace(u53(w.w0, w.w1));
-    const double yt = (double)cy / c.md + c.by * unit_laplace(u53(w.w2, w.w3));
+    // mean of m signs = count / m (exact quotient for the configs' m); a power-of-two m
+    // divides by an exact multiply
+    const double mx = c.md_pow2 ? (double)cx * c.inv_md : (double)cx / c.md;
+    const double my = c.md_pow2 ? (double)cy * c.inv_md : (double)cy / c.md;
+    const double xt = mx + c.bx * unit_laplace(u53(w.w0, w.w1));
+    const double yt = my + c.by * unit_laplace(u53(w.w2, w.w3));
     const double T = c.md * xt * yt;                                     // vert-cor.R:233
     dd_acc(sT, T);
     dd_acc(sT2, T * T);
@@ -384,6 +399,7 @@ __global__ __launch_bounds__(DCOR_BLOCK) void k_sign_pass2(SignConst c,
       uint32_t tie = 0;
 #pragma unroll
       for (int q = 0; q < 8; ++q) tie |= (fast(word(q < 4 ? w0 : w1, q & 3), cx, cy, cc) ? 1u : 0u) << q;
+      if (force_exact) tie = 0xFFu;
       if (tie) {
 #pragma unroll 1
         for (int q = 0; q < 8; ++q)
@@ -398,11 +414,12 @@ __global__ __launch_bounds__(DCOR_BLOCK) void k_sign_pass2(SignConst c,
       const int64_t i0 = j * c.m;
       bool any = false;
       for (int r = 0; r < c.m; ++r) any |= fast(slab[i0 + r], cx, cy, cc);
+      any |= force_exact;
       if (any) {
         for (int r = 0; r < c.m; ++r) {
           const uint32_t w = slab[i0 + r];
           int dx = 0, dy = 0, dc = 0;
-          if (fast(w, dx, dy, dc)) fixup(i0 + r, w, cx, cy, cc, bad_ni);
+          if (fast(w, dx, dy, dc) || force_exact) fixup(i0 + r, w, cx, cy, cc, bad_ni);
         }
       }
       core += cc;
@@ -413,7 +430,7 @@ __global__ __launch_bounds__(DCOR_BLOCK) void k_sign_pass2(SignConst c,
     int dx = 0, dy = 0, cc = 0;
     bool ignore = false;  // NI never reads the tail
     const uint32_t w = slab[i];
-    if (fast(w, dx, dy, cc)) fixup(i, w, dx, dy, cc, ignore);
+    if (fast(w, dx, dy, cc) || force_exact) fixup(i, w, dx, dy, cc, ignore);
     core += cc;
   }
   DD d2[2] = {sT, sT2};
