@@ -60,11 +60,13 @@ __device__ __forceinline__ double u53(uint32_t a, uint32_t b) {
 // z in [0.6875, 1.375), r = fma(z, 1/c, -1) against a 128-entry table, log x = k ln2 +
 // log c + log1p(r) with a degree-8 polynomial (|r| < 2^-7).  ~14 fp64 ops; <= 2.7 ulp.
 __device__ __forceinline__ double dlog(double x) {
+  // The offset's low word is 0, so the reduction lives in the high word (32-bit ops only).
   const uint64_t ix = (uint64_t)__double_as_longlong(x);
-  const uint64_t tmp = ix - 0x3fe6000000000000ull;
-  const int i = (int)((tmp >> 45) & 127u);
-  const int64_t k = (int64_t)tmp >> 52;
-  const double z = __longlong_as_double((long long)(ix - (tmp & (0xfffull << 52))));
+  const uint32_t hi = (uint32_t)(ix >> 32), tmp = hi - 0x3fe60000u;
+  const int i = (int)((tmp >> 13) & 127u);
+  const int k = (int)tmp >> 20;
+  const double z = __longlong_as_double(
+      (long long)(((uint64_t)(hi - (tmp & 0xfff00000u)) << 32) | (uint32_t)ix));
   const double invc = dcor_log_tab[i][0], logc = dcor_log_tab[i][1];
   const double r = fma(z, invc, -1.0), kd = (double)k, r2 = r * r;
   double p = fma(r, DCOR_LOG1P_C8, DCOR_LOG1P_C7);

@@ -376,8 +376,8 @@ __global__ __launch_bounds__(DCOR_BLOCK) void k_sign_pass2(SignConst c,
     const double xt = mx + c.bx * unit_laplace(u53(w.w0, w.w1));
     const double yt = my + c.by * unit_laplace(u53(w.w2, w.w3));
     const double T = c.md * xt * yt;                                     // vert-cor.R:233
-    dd_acc(sT, T);
-    dd_acc(sT2, T * T);
+    ks_acc(sT, T);  // compensated (error ~ k 2^-106): the T mean / sd inputs
+    ks_acc(sT2, T * T);
   };
   if (c.m == 8) {
     // headline geometry: one thread = one batch = two 16-B loads; the next batch's loads
