@@ -68,6 +68,17 @@ def pmc_traffic(path=os.path.join(ROOT, "profiles", "r01_headline_summary.json")
         return None
 
 
+def issue_util(path=os.path.join(ROOT, "profiles", "r01_serial_summary.json")):
+    """Measured VALU issue utilisation of the sign kernels (rocprofv3 PMC, chunks profiled
+    serially: SQ_INSTS_VALU / (256 CUs x GRBM_GUI_ACTIVE/8)), or None."""
+    try:
+        ks = json.load(open(path))["kernels"]
+        return {name.split("::")[1].split("<")[0]: round(v["valu_issue_util"], 3)
+                for name, v in ks.items() if "k_sign_pass" in name and "valu_issue_util" in v}
+    except (OSError, KeyError, ValueError, IndexError):
+        return None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -161,7 +172,11 @@ def main():
                          "kernel": "k_sign_pass1 + k_sign_pass2 (one simulate() call)",
                          "kernel_ms_avg": kern_ms,
                          "work_units_per_rep": W,
-                         "note": "achieved = R * W_rep(SURVEY §8d pinned weights) * 2 / kernel time"},
+                         "valu_issue_util": issue_util(),
+                         "note": "achieved = R * W_rep(SURVEY §8d pinned weights) * 2 / kernel time; "
+                                 "frac > 1 means fewer instructions than the pinned weights assume; "
+                                 "valu_issue_util = measured fraction of the VALU issue ceiling "
+                                 "(profiles/r01_serial_summary.json)"},
             "summary": {"coverage_NI": summ["NI"]["coverage"], "coverage_INT": summ["INT"]["coverage"],
                         "ci_len_NI": summ["NI"]["ci_length"], "ci_len_INT": summ["INT"]["ci_length"]},
         }

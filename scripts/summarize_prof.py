@@ -62,19 +62,48 @@ for kname, cs in counters.items():
         k["valu_active_frac_of_wave_cycles"] = avg["SQ_ACTIVE_INST_VALU"] / avg["SQ_WAVE_CYCLES"]
     if "GRBM_GUI_ACTIVE" in avg and k.get("avg_ns"):
         k["effective_clock_ghz"] = avg["GRBM_GUI_ACTIVE"] / 8 / k["avg_ns"]
+        # VALU issue ceiling: one wave64 VALU instruction per 4 cycles per SIMD = 1 per cycle
+        # per CU (256 CUs); meaningful for kernels profiled without overlap (PIPE=0 runs)
+        if "SQ_INSTS_VALU" in avg:
+            k["valu_issue_util"] = avg["SQ_INSTS_VALU"] / (256 * avg["GRBM_GUI_ACTIVE"] / 8)
     mix = {c: avg[c] for c in avg if c.startswith("SQ_INSTS_VALU_")}
     if mix:
         k["valu_mix_wave_instructions"] = mix
 
+# Wall span of each simulate() call from the kernel trace: the sign kernels of one call run on
+# two streams, so per-kernel averages overlap; bench.py's kernel_ms_avg is this span (events
+# around the call).  A call = the dispatches between consecutive k_accumulate launches.
+trace = os.path.join(src, "prof_trace", "run_kernel_trace.csv")
+if os.path.exists(trace):
+    rows = sorted(csv.DictReader(open(trace)), key=lambda r: int(r["Start_Timestamp"]))
+    spans, cur = [], []
+    for r in rows:
+        name = short(r["Kernel_Name"])
+        if "k_accumulate" in name and "merge" not in name:
+            if cur:
+                spans.append((max(e for _, e in cur) - min(s for s, _ in cur)) / 1e6)
+            cur = []
+        elif "k_sign_" in name or "k_subg_" in name:
+            cur.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"])))
+    if spans:
+        out["simulate_call_span_ms"] = {"calls": len(spans), "avg": sum(spans) / len(spans),
+                                        "min": min(spans), "max": max(spans)}
+
 json.dump(out, open(os.path.join(dst, f"{tag}_summary.json"), "w"), indent=1, sort_keys=True)
 lines = [f"# rocprofv3 summary `{tag}`", "",
-         "| kernel | calls | avg µs | % time | VGPR | HBM read B (corr.) | HBM write B | VALU active / wave-cycles | clock GHz |",
-         "|---|---|---|---|---|---|---|---|---|"]
+         "| kernel | calls | avg µs | % time | VGPR | HBM read B (corr.) | HBM write B | VALU active / wave-cycles | VALU issue util | clock GHz |",
+         "|---|---|---|---|---|---|---|---|---|---|"]
 for kname, k in sorted(out["kernels"].items(), key=lambda kv: -kv[1].get("pct_time", 0)):
     def f(x, fmt="{:.3g}"):
         return fmt.format(x) if isinstance(x, (int, float)) else "—"
     lines.append(f"| {kname} | {k.get('calls', '—')} | {f(k.get('avg_ns', 0) / 1e3)} | {f(k.get('pct_time'))} | "
                  f"{f(k.get('vgpr'))} | {f(k.get('hbm_read_bytes_corrected'))} | {f(k.get('hbm_write_bytes'))} | "
-                 f"{f(k.get('valu_active_frac_of_wave_cycles'))} | {f(k.get('effective_clock_ghz'))} |")
+                 f"{f(k.get('valu_active_frac_of_wave_cycles'))} | {f(k.get('valu_issue_util'))} | "
+                 f"{f(k.get('effective_clock_ghz'))} |")
+if "simulate_call_span_ms" in out:
+    sp = out["simulate_call_span_ms"]
+    lines += ["", f"simulate() call span from the trace (first sign-kernel start to last end, "
+                  f"{sp['calls']} calls): avg {sp['avg']:.3f} ms, min {sp['min']:.3f}, max {sp['max']:.3f} "
+                  "-- compare bench.py roofline.kernel_ms_avg (HIP events around the same call)."]
 open(os.path.join(dst, f"{tag}_summary.md"), "w").write("\n".join(lines) + "\n")
 print("\n".join(lines))
