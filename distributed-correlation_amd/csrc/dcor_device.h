@@ -52,8 +52,10 @@ __device__ __forceinline__ U4 draw(uint32_t idx, uint32_t rep, uint32_t site, ui
 // (2x+1) * 2^-53 with x the top 52 bits of (a, b): in (0, 1), exact.  Built from bits:
 // as_double(1.x) - (1 - 2^-53) is exact (Sterbenz), one v_add_f64.
 __device__ __forceinline__ double u53(uint32_t a, uint32_t b) {
-  const uint64_t bits = 0x3FF0000000000000ull | ((uint64_t)a << 20) | (uint64_t)(b >> 12);
-  return __longlong_as_double((long long)bits) - (1.0 - 0x1p-53);
+  // high word 0x3ff00000 | a >> 12, low word a << 20 | b >> 12: two v_alignbit_b32
+  const uint32_t lo = __builtin_amdgcn_alignbit(a, b, 12u);
+  const uint32_t hi = __builtin_amdgcn_alignbit(0x3ffu, a, 12u);
+  return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo)) - (1.0 - 0x1p-53);
 }
 
 // Division-free log for positive normal x (same code as oracle/orc_log): x = 2^k z with
@@ -79,11 +81,11 @@ __device__ __forceinline__ double dlog(double x) {
   return w + (r + lo);
 }
 
-// sin(pi t), cos(pi t) for t in [0, 2] (same code as oracle/orc_sincospi): j = rint(64 t),
-// d = (64 t - j) pi / 64 (|d| <= pi/128), angle addition with the 129-entry table of
-// sin / cos(pi j / 64) and degree-7 / 8 polynomials in d.  ~19 fp64 ops.
-__device__ __forceinline__ void dsincospi(double t, double* sp, double* cp) {
-  const double t64 = t * 64.0, jd = rint(t64), r = t64 - jd;
+// sin(pi t), cos(pi t) for t in [0, 2], given t64 = 64 t (same code as oracle/orc_sincospi):
+// j = rint(t64), d = (t64 - j) pi / 64 (|d| <= pi/128), angle addition with the 129-entry
+// table of sin / cos(pi j / 64) and degree-7 / 8 polynomials in d.  ~19 fp64 ops.
+__device__ __forceinline__ void dsincospi64(double t64, double* sp, double* cp) {
+  const double jd = rint(t64), r = t64 - jd;
   const int j = (int)jd;
   const double d = fma(r, DCOR_PI64_HI, r * DCOR_PI64_LO), z = d * d;
   const double sd = fma(d * z, fma(z, fma(z, DCOR_SIN_S7, DCOR_SIN_S5), DCOR_SIN_S3), d);
@@ -115,14 +117,28 @@ __device__ __forceinline__ double sqrt_pos(double x) {
   return fma(d, h, g);
 }
 
-__device__ __forceinline__ void normal_pair(const U4& w, double* z1, double* z2) {
+// Box-Muller polar pair: radius r = sqrt(-2 log u1) and (cos, sin)(2 pi u2).
+__device__ __forceinline__ void normal_polar(const U4& w, double* r, double* s, double* c) {
   const double u1 = u53(w.w0, w.w1);
   const double u2 = u53(w.w2, w.w3);
-  const double r = sqrt_pos(-2.0 * dlog(u1));
-  double s, c;
-  dsincospi(2.0 * u2, &s, &c);
+  *r = sqrt_pos(-2.0 * dlog(u1));
+  dsincospi64(u2 * 128.0, s, c);  // t = 2 u2, 64 t exact
+}
+
+__device__ __forceinline__ void normal_pair(const U4& w, double* z1, double* z2) {
+  double r, s, c;
+  normal_polar(w, &r, &s, &c);
   *z1 = r * c;
   *z2 = r * s;
+}
+
+// mu + A (r c, r s) of MASS::mvrnorm (vert-cor.R:389-394) as one fused form per coordinate:
+// fma(r, fma(a01, s, a00 c), mu0) (same code as oracle/orc_mvn_polar).
+__device__ __forceinline__ void mvn_polar(double r, double s, double c, double mu0, double mu1,
+                                          double a00, double a01, double a10, double a11,
+                                          double* x, double* y) {
+  *x = fma(r, fma(a01, s, a00 * c), mu0);
+  *y = fma(r, fma(a11, s, a10 * c), mu1);
 }
 
 // ------------------------------------------------------------- R helpers

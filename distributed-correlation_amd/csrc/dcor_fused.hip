@@ -22,10 +22,9 @@ template <> struct Dgp<DCOR_DGP_GAUSSIAN> {  // MASS::mvrnorm (vert-cor.R:389-39
                                                  uint32_t k0, uint32_t k1, double& x, double& y,
                                                  uint32_t& u24) {
     const U4 w = draw(i, rep, DCOR_SITE_DGP_A, k0, k1);
-    double z1, z2;
-    normal_pair(w, &z1, &z2);
-    x = g.mu0 + (g.a00 * z1 + g.a01 * z2);
-    y = g.mu1 + (g.a10 * z1 + g.a11 * z2);
+    double r, s, cs;
+    normal_polar(w, &r, &s, &cs);
+    mvn_polar(r, s, cs, g.mu0, g.mu1, g.a00, g.a01, g.a10, g.a11, &x, &y);
     u24 = ((w.w1 & 0xFFFu) << 12) | (w.w3 & 0xFFFu);
   }
   static __device__ __forceinline__ void one(const DgpConst& g, uint32_t i, uint32_t rep,
@@ -112,15 +111,16 @@ template <> struct Dgp<DCOR_DGP_MIX_GAUSSIAN> {  // gen_mix_gaussian (ver-cor-su
   static __device__ __forceinline__ void one(const DgpConst& g, uint32_t i, uint32_t rep,
                                              uint32_t k0, uint32_t k1, double& x, double& y) {
     const U4 w = draw(i, rep, DCOR_SITE_DGP_A, k0, k1);
-    double z1, z2;
-    normal_pair(w, &z1, &z2);
+    double r, s, cs;
+    normal_polar(w, &r, &s, &cs);
     const uint32_t u24 = ((w.w1 & 0xFFFu) << 12) | (w.w3 & 0xFFFu);
     const int c = u24 < g.T24 ? 1 : 0;   // label ~ rbinom(1, pi_mix): 1 -> component 1
     const double mx = c ? g.xmu[1][0] : g.xmu[0][0], my = c ? g.xmu[1][1] : g.xmu[0][1];
     const double a00 = c ? g.xa[1][0] : g.xa[0][0], a01 = c ? g.xa[1][1] : g.xa[0][1];
     const double a10 = c ? g.xa[1][2] : g.xa[0][2], a11 = c ? g.xa[1][3] : g.xa[0][3];
-    x = rclip_fin(mx + (a00 * z1 + a01 * z2), 1.0);
-    y = rclip_fin(my + (a10 * z1 + a11 * z2), 1.0);
+    mvn_polar(r, s, cs, mx, my, a00, a01, a10, a11, &x, &y);
+    x = rclip_fin(x, 1.0);
+    y = rclip_fin(y, 1.0);
   }
   static __device__ __forceinline__ void quad(const DgpConst& g, uint32_t i0, uint32_t rep,
                                               uint32_t k0, uint32_t k1, double* x, double* y) {

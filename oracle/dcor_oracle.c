@@ -497,9 +497,9 @@ double orc_log(double x) {
   return w + (r + lo);
 }
 
-/* sin(pi t), cos(pi t) for t in [0, 2] (dcor_device.h dsincospi). */
-void orc_sincospi(double t, double* sp, double* cp) {
-  const double t64 = t * 64.0, jd = rint(t64), r = t64 - jd;
+/* sin(pi t), cos(pi t) for t in [0, 2] given t64 = 64 t (dcor_device.h dsincospi64). */
+void orc_sincospi(double t64, double* sp, double* cp) {
+  const double jd = rint(t64), r = t64 - jd;
   const int j = (int)jd;
   const double d = fma(r, DCOR_PI64_HI, r * DCOR_PI64_LO), z = d * d;
   const double sd = fma(d * z, fma(z, fma(z, DCOR_SIN_S7, DCOR_SIN_S5), DCOR_SIN_S3), d);
@@ -516,14 +516,29 @@ double orc_unit_laplace(double u) {
   return (up > 0) ? -g : g;
 }
 
-void orc_normal_pair(const uint32_t w[4], double* z1, double* z2) {
+/* Box-Muller polar pair: r = sqrt(-2 log u1), (sin, cos)(2 pi u2) (dcor_device.h normal_polar). */
+static void orc_normal_polar(const uint32_t w[4], double* r, double* s, double* c) {
   const double u1 = orc_u53(w[0], w[1]);
   const double u2 = orc_u53(w[2], w[3]);
-  const double r = sqrt(-2.0 * orc_log(u1));
-  double s, c;
-  orc_sincospi(2.0 * u2, &s, &c);
+  *r = sqrt(-2.0 * orc_log(u1));
+  orc_sincospi(u2 * 128.0, s, c);
+}
+
+void orc_normal_pair(const uint32_t w[4], double* z1, double* z2) {
+  double r, s, c;
+  orc_normal_polar(w, &r, &s, &c);
   *z1 = r * c;
   *z2 = r * s;
+}
+
+/* mu + A (r c, r s) of MASS::mvrnorm (vert-cor.R:389-394) as the engine fuses it
+ * (dcor_device.h mvn_polar). */
+static void orc_mvn_polar(const uint32_t w[4], const double mu[2], const double a[4], double* x,
+                          double* y) {
+  double r, s, c;
+  orc_normal_polar(w, &r, &s, &c);
+  *x = fma(r, fma(a[1], s, a[0] * c), mu[0]);
+  *y = fma(r, fma(a[3], s, a[2] * c), mu[1]);
 }
 
 static void blk(uint64_t seed, uint32_t idx, uint32_t rep, uint32_t site, uint32_t w[4]) {
@@ -567,22 +582,16 @@ static void gen_xy(const dcor_cell* c, int64_t rep, double* X, double* Y, double
     uint32_t w[4];
     if (c->dgp == DCOR_DGP_GAUSSIAN) {
       blk(c->seed, (uint32_t)i, (uint32_t)rep, DCOR_SITE_DGP_A, w);
-      double z1, z2;
-      orc_normal_pair(w, &z1, &z2);
-      X[i] = c->mu[0] + (A[0] * z1 + A[1] * z2);
-      Y[i] = c->mu[1] + (A[2] * z1 + A[3] * z2);
+      orc_mvn_polar(w, c->mu, A, &X[i], &Y[i]);
     } else if (c->dgp == DCOR_DGP_MIX_GAUSSIAN) {
       /* gen_mix_gaussian (ver-cor-subG.R:113-133): label = rbinom(1, pi_mix) from the 24
        * bits the normal pair leaves unused, u24 < ceil(pi * 2^24); component mvrnorm;
        * rows iid (the sample.int shuffle keeps the iid-mixture law); clip to [-1, 1]. */
       blk(c->seed, (uint32_t)i, (uint32_t)rep, DCOR_SITE_DGP_A, w);
-      double z1, z2;
-      orc_normal_pair(w, &z1, &z2);
       const uint32_t u24 = ((w[1] & 0xFFFu) << 12) | (w[3] & 0xFFFu);
       const int lab = (double)u24 < T24;
-      const double* mu = lab ? c->mix_mu1 : c->mix_mu0;
-      const double* a = XA[lab];
-      const double x = mu[0] + (a[0] * z1 + a[1] * z2), y = mu[1] + (a[2] * z1 + a[3] * z2);
+      double x, y;
+      orc_mvn_polar(w, lab ? c->mix_mu1 : c->mix_mu0, XA[lab], &x, &y);
       X[i] = fmax(fmin(x, 1.0), -1.0);
       Y[i] = fmax(fmin(y, 1.0), -1.0);
     } else if (c->dgp == DCOR_DGP_BERNOULLI) {

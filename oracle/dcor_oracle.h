@@ -110,7 +110,7 @@ void orc_gen_bounded_factor(const double* u, const double* e1, const double* e2,
 void   orc_philox4x32_10(const uint32_t ctr[4], uint32_t k0, uint32_t k1, uint32_t out[4]);
 double orc_u53(uint32_t a, uint32_t b);
 double orc_log(double x);
-void   orc_sincospi(double t, double* s, double* c);
+void   orc_sincospi(double t64, double* s, double* c);  /* sin, cos(pi t), t64 = 64 t in [0, 128] */
 double orc_unit_laplace(double u);
 void   orc_normal_pair(const uint32_t w[4], double* z1, double* z2);
 

@@ -51,7 +51,7 @@ def test_sincospi_accuracy():
     c = np.zeros(1)
     errs = []
     for v in t:
-        O.lib.orc_sincospi(float(v), s.ctypes.data_as(O._D), c.ctypes.data_as(O._D))
+        O.lib.orc_sincospi(float(v) * 64.0, s.ctypes.data_as(O._D), c.ctypes.data_as(O._D))  # takes 64 t
         errs.append(max(abs(s[0] - math.sin(math.pi * v)), abs(c[0] - math.cos(math.pi * v))))
     assert max(errs) < 1e-15
 
