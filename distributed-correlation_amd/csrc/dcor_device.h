@@ -474,4 +474,161 @@ __device__ __forceinline__ double value_select(const double (&v)[SEL_VPT], int p
   return res;
 }
 
+
+// ---------------------------------------------------- wave-level order statistic
+// One wavefront per replicate (the epilogue kernels): no workgroup barriers, so the four
+// waves of a workgroup finish four replicates independently.  Same value-binning scheme as
+// value_select: a min/max reduction, a 256-bin LDS histogram of the active keys, the bin
+// holding rank k is either ranked directly (<= 64 keys) or becomes the new active set
+// (iterate; each round removes at least one distinct value).  Infinite keys are peeled off
+// first.  Lanes of one wave see each other's LDS writes after wave_sync (in-order LDS).
+struct WaveSel {
+  uint32_t hist[256];
+  double cand[64];
+  int ncand;
+  int pad;
+  double res;
+};
+
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+__device__ __forceinline__ double wave_min(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o, 64));
+  return v;
+}
+__device__ __forceinline__ double wave_max(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
+  return v;
+}
+__device__ __forceinline__ int wave_sum_int(int v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// Monotone bin of v in [0, 255] for the active range [lo, hi]: by value when the range is
+// representable ((v - lo) * 256 / (hi - lo), computed on halves so it cannot overflow), else by
+// the order-preserving integer key of the double (tiny subnormal ranges).
+struct BinMap {
+  double lo, scale;
+  unsigned long long klo;
+  int sh;
+  bool by_value;
+  __device__ __forceinline__ int operator()(double v) const {
+    if (by_value) {
+      const double t = (0.5 * v - 0.5 * lo) * scale;
+      return t < 255.0 ? (int)t : 255;
+    }
+    return (int)((sel_key(v) - klo) >> sh);
+  }
+};
+
+// sort(active keys)[pos] (0-based) over VPL <= 32 keys per lane; NaN keys are never active.
+template <int VPL>
+__device__ __forceinline__ double wave_select(const double (&v)[VPL], int pos, WaveSel* ws) {
+  static_assert(VPL <= 32, "active keys are a 32-bit mask per lane");
+  const int lane = threadIdx.x & 63;
+  const double INF = __longlong_as_double(0x7FF0000000000000LL);
+  uint32_t act = 0;
+#pragma unroll
+  for (int s = 0; s < VPL; ++s) act |= (v[s] == v[s] ? 1u : 0u) << s;
+  const int nact = wave_sum_int(__popc(act));
+  int k = pos;
+  if (k < 0 || k >= nact) return dnan();
+  {  // peel -inf / +inf keys (binning needs a finite range)
+    uint32_t mlo = 0, mhi = 0;
+#pragma unroll
+    for (int s = 0; s < VPL; ++s) {
+      mlo |= (v[s] == -INF ? 1u : 0u) << s;
+      mhi |= (v[s] == INF ? 1u : 0u) << s;
+    }
+    const int nlo = wave_sum_int(__popc(mlo)), nhi = wave_sum_int(__popc(mhi));
+    if (k < nlo) return -INF;
+    if (k >= nact - nhi) return INF;
+    act &= ~(mlo | mhi);
+    k -= nlo;
+  }
+  for (int iter = 0; iter < 80; ++iter) {
+    double lo = INF, hi = -INF;
+#pragma unroll
+    for (int s = 0; s < VPL; ++s)
+      if ((act >> s) & 1u) { lo = fmin(lo, v[s]); hi = fmax(hi, v[s]); }
+    lo = wave_min(lo);
+    hi = wave_max(hi);
+    if (!(hi > lo)) return lo;  // every active key equal
+    BinMap bm;
+    bm.lo = lo;
+    const double h = 0.5 * hi - 0.5 * lo;
+    bm.scale = 128.0 / h;
+    bm.by_value = (h > 0.0) && (bm.scale < INF);
+    bm.klo = sel_key(lo);
+    {
+      const unsigned long long d = sel_key(hi) - bm.klo;
+      const int bits = 64 - __clzll((long long)d);
+      bm.sh = bits > 8 ? bits - 8 : 0;
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) ws->hist[4 * lane + q] = 0u;
+    if (lane == 0) ws->ncand = 0;
+    wave_sync();
+#pragma unroll
+    for (int s = 0; s < VPL; ++s)
+      if ((act >> s) & 1u) atomicAdd(&ws->hist[bm(v[s])], 1u);
+    wave_sync();
+    uint32_t hb[4], s4 = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) { hb[q] = ws->hist[4 * lane + q]; s4 += hb[q]; }
+    uint32_t inc = s4;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t t = __shfl_up(inc, o, 64);
+      if (lane >= o) inc += t;
+    }
+    const uint32_t ex = inc - s4;
+    int B = -1;
+    uint32_t cnt = 0, kk = 0;
+    if ((uint32_t)k >= ex && (uint32_t)k < inc) {
+      uint32_t base = ex;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        if (B < 0 && (uint32_t)k < base + hb[q]) { B = 4 * lane + q; cnt = hb[q]; kk = (uint32_t)k - base; }
+        base += hb[q];
+      }
+    }
+    const int owner = __ffsll((long long)__ballot(B >= 0)) - 1;
+    B = __shfl(B, owner, 64);
+    cnt = __shfl(cnt, owner, 64);
+    kk = __shfl(kk, owner, 64);
+    if (cnt <= 64) {  // rank the bin's keys directly
+#pragma unroll
+      for (int s = 0; s < VPL; ++s)
+        if (((act >> s) & 1u) && bm(v[s]) == B) ws->cand[atomicAdd(&ws->ncand, 1)] = v[s];
+      wave_sync();
+      if ((uint32_t)lane < cnt) {
+        const double x = ws->cand[lane];
+        uint32_t r = 0;
+        for (uint32_t j = 0; j < cnt; ++j) {
+          const double y = ws->cand[j];
+          r += (y < x) || (y == x && j < (uint32_t)lane);
+        }
+        if (r == kk) ws->res = x;
+      }
+      wave_sync();
+      const double res = ws->res;
+      wave_sync();
+      return res;
+    }
+    uint32_t keep = 0;  // the crowded bin becomes the active set
+#pragma unroll
+    for (int s = 0; s < VPL; ++s) keep |= (bm(v[s]) == B ? 1u : 0u) << s;
+    act &= keep;
+    k = (int)kk;
+  }
+  return dnan();
+}
+
 }  // namespace dcor

@@ -6,6 +6,9 @@
 // so the sample loops are straight-line code.  fp64 throughout (R `double`).
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+#include <cstring>
+
 #include "dcor_common.h"
 
 namespace dcor {
@@ -195,6 +198,29 @@ __device__ __forceinline__ void scalar_laplace(uint32_t rep, uint32_t k0, uint32
     lap[2 * threadIdx.x] = unit_laplace(u53(w.w0, w.w1));
     lap[2 * threadIdx.x + 1] = unit_laplace(u53(w.w2, w.w3));
   }
+}
+
+// Wave-level mixquant from Philox (one replicate per wave): the same elements as
+// mixquant_fused, VPL keys per lane.
+template <int VPL>
+__device__ __forceinline__ double wave_mixquant_fused(const MixConst& mx, double c, uint32_t rep,
+                                                      uint32_t k0, uint32_t k1, WaveSel* ws) {
+  const int lane = threadIdx.x & 63;
+  double val[VPL];
+#pragma unroll
+  for (int s = 0; s < VPL / 2; ++s) {
+    const int b = lane + 64 * s;  // Philox block b -> elements 2b, 2b+1
+    val[2 * s] = val[2 * s + 1] = dnan();
+    if (2 * b < mx.nsim) {
+      const U4 wz = draw((uint32_t)b, rep, DCOR_SITE_MIX_Z, k0, k1);
+      const U4 wl = draw((uint32_t)b, rep, DCOR_SITE_MIX_L, k0, k1);
+      double z0, z1;
+      normal_pair(wz, &z0, &z1);
+      val[2 * s] = z0 + c * unit_laplace(u53(wl.w0, wl.w1));
+      if (2 * b + 1 < mx.nsim) val[2 * s + 1] = z1 + c * unit_laplace(u53(wl.w2, wl.w3));
+    }
+  }
+  return wave_select<VPL>(val, mx.pos, ws);
 }
 
 // INT epilogue + CI write shared by the sign kernels (vert-cor.R:281-313).
@@ -446,6 +472,36 @@ __global__ __launch_bounds__(DCOR_BLOCK) void k_sign_pass2(SignConst c,
   }
 }
 
+// Wave-per-replicate epilogue (four replicates per workgroup, no workgroup barriers):
+// NI estimate/CI, INT estimate, mixquant, INT CI (vert-cor.R:233-254, 186-194, 281-313).
+template <int VPL>
+__global__ __launch_bounds__(DCOR_BLOCK) void k_sign_epilogue_w(SignConst c, int64_t nreps,
+                                                                const SignPartial* __restrict__ part,
+                                                                dcor_rep_out* out) {
+  __shared__ WaveSel wsel[DCOR_WAVES];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t r = (int64_t)blockIdx.x * DCOR_WAVES + wv;
+  if (r >= nreps) return;  // whole waves only
+  const uint32_t rep = (uint32_t)(c.rep_begin + r);
+  const U4 wz = draw(4u, rep, DCOR_SITE_SCALAR, c.k0, c.k1);  // SCALAR block 4: Z (vert-cor.R:188)
+  const double lapz = unit_laplace(u53(wz.w0, wz.w1));
+  const SignPartial p = part[r];
+  double o[6];
+  ni_sign_result(c, DD{p.sT[0], p.sT[1]}, DD{p.sT2[0], p.sT2[1]}, (p.flags & 1) != 0, o);
+  double rho, eta, se, cstar;
+  int_sign_point(c, p.core, lapz, rho, eta, se, cstar);
+  double w;
+  if (c.mode_normal)
+    w = wave_mixquant_fused<VPL>(c.mix, cstar, rep, c.k0, c.k1, &wsel[wv]) * se;
+  else
+    w = c.w_laplace;
+  o[3] = rho;
+  o[4] = sin(M_PI / 2.0 * rmax(eta - w, -1.0));
+  o[5] = sin(M_PI / 2.0 * rmin(eta + w, 1.0));
+  if (p.flags & 2) o[3] = o[4] = o[5] = dnan();
+  if (lane == 0) out[r] = dcor_rep_out{o[0], o[1], o[2], o[3], o[4], o[5]};
+}
+
 // Epilogue: NI estimate/CI, INT estimate, mixquant, INT CI (vert-cor.R:233-254, 186-194, 281-313).
 __global__ __launch_bounds__(DCOR_BLOCK) void k_sign_epilogue(SignConst c,
                                                               const SignPartial* __restrict__ part,
@@ -458,6 +514,21 @@ __global__ __launch_bounds__(DCOR_BLOCK) void k_sign_epilogue(SignConst c,
   const SignPartial p = part[blockIdx.x];
   sign_finish(c, rep, DD{p.sT[0], p.sT[1]}, DD{p.sT2[0], p.sT2[1]}, p.core, (p.flags & 1) != 0,
               (p.flags & 2) != 0, lap, &sel, out + blockIdx.x);
+}
+
+static inline void launch_sign_epilogue(const SignConst& c, int64_t nr, const SignPartial* part,
+                                        dcor_rep_out* out, hipStream_t st) {
+  static const int block_epi = [] {
+    const char* v = std::getenv("DCOR_EPILOGUE");
+    return v && std::strcmp(v, "block") == 0;
+  }();
+  const unsigned gw = (unsigned)((nr + DCOR_WAVES - 1) / DCOR_WAVES);
+  if (block_epi)
+    hipLaunchKernelGGL(k_sign_epilogue, dim3((unsigned)nr), dim3(DCOR_BLOCK), 0, st, c, part, out);
+  else if (c.mix.nsim <= 1024)
+    hipLaunchKernelGGL(k_sign_epilogue_w<16>, dim3(gw), dim3(DCOR_BLOCK), 0, st, c, nr, part, out);
+  else
+    hipLaunchKernelGGL(k_sign_epilogue_w<32>, dim3(gw), dim3(DCOR_BLOCK), 0, st, c, nr, part, out);
 }
 
 // ================================ Bernoulli sign family: bit planes (hot, exact) ===
@@ -829,8 +900,7 @@ static int launch_codes_t(SignConst c, int64_t reps, int64_t chunk, const CodesB
                        bf.slab[b], bf.sums[b]);
     hipLaunchKernelGGL(k_sign_pass2<DGP>, dim3((unsigned)nr), dim3(DCOR_BLOCK), 0, st[b], c,
                        bf.slab[b], bf.sums[b], part);
-    hipLaunchKernelGGL(k_sign_epilogue, dim3((unsigned)nr), dim3(DCOR_BLOCK), 0, st[b], c, part,
-                       out + r);
+    launch_sign_epilogue(c, nr, part, out + r, st[b]);
     if (int e = last_err()) return e;
   }
   if (two) {
@@ -860,8 +930,7 @@ int launch_sign_bern(SignConst c, int64_t reps, int64_t chunk, uint64_t* scratch
     c.rep_begin = rep0 + r;
     hipLaunchKernelGGL(k_sign_bern, dim3((unsigned)nr), dim3(DCOR_BLOCK), 0, (hipStream_t)stream,
                        c, scratch, part);
-    hipLaunchKernelGGL(k_sign_epilogue, dim3((unsigned)nr), dim3(DCOR_BLOCK), 0,
-                       (hipStream_t)stream, c, part, out + r);
+    launch_sign_epilogue(c, nr, part, out + r, (hipStream_t)stream);
     if (int e = last_err()) return e;
   }
   return 0;

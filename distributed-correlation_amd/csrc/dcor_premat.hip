@@ -3,6 +3,9 @@
 // on-device draw generator.  One 256-thread workgroup per replicate.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+#include <cstring>
+
 #include "dcor_common.h"
 
 namespace dcor {
@@ -307,11 +310,13 @@ __global__ __launch_bounds__(DCOR_BLOCK) void k_premat_subg_stream(PrematSubgCon
 }
 
 
-// NI result, INT estimate, mixquant, INT CI of replicate `rep` from its five workgroup sums
-// (ver-cor-subG.R:51-59, 91-103; real-data-sims.R:233-243).  All threads call.
-__device__ __forceinline__ void premat_subg_finish(const PrematSubgConst& p, int64_t rep,
-                                                   const DD (&d5)[5], SelScratch* sel,
-                                                   dcor_rep_out* out) {
+// NI result, INT estimate, mixquant, INT CI of replicate `rep` from its five sums
+// (ver-cor-subG.R:51-59, 91-103; real-data-sims.R:233-243).  quant(c*) is the mixquant
+// (workgroup- or wave-level); `writer` is the one thread that stores the record.
+template <class Quant>
+__device__ __forceinline__ void premat_subg_finish_q(const PrematSubgConst& p, int64_t rep,
+                                                     const DD (&d5)[5], Quant&& quant, bool writer,
+                                                     dcor_rep_out* out) {
   const SubgConst& c = p.s;
   double o[6];
   ni_subg_result(c, d5[0], d5[1], d5[2], o);
@@ -322,21 +327,56 @@ __device__ __forceinline__ void premat_subg_finish(const PrematSubgConst& p, int
   if (!p.hrs) {
     const double se_norm = sqrt(sd * sd + c.sn2x2);
     const double cstar = 2.0 / (c.sqrt_n * sd * c.eps_r);
-    const double qq = mixquant_loaded(c.mix, cstar, p.mix_z + rep * c.mix.nsim,
-                                      p.mix_l + rep * c.mix.nsim, sel);
+    const double qq = quant(cstar);
     width = qq * se_norm / c.sqrt_n;
   } else if (sd == 0.0) {
     width = p.crit_sqrt2_s;
   } else {
     const double cstar = (2.0 * c.lr) / (c.sqrt_n * sd * c.eps_r);
-    const double qq = mixquant_loaded(c.mix, cstar, p.mix_z + rep * c.mix.nsim,
-                                      p.mix_l + rep * c.mix.nsim, sel);
+    const double qq = quant(cstar);
     width = qq * (sd / c.sqrt_n);
   }
   o[3] = rho;
   o[4] = rmax(rho - width, -1.0);
   o[5] = rmin(rho + width, 1.0);
-  if (threadIdx.x == 0) out[rep] = dcor_rep_out{o[0], o[1], o[2], o[3], o[4], o[5]};
+  if (writer) out[rep] = dcor_rep_out{o[0], o[1], o[2], o[3], o[4], o[5]};
+}
+
+__device__ __forceinline__ void premat_subg_finish(const PrematSubgConst& p, int64_t rep,
+                                                   const DD (&d5)[5], SelScratch* sel,
+                                                   dcor_rep_out* out) {
+  const MixConst& mx = p.s.mix;
+  premat_subg_finish_q(p, rep, d5, [&](double cs) {
+    return mixquant_loaded(mx, cs, p.mix_z + rep * mx.nsim, p.mix_l + rep * mx.nsim, sel);
+  }, threadIdx.x == 0, out);
+}
+
+// Wave-per-replicate epilogue (four replicates per workgroup, no workgroup barriers): the
+// mixquant keys z + c l are loaded VPL per lane and selected with wave_select.
+template <int VPL>
+__global__ __launch_bounds__(DCOR_BLOCK) void k_premat_subg_epilogue_w(PrematSubgConst p, int64_t reps,
+                                                                       const SubgPartial* __restrict__ part,
+                                                                       dcor_rep_out* out) {
+  __shared__ WaveSel wsel[DCOR_WAVES];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t rep = (int64_t)blockIdx.x * DCOR_WAVES + wv;
+  if (rep >= reps) return;  // whole waves only
+  const SubgPartial q = part[rep];
+  DD d5[5];
+#pragma unroll
+  for (int v = 0; v < 5; ++v) d5[v] = two_sum(q.s[2 * v], q.s[2 * v + 1]);
+  const MixConst& mx = p.s.mix;
+  const double* z = p.mix_z + rep * mx.nsim;
+  const double* l = p.mix_l + rep * mx.nsim;
+  premat_subg_finish_q(p, rep, d5, [&](double cs) {
+    double val[VPL];
+#pragma unroll
+    for (int s = 0; s < VPL; ++s) {
+      const int i = lane + 64 * s;
+      val[s] = i < mx.nsim ? z[i] + cs * l[i] : dnan();  // NaN keys are dropped (R's sort)
+    }
+    return wave_select<VPL>(val, mx.pos, &wsel[wv]);
+  }, lane == 0, out);
 }
 
 // Epilogue of the streaming kernels that hand their sums over through SubgPartial.
@@ -826,8 +866,22 @@ int launch_premat_subg(const PrematSubgConst& c, int64_t reps, void* part, dcor_
   if (c.dict_built != 2)  // 2: a prepared panel known to be coded (dcor_panel)
     hipLaunchKernelGGL(k_premat_subg_stream, dim3((unsigned)reps), dim3(DCOR_BLOCK), 0,
                        (hipStream_t)stream, c, (const int*)c.dict_ok, (SubgPartial*)part);
-  hipLaunchKernelGGL(k_premat_subg_epilogue, dim3((unsigned)reps), dim3(DCOR_BLOCK), 0,
-                     (hipStream_t)stream, c, (const SubgPartial*)part, out);
+  // workgroup-per-replicate epilogue: measured faster here than the wave-per-replicate form
+  // (k_premat_subg_epilogue_w: 2000 loaded keys per wave cost 200+ VGPRs, one wave per SIMD)
+  static const int wave_epi = [] {
+    const char* v = std::getenv("DCOR_EPILOGUE");
+    return v && std::strcmp(v, "wave") == 0;
+  }();
+  const unsigned gw = (unsigned)((reps + DCOR_WAVES - 1) / DCOR_WAVES);
+  if (!wave_epi)
+    hipLaunchKernelGGL(k_premat_subg_epilogue, dim3((unsigned)reps), dim3(DCOR_BLOCK), 0,
+                       (hipStream_t)stream, c, (const SubgPartial*)part, out);
+  else if (c.s.mix.nsim <= 1024)
+    hipLaunchKernelGGL(k_premat_subg_epilogue_w<16>, dim3(gw), dim3(DCOR_BLOCK), 0,
+                       (hipStream_t)stream, c, reps, (const SubgPartial*)part, out);
+  else
+    hipLaunchKernelGGL(k_premat_subg_epilogue_w<32>, dim3(gw), dim3(DCOR_BLOCK), 0,
+                       (hipStream_t)stream, c, reps, (const SubgPartial*)part, out);
   return last_err();
 }
 int launch_accumulate(const dcor_rep_out* d_out, int64_t count, double rho, dcor_accum* acc,
