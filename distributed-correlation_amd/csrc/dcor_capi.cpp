@@ -122,6 +122,8 @@ int make_dgp(const dcor_cell& c, DgpConst& g) {
     const double p11 = 0.25 + c.rho / 4, p10 = 0.25 - c.rho / 4, p01 = p10;  // vert-cor.R:80-83
     g.thr0 = p01 / 0.5; g.thr1 = p11 / 0.5;
     g.T0 = u32_threshold(g.thr0); g.T1 = u32_threshold(g.thr1);
+    g.T0_24 = (uint32_t)std::ceil(g.thr0 * 16777216.0);  // thr <= 1: exact scaling, <= 2^24
+    g.T1_24 = (uint32_t)std::ceil(g.thr1 * 16777216.0);
   } else if (c.dgp == DCOR_DGP_BOUNDED_FACTOR) {
     if (!(c.rho >= 0 && c.rho <= 1)) return fail(DCOR_EINVAL, "gen_bounded_factor: rho in [0,1] required");
     g.cU = std::sqrt(3.0 * c.rho); g.cE = std::sqrt(3.0 * (1.0 - c.rho));  // ver-cor-subG.R:148-149

@@ -17,6 +17,7 @@ struct DgpConst {
   double mu0, mu1, a00, a01, a10, a11;  // Gaussian: X = mu + A z  (MASS::mvrnorm)
   double thr0, thr1;                    // Bernoulli: p01/0.5, p11/0.5
   uint64_t T0, T1;                      // ceil(thr*2^32): u32*2^-32 < thr  <=>  u32 < T
+  uint32_t T0_24, T1_24;                // Bernoulli Y: 24-bit v < ceil(thr*2^24)
   double cU, cU2, cE, cE2;              // bounded factor: -c + (c - -c) * u
   double xmu[2][2], xa[2][4];           // mixture: per-component mu and mvrnorm factor
   uint32_t T24, pad2;                   // mixture label: u24 < T24 = ceil(pi_mix * 2^24)

@@ -53,27 +53,48 @@ template <> struct Dgp<DCOR_DGP_GAUSSIAN> {  // MASS::mvrnorm (vert-cor.R:389-39
 };
 
 template <> struct Dgp<DCOR_DGP_BERNOULLI> {  // gen_bernoulli (vert-cor.R:78-98), 2 samples/block
-  static constexpr bool spare_flip = false;  // INT flips from the FLIP site
-  // u = wa*2^-32 < 0.5 <=> wa < 2^31; v < thr <=> wb < ceil(thr*2^32) (exact).
-  static __device__ __forceinline__ void from_words(const DgpConst& g, uint32_t wa, uint32_t wb,
-                                                    double& x, double& y) {
-    const bool xb = wa < 0x80000000u;
+  // Sample words (wa, wb) = (w0, w1) or (w2, w3) of block i/2: u < 0.5 is the top bit of wa
+  // (wa < 2^31, exact); v < thr is the low 24 bits of wa against ceil(thr 2^24) (|bias| <
+  // 2^-24); the sign family's INT flip is wb >> 8 against ceil(p 2^24) (spare_flip).
+  static constexpr bool spare_flip = true;
+  static __device__ __forceinline__ bool xbit(uint32_t wa) { return wa < 0x80000000u; }
+  static __device__ __forceinline__ bool ybit(const DgpConst& g, uint32_t wa, bool xb) {
+    return (wa & 0xFFFFFFu) < (xb ? g.T1_24 : g.T0_24);
+  }
+  static __device__ __forceinline__ void from_words(const DgpConst& g, uint32_t wa, double& x,
+                                                    double& y) {
+    const bool xb = xbit(wa);
     x = xb ? 1.0 : 0.0;
-    y = ((uint64_t)wb < (xb ? g.T1 : g.T0)) ? 1.0 : 0.0;
+    y = ybit(g, wa, xb) ? 1.0 : 0.0;
+  }
+  static __device__ __forceinline__ void one_u24(const DgpConst& g, uint32_t i, uint32_t rep,
+                                                 uint32_t k0, uint32_t k1, double& x, double& y,
+                                                 uint32_t& u24) {
+    const U4 w = draw(i >> 1, rep, DCOR_SITE_DGP_A, k0, k1);
+    const uint32_t wa = (i & 1) ? w.w2 : w.w0, wb = (i & 1) ? w.w3 : w.w1;
+    from_words(g, wa, x, y);
+    u24 = wb >> 8;
   }
   static __device__ __forceinline__ void one(const DgpConst& g, uint32_t i, uint32_t rep,
                                              uint32_t k0, uint32_t k1, double& x, double& y) {
-    const U4 w = draw(i >> 1, rep, DCOR_SITE_DGP_A, k0, k1);
-    if (i & 1) from_words(g, w.w2, w.w3, x, y); else from_words(g, w.w0, w.w1, x, y);
+    uint32_t u24;
+    one_u24(g, i, rep, k0, k1, x, y, u24);
+  }
+  static __device__ __forceinline__ void quad_u24(const DgpConst& g, uint32_t i0, uint32_t rep,
+                                                  uint32_t k0, uint32_t k1, double* x, double* y,
+                                                  uint32_t* u24) {
+    const U4 a = draw(i0 >> 1, rep, DCOR_SITE_DGP_A, k0, k1);
+    const U4 b = draw((i0 >> 1) + 1, rep, DCOR_SITE_DGP_A, k0, k1);
+    from_words(g, a.w0, x[0], y[0]);
+    from_words(g, a.w2, x[1], y[1]);
+    from_words(g, b.w0, x[2], y[2]);
+    from_words(g, b.w2, x[3], y[3]);
+    u24[0] = a.w1 >> 8; u24[1] = a.w3 >> 8; u24[2] = b.w1 >> 8; u24[3] = b.w3 >> 8;
   }
   static __device__ __forceinline__ void quad(const DgpConst& g, uint32_t i0, uint32_t rep,
                                               uint32_t k0, uint32_t k1, double* x, double* y) {
-    const U4 a = draw(i0 >> 1, rep, DCOR_SITE_DGP_A, k0, k1);
-    const U4 b = draw((i0 >> 1) + 1, rep, DCOR_SITE_DGP_A, k0, k1);
-    from_words(g, a.w0, a.w1, x[0], y[0]);
-    from_words(g, a.w2, a.w3, x[1], y[1]);
-    from_words(g, b.w0, b.w1, x[2], y[2]);
-    from_words(g, b.w2, b.w3, x[3], y[3]);
+    uint32_t u24[4];
+    quad_u24(g, i0, rep, k0, k1, x, y, u24);
   }
   static __device__ __forceinline__ double lap(uint32_t i, uint32_t rep, uint32_t k0, uint32_t k1) {
     const U4 v = draw(i, rep, DCOR_SITE_DGP_B, k0, k1);
@@ -575,16 +596,15 @@ __global__ __launch_bounds__(DCOR_BLOCK) void k_sign_bern(SignConst c, uint64_t*
       const uint32_t i0 = (uint32_t)(4 * g4);
       const U4 a = draw(i0 >> 1, rep, DCOR_SITE_DGP_A, c.k0, c.k1);
       const U4 b = draw((i0 >> 1) + 1, rep, DCOR_SITE_DGP_A, c.k0, c.k1);
-      const U4 fw = draw((uint32_t)g4, rep, DCOR_SITE_FLIP, c.k0, c.k1);
       const uint32_t wa[4] = {a.w0, a.w2, b.w0, b.w2}, wb[4] = {a.w1, a.w3, b.w1, b.w3};
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        if ((int64_t)i0 + q < c.n) {
-          const bool x1 = wa[q] < 0x80000000u;  // Dgp<BERNOULLI>::from_words
-          const bool y1 = (uint64_t)wb[q] < (x1 ? c.g.T1 : c.g.T0);
+        if ((int64_t)i0 + q < c.n) {  // Dgp<BERNOULLI>::one_u24
+          const bool x1 = Dgp<DCOR_DGP_BERNOULLI>::xbit(wa[q]);
+          const bool y1 = Dgp<DCOR_DGP_BERNOULLI>::ybit(c.g, wa[q], x1);
           xb |= (uint32_t)x1 << q;
           yb |= (uint32_t)y1 << q;
-          fb |= (uint32_t)((uint64_t)word(fw, q) < c.flipT) << q;
+          fb |= (uint32_t)((wb[q] >> 8) < c.flipT24) << q;
         }
       }
     }

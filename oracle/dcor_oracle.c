@@ -595,9 +595,10 @@ static void gen_xy(const dcor_cell* c, int64_t rep, double* X, double* Y, double
       X[i] = fmax(fmin(x, 1.0), -1.0);
       Y[i] = fmax(fmin(y, 1.0), -1.0);
     } else if (c->dgp == DCOR_DGP_BERNOULLI) {
+      /* u = top bit of the sample's first word; v = its low 24 bits (engine contract) */
       blk(c->seed, (uint32_t)(i >> 1), (uint32_t)rep, DCOR_SITE_DGP_A, w);
       const int b = 2 * (int)(i & 1);
-      const double u = (double)w[b] * 0x1p-32, v = (double)w[b + 1] * 0x1p-32;
+      const double u = (double)w[b] * 0x1p-32, v = (double)(w[b] & 0xFFFFFFu) * 0x1p-24;
       X[i] = (u < 0.5) ? 1.0 : 0.0;
       Y[i] = (X[i] == 0.0) ? (v < (p01 / 0.5) ? 1.0 : 0.0) : (v < (p11 / 0.5) ? 1.0 : 0.0);
     } else {
@@ -671,6 +672,11 @@ int orc_sim_rep(const void* cellp, int64_t rep, double out[6]) {
           /* the 24 bits of sample i's normal-pair block that Box-Muller leaves unused */
           blk(c->seed, (uint32_t)i, (uint32_t)rep, DCOR_SITE_DGP_A, w);
           const uint32_t u24 = ((w[1] & 0xFFFu) << 12) | (w[3] & 0xFFFu);
+          fl[i] = ((double)u24 * 0x1p-24 < p) ? 1 : 0;
+        } else if (c->dgp == DCOR_DGP_BERNOULLI) {
+          /* the top 24 bits of the sample's second word */
+          blk(c->seed, (uint32_t)(i >> 1), (uint32_t)rep, DCOR_SITE_DGP_A, w);
+          const uint32_t u24 = w[2 * (i & 1) + 1] >> 8;
           fl[i] = ((double)u24 * 0x1p-24 < p) ? 1 : 0;
         } else {
           blk(c->seed, (uint32_t)(i >> 2), (uint32_t)rep, DCOR_SITE_FLIP, w);
