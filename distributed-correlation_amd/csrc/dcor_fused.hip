@@ -282,10 +282,13 @@ __device__ __forceinline__ uint32_t code16(double v, float inv, float nb, float 
   return (uint32_t)__builtin_amdgcn_fmed3f(t, 0.0f, top);  // NaN -> 0 (a NaN mu is flagged)
 }
 __device__ __forceinline__ int sgnq(uint32_t q, uint32_t qm) { return (q > qm) - (q < qm); }
-// sign(q - qm) for 16-bit codes as one subtract + one v_med3_i32 (clamp to [-1, 1]).
+// sign(q - qm) for 16-bit codes as one subtract + one v_med3_i32 (clamp to [-1, 1]); asm
+// keeps the compiler from expanding the clamp into compare/select pairs.
 __device__ __forceinline__ int sgnd(uint32_t q, uint32_t qm) {
   const int d = (int)q - (int)qm;
-  return min(max(d, -1), 1);
+  int r;
+  asm("v_med3_i32 %0, %1, -1, 1" : "=v"(r) : "v"(d));
+  return r;
 }
 
 template <int DGP>
@@ -449,8 +452,8 @@ __global__ __launch_bounds__(DCOR_BLOCK) void k_sign_pass2(SignConst c,
       if (force_exact) tie = 0xFFu;
       if (tie) {
 #pragma unroll 1
-        for (int q = 0; q < 8; ++q)
-          if ((tie >> q) & 1u) fixup(8 * j + q, word(q < 4 ? w0 : w1, q & 3), cx, cy, cc, bad_ni);
+        for (int q = 0; q < 8; ++q)  // re-read the record (L2-hot): no dynamically indexed registers
+          if ((tie >> q) & 1u) fixup(8 * j + q, slab[8 * j + q], cx, cy, cc, bad_ni);
       }
       core += cc;
       batch_T(j, cx, cy);
