@@ -262,6 +262,12 @@ def test_int_only_call_with_n_smaller_than_m(dc, orc):
     dict(n=3000, rho=0.8, eps1=1.0, eps2=1.0, family="subG", dgp="bernoulli"),
     dict(n=1000, rho=0.5, eps1=1.0, eps2=1.0, family="sign", dgp="gaussian", nsim=2000),
     dict(n=999, rho=0.15, eps1=1.5, eps2=0.5, family="sign", dgp="bounded_factor"),
+    # mixquant sizes around the wave-select layouts (16 / 32 keys per lane, partial lanes)
+    dict(n=1500, rho=0.4, eps1=1.0, eps2=1.0, family="sign", dgp="gaussian", nsim=1),
+    dict(n=1500, rho=0.4, eps1=1.0, eps2=1.0, family="sign", dgp="gaussian", nsim=7),
+    dict(n=1500, rho=0.4, eps1=1.0, eps2=1.0, family="sign", dgp="gaussian", nsim=1025),
+    dict(n=1500, rho=0.4, eps1=1.0, eps2=1.0, family="sign", dgp="bernoulli", nsim=2048),
+    dict(n=2500, rho=0.4, eps1=1.0, eps2=1.0, family="subG", dgp="mix_gaussian", nsim=1999),
 ])
 def test_fused_edge_cells(dc, orc, spec):
     from dcor.sim import CellSpec, simulate
