@@ -697,7 +697,33 @@ static int premat_subg_run(const dcor_premat_subg* d, const dcor_panel* panel, d
     p.dict_ok = panel->ok();
     p.dict_built = 2;  // built and known coded: no L2-gather launch
   }
-  const int rc = launch_premat_subg(p, d->reps, part, d_out, stream);
+  int rc = 0;
+  const char* pv = std::getenv("DCOR_PREMAT_PIPELINE");
+  if (panel != nullptr && panel->coded && p.perm && d->reps >= 4096 && !(pv && std::strcmp(pv, "0") == 0)) {
+    // two replicate halves: the first half's (latency-bound) mixquant epilogue runs on the
+    // auxiliary stream beside the second half's (HBM-bound) streaming kernel
+    Pipe* pp = nullptr;
+    if (int st = pipe_get(&pp)) { (void)hipFreeAsync(part, (hipStream_t)stream); return st; }
+    const int64_t half = d->reps / 2;
+    for (int h = 0; h < 2 && !rc; ++h) {
+      const int64_t r0 = h ? half : 0, nr = h ? d->reps - half : half;
+      PrematSubgConst q = p;
+      const int64_t km = p.s.k * p.s.m, n = p.s.n, ns = p.s.mix.nsim;
+      q.perm = p.perm + r0 * km;
+      q.lap_ni_x = p.lap_ni_x + r0 * p.s.k;
+      q.lap_ni_y = p.lap_ni_y + r0 * p.s.k;
+      q.lap_local = p.lap_local + r0 * n;
+      q.lap_central = p.lap_central + r0;
+      q.mix_z = p.mix_z + r0 * ns;
+      q.mix_l = p.mix_l + r0 * ns;
+      rc = launch_premat_subg(q, nr, (char*)part + r0 * 80, d_out + r0, stream, h ? nullptr : pp->s,
+                              pp->fork);
+    }
+    if (!rc && hipEventRecord(pp->join, pp->s) != hipSuccess) rc = (int)hipGetLastError();
+    if (!rc && hipStreamWaitEvent((hipStream_t)stream, pp->join, 0) != hipSuccess) rc = (int)hipGetLastError();
+  } else {
+    rc = launch_premat_subg(p, d->reps, part, d_out, stream);
+  }
   (void)hipFreeAsync(part, (hipStream_t)stream);
   if (rc) return hip_fail((hipError_t)rc, "premat_subg launch");
   return DCOR_OK;

@@ -126,8 +126,10 @@ int launch_sign_fused_codes(const SignConst& c, int64_t reps, int64_t chunk, con
 int launch_subg_fused(const SubgConst& c, int64_t reps, dcor_rep_out* out, void* stream);
 int launch_premat_sign(const PrematSignConst& c, int64_t reps, dcor_rep_out* out, void* stream);
 // part: reps * 80 B scratch (stream -> epilogue partial sums).
+// epi_stream / ev: if non-null the epilogue runs on epi_stream after an event recorded on
+// `stream` behind the streaming kernels (chunk pipelining).
 int launch_premat_subg(const PrematSubgConst& c, int64_t reps, void* part, dcor_rep_out* out,
-                       void* stream);
+                       void* stream, void* epi_stream = nullptr, void* ev = nullptr);
 int launch_accumulate(const dcor_rep_out* d_out, int64_t count, double rho, dcor_accum* acc,
                       void* stream);
 int launch_mixquant(const double* z, const double* l, int32_t nsim, double c, int32_t pos,

@@ -831,7 +831,7 @@ size_t premat_dict_lds_bytes(int64_t n) {
 }
 
 int launch_premat_subg(const PrematSubgConst& c, int64_t reps, void* part, dcor_rep_out* out,
-                       void* stream) {
+                       void* stream, void* epi_stream, void* ev) {
   if (reps <= 0) return 0;
   if (c.dict_codes != nullptr) {
     static_assert(DCOR_BLOCK == DICT_MAX, "dictionary fill assumes one entry per thread");
@@ -873,6 +873,11 @@ int launch_premat_subg(const PrematSubgConst& c, int64_t reps, void* part, dcor_
     return v && std::strcmp(v, "wave") == 0;
   }();
   const unsigned gw = (unsigned)((reps + DCOR_WAVES - 1) / DCOR_WAVES);
+  if (epi_stream != nullptr) {  // epilogue on a second stream, after this chunk's streaming
+    if (hipEventRecord((hipEvent_t)ev, (hipStream_t)stream) != hipSuccess) return last_err();
+    if (hipStreamWaitEvent((hipStream_t)epi_stream, (hipEvent_t)ev, 0) != hipSuccess) return last_err();
+    stream = epi_stream;
+  }
   if (!wave_epi)
     hipLaunchKernelGGL(k_premat_subg_epilogue, dim3((unsigned)reps), dim3(DCOR_BLOCK), 0,
                        (hipStream_t)stream, c, (const SubgPartial*)part, out);

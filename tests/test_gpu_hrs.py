@@ -77,3 +77,20 @@ def test_eps_sweep_summaries(panel):
         assert s["method"] == "INT" and s["ci_low_mean"] <= s["ci_high_mean"]  # rho_hat is not clipped
         assert math.isclose(s["ci_high_q90"], float(np.quantile(runs[:, 5], 0.9)), rel_tol=0, abs_tol=0)
     assert [round(e, 2) for e in hrs.EPS_GRID][:3] == [0.25, 0.35, 0.45] and len(hrs.EPS_GRID) == 23
+
+
+def test_panel_pipelined_halves_bitexact(panel):
+    """Large coded-panel launches split into two stream-pipelined halves; the result must
+    equal the single-stream launch bit for bit."""
+    import os
+    from dcor import hrs
+    z = panel
+    args = (z["age_z"], z["bmi_z"], z["lambda_age_z"], z["lambda_bmi_z"], 2.0, 4100)
+    os.environ["DCOR_PREMAT_PIPELINE"] = "0"
+    try:
+        serial = hrs.hrs_replicates(*args, chunk=4100)
+    finally:
+        del os.environ["DCOR_PREMAT_PIPELINE"]
+    piped = hrs.hrs_replicates(*args, chunk=4100)
+    np.testing.assert_array_equal(piped.view(np.int64), serial.view(np.int64))
+    assert np.isfinite(piped).all()
