@@ -773,41 +773,44 @@ __global__ __launch_bounds__(DCOR_BLOCK) void k_draws(int kind, uint32_t k0, uin
 }
 
 // ========================================================== permutation ===
-// Keyed pseudo-random permutation of [0, n): a 4-round balanced Feistel network on
-// 2b >= ceil(log2 n) bits, cycle-walked into [0, n).  out[r][t] = P_r(t), t < count, is
-// a random ordered subset of size `count` -- the role of sample.int(n, k*m)
-// (real-data-sims.R:131) for the HRS random batches.  Round keys: Philox block
-// (0, rep, site, 0).  Restated in oracle/ (orc_perm) for bit-exact tests.
+// Keyed pseudo-random permutation of [0, n): a 4-round unbalanced Feistel network on exactly
+// bits = ceil(log2 n) bits (high part c = bits - a, low part a = bits / 2; the part widths
+// alternate each round and return after four), cycle-walked into [0, n) -- at least half the
+// domain is accepted, so a wave rarely walks long.  Round functions use only full-rate 24-bit
+// multiplies.  out[r][t] = P_r(t), t < count, is a random ordered subset of size `count`: the
+// role of sample.int(n, k*m) (real-data-sims.R:131) for the HRS random batches.  Round keys:
+// Philox block (0, rep, site, 0).  Restated in oracle/ (orc_perm) for bit-exact tests.
 __device__ __forceinline__ uint32_t feistel_f(uint32_t r, uint32_t k, uint32_t mask) {
-  uint32_t t = (r + k) * 0xCC9E2D51u;
+  uint32_t t = __umul24((r ^ k) & 0xFFFFFFu, 0x9E3779u);
   t ^= t >> 15;
-  t *= 0x1B873593u;
+  t = __umul24(t & 0xFFFFFFu, 0x85EBCBu);
   t ^= t >> 13;
   return t & mask;
 }
 
-__device__ __forceinline__ uint32_t feistel_perm(uint32_t x, uint32_t n, int b, const U4& kk) {
-  const uint32_t mask = (1u << b) - 1u;
+__device__ __forceinline__ uint32_t feistel_perm(uint32_t x, uint32_t n, int a, int c,
+                                                 const U4& kk) {
+  const uint32_t ma = (1u << a) - 1u, mc = (1u << c) - 1u;
   do {
-    uint32_t L = x >> b, R = x & mask;
+    uint32_t H = x >> a, L = x & ma;              // (c bits, a bits)
     uint32_t t;
-    t = L ^ feistel_f(R, kk.w0, mask); L = R; R = t;
-    t = L ^ feistel_f(R, kk.w1, mask); L = R; R = t;
-    t = L ^ feistel_f(R, kk.w2, mask); L = R; R = t;
-    t = L ^ feistel_f(R, kk.w3, mask); L = R; R = t;
-    x = (L << b) | R;
+    t = H ^ feistel_f(L, kk.w0, mc); H = L; L = t;  // (a, c)
+    t = H ^ feistel_f(L, kk.w1, ma); H = L; L = t;  // (c, a)
+    t = H ^ feistel_f(L, kk.w2, mc); H = L; L = t;  // (a, c)
+    t = H ^ feistel_f(L, kk.w3, ma); H = L; L = t;  // (c, a)
+    x = (H << a) | L;
   } while (x >= n);
   return x;
 }
 
 __global__ __launch_bounds__(DCOR_BLOCK) void k_perm(uint32_t k0, uint32_t k1, uint32_t site,
-                                                     int64_t rep_begin, uint32_t n, int b,
+                                                     int64_t rep_begin, uint32_t n, int a, int c,
                                                      int64_t count, int32_t* out) {
   const int64_t r = blockIdx.y;
   const U4 kk = draw(0u, (uint32_t)(rep_begin + r), site, k0, k1);
   for (int64_t t = (int64_t)blockIdx.x * DCOR_BLOCK + threadIdx.x; t < count;
        t += (int64_t)gridDim.x * DCOR_BLOCK)
-    out[r * count + t] = (int32_t)feistel_perm((uint32_t)t, n, b, kk);
+    out[r * count + t] = (int32_t)feistel_perm((uint32_t)t, n, a, c, kk);
 }
 
 // ============================================================ launchers ===
@@ -943,11 +946,11 @@ int launch_perm(uint32_t k0, uint32_t k1, uint32_t site, int64_t rep_begin, int6
   if (reps <= 0 || count <= 0) return 0;
   int bits = 1;
   while ((1ll << bits) < n) ++bits;
-  const int b = (bits + 1) / 2;
+  const int a = bits / 2, c = bits - a;
   int64_t gx = (count + DCOR_BLOCK - 1) / DCOR_BLOCK;
   if (gx > 4096) gx = 4096;
   hipLaunchKernelGGL(k_perm, dim3((unsigned)gx, (unsigned)reps), dim3(DCOR_BLOCK), 0,
-                     (hipStream_t)stream, k0, k1, site, rep_begin, (uint32_t)n, b, count, out);
+                     (hipStream_t)stream, k0, k1, site, rep_begin, (uint32_t)n, a, c, count, out);
   return last_err();
 }
 int launch_dp_sd(const double* x, int64_t n, double lo, double hi, double s_mu, double s_m2,

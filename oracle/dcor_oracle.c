@@ -735,32 +735,37 @@ int orc_sim_reps(const void* cell, int64_t r0, int64_t r1, int threads, double* 
 }
 
 /* ---------------------------------------------- keyed permutation (HRS) --- */
+static uint32_t umul24(uint32_t x, uint32_t y) {
+  return (uint32_t)((uint64_t)(x & 0xFFFFFFu) * (uint64_t)(y & 0xFFFFFFu));
+}
+
 static uint32_t orc_feistel_f(uint32_t r, uint32_t k, uint32_t mask) {
-  uint32_t t = (r + k) * 0xCC9E2D51u;
+  uint32_t t = umul24((r ^ k) & 0xFFFFFFu, 0x9E3779u);
   t ^= t >> 15;
-  t *= 0x1B873593u;
+  t = umul24(t & 0xFFFFFFu, 0x85EBCBu);
   t ^= t >> 13;
   return t & mask;
 }
 
 void orc_perm(uint64_t seed, int site, int64_t rep, int64_t n, int64_t count, int32_t* out) {
-  /* 4-round balanced Feistel on 2b >= ceil(log2 n) bits, cycle-walked into [0, n). */
+  /* 4-round unbalanced Feistel on bits = ceil(log2 n) bits (high c = bits - a, low
+   * a = bits / 2, widths alternating), cycle-walked into [0, n). */
   int bits = 1;
   while ((1ll << bits) < n) ++bits;
-  const int b = (bits + 1) / 2;
-  const uint32_t mask = (1u << b) - 1u;
+  const int a = bits / 2, c = bits - a;
+  const uint32_t ma = (1u << a) - 1u, mc = (1u << c) - 1u;
   uint32_t kk[4];
   blk(seed, 0u, (uint32_t)rep, (uint32_t)site, kk);
   for (int64_t t = 0; t < count; ++t) {
     uint32_t x = (uint32_t)t;
     do {
-      uint32_t L = x >> b, R = x & mask;
+      uint32_t H = x >> a, L = x & ma;
       for (int q = 0; q < 4; ++q) {
-        const uint32_t nt = L ^ orc_feistel_f(R, kk[q], mask);
-        L = R;
-        R = nt;
+        const uint32_t nt = H ^ orc_feistel_f(L, kk[q], (q & 1) ? ma : mc);
+        H = L;
+        L = nt;
       }
-      x = (L << b) | R;
+      x = (H << a) | L;
     } while (x >= (uint32_t)n);
     out[t] = (int32_t)x;
   }

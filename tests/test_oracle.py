@@ -317,3 +317,20 @@ def test_mix_gaussian_dgp_law():
             top = sum(w * stats.norm.sf((1 - m) / s) for w, m, s in comps)
             assert abs(v.mean() - mean) < 5e-3, (pi, j, v.mean(), mean)
             assert abs(np.mean(v == 1.0) - top) < 4e-3, (pi, j)
+
+
+def test_perm_uniformity():
+    """The keyed Feistel permutation (HRS random batches, the role of sample.int): P_r(0)
+    and P_r(1) over many replicate keys are uniform and independent enough (chi-square)."""
+    from scipy import stats
+    n, R = 97, 30_000
+    first = np.array([O.perm(11, 8, r, n, 2) for r in range(R)])
+    for col in (0, 1):
+        cnt = np.bincount(first[:, col], minlength=n)
+        assert stats.chisquare(cnt).pvalue > 1e-4, col
+    assert np.all(first[:, 0] != first[:, 1])
+    # joint residues mod 8 against uniformly random ordered pairs of distinct elements
+    pair = np.bincount((first[:, 0] % 8) * 8 + first[:, 1] % 8, minlength=64)
+    c = np.bincount(np.arange(n) % 8, minlength=8).astype(float)
+    exp = (np.outer(c, c) - np.diag(c)).ravel() / (n * (n - 1)) * R
+    assert stats.chisquare(pair, exp).pvalue > 1e-4
