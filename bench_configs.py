@@ -193,6 +193,27 @@ def c5(R, panel="coded"):
               "encoded once by dcor_panel_create")
 
 
+def c5_e2e(R):
+    """BASELINE C5 end to end: R NI + INT replicates of the HRS estimators at eps = 2 on a
+    coded stand-in panel, noise generated on device per 8192-replicate chunk and streamed
+    (dcor.hrs.hrs_replicates), results copied to the host."""
+    import numpy as np
+    import torch
+    from dcor import hrs
+    age_raw, bmi_raw = hrs.standin_panel(19433, -0.3)
+    z = hrs.standardize_panel(age_raw, bmi_raw, lap=np.zeros(4))
+    args = (z["age_z"], z["bmi_z"], z["lambda_age_z"], z["lambda_bmi_z"], 2.0)
+    hrs.hrs_replicates(*args, 8192)  # warm-up
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    res = hrs.hrs_replicates(*args, R, chunk=8192)
+    torch.cuda.synchronize()
+    t = time.perf_counter() - t0
+    line("C5-e2e", reps=R, seconds=t, reps_per_s=R / t, finite=bool(np.isfinite(res).all()),
+         note="includes on-device Philox noise + keyed permutation generation per chunk and the "
+              "D2H copy of all replicate records")
+
+
 def subg():
     from dcor.sim import CellSpec, simulate
     cell = CellSpec(n=100_000, rho=0.5, eps1=1.0, eps2=1.0, family="subG", dgp="bounded_factor", seed=5)
@@ -204,10 +225,11 @@ def subg():
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--only", default="C1,C2,C3,C4,C5,C5c,S")
+    ap.add_argument("--only", default="C1,C2,C3,C4,C5,C5c,C5e,S")
     ap.add_argument("--c3-reps", type=int, default=2000)
     ap.add_argument("--c4-B", type=int, default=1000)
     ap.add_argument("--c5-R", type=int, default=8192)
+    ap.add_argument("--c5e-R", type=int, default=1_000_000)
     a = ap.parse_args()
     import torch
     torch.cuda.set_device(0)
@@ -218,6 +240,7 @@ def main():
     if "C4" in which: c4(a.c4_B)
     if "C5" in which: c5(a.c5_R)
     if "C5c" in which: c5(a.c5_R, panel="continuous")
+    if "C5e" in which: c5_e2e(a.c5e_R)
     if "S" in which: subg()
 
 
