@@ -441,7 +441,8 @@ int dcor_sim_launch(const dcor_cell* cell, int64_t rep_begin, int64_t rep_count,
       if (budget > ((size_t)8 << 30)) budget = (size_t)8 << 30;
       int64_t maxchunk = (int64_t)(budget / per_rep);
       if (maxchunk < 1) maxchunk = 1;
-      const int64_t nch = (rep_count + maxchunk - 1) / maxchunk;
+      int64_t nch = (rep_count + maxchunk - 1) / maxchunk;
+      if (nch == 1 && rep_count >= 512) nch = 2;  // two chunks at least: pass 2 of one beside pass 1 of the other
       const int64_t chunk = (rep_count + nch - 1) / nch;
       const size_t slab_b = ((size_t)chunk * per_rep + 255) / 256 * 256;
       const size_t sums_b = ((size_t)chunk * (4 * sizeof(double) + 48) + 255) / 256 * 256;
