@@ -579,6 +579,120 @@ __device__ __forceinline__ uint64_t interleave4(const uint64_t (&b)[4], int q) {
          (part1by3(b[3] >> sh) << 3);
 }
 
+// Pass A of one thread for the four samples of group g4 (< ngrp): X, Y and flip bits
+// (Dgp<BERNOULLI>::one_u24; bit q = sample 4 g4 + q).
+__device__ __forceinline__ void bern_gen4(const SignConst& c, uint32_t rep, int64_t g4,
+                                          uint32_t& xb, uint32_t& yb, uint32_t& fb) {
+  xb = yb = fb = 0;
+  const uint32_t i0 = (uint32_t)(4 * g4);
+  const U4 a = draw(i0 >> 1, rep, DCOR_SITE_DGP_A, c.k0, c.k1);
+  const U4 b = draw((i0 >> 1) + 1, rep, DCOR_SITE_DGP_A, c.k0, c.k1);
+  const uint32_t wa[4] = {a.w0, a.w2, b.w0, b.w2}, wb[4] = {a.w1, a.w3, b.w1, b.w3};
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    if ((int64_t)i0 + q < c.n) {
+      const bool x1 = Dgp<DCOR_DGP_BERNOULLI>::xbit(wa[q]);
+      const bool y1 = Dgp<DCOR_DGP_BERNOULLI>::ybit(c.g, wa[q], x1);
+      xb |= (uint32_t)x1 << q;
+      yb |= (uint32_t)y1 << q;
+      fb |= (uint32_t)((wb[q] >> 8) < c.flipT24) << q;
+    }
+  }
+}
+
+// Wave-uniform counts of one 256-sample chunk (ballots of the lanes' 4 sample bits) and its
+// sample-ordered plane words (interleave4).
+struct BernCounts { long long n1x, n1y, n11, fx, fy, f11, ft; };
+__device__ __forceinline__ void bern_ballots(uint32_t xb, uint32_t yb, uint32_t fb, BernCounts& t,
+                                             uint64_t (&BX)[4], uint64_t (&BY)[4],
+                                             uint64_t (&BF)[4]) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    BX[q] = __ballot((xb >> q) & 1u);
+    BY[q] = __ballot((yb >> q) & 1u);
+    BF[q] = __ballot((fb >> q) & 1u);
+    t.n1x += __popcll(BX[q]);
+    t.n1y += __popcll(BY[q]);
+    t.n11 += __popcll(BX[q] & BY[q]);
+    t.fx += __popcll(BF[q] & BX[q]);
+    t.fy += __popcll(BF[q] & BY[q]);
+    t.f11 += __popcll(BF[q] & BX[q] & BY[q]);
+    t.ft += __popcll(BF[q]);
+  }
+}
+
+// Thresholds (vert-cor.R:322-348), the two signs per threshold, the INT flip sum from the
+// combination counts (vert-cor.R:175-183) and the NaN flags.
+struct BernSigns {
+  int sN0x, sN1x, sN0y, sN1y;
+  bool bN0x, bN1x, bN0y, bN1y;
+  bool bad_ni, bad_int;
+  long long core;
+};
+__device__ __forceinline__ BernSigns bern_signs(const SignConst& c, const BernCounts& t,
+                                                const double (&l8)[8]) {
+  BernSigns r;
+  const double c0 = rclip_fin(0.0, c.L), c1 = rclip_fin(1.0, c.L);
+  int sI0x, sI1x, sI0y, sI1y;
+  bool bI0x = false, bI1x = false, bI0y = false, bI1y = false;
+  r.bN0x = r.bN1x = r.bN0y = r.bN1y = false;
+  r.bad_ni = r.bad_int = false;
+  if (c.normalise) {
+    const double nd = c.nd;
+    const double n0x = nd - (double)t.n1x, n0y = nd - (double)t.n1y;
+    double v[4];
+    v[0] = (double)t.n1x * c1 + n0x * c0;
+    v[1] = (double)t.n1x * (c1 * c1) + n0x * (c0 * c0);
+    v[2] = (double)t.n1y * c1 + n0y * c0;
+    v[3] = (double)t.n1y * (c1 * c1) + n0y * (c0 * c0);
+    SignStd st;
+    priv_std_from_sums(c, v, l8, st);
+    const bool thr_nan = (st.muNx != st.muNx) || (st.muNy != st.muNy) || (st.muIx != st.muIx) ||
+                         (st.muIy != st.muIy) || (st.sdNx != st.sdNx) || (st.sdNy != st.sdNy) ||
+                         (st.sdIx != st.sdIx) || (st.sdIy != st.sdIy);
+    r.bad_ni = r.bad_int = thr_nan;
+    r.sN0x = sgn_std(c0, st.muNx, st.sdNx, r.bN0x); r.sN1x = sgn_std(c1, st.muNx, st.sdNx, r.bN1x);
+    r.sN0y = sgn_std(c0, st.muNy, st.sdNy, r.bN0y); r.sN1y = sgn_std(c1, st.muNy, st.sdNy, r.bN1y);
+    sI0x = sgn_std(c0, st.muIx, st.sdIx, bI0x); sI1x = sgn_std(c1, st.muIx, st.sdIx, bI1x);
+    sI0y = sgn_std(c0, st.muIy, st.sdIy, bI0y); sI1y = sgn_std(c1, st.muIy, st.sdIy, bI1y);
+  } else {  // signs of the raw values (vert-cor.R:172-173, 226-227)
+    r.sN0x = r.sN0y = sI0x = sI0y = 0;
+    r.sN1x = r.sN1y = sI1x = sI1y = 1;
+  }
+  const long long N10 = t.n1x - t.n11, N01 = t.n1y - t.n11, N00 = (long long)c.n - t.n1x - t.n1y + t.n11;
+  const long long F10 = t.fx - t.f11, F01 = t.fy - t.f11, F00 = t.ft - t.fx - t.fy + t.f11;
+  r.core = (long long)(sI1x * sI1y) * (2 * t.f11 - t.n11) + (long long)(sI1x * sI0y) * (2 * F10 - N10) +
+           (long long)(sI0x * sI1y) * (2 * F01 - N01) + (long long)(sI0x * sI0y) * (2 * F00 - N00);
+  r.bad_int |= (bI1x && t.n1x > 0) || (bI0x && t.n1x < c.n) || (bI1y && t.n1y > 0) ||
+               (bI0y && t.n1y < c.n);
+  return r;
+}
+
+// NI batch j from the plane popcounts (vert-cor.R:226-239).
+__device__ __forceinline__ void bern_batch(const SignConst& c, const BernSigns& sg,
+                                           const uint64_t* PX, const uint64_t* PY, int64_t j,
+                                           uint32_t rep, DD& sT, DD& sT2, bool& bad_ni) {
+  const int64_t a = j * c.m, b = a + c.m;
+  const int64_t wa = a >> 6, wb = (b - 1) >> 6;
+  int cx1 = 0, cy1 = 0;
+  for (int64_t w = wa; w <= wb; ++w) {
+    uint64_t mask = ~0ull;
+    if (w == wa) mask &= ~0ull << (a & 63);
+    if (w == wb) mask &= ~0ull >> (63 - ((b - 1) & 63));
+    cx1 += __popcll(PX[w] & mask);
+    cy1 += __popcll(PY[w] & mask);
+  }
+  const int cx0 = c.m - cx1, cy0 = c.m - cy1;
+  bad_ni |= (sg.bN1x && cx1) || (sg.bN0x && cx0) || (sg.bN1y && cy1) || (sg.bN0y && cy0);
+  const int cx = sg.sN1x * cx1 + sg.sN0x * cx0, cy = sg.sN1y * cy1 + sg.sN0y * cy0;
+  const U4 w = draw((uint32_t)j, rep, DCOR_SITE_NI_LAP, c.k0, c.k1);   // vert-cor.R:230-231
+  const double xt = (double)cx / c.md + c.bx * unit_laplace(u53(w.w0, w.w1));
+  const double yt = (double)cy / c.md + c.by * unit_laplace(u53(w.w2, w.w3));
+  const double T = c.md * xt * yt;                                     // vert-cor.R:233
+  dd_acc(sT, T);
+  dd_acc(sT2, T * T);
+}
+
 __global__ __launch_bounds__(DCOR_BLOCK) void k_sign_bern(SignConst c, uint64_t* __restrict__ scratch,
                                                           SignPartial* __restrict__ part) {
   __shared__ double red[16 * DCOR_WAVES];
@@ -590,41 +704,14 @@ __global__ __launch_bounds__(DCOR_BLOCK) void k_sign_bern(SignConst c, uint64_t*
   uint64_t* planes = scratch + (size_t)blockIdx.x * 3 * (size_t)nw;
   scalar_laplace(rep, c.k0, c.k1, lap);
   // ---- pass A: generate, ballot into plane words, count (wave-uniform counters)
-  long long n1x = 0, n1y = 0, n11 = 0, fx = 0, fy = 0, f11 = 0, ft = 0;
+  BernCounts t{0, 0, 0, 0, 0, 0, 0};
   const int64_t ngrp = (c.n + 3) / 4;
   const int64_t ngrp_pad = (ngrp + DCOR_BLOCK - 1) / DCOR_BLOCK * DCOR_BLOCK;
   for (int64_t g4 = tid; g4 < ngrp_pad; g4 += DCOR_BLOCK) {  // whole waves stay converged
     uint32_t xb = 0, yb = 0, fb = 0;
-    if (g4 < ngrp) {
-      const uint32_t i0 = (uint32_t)(4 * g4);
-      const U4 a = draw(i0 >> 1, rep, DCOR_SITE_DGP_A, c.k0, c.k1);
-      const U4 b = draw((i0 >> 1) + 1, rep, DCOR_SITE_DGP_A, c.k0, c.k1);
-      const uint32_t wa[4] = {a.w0, a.w2, b.w0, b.w2}, wb[4] = {a.w1, a.w3, b.w1, b.w3};
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        if ((int64_t)i0 + q < c.n) {  // Dgp<BERNOULLI>::one_u24
-          const bool x1 = Dgp<DCOR_DGP_BERNOULLI>::xbit(wa[q]);
-          const bool y1 = Dgp<DCOR_DGP_BERNOULLI>::ybit(c.g, wa[q], x1);
-          xb |= (uint32_t)x1 << q;
-          yb |= (uint32_t)y1 << q;
-          fb |= (uint32_t)((wb[q] >> 8) < c.flipT24) << q;
-        }
-      }
-    }
+    if (g4 < ngrp) bern_gen4(c, rep, g4, xb, yb, fb);
     uint64_t BX[4], BY[4], BF[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      BX[q] = __ballot((xb >> q) & 1u);
-      BY[q] = __ballot((yb >> q) & 1u);
-      BF[q] = __ballot((fb >> q) & 1u);
-      n1x += __popcll(BX[q]);
-      n1y += __popcll(BY[q]);
-      n11 += __popcll(BX[q] & BY[q]);
-      fx += __popcll(BF[q] & BX[q]);
-      fy += __popcll(BF[q] & BY[q]);
-      f11 += __popcll(BF[q] & BX[q] & BY[q]);
-      ft += __popcll(BF[q]);
-    }
+    bern_ballots(xb, yb, fb, t, BX, BY, BF);
     const int64_t w0 = (g4 - lane) / 16;  // first plane word of this wave's chunk
     if (lane < 12 && w0 < nw) {
       const int q = lane & 3, pl = lane >> 2;
@@ -633,7 +720,7 @@ __global__ __launch_bounds__(DCOR_BLOCK) void k_sign_bern(SignConst c, uint64_t*
     }
   }
   // block totals (one lane per wave contributes its wave-uniform counters)
-  long long cnt[7] = {n1x, n1y, n11, fx, fy, f11, ft};
+  long long cnt[7] = {t.n1x, t.n1y, t.n11, t.fx, t.fy, t.f11, t.ft};
   if (lane == 0) {
 #pragma unroll
     for (int q = 0; q < 7; ++q) redi[8 * (tid >> 6) + q] = cnt[q];
@@ -641,86 +728,85 @@ __global__ __launch_bounds__(DCOR_BLOCK) void k_sign_bern(SignConst c, uint64_t*
   __syncthreads();  // also orders the plane stores before pass B (workgroup scope)
 #pragma unroll
   for (int q = 0; q < 7; ++q) {
-    long long t = 0;
+    long long v = 0;
 #pragma unroll
-    for (int w = 0; w < DCOR_WAVES; ++w) t += redi[8 * w + q];
-    cnt[q] = t;
+    for (int w = 0; w < DCOR_WAVES; ++w) v += redi[8 * w + q];
+    cnt[q] = v;
   }
-  const long long N1x = cnt[0], N1y = cnt[1], N11 = cnt[2], Fx = cnt[3], Fy = cnt[4],
-                  F11 = cnt[5], Ft = cnt[6];
-  // ---- thresholds (vert-cor.R:322-348) and the two signs per threshold
-  const double c0 = rclip_fin(0.0, c.L), c1 = rclip_fin(1.0, c.L);
-  bool bad_ni = false, bad_int = false;
-  int sN0x, sN1x, sN0y, sN1y, sI0x, sI1x, sI0y, sI1y;
-  bool bN0x = false, bN1x = false, bN0y = false, bN1y = false;
-  bool bI0x = false, bI1x = false, bI0y = false, bI1y = false;
-  if (c.normalise) {
-    const double nd = c.nd;
-    const double n0x = nd - (double)N1x, n0y = nd - (double)N1y;
-    double v[4];
-    v[0] = (double)N1x * c1 + n0x * c0;
-    v[1] = (double)N1x * (c1 * c1) + n0x * (c0 * c0);
-    v[2] = (double)N1y * c1 + n0y * c0;
-    v[3] = (double)N1y * (c1 * c1) + n0y * (c0 * c0);
-    double l8[8];
+  const BernCounts tot{cnt[0], cnt[1], cnt[2], cnt[3], cnt[4], cnt[5], cnt[6]};
+  double l8[8];
 #pragma unroll
-    for (int q = 0; q < 8; ++q) l8[q] = lap[q];
-    SignStd st;
-    priv_std_from_sums(c, v, l8, st);
-    const bool thr_nan = (st.muNx != st.muNx) || (st.muNy != st.muNy) || (st.muIx != st.muIx) ||
-                         (st.muIy != st.muIy) || (st.sdNx != st.sdNx) || (st.sdNy != st.sdNy) ||
-                         (st.sdIx != st.sdIx) || (st.sdIy != st.sdIy);
-    bad_ni = bad_int = thr_nan;
-    sN0x = sgn_std(c0, st.muNx, st.sdNx, bN0x); sN1x = sgn_std(c1, st.muNx, st.sdNx, bN1x);
-    sN0y = sgn_std(c0, st.muNy, st.sdNy, bN0y); sN1y = sgn_std(c1, st.muNy, st.sdNy, bN1y);
-    sI0x = sgn_std(c0, st.muIx, st.sdIx, bI0x); sI1x = sgn_std(c1, st.muIx, st.sdIx, bI1x);
-    sI0y = sgn_std(c0, st.muIy, st.sdIy, bI0y); sI1y = sgn_std(c1, st.muIy, st.sdIy, bI1y);
-  } else {  // signs of the raw values (vert-cor.R:172-173, 226-227)
-    sN0x = sN0y = sI0x = sI0y = 0;
-    sN1x = sN1y = sI1x = sI1y = 1;
-  }
-  // INT: sum of (2S-1) sign(X) sign(Y) from the combination counts (vert-cor.R:175-183)
-  const long long N10 = N1x - N11, N01 = N1y - N11, N00 = (long long)c.n - N1x - N1y + N11;
-  const long long F10 = Fx - F11, F01 = Fy - F11, F00 = Ft - Fx - Fy + F11;
-  const long long core = (long long)(sI1x * sI1y) * (2 * F11 - N11) +
-                         (long long)(sI1x * sI0y) * (2 * F10 - N10) +
-                         (long long)(sI0x * sI1y) * (2 * F01 - N01) +
-                         (long long)(sI0x * sI0y) * (2 * F00 - N00);
-  bad_int |= (bI1x && N1x > 0) || (bI0x && N1x < c.n) || (bI1y && N1y > 0) || (bI0y && N1y < c.n);
-  // ---- pass B: NI batches from plane popcounts (vert-cor.R:226-239)
-  const uint64_t* PX = planes;
-  const uint64_t* PY = planes + nw;
+  for (int q = 0; q < 8; ++q) l8[q] = lap[q];
+  const BernSigns sg = bern_signs(c, tot, l8);
+  // ---- pass B: NI batches from plane popcounts
+  bool bad_ni = sg.bad_ni;
   DD sT{0.0, 0.0}, sT2{0.0, 0.0};
-  for (int64_t j = tid; j < c.k; j += DCOR_BLOCK) {
-    const int64_t a = j * c.m, b = a + c.m;
-    const int64_t wa = a >> 6, wb = (b - 1) >> 6;
-    int cx1 = 0, cy1 = 0;
-    for (int64_t w = wa; w <= wb; ++w) {
-      uint64_t mask = ~0ull;
-      if (w == wa) mask &= ~0ull << (a & 63);
-      if (w == wb) mask &= ~0ull >> (63 - ((b - 1) & 63));
-      cx1 += __popcll(PX[w] & mask);
-      cy1 += __popcll(PY[w] & mask);
-    }
-    const int cx0 = c.m - cx1, cy0 = c.m - cy1;
-    bad_ni |= (bN1x && cx1) || (bN0x && cx0) || (bN1y && cy1) || (bN0y && cy0);
-    const int cx = sN1x * cx1 + sN0x * cx0, cy = sN1y * cy1 + sN0y * cy0;
-    const U4 w = draw((uint32_t)j, rep, DCOR_SITE_NI_LAP, c.k0, c.k1);   // vert-cor.R:230-231
-    const double xt = (double)cx / c.md + c.bx * unit_laplace(u53(w.w0, w.w1));
-    const double yt = (double)cy / c.md + c.by * unit_laplace(u53(w.w2, w.w3));
-    const double T = c.md * xt * yt;                                     // vert-cor.R:233
-    dd_acc(sT, T);
-    dd_acc(sT2, T * T);
-  }
+  for (int64_t j = tid; j < c.k; j += DCOR_BLOCK) bern_batch(c, sg, planes, planes + nw, j, rep, sT, sT2, bad_ni);
   DD d2[2] = {sT, sT2};
   block_sum_dd<2>(d2, red);
   const long long nbad = block_sum_i(bad_ni ? 1LL : 0LL, redi);
   if (tid == 0) {
     SignPartial p;
     p.sT[0] = d2[0].hi; p.sT[1] = d2[0].lo; p.sT2[0] = d2[1].hi; p.sT2[1] = d2[1].lo;
-    p.core = core;
-    p.flags = (nbad ? 1 : 0) | (bad_int ? 2 : 0);
+    p.core = sg.core;
+    p.flags = (nbad ? 1 : 0) | (sg.bad_int ? 2 : 0);
     part[blockIdx.x] = p;
+  }
+}
+
+// Wave-per-replicate form for n <= BERN_W_NMAX: the planes of a replicate (3 x n/8 B) stay
+// in LDS, four replicates per workgroup run without workgroup barriers, so many more
+// replicates are in flight per CU (the per-replicate fixed work -- scalar Laplace,
+// thresholds, reductions -- is latency that the other waves hide).
+#define BERN_W_NMAX 16384
+#define BERN_W_WORDS (4 * (BERN_W_NMAX / 256))
+__global__ __launch_bounds__(DCOR_BLOCK) void k_sign_bern_w(SignConst c, int64_t nreps,
+                                                            SignPartial* __restrict__ part) {
+  __shared__ uint64_t pls[DCOR_WAVES][3][BERN_W_WORDS];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t r = (int64_t)blockIdx.x * DCOR_WAVES + wv;
+  if (r >= nreps) return;  // whole waves only
+  const uint32_t rep = (uint32_t)(c.rep_begin + r);
+  const int64_t nw = 4 * ((c.n + 255) / 256);
+  // scalar Laplace blocks 0..3 (NI / INT mu, m2 of X, Y): lane q < 4 draws block q
+  double la = 0.0, lb = 0.0;
+  if (lane < 4) {
+    const U4 w = draw((uint32_t)lane, rep, DCOR_SITE_SCALAR, c.k0, c.k1);
+    la = unit_laplace(u53(w.w0, w.w1));
+    lb = unit_laplace(u53(w.w2, w.w3));
+  }
+  double l8[8];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) { l8[2 * q] = __shfl(la, q, 64); l8[2 * q + 1] = __shfl(lb, q, 64); }
+  // ---- pass A
+  BernCounts t{0, 0, 0, 0, 0, 0, 0};
+  const int64_t ngrp = (c.n + 3) / 4;
+  for (int64_t g0 = 0; g0 < ngrp; g0 += 64) {
+    const int64_t g4 = g0 + lane;
+    uint32_t xb = 0, yb = 0, fb = 0;
+    if (g4 < ngrp) bern_gen4(c, rep, g4, xb, yb, fb);
+    uint64_t BX[4], BY[4], BF[4];
+    bern_ballots(xb, yb, fb, t, BX, BY, BF);
+    const int64_t w0 = g0 / 16;
+    if (lane < 12 && w0 + (lane & 3) < nw) {
+      const int q = lane & 3, pl = lane >> 2;
+      pls[wv][pl][w0 + q] = pl == 0 ? interleave4(BX, q) : (pl == 1 ? interleave4(BY, q) : interleave4(BF, q));
+    }
+  }
+  wave_sync();  // plane words written by lanes 0..11 are read by every lane below
+  const BernSigns sg = bern_signs(c, t, l8);
+  bool bad_ni = sg.bad_ni;
+  DD sT{0.0, 0.0}, sT2{0.0, 0.0};
+  for (int64_t j = lane; j < c.k; j += 64) bern_batch(c, sg, pls[wv][0], pls[wv][1], j, rep, sT, sT2, bad_ni);
+  sT = wave_sum_dd(sT);
+  sT2 = wave_sum_dd(sT2);
+  const bool any_bad = __ballot(bad_ni) != 0;
+  if (lane == 0) {
+    SignPartial p;
+    p.sT[0] = sT.hi; p.sT[1] = sT.lo; p.sT2[0] = sT2.hi; p.sT2[1] = sT2.lo;
+    p.core = sg.core;
+    p.flags = (any_bad ? 1 : 0) | (sg.bad_int ? 2 : 0);
+    part[r] = p;
   }
 }
 
@@ -951,8 +1037,12 @@ int launch_sign_bern(SignConst c, int64_t reps, int64_t chunk, uint64_t* scratch
   for (int64_t r = 0; r < reps; r += chunk) {
     const int64_t nr = (reps - r < chunk) ? reps - r : chunk;
     c.rep_begin = rep0 + r;
-    hipLaunchKernelGGL(k_sign_bern, dim3((unsigned)nr), dim3(DCOR_BLOCK), 0, (hipStream_t)stream,
-                       c, scratch, part);
+    if (c.n <= BERN_W_NMAX)
+      hipLaunchKernelGGL(k_sign_bern_w, dim3((unsigned)((nr + DCOR_WAVES - 1) / DCOR_WAVES)),
+                         dim3(DCOR_BLOCK), 0, (hipStream_t)stream, c, nr, part);
+    else
+      hipLaunchKernelGGL(k_sign_bern, dim3((unsigned)nr), dim3(DCOR_BLOCK), 0, (hipStream_t)stream,
+                         c, scratch, part);
     launch_sign_epilogue(c, nr, part, out + r, (hipStream_t)stream);
     if (int e = last_err()) return e;
   }
