@@ -227,6 +227,11 @@ int make_subg(int64_t n, double eps1, double eps2, double eta1, double eta2, dou
     return fail(DCOR_EKLT1, "correlation_NI_subG: k < 1 (ver-cor-subG.R:38)");
   }
   c.m = (int32_t)md; c.k = (int64_t)kd; c.md = md; c.kd = kd;
+  {
+    int e = 0;
+    c.md_pow2 = (std::frexp(md, &e) == 0.5) ? 1 : 0;
+    c.inv_md = c.md_pow2 ? std::ldexp(1.0, 1 - e) : 0.0;
+  }
   c.bx = 2.0 * c.l1 / (md * eps1);                                       // :48
   c.by = 2.0 * c.l2 / (md * eps2);                                       // :49
   c.m_over_k = md / kd;                                                  // :51

@@ -65,6 +65,8 @@ struct SubgConst {
   double ls, lr, bs;                // lambda_s, lambda_r, 2*lambda_s/eps_s
   double s_central, sn2x2;          // 2*lr/(n*eps_r), 2*(s_central^2)
   double sqrt_n, eps_r;
+  int32_t md_pow2, pad4;            // m is a power of two: sum / m == sum * inv_md
+  double inv_md;
 };
 
 // Pre-materialised sign family.

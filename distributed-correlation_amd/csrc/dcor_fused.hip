@@ -923,8 +923,8 @@ __global__ __launch_bounds__(DCOR_BLOCK) void k_subg_fused(SubgConst c, dcor_rep
   auto int_term = [&](double x, double y, double l) {
     const double S = c.sender_is_X ? x : y, O = c.sender_is_X ? y : x;
     const double Uc = rclip_fin((rclip_fin(S, c.ls) + c.bs * l) * O, c.lr);  // ver-cor-subG.R:88-90
-    dd_acc(sU, Uc);
-    dd_acc(sU2, Uc * Uc);
+    ks_acc(sU, Uc);  // compensated sums (error ~ n 2^-106): the mean / sd of Uc
+    ks_acc(sU2, Uc * Uc);
   };
   for (int64_t j = tid; j < c.k; j += DCOR_BLOCK) {
     double sx = 0.0, sy = 0.0;
@@ -937,12 +937,14 @@ __global__ __launch_bounds__(DCOR_BLOCK) void k_subg_fused(SubgConst c, dcor_rep
       int_term(x, y, l);
     }
     const U4 w = draw((uint32_t)j, rep, DCOR_SITE_NI_LAP, c.k0, c.k1);
-    const double xt = sx / c.md + c.bx * unit_laplace(u53(w.w0, w.w1)); // :48
-    const double yt = sy / c.md + c.by * unit_laplace(u53(w.w2, w.w3)); // :49
-    dd_acc(sP, xt * yt);
+    const double mx = c.md_pow2 ? sx * c.inv_md : sx / c.md;            // exact for m = 2^e
+    const double my = c.md_pow2 ? sy * c.inv_md : sy / c.md;
+    const double xt = mx + c.bx * unit_laplace(u53(w.w0, w.w1));        // :48
+    const double yt = my + c.by * unit_laplace(u53(w.w2, w.w3));        // :49
+    ks_acc(sP, xt * yt);
     const double T = c.md * xt * yt;                                     // :55
-    dd_acc(sT, T);
-    dd_acc(sT2, T * T);
+    ks_acc(sT, T);
+    ks_acc(sT2, T * T);
   }
   for (int64_t i = c.k * c.m + tid; i < c.n; i += DCOR_BLOCK) {
     double x, y, l;
