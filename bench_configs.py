@@ -27,16 +27,18 @@ FP64_PEAK_UNITS = 3.93e13
 HBM_PEAK = 8.0e12
 
 
-def timed(fn, reps=3):
+def timed(fn, reps=3, inner=1):
+    """Best of `reps` timings of `inner` back-to-back calls (per call)."""
     import torch
     fn()
     torch.cuda.synchronize()
     best = 1e30
     for _ in range(reps):
         t0 = time.perf_counter()
-        fn()
+        for _ in range(inner):
+            fn()
         torch.cuda.synchronize()
-        best = min(best, time.perf_counter() - t0)
+        best = min(best, (time.perf_counter() - t0) / inner)
     return best
 
 
@@ -75,7 +77,7 @@ def c1():
     from oracle.oracle import sim_reps
     cell = CellSpec(n=1000, rho=0.5, eps1=1.0, eps2=1.0, mu=(0.5, 0.5), sigma=(2.0, 2.0), seed=1_000_073)
     B = 1000
-    t = timed(lambda: simulate(cell, B))
+    t = timed(lambda: simulate(cell, B), reps=5, inner=20)
     t0 = time.perf_counter()
     sim_reps(cell.to_c(), 0, B, threads=1)
     t1 = time.perf_counter() - t0
@@ -177,7 +179,7 @@ def c5(R, panel="coded"):
     pn = C.c_void_p()      # the panel is encoded once for the whole sweep (dcor_panel_create)
     _lib.check(_lib.lib.dcor_panel_create(P(X), P(Y), n, None, C.byref(pn)))
     t = timed(lambda: _lib.check(_lib.lib.dcor_premat_subg_panel_launch(C.byref(d), pn, P(out), None)),
-              reps=5)
+              reps=5, inner=8)
     per_rep = 8 * n + 4 * k * m + 16 * k + 8 * nsim    # SURVEY §8d pinned: 404,648 B
     read_rep = 8 * n + 4 * k * m + 16 * k + 8 + 16 * nsim  # bytes the ABI actually reads (z, l apart)
     ok = C.c_int(-1)
@@ -218,7 +220,7 @@ def subg():
     from dcor.sim import CellSpec, simulate
     cell = CellSpec(n=100_000, rho=0.5, eps1=1.0, eps2=1.0, family="subG", dgp="bounded_factor", seed=5)
     R = 4096
-    t = timed(lambda: simulate(cell, R))
+    t = timed(lambda: simulate(cell, R), reps=3, inner=4)
     u = R * (292 * cell.n + 183 * 12500 + 2e5)
     line("S", reps=R, seconds=t, reps_per_s=R / t, roofline_frac=u / t / FP64_PEAK_UNITS)
 
