@@ -6,11 +6,13 @@
 // device every compute entry fails with DCOR_ENODEV.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <utility>
 #include <vector>
 
 #include "../../include/dcor.h"
@@ -360,20 +362,47 @@ double dcor_lambda_from_priv(double lo, double hi, double mean, double sd) {
 }
 
 double dcor_qnorm(double p) {
-  // Lower-tail solve on min(p, 1-p): Abramowitz-Stegun 26.2.23 start, Halley on erfc.
+  // R's qnorm(p, 0, 1) (qnorm.c: Wichura's AS241, lower tail, log.p = FALSE), same operation
+  // order, so crit = qnorm(1 - alpha/2) is R's double.
   if (std::isnan(p) || p < 0 || p > 1) return NAN;
   if (p == 0) return -INFINITY;
   if (p == 1) return INFINITY;
-  const double pp = (p < 0.5) ? p : 1.0 - p;
-  const double t = std::sqrt(-2.0 * std::log(pp));
-  double x = -(t - (2.515517 + 0.802853 * t + 0.010328 * t * t) /
-                       (1.0 + 1.432788 * t + 0.189269 * t * t + 0.001308 * t * t * t));
-  for (int it = 0; it < 6; ++it) {
-    const double e = 0.5 * std::erfc(-x / 1.4142135623730951) - pp;
-    const double u = e * 2.5066282746310002 * std::exp(0.5 * x * x);
-    x = x - u / (1.0 + 0.5 * x * u);
+  const double q = p - 0.5;
+  double r, val;
+  if (std::fabs(q) <= .425) {
+    r = .180625 - q * q;
+    return q * (((((((r * 2509.0809287301226727 + 33430.575583588128105) * r +
+                     67265.770927008700853) * r + 45921.953931549871457) * r +
+                   13731.693765509461125) * r + 1971.5909503065514427) * r +
+                 133.14166789178437745) * r + 3.387132872796366608) /
+           (((((((r * 5226.495278852545925 + 28729.085735721942674) * r +
+                 39307.89580009271061) * r + 21213.794301586595867) * r +
+               5394.1960214247511077) * r + 687.1870074920579083) * r +
+             42.313330701600911252) * r + 1.);
   }
-  return (p < 0.5) ? x : -x;
+  r = std::sqrt(-std::log((q > 0) ? (0.5 - p + 0.5) : p));
+  if (r <= 5.) {
+    r += -1.6;
+    val = (((((((r * 7.7454501427834140764e-4 + .0227238449892691845833) * r +
+                .24178072517745061177) * r + 1.27045825245236838258) * r +
+              3.64784832476320460504) * r + 5.7694972214606914055) * r +
+            4.6303378461565452959) * r + 1.42343711074968357734) /
+          (((((((r * 1.05075007164441684324e-9 + 5.475938084995344946e-4) * r +
+                .0151986665636164571966) * r + .14810397642748007459) * r +
+              .68976733498510000455) * r + 1.6763848301838038494) * r +
+            2.05319162663775882187) * r + 1.);
+  } else {
+    r += -5.;
+    val = (((((((r * 2.01033439929228813265e-7 + 2.71155556874348757815e-5) * r +
+                .0012426609473880784386) * r + .026532189526576123093) * r +
+              .29656057182850489123) * r + 1.7848265399172913358) * r +
+            5.4637849111641143699) * r + 6.6579046435011037772) /
+          (((((((r * 2.04426310338993978564e-15 + 1.4215117583164458887e-7) * r +
+                1.8463183175100546818e-5) * r + 7.868691311456132591e-4) * r +
+              .0148753612908506148525) * r + .13692988092273580531) * r +
+            .59983220655588793769) * r + 1.);
+  }
+  return (q < 0.0) ? -val : val;
 }
 
 int dcor_batch_geometry(int64_t n, double eps1, double eps2, int family, int hrs, int64_t km[2]) {
@@ -980,6 +1009,341 @@ int dcor_draws_launch(int kind, uint64_t seed, int site, int64_t rep_begin, int6
   const int rc = launch_draws(kind, (uint32_t)seed, (uint32_t)(seed >> 32), (uint32_t)site,
                               rep_begin, reps, count, d_out, stream);
   if (rc) return hip_fail((hipError_t)rc, "draws launch");
+  return DCOR_OK;
+}
+
+}  // extern "C"
+
+// ======================================================= R-stream mode (f4) ===
+// Replicates consume R's own streams (set.seed(cell.seed), then SURVEY.md Appendix A's draw
+// order), so dcor_rstream_grid_run returns run_sim_one's per-seed numbers.  Kernels:
+// dcor_rstream.hip; estimators: the pre-materialised kernels (dcor_premat.hip).
+namespace {
+
+// set.seed(seed): RNG_Init's scrambling, 625 words, word 0 (the position) set to 624
+void rs_seed(int32_t seed, RsState& s) {
+  std::memset(&s, 0, sizeof(s));
+  uint32_t x = (uint32_t)seed;
+  for (int j = 0; j < 50; ++j) x = 69069u * x + 1u;
+  x = 69069u * x + 1u;
+  for (int j = 0; j < 624; ++j) { x = 69069u * x + 1u; s.mt[j] = x; }
+  s.mti = 624;
+}
+
+// MASS::mvrnorm's factor V diag(sqrt(ev)): eigen(Sigma, symmetric = TRUE) is LAPACK dsyevr;
+// for 2x2 dsytrd is the identity and dstemr's n = 2 branch calls dlaev2 (eigenvector
+// (cs, sn) of the larger root, (-sn, cs) of the smaller); R reverses to decreasing order.
+// The product with diag() follows dgemm: C = 0; C += D(l, j) * V(i, l).
+void rs_mvrnorm_factor(const double sigma[2], double rho, double A[4]) {
+  const double a = sigma[0] * sigma[0], b = sigma[0] * sigma[1] * rho, c = sigma[1] * sigma[1];
+  const double sm = a + c, df = a - c, adf = std::fabs(df), tb = b + b, ab = std::fabs(tb);
+  const double acmx = (std::fabs(a) > std::fabs(c)) ? a : c, acmn = (std::fabs(a) > std::fabs(c)) ? c : a;
+  double rt;
+  if (adf > ab) { const double t = ab / adf; rt = adf * std::sqrt(1.0 + t * t); }
+  else if (adf < ab) { const double t = adf / ab; rt = ab * std::sqrt(1.0 + t * t); }
+  else rt = ab * std::sqrt(2.0);
+  double rt1, rt2;
+  int sgn1;
+  if (sm < 0.0) { rt1 = 0.5 * (sm - rt); sgn1 = -1; rt2 = (acmx / rt1) * acmn - (b / rt1) * b; }
+  else if (sm > 0.0) { rt1 = 0.5 * (sm + rt); sgn1 = 1; rt2 = (acmx / rt1) * acmn - (b / rt1) * b; }
+  else { rt1 = 0.5 * rt; rt2 = -0.5 * rt; sgn1 = 1; }
+  double cs;
+  int sgn2;
+  if (df >= 0.0) { cs = df + rt; sgn2 = 1; } else { cs = df - rt; sgn2 = -1; }
+  double cs1, sn1;
+  if (std::fabs(cs) > ab) {
+    const double ct = -tb / cs;
+    sn1 = 1.0 / std::sqrt(1.0 + ct * ct);
+    cs1 = ct * sn1;
+  } else if (ab == 0.0) {
+    cs1 = 1.0; sn1 = 0.0;
+  } else {
+    const double tn = -cs / tb;
+    cs1 = 1.0 / std::sqrt(1.0 + tn * tn);
+    sn1 = tn * cs1;
+  }
+  if (sgn1 == sgn2) { const double tn = cs1; cs1 = -sn1; sn1 = tn; }
+  bool swap = false;
+  if (rt1 < rt2) { std::swap(rt1, rt2); swap = true; }
+  // R's columns: 1 = eigenvector of rt1, 2 = of rt2
+  const double V11 = swap ? -sn1 : cs1, V21 = swap ? cs1 : sn1;
+  const double V12 = swap ? cs1 : -sn1, V22 = swap ? sn1 : cs1;
+  const double d0 = std::sqrt(std::fmax(rt1, 0.0)), d1 = std::sqrt(std::fmax(rt2, 0.0));
+  A[0] = (0.0 + d0 * V11) + 0.0 * V12;
+  A[1] = (0.0 + 0.0 * V11) + d1 * V12;
+  A[2] = (0.0 + d0 * V21) + 0.0 * V22;
+  A[3] = (0.0 + 0.0 * V21) + d1 * V22;
+}
+
+struct RsPlan {
+  RsCell c;
+  int64_t rep_max;       // words per replicate, upper bound (exp_rand takes <= 17 words)
+  size_t per_rep;        // device bytes per replicate in flight
+};
+
+int rs_plan(const dcor_cell& cell, RsPlan& p) {
+  std::memset(&p, 0, sizeof(p));
+  RsCell& c = p.c;
+  const int64_t n = cell.n;
+  if (n < 1 || !(cell.eps1 > 0) || !(cell.eps2 > 0) || cell.nsim < 1)
+    return fail(DCOR_EINVAL, "rstream: bad n / eps / nsim");
+  if (cell.family != DCOR_FAMILY_SIGN && cell.family != DCOR_FAMILY_SUBG)
+    return fail(DCOR_EINVAL, "rstream: bad family");
+  if (cell.dgp != DCOR_DGP_GAUSSIAN && cell.dgp != DCOR_DGP_BERNOULLI &&
+      cell.dgp != DCOR_DGP_BOUNDED_FACTOR)
+    return fail(DCOR_EINVAL, "rstream: DGP not available in R-stream mode (gen_mix_gaussian)");
+  if (cell.seed > 0x7fffffffull) return fail(DCOR_EINVAL, "rstream: set.seed takes a 32-bit integer");
+  c.n = n; c.nsim = cell.nsim; c.family = cell.family; c.dgp = cell.dgp;
+  const bool subg = cell.family == DCOR_FAMILY_SUBG;
+  c.normalise = (!subg && cell.normalise) ? 1 : 0;
+  double m = std::ceil(8.0 / (cell.eps1 * cell.eps2));
+  if (subg && m > (double)n) m = (double)n;
+  const double kd = std::floor((double)n / m);
+  if (!(kd >= 1)) return fail(DCOR_EKLT1, "Need at least one full batch (k < 1)");
+  c.k = (int64_t)kd;
+  if (subg) {
+    c.has_mix = 1;
+  } else {
+    const double eps_r = (cell.eps1 >= cell.eps2) ? cell.eps2 : cell.eps1;
+    int mode = cell.ci_mode;
+    if (mode == DCOR_MODE_AUTO) mode = (std::sqrt((double)n) * eps_r > 0.5) ? DCOR_MODE_NORMAL : DCOR_MODE_LAPLACE;
+    c.has_mix = (mode == DCOR_MODE_NORMAL) ? 1 : 0;
+  }
+  // DGP (vert-cor.R:78-98,389-394; ver-cor-subG.R:141-154)
+  if (cell.dgp == DCOR_DGP_GAUSSIAN) {
+    c.dgp_words = 4 * n;
+    rs_mvrnorm_factor(cell.sigma, cell.rho, c.A);
+    c.mu[0] = cell.mu[0]; c.mu[1] = cell.mu[1];
+  } else if (cell.dgp == DCOR_DGP_BERNOULLI) {
+    c.dgp_words = 2 * n;
+    const double p11 = 0.25 + cell.rho / 4, p10 = 0.25 - cell.rho / 4, p01 = p10;
+    c.bern_t0 = p01 / 0.5; c.bern_t1 = p11 / 0.5;
+  } else {
+    c.cU = std::sqrt(3 * cell.rho); c.cE = std::sqrt(3 * (1 - cell.rho));
+    // runif(n, a, b): non-finite bounds give NaN, a == b gives a, neither draws
+    c.u_draw = (std::isfinite(c.cU) && -c.cU != c.cU) ? 1 : 0;
+    c.e_draw = (std::isfinite(c.cE) && -c.cE != c.cE) ? 1 : 0;
+    c.u_const = std::isfinite(c.cU) ? -c.cU : NAN;
+    c.e_const = std::isfinite(c.cE) ? -c.cE : NAN;
+    c.dgp_words = (c.u_draw + 2 * c.e_draw) * n;
+  }
+  int64_t pre = c.dgp_words;
+  if (!subg) {
+    const double eps_s = (cell.eps1 >= cell.eps2) ? cell.eps1 : cell.eps2;
+    const double pp = std::exp(eps_s) / (std::exp(eps_s) + 1);          // vert-cor.R:174
+    if (pp == 0.0 || pp == 1.0) { c.flip_on = 0; c.flip_const = (pp == 1.0); }
+    else {
+      const double pm = std::fmin(pp, 1. - pp);
+      c.flip_on = 1; c.flip_q = 1. - pm; c.flip_inv = (pp > 0.5) ? 1 : 0;
+    }
+    pre += 2 * (c.normalise ? 4 : 0) + 2 * c.k + (c.flip_on ? n : 0) + 1;
+  } else {
+    pre += 2 * c.k + n + 1;
+  }
+  if (c.has_mix) pre += 2 * c.nsim;
+  c.pre = pre;
+  p.rep_max = pre + (c.has_mix ? 18 * c.nsim : 0);
+  const int64_t fw = (n + 31) / 32;
+  p.per_rep = (size_t)p.rep_max * 4 + (size_t)c.nsim * 8 * 3 + (size_t)n * 16 + 64 +
+              (size_t)c.k * 16 + (size_t)fw * 4 + (subg ? (size_t)n * 8 : 0) + 8 + 16 +
+              sizeof(dcor_rep_out) + 256;
+  return DCOR_OK;
+}
+
+size_t al256(size_t b) { return (b + 255) & ~(size_t)255; }
+
+// Carve cell c's buffers for rc replicates out of `base` (advanced).
+void rs_carve(RsPlan& p, int32_t rc, char*& base) {
+  RsCell& c = p.c;
+  auto take = [&](size_t bytes) { char* q = base; base += al256(bytes); return (void*)q; };
+  const int64_t n = c.n, k = c.k, nsim = c.nsim, fw = (n + 31) / 32;
+  c.words = (uint32_t*)take(((size_t)rc * p.rep_max + 624) * 4);
+  c.rep_off = (int64_t*)take((size_t)rc * 8);
+  c.exp_end = (int64_t*)take((size_t)rc * 8);
+  c.expv = (double*)take((size_t)rc * nsim * 8);
+  c.X = (double*)take((size_t)rc * n * 8);
+  c.Y = (double*)take((size_t)rc * n * 8);
+  c.lap_nsc = (double*)take((size_t)rc * 32);
+  c.lap_isc = (double*)take((size_t)rc * 32);
+  c.lap_x = (double*)take((size_t)rc * k * 8);
+  c.lap_y = (double*)take((size_t)rc * k * 8);
+  c.flips = (uint32_t*)take((size_t)rc * fw * 4);
+  c.lap_local = (c.family == DCOR_FAMILY_SUBG) ? (double*)take((size_t)rc * n * 8) : nullptr;
+  c.lap_scalar = (double*)take((size_t)rc * 8);
+  c.mix_z = (double*)take((size_t)rc * nsim * 8);
+  c.mix_l = (double*)take((size_t)rc * nsim * 8);
+}
+
+size_t rs_cell_bytes(const RsPlan& p, int32_t rc) {
+  const RsCell& c = p.c;
+  const int64_t n = c.n, k = c.k, nsim = c.nsim, fw = (n + 31) / 32;
+  return al256(((size_t)rc * p.rep_max + 624) * 4) + 2 * al256((size_t)rc * 8) +
+         al256((size_t)rc * nsim * 8) + 2 * al256((size_t)rc * n * 8) + 2 * al256((size_t)rc * 32) +
+         2 * al256((size_t)rc * k * 8) + al256((size_t)rc * fw * 4) +
+         ((c.family == DCOR_FAMILY_SUBG) ? al256((size_t)rc * n * 8) : 0) + al256((size_t)rc * 8) +
+         2 * al256((size_t)rc * nsim * 8);
+}
+
+// The estimators over one chunk of materialised replicates of one cell.
+int rs_estimate(const dcor_cell& cell, const RsCell& c, int64_t reps, dcor_rep_out* d_out) {
+  if (cell.family == DCOR_FAMILY_SIGN) {
+    dcor_premat_sign d;
+    std::memset(&d, 0, sizeof(d));
+    d.n = c.n; d.reps = reps; d.eps1 = cell.eps1; d.eps2 = cell.eps2; d.alpha = cell.alpha;
+    d.normalise = cell.normalise; d.ci_mode = cell.ci_mode; d.nsim = c.nsim;
+    d.X = c.X; d.Y = c.Y; d.xy_stride = c.n;
+    d.lap_ni_sc = c.lap_nsc; d.lap_ni_x = c.lap_x; d.lap_ni_y = c.lap_y; d.lap_int_sc = c.lap_isc;
+    d.flips = c.flips; d.lap_z = c.lap_scalar; d.mix_z = c.mix_z; d.mix_l = c.mix_l;
+    return dcor_premat_sign_launch(&d, d_out, nullptr);
+  }
+  dcor_premat_subg d;
+  std::memset(&d, 0, sizeof(d));
+  d.n = c.n; d.reps = reps; d.eps1 = cell.eps1; d.eps2 = cell.eps2; d.eta1 = cell.eta1;
+  d.eta2 = cell.eta2; d.alpha = cell.alpha; d.hrs = 0;
+  d.lam_x = d.lam_y = d.lam_s = d.lam_o = d.lam_r = d.delta = NAN;
+  d.nsim = c.nsim; d.X = c.X; d.Y = c.Y; d.xy_stride = c.n; d.perm = nullptr;
+  d.lap_ni_x = c.lap_x; d.lap_ni_y = c.lap_y; d.lap_local = c.lap_local;
+  d.lap_central = c.lap_scalar; d.mix_z = c.mix_z; d.mix_l = c.mix_l;
+  return dcor_premat_subg_launch(&d, d_out, nullptr);
+}
+
+size_t rs_budget() {
+  const char* e = std::getenv("DCOR_RS_BUDGET_MB");
+  const long mb = e ? std::atol(e) : 4096;
+  return (size_t)(mb > 16 ? mb : 16) << 20;
+}
+
+}  // namespace
+
+extern "C" {
+
+int dcor_rstream_grid_run(const dcor_cell* cells, int ncells, int64_t B, dcor_accum* h_acc,
+                          dcor_rep_out* h_detail) {
+  if (!cells || ncells < 0 || B < 1 || !h_acc) return fail(DCOR_EINVAL, "bad grid arguments");
+  if (int st = need_device()) return st;
+  std::vector<RsPlan> plan((size_t)ncells);
+  for (int i = 0; i < ncells; ++i)
+    if (int st = rs_plan(cells[i], plan[(size_t)i])) return st;
+  const size_t budget = rs_budget();
+  int i0 = 0;
+  while (i0 < ncells) {
+    // a batch of cells whose streams run side by side (one wave each)
+    size_t sum = 0;
+    int nb = 0;
+    const int64_t rc_min = std::min<int64_t>(B, 8);
+    while (i0 + nb < ncells && nb < 65535) {
+      const size_t add = plan[(size_t)(i0 + nb)].per_rep;
+      if (nb > 0 && (sum + add) * (size_t)rc_min > budget) break;
+      sum += add;
+      ++nb;
+    }
+    int64_t rc = (int64_t)(budget / std::max<size_t>(sum, 1));
+    rc = std::max<int64_t>(1, std::min<int64_t>({rc, B, (int64_t)(0x7fffffff / nb)}));
+    size_t bytes = 0;
+    for (int i = 0; i < nb; ++i) bytes += rs_cell_bytes(plan[(size_t)(i0 + i)], (int32_t)rc);
+    DevBuf buf, dst, dcells, dout, acc;
+    HIPCHK(buf.alloc(bytes));
+    HIPCHK(dst.alloc(sizeof(RsState) * (size_t)nb));
+    HIPCHK(dcells.alloc(sizeof(RsCell) * (size_t)nb));
+    HIPCHK(dout.alloc(sizeof(dcor_rep_out) * (size_t)B * (size_t)nb));
+    HIPCHK(acc.alloc(sizeof(dcor_accum) * 2));
+    std::vector<RsState> hst((size_t)nb);
+    std::vector<RsCell> hc((size_t)nb);
+    char* base = buf.as<char>();
+    for (int i = 0; i < nb; ++i) {
+      rs_seed((int32_t)cells[i0 + i].seed, hst[(size_t)i]);
+      RsPlan& p = plan[(size_t)(i0 + i)];
+      rs_carve(p, (int32_t)rc, base);
+      p.c.st = dst.as<RsState>() + i;
+      hc[(size_t)i] = p.c;
+    }
+    HIPCHK(hipMemcpy(dst.p, hst.data(), sizeof(RsState) * (size_t)nb, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(dcells.p, hc.data(), sizeof(RsCell) * (size_t)nb, hipMemcpyHostToDevice));
+    for (int64_t done = 0; done < B; done += rc) {
+      const int32_t rcc = (int32_t)std::min<int64_t>(rc, B - done);
+      int e = launch_rs_stream(dcells.as<RsCell>(), nb, rcc, nullptr);
+      if (e) return hip_fail((hipError_t)e, "rstream stream launch");
+      e = launch_rs_materialise(dcells.as<RsCell>(), nb, rcc, nullptr);
+      if (e) return hip_fail((hipError_t)e, "rstream materialise launch");
+      for (int i = 0; i < nb; ++i)
+        if (int st = rs_estimate(cells[i0 + i], hc[(size_t)i], rcc,
+                                 dout.as<dcor_rep_out>() + (size_t)i * B + done)) return st;
+    }
+    for (int i = 0; i < nb; ++i) {
+      dcor_rep_out* o = dout.as<dcor_rep_out>() + (size_t)i * B;
+      if (int st = dcor_accumulate_launch(o, B, cells[i0 + i].rho, acc.as<dcor_accum>(), nullptr))
+        return st;
+      HIPCHK(hipMemcpy(h_acc + 2 * (i0 + i), acc.p, sizeof(dcor_accum) * 2, hipMemcpyDeviceToHost));
+      if (h_detail)
+        HIPCHK(hipMemcpy(h_detail + (size_t)(i0 + i) * B, o, sizeof(dcor_rep_out) * (size_t)B,
+                         hipMemcpyDeviceToHost));
+    }
+    i0 += nb;
+  }
+  return DCOR_OK;
+}
+
+int dcor_rstream_draws(const dcor_cell* cell, int64_t reps, const dcor_rs_draws* h) {
+  if (!cell || !h || reps < 1 || reps > 65535) return fail(DCOR_EINVAL, "bad rstream_draws arguments");
+  if (int st = need_device()) return st;
+  RsPlan p;
+  if (int st = rs_plan(*cell, p)) return st;
+  const int32_t rc = (int32_t)reps;
+  DevBuf buf, dst, dcell;
+  HIPCHK(buf.alloc(rs_cell_bytes(p, rc)));
+  HIPCHK(dst.alloc(sizeof(RsState)));
+  HIPCHK(dcell.alloc(sizeof(RsCell)));
+  RsState hs;
+  rs_seed((int32_t)cell->seed, hs);
+  char* base = buf.as<char>();
+  rs_carve(p, rc, base);
+  p.c.st = dst.as<RsState>();
+  HIPCHK(hipMemcpy(dst.p, &hs, sizeof(hs), hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(dcell.p, &p.c, sizeof(RsCell), hipMemcpyHostToDevice));
+  int e = launch_rs_stream(dcell.as<RsCell>(), 1, rc, nullptr);
+  if (!e) e = launch_rs_materialise(dcell.as<RsCell>(), 1, rc, nullptr);
+  if (e) return hip_fail((hipError_t)e, "rstream launch");
+  const RsCell& c = p.c;
+  const size_t R = (size_t)reps, n = (size_t)c.n, k = (size_t)c.k, ns = (size_t)c.nsim;
+  auto get = [&](void* dst_h, const void* src_d, size_t bytes) -> int {
+    if (dst_h && src_d) HIPCHK(hipMemcpy(dst_h, src_d, bytes, hipMemcpyDeviceToHost));
+    return DCOR_OK;
+  };
+  int st = 0;
+  st |= get(h->X, c.X, R * n * 8);
+  st |= get(h->Y, c.Y, R * n * 8);
+  st |= get(h->lap_ni_sc, c.lap_nsc, R * 32);
+  st |= get(h->lap_int_sc, c.lap_isc, R * 32);
+  st |= get(h->lap_ni_x, c.lap_x, R * k * 8);
+  st |= get(h->lap_ni_y, c.lap_y, R * k * 8);
+  st |= get(h->flips, c.flips, R * ((n + 31) / 32) * 4);
+  st |= get(h->lap_local, c.lap_local, R * n * 8);
+  st |= get(h->lap_scalar, c.lap_scalar, R * 8);
+  st |= get(h->mix_z, c.mix_z, R * ns * 8);
+  st |= get(h->mix_l, c.mix_l, R * ns * 8);
+  return st ? DCOR_EHIP : DCOR_OK;
+}
+
+int dcor_rstream_words(int32_t seed, int64_t count, uint32_t* h_out) {
+  if (!h_out || count < 1 || count > ((int64_t)1 << 30)) return fail(DCOR_EINVAL, "bad rstream_words arguments");
+  if (int st = need_device()) return st;
+  RsCell c;
+  std::memset(&c, 0, sizeof(c));
+  c.pre = count;
+  DevBuf words, idx, dst, dcell;
+  HIPCHK(words.alloc(sizeof(uint32_t) * (size_t)(count + 624)));
+  HIPCHK(idx.alloc(16));
+  HIPCHK(dst.alloc(sizeof(RsState)));
+  HIPCHK(dcell.alloc(sizeof(RsCell)));
+  RsState hs;
+  rs_seed(seed, hs);
+  c.st = dst.as<RsState>(); c.words = words.as<uint32_t>();
+  c.rep_off = idx.as<int64_t>(); c.exp_end = idx.as<int64_t>() + 1;
+  HIPCHK(hipMemcpy(dst.p, &hs, sizeof(hs), hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(dcell.p, &c, sizeof(RsCell), hipMemcpyHostToDevice));
+  const int e = launch_rs_stream(dcell.as<RsCell>(), 1, 1, nullptr);
+  if (e) return hip_fail((hipError_t)e, "rstream words launch");
+  HIPCHK(hipMemcpy(h_out, words.p, sizeof(uint32_t) * (size_t)count, hipMemcpyDeviceToHost));
   return DCOR_OK;
 }
 

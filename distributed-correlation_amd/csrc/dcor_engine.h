@@ -145,4 +145,39 @@ int launch_perm(uint32_t k0, uint32_t k1, uint32_t site, int64_t rep_begin, int6
 int launch_dp_sd(const double* x, int64_t n, double lo, double hi, double s_mu, double s_m2,
                  const double* lap2, double* out2, void* stream);
 
+// R-stream mode (dcor_rstream.hip): R's Mersenne-Twister state as set.seed leaves it.
+struct RsState {
+  uint32_t mt[624];
+  int32_t mti;
+  int32_t pad[3];
+};
+// One grid cell of an R-stream batch: the replicate's word layout,
+// the host-evaluated transform constants, and the cell's device buffers for a chunk of rc
+// replicates (carved from one allocation by the host).
+struct RsCell {
+  int64_t n, k, nsim;
+  int64_t dgp_words;   // words of the DGP segment
+  int64_t pre;         // words of a replicate before its exp_rand segment (or all of them)
+  int32_t family, dgp, normalise, has_mix;
+  int32_t flip_on, flip_inv, flip_const, u_draw, e_draw, pad;
+  double flip_q;       // rbinom(1, pp): ix = (u >= flip_q)
+  double A[4], mu[2];  // mvrnorm: X = mu + ((0 + z1 A0) + z2 A1), Y likewise with A2, A3
+  double bern_t0, bern_t1;
+  double cU, cE, u_const, e_const;
+  RsState* st;
+  uint32_t* words;     // rc * rep_max + 624 tempered words
+  int64_t* rep_off;    // [rc] first word of each replicate
+  int64_t* exp_end;    // [rc] first word after each replicate's exp_rand segment
+  double* expv;        // [rc][nsim] rexp values
+  double *X, *Y;       // [rc][n]
+  double *lap_nsc, *lap_isc;   // [rc][4] standardisation draws (sign, normalise)
+  double *lap_x, *lap_y;       // [rc][k]
+  uint32_t* flips;             // [rc][ceil(n/32)]
+  double* lap_local;           // [rc][n] (sub-G)
+  double* lap_scalar;          // [rc] Z (sign) / central (sub-G)
+  double *mix_z, *mix_l;       // [rc][nsim]
+};
+int launch_rs_stream(RsCell* d_cells, int ncells, int32_t rc, void* stream);
+int launch_rs_materialise(const RsCell* d_cells, int ncells, int32_t rc, void* stream);
+
 }  // namespace dcor

@@ -1,0 +1,349 @@
+// dcor_rstream.hip -- R-stream mode: replicates consume R's OWN random
+// streams, so run_sim_one(..., seed) on the GPU returns the reference's per-seed numbers.
+//
+// R's generator is one sequential Mersenne-Twister stream per set.seed() (vert-cor.R:364;
+// ver-cor-subG.R:169), consumed in the call order of SURVEY.md Appendix A.  The engine keeps
+// that contract and puts the parallelism where R's stream allows it:
+//   k_rs_stream       one wave per grid cell: MT19937 blocks of 624 words (the recurrence
+//                     is wave-parallel: every dependency is >= 227 words back), tempered
+//                     words streamed to HBM, and the only data-dependent consumption --
+//                     exp_rand inside mixquant -- walked in order, so every replicate's
+//                     offset in the stream is known.  The MT state is persistent across
+//                     chunks of replicates (.Random.seed semantics).
+//   k_rs_materialise  one workgroup per (cell, replicate): words -> R's variates (inversion
+//                     rnorm with AS241 qnorm, mvrnorm's eigen factor, runif, rbinom,
+//                     extraDistr rlaplace), written in the explicit-input layout.
+//   then the pre-materialised estimator kernels (dcor_premat.hip) per cell.
+// Every transform uses IEEE basic operations, explicit fma and R's operation order
+// (-ffp-contract=off); log is the accurate double-double rs_log (csrc/dcor_tables.h), so the
+// GPU matches the CPU restatement oracle/dcor_rstream.c bit for bit.
+#include <hip/hip_runtime.h>
+
+#include "dcor_device.h"
+#include "dcor_engine.h"
+
+namespace dcor {
+
+// ------------------------------------------------------------ R variates ---
+__device__ __forceinline__ double rs_unif(uint32_t w) {
+  // MT_genrand's y * 2.3283064365386963e-10, then unif_rand's fixup into (0, 1)
+  const double x = (double)w * 2.3283064365386963e-10;
+  if (x <= 0.0) return 0.5 * 2.328306437080797e-10;
+  return x;  // (1 - x) > 0 for every 32-bit word
+}
+
+__device__ __forceinline__ void rs_two_sum(double a, double b, double& s, double& e) {
+  const double t = a + b, bb = t - a;
+  s = t;
+  e = (a - (t - bb)) + (b - bb);
+}
+
+__device__ double rs_log(double x) {
+  // x positive normal.  log x = k ln2 + log c + log1p(r), r = z*invc - 1 exact as a pair,
+  // r^2/2 in double-double, the r^3 .. r^10 tail in double, log c as a double-double.
+  const uint64_t ix = (uint64_t)__double_as_longlong(x);
+  const uint64_t tmp = ix - 0x3fe6000000000000ull;
+  const int i = (int)((tmp >> 45) & 127u);
+  const int64_t k = (int64_t)tmp >> 52;
+  const double z = __longlong_as_double((long long)(ix - (tmp & (0xfffull << 52))));
+  const double invc = dcor_log_tab[i][0], lch = dcor_log_tab[i][1], lcl = dcor_log_tab_lo[i];
+  const double p = z * invc;
+  const double pe = fma(z, invc, -p);
+  double r1, r2;
+  rs_two_sum(p - 1.0, pe, r1, r2);
+  const double s2 = r1 * r1;
+  const double s2e = fma(r1, r1, -s2);
+  const double h = -0.5 * s2;
+  const double hl = -0.5 * (s2e + 2.0 * r1 * r2);
+  double t = DCOR_RS_LOG1P_C10;
+  t = fma(t, r1, DCOR_RS_LOG1P_C9);
+  t = fma(t, r1, DCOR_RS_LOG1P_C8);
+  t = fma(t, r1, DCOR_RS_LOG1P_C7);
+  t = fma(t, r1, DCOR_RS_LOG1P_C6);
+  t = fma(t, r1, DCOR_RS_LOG1P_C5);
+  t = fma(t, r1, DCOR_RS_LOG1P_C4);
+  t = fma(t, r1, DCOR_RS_LOG1P_C3);
+  const double tail = (r1 * s2) * t;
+  double a1, a2;
+  rs_two_sum(r1, h, a1, a2);
+  const double kd = (double)k;
+  double s, se, s3, se3;
+  rs_two_sum(kd * DCOR_LN2_HI, lch, s, se);
+  rs_two_sum(s, a1, s3, se3);
+  const double lo = se + se3 + (a2 + hl + r2 + tail) + (kd * DCOR_LN2_LO + lcl);
+  return s3 + lo;
+}
+
+__device__ double rs_qnorm5(double p) {
+  // R's qnorm(p) (qnorm.c, Wichura's AS241) for p in (0, 1), lower tail
+  const double q = p - 0.5;
+  double r, val;
+  if (fabs(q) <= .425) {
+    r = .180625 - q * q;
+    return q * (((((((r * 2509.0809287301226727 + 33430.575583588128105) * r +
+                     67265.770927008700853) * r + 45921.953931549871457) * r +
+                   13731.693765509461125) * r + 1971.5909503065514427) * r +
+                 133.14166789178437745) * r + 3.387132872796366608) /
+           (((((((r * 5226.495278852545925 + 28729.085735721942674) * r +
+                 39307.89580009271061) * r + 21213.794301586595867) * r +
+               5394.1960214247511077) * r + 687.1870074920579083) * r +
+             42.313330701600911252) * r + 1.);
+  }
+  r = (q > 0) ? (0.5 - p + 0.5) : p;
+  r = sqrt_pos(-rs_log(r));
+  if (r <= 5.) {
+    r += -1.6;
+    val = (((((((r * 7.7454501427834140764e-4 + .0227238449892691845833) * r +
+                .24178072517745061177) * r + 1.27045825245236838258) * r +
+              3.64784832476320460504) * r + 5.7694972214606914055) * r +
+            4.6303378461565452959) * r + 1.42343711074968357734) /
+          (((((((r * 1.05075007164441684324e-9 + 5.475938084995344946e-4) * r +
+                .0151986665636164571966) * r + .14810397642748007459) * r +
+              .68976733498510000455) * r + 1.6763848301838038494) * r +
+            2.05319162663775882187) * r + 1.);
+  } else {
+    r += -5.;
+    val = (((((((r * 2.01033439929228813265e-7 + 2.71155556874348757815e-5) * r +
+                .0012426609473880784386) * r + .026532189526576123093) * r +
+              .29656057182850489123) * r + 1.7848265399172913358) * r +
+            5.4637849111641143699) * r + 6.6579046435011037772) /
+          (((((((r * 2.04426310338993978564e-15 + 1.4215117583164458887e-7) * r +
+                1.8463183175100546818e-5) * r + 7.868691311456132591e-4) * r +
+              .0148753612908506148525) * r + .13692988092273580531) * r +
+            .59983220655588793769) * r + 1.);
+  }
+  return (q < 0.0) ? -val : val;
+}
+
+// norm_rand(), INVERSION: u = (int)(2^27 u1) + u2; qnorm5(u / 2^27)
+__device__ __forceinline__ double rs_norm(uint32_t w1, uint32_t w2) {
+  const double BIG = 134217728.0;
+  const double u = (double)(int)(BIG * rs_unif(w1)) + rs_unif(w2);
+  return rs_qnorm5(u / BIG);
+}
+
+// extraDistr::rlaplace(1, 0, 1) of one word: u = runif(-.5, .5); -sign(u) log(1 - 2|u|)
+__device__ __forceinline__ double rs_lap(uint32_t w) {
+  const double u = -0.5 + 1.0 * rs_unif(w);
+  if (u == 0.0) return 0.0;
+  const double l = rs_log(1.0 - 2.0 * fabs(u));
+  return (u > 0) ? -l : l;
+}
+
+// ------------------------------------------------------------- k_rs_stream ---
+#define RS_N 624
+#define RS_M 397
+
+__device__ const double rs_exp_q[16] = {
+    0.6931471805599453, 0.9333736875190459, 0.9888777961838675, 0.9984959252914960040,
+    0.9998292811061389, 0.9999833164100727, 0.9999985691438767, 0.9999998906925558,
+    0.9999999924734159, 0.9999999995283275, 0.9999999999728814, 0.9999999999985598,
+    0.9999999999999289, 0.9999999999999968, 0.9999999999999999, 1.0000000000000000};
+
+__global__ __launch_bounds__(64) void k_rs_stream(RsCell* cells, int32_t rc) {
+  __shared__ uint32_t mt[RS_N];
+  __shared__ uint32_t tb[RS_N];
+  RsCell& c = cells[blockIdx.x];
+  const int lane = threadIdx.x;
+  RsState* st = c.st;
+  for (int t = lane; t < RS_N; t += 64) mt[t] = st->mt[t];
+  int mti = st->mti;
+  __syncthreads();
+  uint32_t* out = c.words;
+  int64_t cur = 0;
+  int32_t r = 0;
+  int phase = 0;                 // 0: fixed words before the exp segment, 1: exp, 2: rbinom
+  int64_t left = c.pre;
+  int64_t j = 0;                 // exp draw index
+  int es = 0, ei = 0;            // exp_rand sub-state, loop counter
+  double ea = 0, eu = 0, emin = 0;
+  if (lane == 0) c.rep_off[0] = 0;
+  while (r < rc) {
+    if (mti >= RS_N) {           // MT19937 block: mt[kk] from mt[kk+1] (old) and
+      for (int base = 0; base < RS_N; base += 64) {  // mt[kk+397] (old) / mt[kk-227] (new)
+        const int kk = base + lane;
+        uint32_t nv = 0;
+        if (kk < RS_N) {
+          const uint32_t y = (mt[kk] & 0x80000000u) | (mt[kk == RS_N - 1 ? 0 : kk + 1] & 0x7fffffffu);
+          const uint32_t src = mt[kk < RS_N - RS_M ? kk + RS_M : kk - (RS_N - RS_M)];
+          nv = src ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+        }
+        __syncthreads();
+        if (kk < RS_N) mt[kk] = nv;
+        __syncthreads();
+      }
+      mti = 0;
+    }
+    const int avail = RS_N - mti;
+    for (int t = lane; t < avail; t += 64) {
+      uint32_t y = mt[mti + t];
+      y ^= (y >> 11);
+      y ^= (y << 7) & 0x9d2c5680u;
+      y ^= (y << 15) & 0xefc60000u;
+      y ^= (y >> 18);
+      tb[t] = y;
+      out[cur + t] = y;
+    }
+    __syncthreads();
+    int used = 0;
+    while (used < avail && r < rc) {
+      if (phase != 1) {
+        const int64_t take = (left < (int64_t)(avail - used)) ? left : (int64_t)(avail - used);
+        used += (int)take;
+        left -= take;
+        if (left == 0) {
+          if (phase == 0 && c.has_mix) {
+            phase = 1; j = 0; es = 0;
+          } else {
+            ++r;
+            if (r < rc && lane == 0) c.rep_off[r] = cur + used;
+            phase = 0; left = c.pre;
+          }
+        }
+      } else {
+        const double u = rs_unif(tb[used]);
+        ++used;
+        bool done = false;
+        double e = 0;
+        if (es == 0) {           // exp_rand: u doubled until > 1, a += ln 2 each time
+          ea = 0.;
+          eu = u;
+          for (;;) {
+            eu += eu;
+            if (eu > 1.) break;
+            ea += rs_exp_q[0];
+          }
+          eu -= 1.;
+          if (eu <= rs_exp_q[0]) { e = ea + eu; done = true; } else { es = 1; }
+        } else if (es == 1) {    // ustar = unif_rand(), umin = ustar
+          emin = u; ei = 0; es = 2;
+        } else {                 // do { ustar; umin = min; i++ } while (u > q[i])
+          if (emin > u) emin = u;
+          ++ei;
+          if (!(eu > rs_exp_q[ei])) { e = ea + emin * rs_exp_q[0]; done = true; }
+        }
+        if (done) {
+          if (lane == 0) c.expv[(int64_t)r * c.nsim + j] = e;
+          es = 0;
+          if (++j == c.nsim) {
+            if (lane == 0) c.exp_end[r] = cur + used;
+            phase = 2; left = c.nsim;
+          }
+        }
+      }
+    }
+    cur += used;
+    mti += used;
+    __syncthreads();
+  }
+  for (int t = lane; t < RS_N; t += 64) st->mt[t] = mt[t];
+  if (lane == 0) st->mti = mti;
+}
+
+// -------------------------------------------------------- k_rs_materialise ---
+__global__ __launch_bounds__(256) void k_rs_materialise(const RsCell* cells, int32_t rc) {
+  const RsCell& c = cells[blockIdx.x / rc];
+  const int64_t r = blockIdx.x % rc;
+  const uint32_t* w = c.words + c.rep_off[r];
+  const int64_t n = c.n, k = c.k, nsim = c.nsim;
+  const int tid = threadIdx.x;
+  double* X = c.X + r * n;
+  double* Y = c.Y + r * n;
+  // 1. DGP
+  if (c.dgp == DCOR_DGP_GAUSSIAN) {
+    // matrix(rnorm(2n), n): column 1 = draws 0..n-1, column 2 = draws n..2n-1;
+    // mu + (V diag(sqrt(ev))) %*% t(Z) in dgemm's order
+    for (int64_t i = tid; i < n; i += 256) {
+      const double z1 = rs_norm(w[2 * i], w[2 * i + 1]);
+      const double z2 = rs_norm(w[2 * (n + i)], w[2 * (n + i) + 1]);
+      X[i] = c.mu[0] + ((0.0 + z1 * c.A[0]) + z2 * c.A[1]);
+      Y[i] = c.mu[1] + ((0.0 + z1 * c.A[2]) + z2 * c.A[3]);
+    }
+  } else if (c.dgp == DCOR_DGP_BERNOULLI) {
+    for (int64_t i = tid; i < n; i += 256) {   // u <- runif(n); v <- runif(n)
+      const double u = rs_unif(w[i]), v = rs_unif(w[n + i]);
+      const double x = (u < 0.5) ? 1.0 : 0.0;
+      X[i] = x;
+      Y[i] = (x == 0.0) ? ((v < c.bern_t0) ? 1.0 : 0.0) : ((v < c.bern_t1) ? 1.0 : 0.0);
+    }
+  } else {  // bounded factor: U, E1, E2 <- runif(n, -c, c); a == b draws nothing
+    const int64_t oe1 = c.u_draw ? n : 0, oe2 = oe1 + (c.e_draw ? n : 0);
+    for (int64_t i = tid; i < n; i += 256) {
+      const double U = c.u_draw ? (-c.cU + (c.cU - -c.cU) * rs_unif(w[i])) : c.u_const;
+      const double E1 = c.e_draw ? (-c.cE + (c.cE - -c.cE) * rs_unif(w[oe1 + i])) : c.e_const;
+      const double E2 = c.e_draw ? (-c.cE + (c.cE - -c.cE) * rs_unif(w[oe2 + i])) : c.e_const;
+      X[i] = U + E1;
+      Y[i] = U + E2;
+    }
+  }
+  int64_t o = c.dgp_words;
+  double* lx = c.lap_x + r * k;
+  double* ly = c.lap_y + r * k;
+  if (c.family == DCOR_FAMILY_SIGN) {
+    // 2. ci_NI_signbatch: standardisation (4), rLap(k) X, rLap(k) Y
+    // 3. ci_INT_signflip: standardisation (4), rbinom(n, 1, p), Z
+    const int64_t nrm = c.normalise ? 4 : 0;
+    if (tid < 4) {
+      c.lap_nsc[r * 4 + tid] = c.normalise ? rs_lap(w[o + tid]) : 0.0;
+      c.lap_isc[r * 4 + tid] = c.normalise ? rs_lap(w[o + nrm + 2 * k + tid]) : 0.0;
+    }
+    for (int64_t i = tid; i < k; i += 256) {
+      lx[i] = rs_lap(w[o + nrm + i]);
+      ly[i] = rs_lap(w[o + nrm + k + i]);
+    }
+    o += 2 * nrm + 2 * k;
+    uint32_t* fw = c.flips + r * ((n + 31) / 32);
+    for (int64_t b = tid; b < (n + 31) / 32; b += 256) {
+      uint32_t bits = 0;
+      for (int t = 0; t < 32; ++t) {
+        const int64_t i = b * 32 + t;
+        if (i >= n) break;
+        // rbinom(1, pp): p = min(pp, 1 - pp), ix = (u >= 1 - p), S = pp > .5 ? 1 - ix : ix
+        uint32_t s = c.flip_const;
+        if (c.flip_on) s = ((rs_unif(w[o + i]) < c.flip_q) ? 0u : 1u) ^ (uint32_t)c.flip_inv;
+        bits |= s << t;
+      }
+      fw[b] = bits;
+    }
+    o += c.flip_on ? n : 0;
+  } else {
+    // 2. correlation_NI_subG: rLap(k) X, rLap(k) Y;  3. ci_INT_subG: rLap(n), rLap(1)
+    for (int64_t i = tid; i < k; i += 256) {
+      lx[i] = rs_lap(w[o + i]);
+      ly[i] = rs_lap(w[o + k + i]);
+    }
+    o += 2 * k;
+    double* ll = c.lap_local + r * n;
+    for (int64_t i = tid; i < n; i += 256) ll[i] = rs_lap(w[o + i]);
+    o += n;
+  }
+  if (tid == 0) c.lap_scalar[r] = rs_lap(w[o]);
+  o += 1;
+  // 4. mixquant: rnorm(nsim), rexp(nsim) (walked by k_rs_stream), rbinom(nsim, 1, .5)
+  double* mz = c.mix_z + r * nsim;
+  double* ml = c.mix_l + r * nsim;
+  if (c.has_mix) {
+    const uint32_t* wb = c.words + c.exp_end[r];
+    const double* ev = c.expv + r * nsim;
+    for (int64_t jj = tid; jj < nsim; jj += 256) {
+      mz[jj] = rs_norm(w[o + 2 * jj], w[o + 2 * jj + 1]);
+      const double e = ev[jj];
+      ml[jj] = (rs_unif(wb[jj]) < 0.5) ? -e : e;   // e * (2 * rbinom(1, .5) - 1)
+    }
+  } else {
+    for (int64_t jj = tid; jj < nsim; jj += 256) { mz[jj] = 0.0; ml[jj] = 0.0; }
+  }
+}
+
+int launch_rs_stream(RsCell* d_cells, int ncells, int32_t rc, void* stream) {
+  hipLaunchKernelGGL(k_rs_stream, dim3(ncells), dim3(64), 0, (hipStream_t)stream, d_cells, rc);
+  return (int)hipGetLastError();
+}
+
+int launch_rs_materialise(const RsCell* d_cells, int ncells, int32_t rc, void* stream) {
+  hipLaunchKernelGGL(k_rs_materialise, dim3((unsigned)(ncells * rc)), dim3(256), 0,
+                     (hipStream_t)stream, d_cells, rc);
+  return (int)hipGetLastError();
+}
+
+}  // namespace dcor

@@ -13,3 +13,4 @@ from .sim import (CellSpec, headline_cell, paper_grid, run_cell, run_grid, run_s
                   run_sim_one_subG, simulate, subg_grid, vert_cor_grid)
 
 __version__ = "0.1.0"
+from . import rstream  # noqa: F401,E402

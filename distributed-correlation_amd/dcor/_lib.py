@@ -91,6 +91,13 @@ class PrematSubg(C.Structure):
 _D = C.POINTER(C.c_double)
 _I64 = C.POINTER(C.c_int64)
 
+
+class RsDraws(C.Structure):
+    """dcor_rs_draws: host buffers of the R-stream mode's materialised draws."""
+    _fields_ = [("X", _D), ("Y", _D), ("lap_ni_sc", _D), ("lap_int_sc", _D), ("lap_ni_x", _D),
+                ("lap_ni_y", _D), ("flips", C.POINTER(C.c_uint32)), ("lap_local", _D),
+                ("lap_scalar", _D), ("mix_z", _D), ("mix_l", _D)]
+
 # name -> (restype, argtypes); this list IS the exported ABI (checked against the header
 # by tests/test_abi.py).
 SIGNATURES = {
@@ -108,6 +115,10 @@ SIGNATURES = {
     "dcor_accum_merge": (None, [C.POINTER(Accum), C.POINTER(Accum)]),
     "dcor_accum_finalize": (None, [C.POINTER(Accum), C.c_double, C.POINTER(Summary)]),
     "dcor_grid_run": (C.c_int, [C.POINTER(Cell), C.c_int, C.c_int64, C.POINTER(Accum), C.POINTER(RepOut)]),
+    "dcor_rstream_grid_run": (C.c_int, [C.POINTER(Cell), C.c_int, C.c_int64, C.POINTER(Accum),
+                                        C.POINTER(RepOut)]),
+    "dcor_rstream_draws": (C.c_int, [C.POINTER(Cell), C.c_int64, C.POINTER(RsDraws)]),
+    "dcor_rstream_words": (C.c_int, [C.c_int32, C.c_int64, C.POINTER(C.c_uint32)]),
     "dcor_premat_sign_launch": (C.c_int, [C.POINTER(PrematSign), _P, _P]),
     "dcor_premat_subg_launch": (C.c_int, [C.POINTER(PrematSubg), _P, _P]),
     "dcor_panel_dict_probe": (C.c_int, [_P, _P, C.c_int64, C.POINTER(C.c_int)]),

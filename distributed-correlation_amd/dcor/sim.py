@@ -168,16 +168,18 @@ def run_cell(cell: CellSpec, B: int, detail: bool = True, chunk: int = 1 << 16, 
 
 # ---------------------------------------------------------- R-shaped drivers
 def run_sim_one(n, rho, eps1, eps2, mu=(0.0, 0.0), sigma=(1.0, 1.0), B=1000, alpha=0.05,
-                ci_mode="auto", normalise=True, seed=2025, dgp="gaussian") -> dict:
-    """run_sim_one of vert-cor.R:356-444 (sign family; dgp='bernoulli' wires gen_bernoulli)."""
+                ci_mode="auto", normalise=True, seed=2025, dgp="gaussian", rng="philox") -> dict:
+    """run_sim_one of vert-cor.R:356-444 (sign family; dgp='bernoulli' wires gen_bernoulli).
+    rng='R' replays R's own stream for set.seed(seed) (dcor.rstream)."""
     cell = CellSpec(n=n, rho=rho, eps1=eps1, eps2=eps2, family="sign", dgp=dgp, alpha=alpha,
                     mu=mu, sigma=sigma, normalise=normalise, ci_mode=ci_mode, seed=seed)
-    return run_cell(cell, B)
+    return _run(cell, B, rng)
 
 
 def run_sim_one_subG(n, rho, eps1, eps2, dgp_fun="bounded_factor", dgp_args=None, B=1000,
-                     alpha=0.05, use_subG=True, ci_mode="auto", seed=2025) -> dict:
-    """run_sim_one of ver-cor-subG.R:159-222.  use_subG=FALSE routes to the sign family."""
+                     alpha=0.05, use_subG=True, ci_mode="auto", seed=2025, rng="philox") -> dict:
+    """run_sim_one of ver-cor-subG.R:159-222.  use_subG=FALSE routes to the sign family.
+    rng='R' replays R's own stream for set.seed(seed) (dcor.rstream)."""
     args = dict(dgp_args or {})
     mix = {}
     if dgp_fun == "mix_gaussian":  # gen_mix_gaussian(mu0, sigma0, mu1, sigma1, pi_mix)
@@ -186,6 +188,15 @@ def run_sim_one_subG(n, rho, eps1, eps2, dgp_fun="bounded_factor", dgp_args=None
     cell = CellSpec(n=n, rho=rho, eps1=eps1, eps2=eps2, family="subG" if use_subG else "sign",
                     dgp=dgp_fun, alpha=alpha, ci_mode=ci_mode, seed=seed,
                     mu=args.get("mu", (0.0, 0.0)), sigma=args.get("sigma", (1.0, 1.0)), **mix)
+    return _run(cell, B, rng)
+
+
+def _run(cell: CellSpec, B: int, rng: str) -> dict:
+    if rng == "R":
+        from .rstream import run_cell as run_cell_r
+        return run_cell_r(cell, B)
+    if rng != "philox":
+        raise ValueError(f"rng must be 'philox' or 'R', not {rng!r}")
     return run_cell(cell, B)
 
 

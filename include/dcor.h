@@ -135,6 +135,33 @@ void dcor_accum_finalize(const dcor_accum* acc, double rho, dcor_summary* out);
 int dcor_grid_run(const dcor_cell* cells, int ncells, int64_t B, dcor_accum* h_acc,
                   dcor_rep_out* h_detail);
 
+/* ---- R-stream mode ------------------------------------- */
+/* The same grid as dcor_grid_run, but every replicate consumes R's OWN random stream: cell
+ * i starts from set.seed(cells[i].seed) (R's Mersenne-Twister / Inversion defaults) and
+ * draws in run_sim_one's call order (vert-cor.R:364,392-419; ver-cor-subG.R:169,174-198;
+ * SURVEY.md Appendix A): mvrnorm / gen_bernoulli / gen_bounded_factor, priv_standardize and
+ * batch Laplace (extraDistr::rlaplace), rbinom flips, mixquant's rnorm / rexp / rbinom.
+ * Replicate b of a cell therefore equals the reference's replicate b for that seed, up to
+ * libm rounding of log.  seed must fit set.seed's 32-bit integer; DGPs:
+ * Gaussian, Bernoulli, bounded factor.  Synchronous, host buffers, like dcor_grid_run. */
+int dcor_rstream_grid_run(const dcor_cell* cells, int ncells, int64_t B, dcor_accum* h_acc,
+                          dcor_rep_out* h_detail);
+/* The explicit inputs R-stream replicates 0 .. reps-1 of one cell consume (HOST buffers,
+ * rep-major; a NULL pointer skips that array): the parity hook of the R-stream mode. */
+typedef struct dcor_rs_draws {
+  double *X, *Y;                  /* [reps][n]                                        */
+  double *lap_ni_sc, *lap_int_sc; /* [reps][4] unit Laplace (sign family, normalise)   */
+  double *lap_ni_x, *lap_ni_y;    /* [reps][k]                                        */
+  uint32_t* flips;                /* [reps][ceil(n/32)] rbinom(n, 1, p) bits (sign)    */
+  double* lap_local;              /* [reps][n] (sub-G)                                */
+  double* lap_scalar;             /* [reps] Z (sign) / central Laplace (sub-G)        */
+  double *mix_z, *mix_l;          /* [reps][nsim] rnorm, rexp*(2*rbinom-1)             */
+} dcor_rs_draws;
+int dcor_rstream_draws(const dcor_cell* cell, int64_t reps, const dcor_rs_draws* h);
+/* The first `count` tempered Mersenne-Twister words after set.seed(seed), from the GPU
+ * generator (unif_rand() = fixup(word * 2^-32)). */
+int dcor_rstream_words(int32_t seed, int64_t count, uint32_t* h_out);
+
 /* ---- pre-materialised (explicit-input) batch mode: HBM streaming --------- */
 /* Sign family, R replicates.  Per-replicate arrays are laid out rep-major with
  * the given strides (a stride of 0 shares one array across replicates). */

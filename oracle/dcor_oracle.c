@@ -81,19 +81,11 @@ static double r_clip_lohi(double x, double lo, double hi) {
 /* qnorm: Abramowitz-Stegun 26.2.23 start + Halley steps on erfc.  Only ever
  * evaluated at 1 - alpha/2; checked against scipy.special.ndtri in tests. */
 double orc_qnorm(double p) {
+  /* R's qnorm (AS241), restated in dcor_rstream.c; the central branch needs no log */
   if (isnan(p) || p < 0 || p > 1) return NAN;
   if (p == 0) return -INFINITY;
   if (p == 1) return INFINITY;
-  const double pp = (p < 0.5) ? p : 1.0 - p; /* exact (Sterbenz) */
-  const double t = sqrt(-2.0 * log(pp));
-  double x = -(t - (2.515517 + 0.802853 * t + 0.010328 * t * t) /
-                       (1.0 + 1.432788 * t + 0.189269 * t * t + 0.001308 * t * t * t));
-  for (int it = 0; it < 6; ++it) { /* lower tail: F(x) = erfc(-x/sqrt2)/2 */
-    const double e = 0.5 * erfc(-x / 1.4142135623730951) - pp;
-    const double u = e * 2.5066282746310002 * exp(0.5 * x * x);
-    x = x - u / (1.0 + 0.5 * x * u);
-  }
-  return (p < 0.5) ? x : -x;
+  return orc_rs_qnorm5(p);
 }
 
 /* ------------------------------------------------ calibration (subG.R:1-7) */

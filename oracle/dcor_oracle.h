@@ -129,6 +129,42 @@ void orc_gen_laplace(uint64_t seed, int64_t rep, int site, int64_t count, double
 /* Keyed pseudo-random permutation of [0, n) (the engine's dcor_perm_launch). */
 void orc_perm(uint64_t seed, int site, int64_t rep, int64_t n, int64_t count, int32_t* out);
 
+/* ---- R's own streams (dcor_rstream.c) -------------------- */
+typedef struct orc_rs_state { uint32_t mt[624]; int32_t mti; } orc_rs_state;
+void     orc_rs_set_seed(orc_rs_state* st, int32_t seed);   /* set.seed(seed)            */
+uint32_t orc_rs_word(orc_rs_state* st);                     /* MT19937 tempered word     */
+double   orc_rs_word_unif(uint32_t w);                      /* word -> unif_rand value   */
+double   orc_rs_unif(orc_rs_state* st);                     /* unif_rand()               */
+double   orc_rs_norm(orc_rs_state* st);                     /* norm_rand() (INVERSION)   */
+double   orc_rs_norm_words(uint32_t w1, uint32_t w2);
+double   orc_rs_exp(orc_rs_state* st);                      /* exp_rand()                */
+double   orc_rs_rbinom1(orc_rs_state* st, double pp);       /* rbinom(1, 1, pp)          */
+double   orc_rs_runif(orc_rs_state* st, double a, double b);/* runif(1, a, b)            */
+double   orc_rs_laplace_unit_word(uint32_t w);              /* rlaplace(1, 0, 1) of a word */
+double   orc_rs_log(double x);                              /* accurate double-double log */
+double   orc_rs_qnorm5(double p);                           /* R's qnorm (AS241)         */
+extern const double orc_rs_exp_q[16];
+void orc_rs_eigen2(double a, double b, double c, double values[2], double vectors[4]);
+void orc_rs_mvrnorm_factor(const double sigma[2], double rho, double A[4]);
+
+/* One replicate's draws in R's call order, materialised in the
+ * explicit-input layout of the pre-materialised engine. */
+typedef struct orc_rs_draws {
+  double *X, *Y;              /* [n]                                                  */
+  double lap_sc[8];           /* sign: NI mu_X m2_X mu_Y m2_Y, INT mu_X m2_X mu_Y m2_Y */
+  double *lap_ni_x, *lap_ni_y;/* [k]                                                  */
+  uint8_t* flips;             /* sign: [n] rbinom(n, 1, p)                            */
+  double* lap_local;          /* sub-G: [n] rLap(n)                                   */
+  double lap_scalar;          /* sign: Z; sub-G: the central rLap(1)                  */
+  double *mix_z, *mix_l;      /* [nsim] (when has_mix)                                */
+  int has_mix;
+  int64_t k;
+} orc_rs_draws;
+int orc_rs_geometry(const void* cell, int64_t* k_out, int* mix_out);
+int orc_rs_draw_rep(orc_rs_state* st, const void* cell, orc_rs_draws* d);
+/* run_sim_one with R's streams: set.seed(cell->seed), B replicates; out B x 6. */
+int orc_rs_sim(const void* cell, int64_t B, double* out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -228,3 +228,110 @@ def gen_xy(cell_struct, rep):
     lib.orc_gen_xy(C.cast(C.pointer(cell_struct), C.c_void_p), rep, X.ctypes.data_as(_D),
                    Y.ctypes.data_as(_D))
     return X, Y
+
+
+# ------------------------------------------------------------ R's own streams (f4)
+class RsState(C.Structure):
+    """R's Mersenne-Twister state (.Random.seed[3:627]) and position."""
+    _fields_ = [("mt", C.c_uint32 * 624), ("mti", C.c_int32)]
+
+
+class RsDraws(C.Structure):
+    _fields_ = [("X", _D), ("Y", _D), ("lap_sc", C.c_double * 8), ("lap_ni_x", _D),
+                ("lap_ni_y", _D), ("flips", _U8), ("lap_local", _D), ("lap_scalar", C.c_double),
+                ("mix_z", _D), ("mix_l", _D), ("has_mix", C.c_int), ("k", C.c_int64)]
+
+
+_PS = C.POINTER(RsState)
+for _n, (_r, _a) in {
+    "orc_rs_set_seed": (None, [_PS, C.c_int32]),
+    "orc_rs_word": (C.c_uint32, [_PS]),
+    "orc_rs_word_unif": (C.c_double, [C.c_uint32]),
+    "orc_rs_unif": (C.c_double, [_PS]),
+    "orc_rs_norm": (C.c_double, [_PS]),
+    "orc_rs_norm_words": (C.c_double, [C.c_uint32, C.c_uint32]),
+    "orc_rs_exp": (C.c_double, [_PS]),
+    "orc_rs_rbinom1": (C.c_double, [_PS, C.c_double]),
+    "orc_rs_runif": (C.c_double, [_PS, C.c_double, C.c_double]),
+    "orc_rs_laplace_unit_word": (C.c_double, [C.c_uint32]),
+    "orc_rs_log": (C.c_double, [C.c_double]),
+    "orc_rs_qnorm5": (C.c_double, [C.c_double]),
+    "orc_rs_eigen2": (None, [C.c_double] * 3 + [_D, _D]),
+    "orc_rs_mvrnorm_factor": (None, [_D, C.c_double, _D]),
+    "orc_rs_geometry": (C.c_int, [C.c_void_p, _I64, C.POINTER(C.c_int)]),
+    "orc_rs_draw_rep": (C.c_int, [_PS, C.c_void_p, C.POINTER(RsDraws)]),
+    "orc_rs_sim": (C.c_int, [C.c_void_p, C.c_int64, _D]),
+}.items():
+    _f = getattr(lib, _n)
+    _f.restype = _r
+    _f.argtypes = _a
+
+
+def rs_state(seed: int) -> RsState:
+    """set.seed(seed)."""
+    st = RsState()
+    lib.orc_rs_set_seed(C.byref(st), int(seed))
+    return st
+
+
+def rs_stream(seed: int, kind: str, count: int, *args) -> np.ndarray:
+    """`count` draws of R's runif/rnorm/rexp/rbinom1/word after set.seed(seed)."""
+    st = rs_state(seed)
+    f = {"unif": lib.orc_rs_unif, "norm": lib.orc_rs_norm, "exp": lib.orc_rs_exp,
+         "rbinom1": lib.orc_rs_rbinom1, "runif": lib.orc_rs_runif, "word": lib.orc_rs_word}[kind]
+    out = [f(C.byref(st), *args) for _ in range(count)]
+    return np.array(out, dtype=np.uint32 if kind == "word" else np.float64)
+
+
+def rs_eigen2(a, b, c):
+    """eigen(matrix(c(a, b, b, c), 2), symmetric = TRUE) -> (values[2], vectors 2x2)."""
+    v = np.zeros(2)
+    V = np.zeros(4)
+    lib.orc_rs_eigen2(a, b, c, v.ctypes.data_as(_D), V.ctypes.data_as(_D))
+    return v, V.reshape(2, 2).T
+
+
+def rs_mvrnorm_factor(sigma, rho):
+    s = np.ascontiguousarray(sigma, dtype=np.float64)
+    A = np.zeros(4)
+    lib.orc_rs_mvrnorm_factor(s.ctypes.data_as(_D), rho, A.ctypes.data_as(_D))
+    return A
+
+
+def rs_draw_reps(cell_struct, reps: int) -> list:
+    """The first `reps` replicates' draws of a cell in R's order, after set.seed(cell.seed)."""
+    cp = C.cast(C.pointer(cell_struct), C.c_void_p)
+    k = C.c_int64()
+    mix = C.c_int()
+    st_ = lib.orc_rs_geometry(cp, C.byref(k), C.byref(mix))
+    if st_:
+        raise RuntimeError(f"oracle status {st_}")
+    n, nsim = cell_struct.n, cell_struct.nsim
+    st = rs_state(cell_struct.seed)
+    out = []
+    for _ in range(reps):
+        a = {"X": np.zeros(n), "Y": np.zeros(n), "lap_ni_x": np.zeros(k.value),
+             "lap_ni_y": np.zeros(k.value), "flips": np.zeros(n, dtype=np.uint8),
+             "lap_local": np.zeros(n), "mix_z": np.zeros(nsim), "mix_l": np.zeros(nsim)}
+        d = RsDraws()
+        for key in ("X", "Y", "lap_ni_x", "lap_ni_y", "lap_local", "mix_z", "mix_l"):
+            setattr(d, key, a[key].ctypes.data_as(_D))
+        d.flips = a["flips"].ctypes.data_as(_U8)
+        s = lib.orc_rs_draw_rep(C.byref(st), cp, C.byref(d))
+        if s:
+            raise RuntimeError(f"oracle status {s}")
+        a["lap_sc"] = np.array(d.lap_sc[:])
+        a["lap_scalar"] = d.lap_scalar
+        a["has_mix"] = d.has_mix
+        a["k"] = d.k
+        out.append(a)
+    return out
+
+
+def rs_sim(cell_struct, B: int) -> np.ndarray:
+    """run_sim_one's B replicates with R's own streams -> [B, 6]."""
+    out = np.zeros((B, 6))
+    st = lib.orc_rs_sim(C.cast(C.pointer(cell_struct), C.c_void_p), B, out.ctypes.data_as(_D))
+    if st:
+        raise RuntimeError(f"oracle status {st}")
+    return out

@@ -44,7 +44,7 @@ def test_struct_layout_matches_header():
     from dcor import _lib
     structs = {"dcor_cell": _lib.Cell, "dcor_rep_out": _lib.RepOut, "dcor_accum": _lib.Accum,
                "dcor_summary": _lib.Summary, "dcor_premat_sign": _lib.PrematSign,
-               "dcor_premat_subg": _lib.PrematSubg}
+               "dcor_premat_subg": _lib.PrematSubg, "dcor_rs_draws": _lib.RsDraws}
     lines = ['#include <stdio.h>', '#include <stddef.h>', f'#include "{HEADER}"', "int main(void){"]
     for cname, py in structs.items():
         lines.append(f'printf("{cname} %zu\\n", sizeof({cname}));')
@@ -71,7 +71,9 @@ def test_host_calibration_matches_r_formulas():
             ls, lr = dcor.lambda_INT_n(n, 1, 1, eps_s)
             assert ls == min(2 * math.sqrt(math.log(n)), 2 * math.sqrt(3))
             assert lr == 5 * 1 * min(math.log(n), 6) / min(eps_s, 1)
-    assert dcor.qnorm(0.975) == 1.959963984540054
+    from oracle.oracle import lib as olib
+    assert dcor.qnorm(0.975) == olib.orc_rs_qnorm5(0.975)  # R's qnorm: AS241, same operation order
+    assert abs(dcor.qnorm(0.975) - 1.959963984540054) <= 4.5e-16
     # real-data-sims.R:170-174, 103-106
     assert dcor.lambda_receiver_from_noise(2.0, 3.0, 2.0, 1e-4) == (2.0 + (2 * 2.0 / 2.0) * math.log(1e4)) * 3.0
     assert dcor.lambda_from_priv(45, 90, {"mean": 65.0, "sd": 10.0}) == 2.5

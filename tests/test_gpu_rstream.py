@@ -1,0 +1,115 @@
+"""GPU parity of the R-stream mode against its CPU restatement
+(oracle/dcor_rstream.c, pinned to values R prints: tests/test_rstream.py).
+
+Bar: the Mersenne-Twister words and every materialised draw bit-exact; estimators and CI
+endpoints within 1e-12 relative (the pre-materialised kernels' bar)."""
+import os
+
+import numpy as np
+import pytest
+
+from helpers import assert_close
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def dc():
+    import torch
+    assert torch.cuda.is_available()
+    import dcor
+    return dcor
+
+
+@pytest.fixture(scope="module")
+def orc():
+    from oracle import oracle
+    return oracle
+
+
+def _spec(dc, **kw):
+    base = dict(n=1000, rho=0.5, eps1=1.0, eps2=1.0, family="sign", dgp="gaussian",
+                mu=(0.5, 0.5), sigma=(2.0, 2.0), seed=1_000_073)
+    base.update(kw)
+    return dc.CellSpec(**base)
+
+
+CELLS = {
+    "sign-gauss": dict(),
+    "sign-gauss-neg": dict(rho=-0.65, eps1=1.5, eps2=0.5, n=1501, seed=1_000_017),
+    "sign-gauss-rho0": dict(rho=0.0, eps1=0.5, eps2=1.5, n=777, seed=1_000_001),
+    "sign-bern": dict(dgp="bernoulli", mu=(0, 0), sigma=(1, 1), rho=0.3, n=999, seed=1_000_042),
+    "sign-nonorm-laplace": dict(normalise=False, ci_mode="laplace", n=640),
+    "subG-bounded": dict(family="subG", dgp="bounded_factor", rho=0.3, n=1001, mu=(0, 0), sigma=(1, 1)),
+    "subG-bounded-rho0": dict(family="subG", dgp="bounded_factor", rho=0.0, n=512, mu=(0, 0), sigma=(1, 1)),
+    "subG-gauss": dict(family="subG", dgp="gaussian", rho=0.8, n=2048, mu=(0, 0), sigma=(1, 1),
+                       eps1=0.2, eps2=0.2, seed=1_000_300),
+}
+
+
+@pytest.mark.parametrize("seed", [1, 42, 1_000_073])
+def test_mt_words_bitexact(dc, orc, seed):
+    got = dc.rstream.words(seed, 5000)
+    want = orc.rs_stream(seed, "word", 5000)
+    np.testing.assert_array_equal(got, want)
+
+
+@pytest.mark.parametrize("name", list(CELLS))
+def test_draws_bitexact(dc, orc, name):
+    spec = _spec(dc, **CELLS[name])
+    reps = 3
+    got = dc.rstream.draws(spec, reps)
+    ref = orc.rs_draw_reps(spec.to_c(), reps)
+    sub = spec.family == "subG"
+    for r in range(reps):
+        a, g = ref[r], {k: v[r] for k, v in got.items()}
+        np.testing.assert_array_equal(g["X"], a["X"], err_msg=f"X rep {r}")
+        np.testing.assert_array_equal(g["Y"], a["Y"], err_msg=f"Y rep {r}")
+        np.testing.assert_array_equal(g["lap_ni_x"], a["lap_ni_x"])
+        np.testing.assert_array_equal(g["lap_ni_y"], a["lap_ni_y"])
+        assert g["lap_scalar"] == a["lap_scalar"]
+        if sub:
+            np.testing.assert_array_equal(g["lap_local"], a["lap_local"])
+        else:
+            if spec.normalise:
+                np.testing.assert_array_equal(g["lap_ni_sc"], a["lap_sc"][:4])
+                np.testing.assert_array_equal(g["lap_int_sc"], a["lap_sc"][4:])
+            bits = np.unpackbits(g["flips"].view(np.uint8), bitorder="little")[:spec.n]
+            np.testing.assert_array_equal(bits, a["flips"])
+        if a["has_mix"]:
+            np.testing.assert_array_equal(g["mix_z"], a["mix_z"])
+            np.testing.assert_array_equal(g["mix_l"], a["mix_l"])
+
+
+def test_grid_matches_oracle_replicate_by_replicate(dc, orc):
+    specs = [_spec(dc, **kw) for kw in CELLS.values()]
+    B = 12
+    res = dc.rstream.run_grid(specs, B)
+    for spec, r in zip(specs, res):
+        ref = orc.rs_sim(spec.to_c(), B)
+        assert_close(r["records"], ref, what=str(spec))
+
+
+def test_chunked_streams_are_continuous(dc):
+    """A small device budget splits B into chunks: the MT state carries over exactly."""
+    specs = [_spec(dc, **CELLS["sign-gauss"]), _spec(dc, **CELLS["subG-bounded"])]
+    full = dc.rstream.run_grid(specs, 40)
+    old = os.environ.get("DCOR_RS_BUDGET_MB")
+    os.environ["DCOR_RS_BUDGET_MB"] = "17"
+    try:
+        small = dc.rstream.run_grid(specs, 40)
+    finally:
+        if old is None:
+            del os.environ["DCOR_RS_BUDGET_MB"]
+        else:
+            os.environ["DCOR_RS_BUDGET_MB"] = old
+    for a, b in zip(full, small):
+        np.testing.assert_array_equal(a["records"], b["records"])
+
+
+def test_run_sim_one_rng_r(dc, orc):
+    res = dc.run_sim_one(n=1000, rho=0.5, eps1=1.0, eps2=1.0, mu=(0.5, 0.5), sigma=(2.0, 2.0),
+                         B=20, seed=1_000_073, rng="R")
+    ref = orc.rs_sim(_spec(dc).to_c(), 20)
+    assert_close(np.stack([res["detail"][k] for k in ("ni_hat", "ni_low", "ni_up", "int_hat",
+                                                      "int_low", "int_up")], 1), ref)
