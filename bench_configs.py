@@ -8,6 +8,9 @@ C4  legacy paper sweep: {sign: gaussian, bernoulli; sub-G: gaussian, bounded fac
 C5  HRS BMI-vs-Age pre-materialised streaming (synthetic stand-in panel n=19,433, eps=2): noise
     generated on device into HBM, then the streaming kernel is timed -> replicates/s and HBM GB/s
 S   sub-G fused, bounded factor, n=1e5, rho=.5, eps=(1,1)
+R1  R-stream mode (R's own Mersenne-Twister streams) on the C1 cell: GPU vs the
+    CPU restatement (1 thread)
+RG  R-stream mode on vert-cor.R's own 144-cell sign-family grid, B = 250 (vert-cor.R:486-553)
 Run on one GPU: python bench_configs.py [--only C2,C5] > profiles/rNN_configs.jsonl
 """
 import argparse
@@ -225,9 +228,47 @@ def subg():
     line("S", reps=R, seconds=t, reps_per_s=R / t, roofline_frac=u / t / FP64_PEAK_UNITS)
 
 
+def rstream_c1():
+    from dcor import rstream
+    from dcor.sim import CellSpec
+    from oracle.oracle import rs_sim
+    cell = CellSpec(n=1000, rho=0.5, eps1=1.0, eps2=1.0, mu=(0.5, 0.5), sigma=(2.0, 2.0), seed=1_000_073)
+    B = 1000
+    t = timed(lambda: rstream.run_cell(cell, B, detail=False), reps=3)
+    Bc = 200
+    t0 = time.perf_counter()
+    rs_sim(cell.to_c(), Bc)
+    tc = (time.perf_counter() - t0) / Bc * B
+    line("R1", reps=B, gpu_s=t, gpu_reps_per_s=B / t, cpu_1thread_s=tc, cpu_1thread_reps_per_s=B / tc,
+         cpu_sample=f"{Bc} replicates timed, scaled to {B}",
+         note="both sides replay R's stream for set.seed(1000073); GPU time includes allocation and D2H")
+
+
+def rstream_grid():
+    from dcor import rstream
+    from dcor.sim import vert_cor_grid
+    from oracle.oracle import rs_sim
+    cells = vert_cor_grid()
+    B = 250
+    t = timed(lambda: rstream.run_grid(cells, B, detail=False), reps=1)
+    # CPU restatement on a sample: the smallest and the largest n of the grid, 10 reps each
+    samp = [cells[0], cells[5]]
+    tc = 0.0
+    for c in samp:
+        t0 = time.perf_counter()
+        rs_sim(c.to_c(), 10)
+        tc += (time.perf_counter() - t0) / 10
+    n_mean = sum(c.n for c in cells) / len(cells)
+    cpu_proj = tc / sum(c.n for c in samp) * n_mean * len(cells) * B
+    line("RG", cells=len(cells), reps_per_cell=B, seconds=t, reps_per_s=len(cells) * B / t,
+         cpu_1thread_projected_s=cpu_proj,
+         cpu_sample="10 reps of the n=1000 and n=9000 cells, per-sample cost scaled to the grid",
+         note="R's own streams (set.seed(1e6+i)); cells run side by side, one MT wave each")
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--only", default="C1,C2,C3,C4,C5,C5c,C5e,S")
+    ap.add_argument("--only", default="C1,C2,C3,C4,C5,C5c,C5e,S,R1,RG")
     ap.add_argument("--c3-reps", type=int, default=2000)
     ap.add_argument("--c4-B", type=int, default=1000)
     ap.add_argument("--c5-R", type=int, default=8192)
@@ -244,6 +285,8 @@ def main():
     if "C5c" in which: c5(a.c5_R, panel="continuous")
     if "C5e" in which: c5_e2e(a.c5e_R)
     if "S" in which: subg()
+    if "R1" in which: rstream_c1()
+    if "RG" in which: rstream_grid()
 
 
 if __name__ == "__main__":

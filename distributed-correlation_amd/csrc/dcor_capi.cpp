@@ -1157,7 +1157,7 @@ void rs_carve(RsPlan& p, int32_t rc, char*& base) {
   RsCell& c = p.c;
   auto take = [&](size_t bytes) { char* q = base; base += al256(bytes); return (void*)q; };
   const int64_t n = c.n, k = c.k, nsim = c.nsim, fw = (n + 31) / 32;
-  c.words = (uint32_t*)take(((size_t)rc * p.rep_max + 624) * 4);
+  c.words = (uint32_t*)take(((size_t)rc * p.rep_max + 2 * 624 + 64) * 4);
   c.rep_off = (int64_t*)take((size_t)rc * 8);
   c.exp_end = (int64_t*)take((size_t)rc * 8);
   c.expv = (double*)take((size_t)rc * nsim * 8);
@@ -1177,7 +1177,7 @@ void rs_carve(RsPlan& p, int32_t rc, char*& base) {
 size_t rs_cell_bytes(const RsPlan& p, int32_t rc) {
   const RsCell& c = p.c;
   const int64_t n = c.n, k = c.k, nsim = c.nsim, fw = (n + 31) / 32;
-  return al256(((size_t)rc * p.rep_max + 624) * 4) + 2 * al256((size_t)rc * 8) +
+  return al256(((size_t)rc * p.rep_max + 2 * 624 + 64) * 4) + 2 * al256((size_t)rc * 8) +
          al256((size_t)rc * nsim * 8) + 2 * al256((size_t)rc * n * 8) + 2 * al256((size_t)rc * 32) +
          2 * al256((size_t)rc * k * 8) + al256((size_t)rc * fw * 4) +
          ((c.family == DCOR_FAMILY_SUBG) ? al256((size_t)rc * n * 8) : 0) + al256((size_t)rc * 8) +
@@ -1239,6 +1239,8 @@ int dcor_rstream_grid_run(const dcor_cell* cells, int ncells, int64_t B, dcor_ac
     }
     int64_t rc = (int64_t)(budget / std::max<size_t>(sum, 1));
     rc = std::max<int64_t>(1, std::min<int64_t>({rc, B, (int64_t)(0x7fffffff / nb)}));
+    if (const char* e = std::getenv("DCOR_RS_MAX_CHUNK"))   // test hook: force short chunks
+      rc = std::max<int64_t>(1, std::min<int64_t>(rc, std::atol(e)));
     size_t bytes = 0;
     for (int i = 0; i < nb; ++i) bytes += rs_cell_bytes(plan[(size_t)(i0 + i)], (int32_t)rc);
     DevBuf buf, dst, dcells, dout, acc;
@@ -1331,7 +1333,7 @@ int dcor_rstream_words(int32_t seed, int64_t count, uint32_t* h_out) {
   std::memset(&c, 0, sizeof(c));
   c.pre = count;
   DevBuf words, idx, dst, dcell;
-  HIPCHK(words.alloc(sizeof(uint32_t) * (size_t)(count + 624)));
+  HIPCHK(words.alloc(sizeof(uint32_t) * (size_t)(count + 2 * 624 + 64)));
   HIPCHK(idx.alloc(16));
   HIPCHK(dst.alloc(sizeof(RsState)));
   HIPCHK(dcell.alloc(sizeof(RsCell)));

@@ -133,116 +133,246 @@ __device__ __forceinline__ double rs_lap(uint32_t w) {
 // ------------------------------------------------------------- k_rs_stream ---
 #define RS_N 624
 #define RS_M 397
+#define RS_EXP_MAXW 17   // exp_rand consumes at most 1 + 1 + 15 words
 
-__device__ const double rs_exp_q[16] = {
-    0.6931471805599453, 0.9333736875190459, 0.9888777961838675, 0.9984959252914960040,
-    0.9998292811061389, 0.9999833164100727, 0.9999985691438767, 0.9999998906925558,
-    0.9999999924734159, 0.9999999995283275, 0.9999999999728814, 0.9999999999985598,
-    0.9999999999999289, 0.9999999999999968, 0.9999999999999999, 1.0000000000000000};
+// exp_rand's q[k-1] = sum_{j<=k} ln2^j / j! (R's sexp.c table)
+#define RS_Q0 0.6931471805599453
+#define RS_Q_TABLE                                                                            \
+  {0.6931471805599453, 0.9333736875190459, 0.9888777961838675, 0.9984959252914960040,       \
+   0.9998292811061389, 0.9999833164100727, 0.9999985691438767, 0.9999998906925558,         \
+   0.9999999924734159, 0.9999999995283275, 0.9999999999728814, 0.9999999999985598,         \
+   0.9999999999999289, 0.9999999999999968, 0.9999999999999999, 1.0000000000000000}
 
+__device__ __forceinline__ uint32_t rs_temper(uint32_t y) {
+  y ^= (y >> 11);
+  y ^= (y << 7) & 0x9d2c5680u;
+  y ^= (y << 15) & 0xefc60000u;
+  y ^= (y >> 18);
+  return y;
+}
+
+__device__ __forceinline__ uint32_t rs_untemper(uint32_t y) {
+  y ^= y >> 18;
+  y ^= (y << 15) & 0xefc60000u;
+  uint32_t x = y;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) x = y ^ ((x << 7) & 0x9d2c5680u);
+  y = x;
+  x = y ^ (y >> 11);
+  x = y ^ (x >> 11);
+  return x;
+}
+
+__device__ __forceinline__ int rs_rl(int v, int s) { return __builtin_amdgcn_readlane(v, s); }
+__device__ __forceinline__ int rs_u(int v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ int rs_wrap(int x) { return (x >= 2 * 624) ? x - 2 * 624 : x; }
+__device__ __forceinline__ int64_t rs_u64(int64_t v) {
+  const int lo = rs_u((int)v), hi = rs_u((int)(v >> 32));
+  return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+__device__ __forceinline__ double rs_rld(double v, int s) {
+  const long long b = __double_as_longlong(v);
+  const int lo = rs_rl((int)b, s), hi = rs_rl((int)(b >> 32), s);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
+// One wave per cell.  mt[] holds the raw state of the newest block; ring[] the tempered words
+// of the last two blocks (slot = absolute word index mod 1248), so exp_rand draws can look
+// up to 17 words ahead while the walk stays at most one block behind generation.
+// Positions are chunk-relative: P words consumed, Q words produced (and written to HBM).
 __global__ __launch_bounds__(64) void k_rs_stream(RsCell* cells, int32_t rc) {
   __shared__ uint32_t mt[RS_N];
-  __shared__ uint32_t tb[RS_N];
-  RsCell& c = cells[blockIdx.x];
+  __shared__ uint32_t ring[2 * RS_N];
+  // every field in registers: the kernel's stores could alias the descriptor, and a reload
+  // from global memory inside the walk costs an L2 round trip per draw
+  const RsCell& cg = cells[blockIdx.x];
+  const int64_t c_pre = cg.pre, c_nsim = cg.nsim;
+  const int c_has_mix = cg.has_mix;
+  // global (not flat) stores: a flat store also counts in lgkmcnt, so every LDS wait behind
+  // it would wait for the store to reach memory
+#define RS_G __attribute__((address_space(1)))
+  RS_G int64_t* const rep_off = (RS_G int64_t*)cg.rep_off;
+  RS_G int64_t* const exp_end = (RS_G int64_t*)cg.exp_end;
+  RS_G double* const gexpv = (RS_G double*)cg.expv;
   const int lane = threadIdx.x;
-  RsState* st = c.st;
+  RsState* st = cg.st;
   for (int t = lane; t < RS_N; t += 64) mt[t] = st->mt[t];
-  int mti = st->mti;
+  // uniform by construction: readfirstlane keeps the walk's counters in scalar registers
+  const int mti0 = __builtin_amdgcn_readfirstlane(st->mti);
+  int par = __builtin_amdgcn_readfirstlane(st->pad[0]) & 1;  // ring half of mt[]'s block
+  const int par0 = par;
   __syncthreads();
-  uint32_t* out = c.words;
-  int64_t cur = 0;
-  int32_t r = 0;
-  int phase = 0;                 // 0: fixed words before the exp segment, 1: exp, 2: rbinom
-  int64_t left = c.pre;
-  int64_t j = 0;                 // exp draw index
-  int es = 0, ei = 0;            // exp_rand sub-state, loop counter
-  double ea = 0, eu = 0, emin = 0;
-  if (lane == 0) c.rep_off[0] = 0;
-  while (r < rc) {
-    if (mti >= RS_N) {           // MT19937 block: mt[kk] from mt[kk+1] (old) and
-      for (int base = 0; base < RS_N; base += 64) {  // mt[kk+397] (old) / mt[kk-227] (new)
-        const int kk = base + lane;
-        uint32_t nv = 0;
-        if (kk < RS_N) {
-          const uint32_t y = (mt[kk] & 0x80000000u) | (mt[kk == RS_N - 1 ? 0 : kk + 1] & 0x7fffffffu);
-          const uint32_t src = mt[kk < RS_N - RS_M ? kk + RS_M : kk - (RS_N - RS_M)];
-          nv = src ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
-        }
-        __syncthreads();
-        if (kk < RS_N) mt[kk] = nv;
-        __syncthreads();
-      }
-      mti = 0;
+  RS_G uint32_t* const out = (RS_G uint32_t*)cg.words;
+  int64_t P = 0, Q = 0;
+  if (mti0 < RS_N) {                      // the rest of the current block comes first
+    for (int t = lane; t < RS_N; t += 64) {
+      const uint32_t w = rs_temper(mt[t]);
+      ring[par * RS_N + t] = w;
+      if (t >= mti0) out[t - mti0] = w;
     }
-    const int avail = RS_N - mti;
-    for (int t = lane; t < avail; t += 64) {
-      uint32_t y = mt[mti + t];
-      y ^= (y >> 11);
-      y ^= (y << 7) & 0x9d2c5680u;
-      y ^= (y << 15) & 0xefc60000u;
-      y ^= (y >> 18);
-      tb[t] = y;
-      out[cur + t] = y;
-    }
-    __syncthreads();
-    int used = 0;
-    while (used < avail && r < rc) {
-      if (phase != 1) {
-        const int64_t take = (left < (int64_t)(avail - used)) ? left : (int64_t)(avail - used);
-        used += (int)take;
-        left -= take;
-        if (left == 0) {
-          if (phase == 0 && c.has_mix) {
-            phase = 1; j = 0; es = 0;
-          } else {
-            ++r;
-            if (r < rc && lane == 0) c.rep_off[r] = cur + used;
-            phase = 0; left = c.pre;
-          }
-        }
-      } else {
-        const double u = rs_unif(tb[used]);
-        ++used;
-        bool done = false;
-        double e = 0;
-        if (es == 0) {           // exp_rand: u doubled until > 1, a += ln 2 each time
-          ea = 0.;
-          eu = u;
-          for (;;) {
-            eu += eu;
-            if (eu > 1.) break;
-            ea += rs_exp_q[0];
-          }
-          eu -= 1.;
-          if (eu <= rs_exp_q[0]) { e = ea + eu; done = true; } else { es = 1; }
-        } else if (es == 1) {    // ustar = unif_rand(), umin = ustar
-          emin = u; ei = 0; es = 2;
-        } else {                 // do { ustar; umin = min; i++ } while (u > q[i])
-          if (emin > u) emin = u;
-          ++ei;
-          if (!(eu > rs_exp_q[ei])) { e = ea + emin * rs_exp_q[0]; done = true; }
-        }
-        if (done) {
-          if (lane == 0) c.expv[(int64_t)r * c.nsim + j] = e;
-          es = 0;
-          if (++j == c.nsim) {
-            if (lane == 0) c.exp_end[r] = cur + used;
-            phase = 2; left = c.nsim;
-          }
-        }
-      }
-    }
-    cur += used;
-    mti += used;
+    Q = RS_N - mti0;
     __syncthreads();
   }
-  for (int t = lane; t < RS_N; t += 64) st->mt[t] = mt[t];
-  if (lane == 0) st->mti = mti;
+  // ring slot of the consumption point P (absolute word index mod 1248)
+  int pslot = (par0 * RS_N + mti0) % (2 * RS_N);
+  // One MT19937 block in three phases, each issuing all of its LDS reads before any write:
+  // kk < 227 reads mt[kk+397] (old); 227 <= kk < 454 reads mt[kk-227] (new, phase 1);
+  // kk >= 454 reads mt[kk-227] (new, phase 2) and, for kk = 623, mt[0] (new).
+  auto mt_phase = [&](int k0, int k1) {
+    constexpr int S = 4;
+    uint32_t a[S], b[S], src[S];
+#pragma unroll
+    for (int i = 0; i < S; ++i) {
+      const int kk = k0 + lane + 64 * i;
+      if (kk < k1) {
+        a[i] = mt[kk];
+        b[i] = mt[kk == RS_N - 1 ? 0 : kk + 1];
+        src[i] = mt[kk < RS_N - RS_M ? kk + RS_M : kk - (RS_N - RS_M)];
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < S; ++i) {
+      const int kk = k0 + lane + 64 * i;
+      if (kk < k1) {
+        const uint32_t y = (a[i] & 0x80000000u) | (b[i] & 0x7fffffffu);
+        mt[kk] = src[i] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+      }
+    }
+    __syncthreads();
+  };
+  auto next_block = [&]() {
+    mt_phase(0, RS_N - RS_M);
+    mt_phase(RS_N - RS_M, 2 * (RS_N - RS_M));
+    mt_phase(2 * (RS_N - RS_M), RS_N);
+    par ^= 1;
+    for (int t = lane; t < RS_N; t += 64) {
+      const uint32_t w = rs_temper(mt[t]);
+      ring[par * RS_N + t] = w;
+      out[Q + t] = w;
+    }
+    Q += RS_N;
+    __syncthreads();
+  };
+  constexpr double q[16] = RS_Q_TABLE;
+  int32_t r = 0;
+  int phase = 0;                          // 0: fixed words before exp_rand, 1: exp, 2: rbinom
+  int64_t left = c_pre, j = 0;
+  if (lane == 0) rep_off[0] = 0;
+  while (r < rc) {
+    // the walk is uniform; say so, or the structurizer keeps it in vector registers under
+    // exec masks
+    P = rs_u64(P); Q = rs_u64(Q); j = rs_u64(j); left = rs_u64(left);
+    r = rs_u(r); phase = rs_u(phase); par = rs_u(par); pslot = rs_u(pslot);
+    if (phase != 1) {
+      if (P == Q) { next_block(); continue; }
+      const int64_t take = (left < Q - P) ? left : Q - P;
+      P += take;
+      pslot = (int)((pslot + take % (2 * RS_N)) % (2 * RS_N));
+      left -= take;
+      if (left == 0) {
+        if (phase == 0 && c_has_mix) {
+          phase = 1; j = 0;
+        } else {
+          ++r;
+          if (r < rc && lane == 0) rep_off[r] = P;
+          phase = 0; left = c_pre;
+        }
+      }
+      continue;
+    }
+    if (P + RS_EXP_MAXW > Q) { next_block(); continue; }
+    // Window of 64 words at P.  Lane l evaluates "an exp_rand draw starting at P + l": R's
+    // doubling loop and the draw's length (1, or 2 + the index i where u <= q[i]) depend on
+    // that one word only.  The chain of draw starts is then a scalar walk over a ballot of
+    // the one-word draws (a run of them is one count-trailing-zeros), visiting only the long
+    // draws one by one; finally every start lane computes and stores its own value.
+    const int64_t pos = P + lane;
+    double a = 0., eu = 0.;
+    int len = 1;
+    if (pos < Q) {
+      eu = rs_unif(ring[rs_wrap(pslot + lane)]);
+      for (;;) {
+        eu += eu;
+        if (eu > 1.) break;
+        a += q[0];
+      }
+      eu -= 1.;
+      if (!(eu <= q[0])) {
+        int ie = 1;
+#pragma unroll
+        for (int t = 1; t < 15; ++t) ie += (eu > q[t]) ? 1 : 0;
+        len = 2 + ie;
+      }
+    }
+    // Chain of draw starts from lane 0 by pointer doubling: lane l holds the set M of chain
+    // positions reachable from l and the first position J past it; six rounds of
+    // M |= M[J], J = J[J] cover the window.
+    const int64_t rem = c_nsim - j;
+    const int64_t lim = Q - RS_EXP_MAXW - P;   // a draw may start at s <= lim
+    uint64_t M = 1ull << lane;
+    int J = lane + len;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+      const int src = (J < 64) ? J : 63;
+      const uint32_t mlo = (uint32_t)__shfl((int)(uint32_t)M, src);
+      const uint32_t mhi = (uint32_t)__shfl((int)(uint32_t)(M >> 32), src);
+      const int jj = __shfl(J, src);
+      if (J < 64) { M |= ((uint64_t)mhi << 32) | mlo; J = jj; }
+    }
+    const uint64_t chain = ((uint64_t)(uint32_t)rs_rl((int)(M >> 32), 0) << 32) |
+                           (uint32_t)rs_rl((int)(uint32_t)M, 0);
+    uint64_t starts = (lim >= 63) ? chain : (chain & ((2ull << lim) - 1ull));
+    int64_t cnt = __builtin_popcountll(starts);
+    while (cnt > rem) {                        // the segment ends inside this window
+      starts &= ~(1ull << (63 - __builtin_clzll(starts)));
+      --cnt;
+    }
+    const int last = 63 - __builtin_clzll(starts);
+    const int s = rs_u(last + rs_rl(len, last));
+    if ((starts >> lane) & 1ull) {
+      double e;
+      if (len == 1) {
+        e = a + eu;
+      } else {                            // umin over the len - 1 following words
+        uint32_t wmin = 0xffffffffu;
+        for (int t = 1; t < len; ++t) {
+          const uint32_t w2 = ring[rs_wrap(pslot + lane + t)];
+          wmin = (w2 < wmin) ? w2 : wmin;
+        }
+        e = a + rs_unif(wmin) * q[0];
+      }
+      const int idx = __builtin_popcountll(starts & ((1ull << lane) - 1ull));
+      gexpv[(int64_t)r * c_nsim + j + idx] = e;
+    }
+    j += cnt;
+    P += s;
+    pslot = rs_wrap(pslot + s);
+    if (j == c_nsim) {
+      if (lane == 0) exp_end[r] = P;
+      phase = 2; left = c_nsim;
+    }
+  }
+  // .Random.seed at the consumption point P: in the newest block, just past it, or (after an
+  // exp_rand look-ahead) in the previous block, whose raw state is the untempered ring half
+  const int64_t o = P + mti0;              // words since the start of the chunk's first block
+  const int64_t blk = o / RS_N, newest = (Q + mti0) / RS_N - 1;
+  const int off = (int)(o % RS_N);
+  if (blk > newest) {                     // P == Q at a block boundary
+    for (int t = lane; t < RS_N; t += 64) st->mt[t] = mt[t];
+    if (lane == 0) { st->mti = RS_N; st->pad[0] = par; }
+  } else if (blk == newest) {
+    for (int t = lane; t < RS_N; t += 64) st->mt[t] = mt[t];
+    if (lane == 0) { st->mti = off; st->pad[0] = par; }
+  } else {
+    for (int t = lane; t < RS_N; t += 64) st->mt[t] = rs_untemper(ring[(par ^ 1) * RS_N + t]);
+    if (lane == 0) { st->mti = off; st->pad[0] = par ^ 1; }
+  }
 }
 
 // -------------------------------------------------------- k_rs_materialise ---
 __global__ __launch_bounds__(256) void k_rs_materialise(const RsCell* cells, int32_t rc) {
-  const RsCell& c = cells[blockIdx.x / rc];
+  const RsCell c = cells[blockIdx.x / rc];  // by value: the stores below cannot alias it
   const int64_t r = blockIdx.x % rc;
   const uint32_t* w = c.words + c.rep_off[r];
   const int64_t n = c.n, k = c.k, nsim = c.nsim;

@@ -90,21 +90,23 @@ def test_grid_matches_oracle_replicate_by_replicate(dc, orc):
         assert_close(r["records"], ref, what=str(spec))
 
 
-def test_chunked_streams_are_continuous(dc):
-    """A small device budget splits B into chunks: the MT state carries over exactly."""
-    specs = [_spec(dc, **CELLS["sign-gauss"]), _spec(dc, **CELLS["subG-bounded"])]
-    full = dc.rstream.run_grid(specs, 40)
-    old = os.environ.get("DCOR_RS_BUDGET_MB")
-    os.environ["DCOR_RS_BUDGET_MB"] = "17"
+@pytest.mark.parametrize("max_chunk", [1, 3, 7])
+def test_chunked_streams_are_continuous(dc, orc, max_chunk):
+    """Short chunks: the Mersenne-Twister state (.Random.seed) carries over exactly, including
+    a chunk ending just behind an exp_rand look-ahead (nsim = 3: the untempered-ring path)."""
+    specs = [_spec(dc, **CELLS["sign-gauss"]), _spec(dc, **CELLS["subG-bounded"]),
+             _spec(dc, family="subG", dgp="bounded_factor", rho=0.4, n=40, nsim=3, mu=(0, 0),
+                   sigma=(1, 1), eps1=2.0, eps2=2.0, seed=77)]
+    B = 60
+    full = dc.rstream.run_grid(specs, B)
+    os.environ["DCOR_RS_MAX_CHUNK"] = str(max_chunk)
     try:
-        small = dc.rstream.run_grid(specs, 40)
+        small = dc.rstream.run_grid(specs, B)
     finally:
-        if old is None:
-            del os.environ["DCOR_RS_BUDGET_MB"]
-        else:
-            os.environ["DCOR_RS_BUDGET_MB"] = old
-    for a, b in zip(full, small):
+        del os.environ["DCOR_RS_MAX_CHUNK"]
+    for spec, a, b in zip(specs, full, small):
         np.testing.assert_array_equal(a["records"], b["records"])
+    assert_close(small[2]["records"], orc.rs_sim(specs[2].to_c(), B))
 
 
 def test_run_sim_one_rng_r(dc, orc):
