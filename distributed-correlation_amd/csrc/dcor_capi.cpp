@@ -294,11 +294,14 @@ int pipe_get(Pipe** out) {
   return DCOR_OK;
 }
 
-int arena_get(size_t bytes, void** out) {
+// R-stream mode's arena (words, draws, replicate records): same lifetime rules.
+Arena g_rs_arena[64];
+
+int arena_get_in(Arena* arenas, size_t bytes, void** out) {
   int dev = 0;
   HIPCHK(hipGetDevice(&dev));
   if (dev < 0 || dev >= 64) return fail(DCOR_EINVAL, "device id out of range");
-  Arena& a = g_arena[dev];
+  Arena& a = arenas[dev];
   if (a.bytes < bytes) {
     if (a.p) { HIPCHK(hipDeviceSynchronize()); HIPCHK(hipFree(a.p)); a.p = nullptr; a.bytes = 0; }
     if (hipMalloc(&a.p, bytes) != hipSuccess) {
@@ -311,6 +314,8 @@ int arena_get(size_t bytes, void** out) {
   *out = a.p;
   return DCOR_OK;
 }
+
+int arena_get(size_t bytes, void** out) { return arena_get_in(g_arena, bytes, out); }
 
 // Monotone code map of clip(v): base + [0, 2R) -> [0, levels).  Only affects speed (how many
 // samples tie a threshold's code), never results.
@@ -985,6 +990,9 @@ int dcor_shutdown(void) {
   for (auto& a : g_arena) {
     if (a.p) { (void)hipFree(a.p); a.p = nullptr; a.bytes = 0; }
   }
+  for (auto& a : g_rs_arena) {
+    if (a.p) { (void)hipFree(a.p); a.p = nullptr; a.bytes = 0; }
+  }
   for (auto& p : g_pipe) {
     if (p.s) {
       (void)hipStreamSynchronize(p.s);
@@ -1207,6 +1215,11 @@ int rs_estimate(const dcor_cell& cell, const RsCell& c, int64_t reps, dcor_rep_o
   return dcor_premat_subg_launch(&d, d_out, nullptr);
 }
 
+struct View {  // a typed window into the R-stream arena
+  void* p;
+  template <class T> T* as() const { return static_cast<T*>(p); }
+};
+
 size_t rs_budget() {
   const char* e = std::getenv("DCOR_RS_BUDGET_MB");
   const long mb = e ? std::atol(e) : 4096;
@@ -1243,12 +1256,16 @@ int dcor_rstream_grid_run(const dcor_cell* cells, int ncells, int64_t B, dcor_ac
       rc = std::max<int64_t>(1, std::min<int64_t>(rc, std::atol(e)));
     size_t bytes = 0;
     for (int i = 0; i < nb; ++i) bytes += rs_cell_bytes(plan[(size_t)(i0 + i)], (int32_t)rc);
-    DevBuf buf, dst, dcells, dout, acc;
-    HIPCHK(buf.alloc(bytes));
-    HIPCHK(dst.alloc(sizeof(RsState) * (size_t)nb));
-    HIPCHK(dcells.alloc(sizeof(RsCell) * (size_t)nb));
-    HIPCHK(dout.alloc(sizeof(dcor_rep_out) * (size_t)B * (size_t)nb));
-    HIPCHK(acc.alloc(sizeof(dcor_accum) * 2));
+    // one library-owned arena (kept across calls): cell buffers | states | descriptors |
+    // replicate records | accumulators
+    const size_t off_st = bytes, off_cells = off_st + al256(sizeof(RsState) * (size_t)nb);
+    const size_t off_out = off_cells + al256(sizeof(RsCell) * (size_t)nb);
+    const size_t off_acc = off_out + al256(sizeof(dcor_rep_out) * (size_t)B * (size_t)nb);
+    void* arena = nullptr;
+    if (int st = arena_get_in(g_rs_arena, off_acc + al256(sizeof(dcor_accum) * 2 * (size_t)nb), &arena))
+      return st;
+    const View buf{arena}, dst{(char*)arena + off_st}, dcells{(char*)arena + off_cells},
+        dout{(char*)arena + off_out}, acc{(char*)arena + off_acc};
     std::vector<RsState> hst((size_t)nb);
     std::vector<RsCell> hc((size_t)nb);
     char* base = buf.as<char>();
@@ -1273,13 +1290,13 @@ int dcor_rstream_grid_run(const dcor_cell* cells, int ncells, int64_t B, dcor_ac
     }
     for (int i = 0; i < nb; ++i) {
       dcor_rep_out* o = dout.as<dcor_rep_out>() + (size_t)i * B;
-      if (int st = dcor_accumulate_launch(o, B, cells[i0 + i].rho, acc.as<dcor_accum>(), nullptr))
-        return st;
-      HIPCHK(hipMemcpy(h_acc + 2 * (i0 + i), acc.p, sizeof(dcor_accum) * 2, hipMemcpyDeviceToHost));
-      if (h_detail)
-        HIPCHK(hipMemcpy(h_detail + (size_t)(i0 + i) * B, o, sizeof(dcor_rep_out) * (size_t)B,
-                         hipMemcpyDeviceToHost));
+      if (int st = dcor_accumulate_launch(o, B, cells[i0 + i].rho, acc.as<dcor_accum>() + 2 * i,
+                                          nullptr)) return st;
     }
+    HIPCHK(hipMemcpy(h_acc + 2 * i0, acc.p, sizeof(dcor_accum) * 2 * (size_t)nb, hipMemcpyDeviceToHost));
+    if (h_detail)
+      HIPCHK(hipMemcpy(h_detail + (size_t)i0 * B, dout.p, sizeof(dcor_rep_out) * (size_t)B * (size_t)nb,
+                       hipMemcpyDeviceToHost));
     i0 += nb;
   }
   return DCOR_OK;
