@@ -113,11 +113,16 @@ dp_sd <- function(x, lo, hi, eps1, eps2) {
 ## family: "sign" (vert-cor.R) or "subG" (ver-cor-subG.R);
 ## dgp: "gaussian"/"bernoulli"/"bounded_factor"/"mix_gaussian" (gen_mix_gaussian, whose
 ## arguments come in `mix`, defaults as ver-cor-subG.R:113-116).
+## rng: "philox" (counter-based streams, shardable by replicate) or "R" (R's own
+## Mersenne-Twister stream from set.seed(1e6 + i) per cell: the reference's per-seed numbers;
+## gaussian / bernoulli / bounded_factor).
 dcor_grid <- function(design, B = 250, alpha = 0.05, mu = c(0, 0), sigma = c(1, 1),
                       family = "sign", dgp = "gaussian", ci_mode = "auto", normalise = TRUE,
                       detail = FALSE,
                       mix = list(mu0 = c(0, 0), sigma0 = c(1, 1), mu1 = c(3, 3),
-                                 sigma1 = c(2, 0.5), pi_mix = 0.5)) {
+                                 sigma1 = c(2, 0.5), pi_mix = 0.5),
+                      rng = c("philox", "R")) {
+  rng <- match.arg(rng)
   nc <- nrow(design)
   fam <- rep(match(family, c("sign", "subG")) - 1L, length.out = nc)
   dg <- rep(match(dgp, c("gaussian", "bernoulli", "bounded_factor", "mix_gaussian")) - 1L,
@@ -128,7 +133,8 @@ dcor_grid <- function(design, B = 250, alpha = 0.05, mu = c(0, 0), sigma = c(1, 
              rep(mu[1], nc), rep(mu[2], nc), rep(sigma[1], nc), rep(sigma[2], nc),
              rep(as.logical(normalise), nc),
              rep(match(ci_mode, c("auto", "normal", "laplace")) - 1L, nc),
-             as.double(1e6 + seq_len(nc)), as.double(B), as.logical(detail), mixv)
+             as.double(1e6 + seq_len(nc)), as.double(B), as.logical(detail), mixv,
+             identical(rng, "R"))
   s <- matrix(r[[1]], ncol = 5, byrow = TRUE,
               dimnames = list(NULL, c("mse", "bias", "var", "coverage", "ci_length")))
   summ <- data.frame(design[rep(seq_len(nc), each = 2), , drop = FALSE],

@@ -117,7 +117,7 @@ SEXP dcor_R_ci_INT_subG(SEXP X, SEXP Y, SEXP e1, SEXP e2, SEXP eta1, SEXP eta2, 
 /* One grid on the current device: cells given as parallel vectors (one element per cell). */
 SEXP dcor_R_grid_run(SEXP family, SEXP dgp, SEXP n, SEXP rho, SEXP eps1, SEXP eps2, SEXP alpha,
                      SEXP mu1, SEXP mu2, SEXP s1, SEXP s2, SEXP normalise, SEXP mode, SEXP seed,
-                     SEXP B, SEXP want_detail, SEXP mix) {
+                     SEXP B, SEXP want_detail, SEXP mix, SEXP rng_r) {
   /* mix: gen_mix_gaussian's mu0[2], sigma0[2], mu1[2], sigma1[2], pi_mix (ver-cor-subG.R:113-116) */
   if (XLENGTH(mix) != 9) Rf_error("dcor_grid: mix must hold 9 numbers");
   const double* mx = REAL(mix);
@@ -149,8 +149,12 @@ SEXP dcor_R_grid_run(SEXP family, SEXP dgp, SEXP n, SEXP rho, SEXP eps1, SEXP ep
   SEXP acc = PROTECT(allocVector(RAWSXP, (R_xlen_t)nc * 2 * sizeof(dcor_accum)));
   SEXP det = PROTECT(Rf_asLogical(want_detail) ? allocVector(REALSXP, (R_xlen_t)nc * b * 6)
                                                : allocVector(REALSXP, 0));
-  const int st = dcor_grid_run(cells, nc, b, (dcor_accum*)RAW(acc),
-                               XLENGTH(det) ? (dcor_rep_out*)REAL(det) : NULL);
+  /* rng_r: R's own streams (dcor_rstream_grid_run) instead of the Philox engine */
+  const int st = Rf_asLogical(rng_r)
+      ? dcor_rstream_grid_run(cells, nc, b, (dcor_accum*)RAW(acc),
+                              XLENGTH(det) ? (dcor_rep_out*)REAL(det) : NULL)
+      : dcor_grid_run(cells, nc, b, (dcor_accum*)RAW(acc),
+                      XLENGTH(det) ? (dcor_rep_out*)REAL(det) : NULL);
   if (st) { UNPROTECT(2); dcor_stop(st); }
   /* summaries: [cell][method][mse, bias, var, coverage, ci_length] */
   SEXP sm = PROTECT(allocVector(REALSXP, (R_xlen_t)nc * 2 * 5));
@@ -175,7 +179,7 @@ static const R_CallMethodDef calls[] = {
     {"dcor_R_ci_INT_signflip", (DL_FUNC)&dcor_R_ci_INT_signflip, 12},
     {"dcor_R_correlation_NI_subG", (DL_FUNC)&dcor_R_correlation_NI_subG, 13},
     {"dcor_R_ci_INT_subG", (DL_FUNC)&dcor_R_ci_INT_subG, 16},
-    {"dcor_R_grid_run", (DL_FUNC)&dcor_R_grid_run, 17},
+    {"dcor_R_grid_run", (DL_FUNC)&dcor_R_grid_run, 18},
     {NULL, NULL, 0}};
 
 void R_init_dcor_r(DllInfo* dll) {
