@@ -1367,3 +1367,74 @@ int dcor_rstream_words(int32_t seed, int64_t count, uint32_t* h_out) {
 }
 
 }  // extern "C"
+
+extern "C" {
+
+int dcor_rstream_hrs_draws(int64_t n, int64_t k, int64_t m, int64_t nsim, int64_t runs,
+                           const int32_t* h_ni_seeds, const int32_t* h_int_seeds, int32_t* d_perm,
+                           double* d_lap_x, double* d_lap_y, double* d_lap_local,
+                           double* d_lap_central, double* d_mix_z, double* d_mix_l, void* stream) {
+  if (n < 2 || n > RS_HRS_NMAX || k < 1 || m < 1 || k * m > n || nsim < 1 || runs < 0 ||
+      runs > 0x7fffffff)
+    return fail(DCOR_EINVAL, "rstream_hrs_draws: need 2 <= n <= %d, k*m <= n, nsim >= 1",
+                RS_HRS_NMAX);
+  if (h_ni_seeds && (!d_perm || !d_lap_x || !d_lap_y))
+    return fail(DCOR_EINVAL, "rstream_hrs_draws: NI outputs missing");
+  if (h_int_seeds && (!d_lap_local || !d_lap_central || !d_mix_z || !d_mix_l))
+    return fail(DCOR_EINVAL, "rstream_hrs_draws: INT outputs missing");
+  if (runs == 0) return DCOR_OK;
+  if (int st = need_device()) return st;
+  if (h_ni_seeds) {
+    DevBuf ds;
+    if (int st = upload(ds, h_ni_seeds, (size_t)runs)) return st;
+    const int e = launch_rs_hrs_ni(ds.as<int32_t>(), runs, n, k * m, k, d_perm, d_lap_x, d_lap_y,
+                                   stream);
+    if (e) return hip_fail((hipError_t)e, "rstream hrs NI launch");
+    HIPCHK(hipStreamSynchronize((hipStream_t)stream));
+  }
+  if (h_int_seeds) {
+    const int64_t pre = n + 1 + 2 * nsim, rep_max = pre + 18 * nsim;
+    const size_t per_run = al256(((size_t)rep_max + 2 * 624 + 64) * 4) + 2 * al256(8) +
+                           al256((size_t)nsim * 8) + sizeof(RsState) + sizeof(RsCell);
+    const int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(runs, (int64_t)(rs_budget() / per_run)));
+    std::vector<RsState> hst((size_t)chunk);
+    std::vector<RsCell> hc((size_t)chunk);
+    for (int64_t r0 = 0; r0 < runs; r0 += chunk) {
+      const int64_t nr = std::min<int64_t>(chunk, runs - r0);
+      const size_t words_b = al256(((size_t)rep_max + 2 * 624 + 64) * 4);
+      const size_t off_st = (size_t)nr * (words_b + 2 * al256(8) + al256((size_t)nsim * 8));
+      const size_t off_cells = off_st + al256(sizeof(RsState) * (size_t)nr);
+      void* arena = nullptr;
+      if (int st = arena_get_in(g_rs_arena, off_cells + al256(sizeof(RsCell) * (size_t)nr), &arena))
+        return st;
+      char* base = (char*)arena;
+      RsState* dst = (RsState*)((char*)arena + off_st);
+      for (int64_t i = 0; i < nr; ++i) {
+        RsCell& c = hc[(size_t)i];
+        std::memset(&c, 0, sizeof(c));
+        c.n = n; c.k = 0; c.nsim = nsim; c.family = RS_FAMILY_HRS_INT; c.has_mix = 1;
+        c.pre = pre;
+        c.words = (uint32_t*)base; base += words_b;
+        c.rep_off = (int64_t*)base; base += al256(8);
+        c.exp_end = (int64_t*)base; base += al256(8);
+        c.expv = (double*)base; base += al256((size_t)nsim * 8);
+        c.lap_local = d_lap_local + (size_t)(r0 + i) * (size_t)n;
+        c.lap_scalar = d_lap_central + (r0 + i);
+        c.mix_z = d_mix_z + (size_t)(r0 + i) * (size_t)nsim;
+        c.mix_l = d_mix_l + (size_t)(r0 + i) * (size_t)nsim;
+        c.st = dst + i;
+        rs_seed(h_int_seeds[r0 + i], hst[(size_t)i]);
+      }
+      HIPCHK(hipMemcpy(dst, hst.data(), sizeof(RsState) * (size_t)nr, hipMemcpyHostToDevice));
+      RsCell* dcells = (RsCell*)((char*)arena + off_cells);
+      HIPCHK(hipMemcpy(dcells, hc.data(), sizeof(RsCell) * (size_t)nr, hipMemcpyHostToDevice));
+      int e = launch_rs_stream(dcells, (int)nr, 1, stream);
+      if (!e) e = launch_rs_materialise(dcells, (int)nr, 1, stream);
+      if (e) return hip_fail((hipError_t)e, "rstream hrs INT launch");
+      HIPCHK(hipStreamSynchronize((hipStream_t)stream));
+    }
+  }
+  return DCOR_OK;
+}
+
+}  // extern "C"

@@ -177,7 +177,14 @@ struct RsCell {
   double* lap_scalar;          // [rc] Z (sign) / central (sub-G)
   double *mix_z, *mix_l;       // [rc][nsim]
 };
+// RsCell.family for the HRS INT runs: rLap(n), rLap(1), mixquant (real-data-sims.R:375-402)
+#define RS_FAMILY_HRS_INT 2
 int launch_rs_stream(RsCell* d_cells, int ncells, int32_t rc, void* stream);
+// The HRS NI runs: sample.int(n, k*m) and rLap(k) twice after set.seed(seeds[r]); n <= RS_HRS_NMAX.
+#define RS_HRS_NMAX 36000
+size_t rs_hrs_ni_lds_bytes(int64_t n);
+int launch_rs_hrs_ni(const int32_t* d_seeds, int64_t runs, int64_t n, int64_t km, int64_t k,
+                     int32_t* perm, double* lx, double* ly, void* stream);
 int launch_rs_materialise(const RsCell* d_cells, int ncells, int32_t rc, void* stream);
 
 }  // namespace dcor

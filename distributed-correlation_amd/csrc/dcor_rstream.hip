@@ -163,6 +163,7 @@ __device__ __forceinline__ uint32_t rs_untemper(uint32_t y) {
   return x;
 }
 
+#define RS_G __attribute__((address_space(1)))
 __device__ __forceinline__ int rs_rl(int v, int s) { return __builtin_amdgcn_readlane(v, s); }
 __device__ __forceinline__ int rs_u(int v) { return __builtin_amdgcn_readfirstlane(v); }
 __device__ __forceinline__ int rs_wrap(int x) { return (x >= 2 * 624) ? x - 2 * 624 : x; }
@@ -174,6 +175,49 @@ __device__ __forceinline__ double rs_rld(double v, int s) {
   const long long b = __double_as_longlong(v);
   const int lo = rs_rl((int)b, s), hi = rs_rl((int)(b >> 32), s);
   return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
+// One MT19937 block in three phases, each issuing all of its LDS reads before any write:
+// kk < 227 reads mt[kk+397] (old); 227 <= kk < 454 reads mt[kk-227] (new, phase 1);
+// kk >= 454 reads mt[kk-227] (new, phase 2) and, for kk = 623, mt[0] (new).  One wave.
+__device__ __forceinline__ void rs_mt_phase(uint32_t* mt, int lane, int k0, int k1) {
+  constexpr int S = 4;
+  uint32_t a[S], b[S], src[S];
+#pragma unroll
+  for (int i = 0; i < S; ++i) {
+    const int kk = k0 + lane + 64 * i;
+    if (kk < k1) {
+      a[i] = mt[kk];
+      b[i] = mt[kk == RS_N - 1 ? 0 : kk + 1];
+      src[i] = mt[kk < RS_N - RS_M ? kk + RS_M : kk - (RS_N - RS_M)];
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < S; ++i) {
+    const int kk = k0 + lane + 64 * i;
+    if (kk < k1) {
+      const uint32_t y = (a[i] & 0x80000000u) | (b[i] & 0x7fffffffu);
+      mt[kk] = src[i] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+    }
+  }
+  __syncthreads();
+}
+__device__ __forceinline__ void rs_mt_block(uint32_t* mt, int lane) {
+  rs_mt_phase(mt, lane, 0, RS_N - RS_M);
+  rs_mt_phase(mt, lane, RS_N - RS_M, 2 * (RS_N - RS_M));
+  rs_mt_phase(mt, lane, 2 * (RS_N - RS_M), RS_N);
+}
+
+// set.seed(seed): RNG_Init's scrambling and 625 words (word 0, the position, is 624)
+__device__ __forceinline__ void rs_seed_mt(uint32_t* mt, int32_t seed, int lane) {
+  if (lane == 0) {
+    uint32_t s = (uint32_t)seed;
+    for (int j = 0; j < 50; ++j) s = 69069u * s + 1u;
+    s = 69069u * s + 1u;
+    for (int j = 0; j < RS_N; ++j) { s = 69069u * s + 1u; mt[j] = s; }
+  }
+  __syncthreads();
 }
 
 // One wave per cell.  mt[] holds the raw state of the newest block; ring[] the tempered words
@@ -190,7 +234,6 @@ __global__ __launch_bounds__(64) void k_rs_stream(RsCell* cells, int32_t rc) {
   const int c_has_mix = cg.has_mix;
   // global (not flat) stores: a flat store also counts in lgkmcnt, so every LDS wait behind
   // it would wait for the store to reach memory
-#define RS_G __attribute__((address_space(1)))
   RS_G int64_t* const rep_off = (RS_G int64_t*)cg.rep_off;
   RS_G int64_t* const exp_end = (RS_G int64_t*)cg.exp_end;
   RS_G double* const gexpv = (RS_G double*)cg.expv;
@@ -215,36 +258,8 @@ __global__ __launch_bounds__(64) void k_rs_stream(RsCell* cells, int32_t rc) {
   }
   // ring slot of the consumption point P (absolute word index mod 1248)
   int pslot = (par0 * RS_N + mti0) % (2 * RS_N);
-  // One MT19937 block in three phases, each issuing all of its LDS reads before any write:
-  // kk < 227 reads mt[kk+397] (old); 227 <= kk < 454 reads mt[kk-227] (new, phase 1);
-  // kk >= 454 reads mt[kk-227] (new, phase 2) and, for kk = 623, mt[0] (new).
-  auto mt_phase = [&](int k0, int k1) {
-    constexpr int S = 4;
-    uint32_t a[S], b[S], src[S];
-#pragma unroll
-    for (int i = 0; i < S; ++i) {
-      const int kk = k0 + lane + 64 * i;
-      if (kk < k1) {
-        a[i] = mt[kk];
-        b[i] = mt[kk == RS_N - 1 ? 0 : kk + 1];
-        src[i] = mt[kk < RS_N - RS_M ? kk + RS_M : kk - (RS_N - RS_M)];
-      }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int i = 0; i < S; ++i) {
-      const int kk = k0 + lane + 64 * i;
-      if (kk < k1) {
-        const uint32_t y = (a[i] & 0x80000000u) | (b[i] & 0x7fffffffu);
-        mt[kk] = src[i] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
-      }
-    }
-    __syncthreads();
-  };
   auto next_block = [&]() {
-    mt_phase(0, RS_N - RS_M);
-    mt_phase(RS_N - RS_M, 2 * (RS_N - RS_M));
-    mt_phase(2 * (RS_N - RS_M), RS_N);
+    rs_mt_block(mt, lane);
     par ^= 1;
     for (int t = lane; t < RS_N; t += 64) {
       const uint32_t w = rs_temper(mt[t]);
@@ -377,6 +392,20 @@ __global__ __launch_bounds__(256) void k_rs_materialise(const RsCell* cells, int
   const uint32_t* w = c.words + c.rep_off[r];
   const int64_t n = c.n, k = c.k, nsim = c.nsim;
   const int tid = threadIdx.x;
+  if (c.family == RS_FAMILY_HRS_INT) {
+    // run_INT_once (real-data-sims.R:375-402): rLap(n), rLap(1), mixquant(nsim = 2000)
+    double* ll = c.lap_local + r * n;
+    for (int64_t i = tid; i < n; i += 256) ll[i] = rs_lap(w[i]);
+    if (tid == 0) c.lap_scalar[r] = rs_lap(w[n]);
+    const uint32_t* wz = w + n + 1;
+    const uint32_t* wb = c.words + c.exp_end[r];
+    const double* ev = c.expv + r * nsim;
+    for (int64_t jj = tid; jj < nsim; jj += 256) {
+      c.mix_z[r * nsim + jj] = rs_norm(wz[2 * jj], wz[2 * jj + 1]);
+      c.mix_l[r * nsim + jj] = (rs_unif(wb[jj]) < 0.5) ? -ev[jj] : ev[jj];
+    }
+    return;
+  }
   double* X = c.X + r * n;
   double* Y = c.Y + r * n;
   // 1. DGP
@@ -463,6 +492,90 @@ __global__ __launch_bounds__(256) void k_rs_materialise(const RsCell* cells, int
   } else {
     for (int64_t jj = tid; jj < nsim; jj += 256) { mz[jj] = 0.0; ml[jj] = 0.0; }
   }
+}
+
+// ------------------------------------------------------------ k_rs_hrs_ni ---
+// run_NI_once (real-data-sims.R:357-373) on R's stream: set.seed(seeds[r]), then
+// correlation_NI_subG's draws -- idx <- sample.int(n, k*m) (:131) and rLap(k) twice
+// (:136-137).  sample.int without replacement is do_sample's partial Fisher-Yates over
+// x[0..n) with R_unif_index's rejection sampling (rbits: 16 bits per word), inherently
+// sequential: one wave per run keeps x[] in LDS and walks it in uniform control flow;
+// MT blocks are regenerated wave-parallel.  Then the 2k Laplace words, lane-parallel.
+__global__ __launch_bounds__(64) void k_rs_hrs_ni(const int32_t* __restrict__ seeds, int64_t n,
+                                                  int64_t km, int64_t k, int32_t* __restrict__ perm,
+                                                  double* __restrict__ lx, double* __restrict__ ly) {
+  extern __shared__ uint32_t rs_sm[];
+  uint32_t* mt = rs_sm;
+  uint32_t* wb = rs_sm + RS_N;
+  int32_t* x = reinterpret_cast<int32_t*>(rs_sm + 2 * RS_N);
+  const int lane = threadIdx.x;
+  const int64_t r = blockIdx.x;
+  rs_seed_mt(mt, seeds[r], lane);
+  for (int64_t i = lane; i < n; i += 64) x[i] = (int32_t)i;
+  int pos = RS_N;                          // set.seed leaves mti = 624: first use regenerates
+  auto refill = [&]() {
+    __syncthreads();
+    rs_mt_block(mt, lane);
+    for (int t = lane; t < RS_N; t += 64) wb[t] = rs_temper(mt[t]);
+    __syncthreads();
+    pos = 0;
+  };
+  __syncthreads();
+  RS_G int32_t* const pr = (RS_G int32_t*)(perm + r * km);
+  int64_t dn = n;
+  for (int64_t i = 0; i < km; ++i, --dn) {
+    dn = rs_u64(dn);
+    const int bits = (dn <= 1) ? 0 : 64 - __builtin_clzll((unsigned long long)(dn - 1));  // ceil(log2 dn)
+    const uint64_t mask = (bits >= 63) ? ~0ull : ((1ull << bits) - 1ull);
+    uint64_t v;
+    do {                                    // R_unif_index: rbits(bits) until < dn
+      v = 0;
+      for (int nn = 0; nn <= bits; nn += 16) {
+        if (pos == RS_N) refill();
+        pos = rs_u(pos);
+        v = 65536ull * v + (wb[pos] >> 16);  // floor(unif_rand() * 65536)
+        ++pos;
+      }
+      v &= mask;
+    } while ((int64_t)v >= dn);
+    if (lane == 0) {
+      const int32_t j = (int32_t)v;
+      pr[i] = x[j];                         // iy[i] = x[j] + 1 (0-based here)
+      x[j] = x[dn - 1];
+    }
+  }
+  // rLap(k) for X, then rLap(k) for Y: the next 2k words
+  int64_t t0 = 0;
+  const int64_t tot = 2 * k;
+  while (t0 < tot) {
+    if (pos == RS_N) refill();
+    pos = rs_u(pos);
+    const int64_t take = ((int64_t)(RS_N - pos) < tot - t0) ? (int64_t)(RS_N - pos) : tot - t0;
+    for (int64_t q = lane; q < take; q += 64) {
+      const double l = rs_lap(wb[pos + q]);
+      const int64_t t = t0 + q;
+      if (t < k) lx[r * k + t] = l; else ly[r * k + (t - k)] = l;
+    }
+    pos += (int)take;
+    t0 += take;
+  }
+}
+
+size_t rs_hrs_ni_lds_bytes(int64_t n) { return (size_t)(2 * RS_N + n) * 4; }
+
+int launch_rs_hrs_ni(const int32_t* d_seeds, int64_t runs, int64_t n, int64_t km, int64_t k,
+                     int32_t* perm, double* lx, double* ly, void* stream) {
+  const size_t lds = rs_hrs_ni_lds_bytes(n);
+  static bool attr = false;
+  if (!attr) {
+    const hipError_t e = hipFuncSetAttribute((const void*)k_rs_hrs_ni,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
+    if (e != hipSuccess) return (int)e;
+    attr = true;
+  }
+  hipLaunchKernelGGL(k_rs_hrs_ni, dim3((unsigned)runs), dim3(64), lds, (hipStream_t)stream, d_seeds,
+                     n, km, k, perm, lx, ly);
+  return (int)hipGetLastError();
 }
 
 int launch_rs_stream(RsCell* d_cells, int ncells, int32_t rc, void* stream) {

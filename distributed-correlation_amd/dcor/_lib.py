@@ -119,6 +119,9 @@ SIGNATURES = {
                                         C.POINTER(RepOut)]),
     "dcor_rstream_draws": (C.c_int, [C.POINTER(Cell), C.c_int64, C.POINTER(RsDraws)]),
     "dcor_rstream_words": (C.c_int, [C.c_int32, C.c_int64, C.POINTER(C.c_uint32)]),
+    "dcor_rstream_hrs_draws": (C.c_int, [C.c_int64, C.c_int64, C.c_int64, C.c_int64, C.c_int64,
+                                         C.POINTER(C.c_int32), C.POINTER(C.c_int32), _P, _P, _P, _P,
+                                         _P, _P, _P, _P]),
     "dcor_premat_sign_launch": (C.c_int, [C.POINTER(PrematSign), _P, _P]),
     "dcor_premat_subg_launch": (C.c_int, [C.POINTER(PrematSubg), _P, _P]),
     "dcor_panel_dict_probe": (C.c_int, [_P, _P, C.c_int64, C.POINTER(C.c_int)]),

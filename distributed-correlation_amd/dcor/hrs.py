@@ -66,14 +66,29 @@ SITE_NI_LAP_X, SITE_NI_LAP_Y, SITE_INT_LOCAL, SITE_INT_CENTRAL, SITE_MIX_Z, SITE
 DRAW_LAPLACE, DRAW_NORMAL = 0, 1
 
 
+def r_seeds(idx: int, reps, rep_begin: int = 0):
+    """The reference's per-run seeds at eps index idx (1-based, which(eps_grid == eps)) for
+    runs rep = rep_begin+1 .. rep_begin+reps: set.seed(10 + 37 rep + 1000 idx) before
+    run_NI_once and set.seed(20 + 41 rep + 1000 idx) before run_INT_once
+    (real-data-sims.R:404, 423)."""
+    rep = np.arange(rep_begin + 1, rep_begin + reps + 1, dtype=np.int64)
+    return ((10 + 37 * rep + 1000 * idx).astype(np.int32), (20 + 41 * rep + 1000 * idx).astype(np.int32))
+
+
 def hrs_replicates(age_z, bmi_z, lam_age, lam_bmi, eps, reps, seed_ni=NI_SEED, seed_int=INT_SEED,
-                   nsim=2000, rep_begin=0, chunk=8192, alpha=0.05, keep_noise=False):
+                   nsim=2000, rep_begin=0, chunk=8192, alpha=0.05, keep_noise=False, rng="philox",
+                   eps_idx=None):
     """`reps` NI + INT replicates of the HRS estimators on one standardised panel at one eps:
     correlation_NI_subG(lambda_X = lam_age, lambda_Y = lam_bmi) and ci_INT_subG(AGE sends,
     lambda_receiver_from_noise, delta_clip = 1/n) (real-data-sims.R:357-400).  The panel is
     encoded once (dcor_panel_create); noise is generated in HBM per chunk and streamed by the
     pre-materialised kernel.  Returns float64 [reps, 6] (ni_hat, ni_lo, ni_hi, int_hat, int_lo,
-    int_hi) and, with keep_noise, the host copies of every noise array."""
+    int_hi) and, with keep_noise, the host copies of every noise array.
+
+    rng='R' replays the reference's own streams instead: run rep (1-based, rep_begin + 1 ..)
+    draws its NI noise after set.seed(10 + 37 rep + 1000 eps_idx) and its INT noise after
+    set.seed(20 + 41 rep + 1000 eps_idx) (dcor_rstream_hrs_draws), so every run is the
+    reference's run for that seed; seed_ni / seed_int are then unused."""
     import ctypes as C
 
     import torch
@@ -98,18 +113,29 @@ def hrs_replicates(age_z, bmi_z, lam_age, lam_bmi, eps, reps, seed_ni=NI_SEED, s
     mz, ml = torch.empty((cr, nsim), **f64), torch.empty((cr, nsim), **f64)
     out = torch.empty((reps, 6), **f64)
     noise = {key: [] for key in ("perm", "lap_x", "lap_y", "lap_local", "lap_central", "mix_z", "mix_l")}
+    if rng not in ("philox", "R"):
+        raise ValueError(f"rng must be 'philox' or 'R', not {rng!r}")
+    if rng == "R" and eps_idx is None:
+        raise ValueError("rng='R' needs eps_idx (the 1-based position of eps in the sweep)")
     try:
         for r0 in range(0, reps, cr):
             nr = min(cr, reps - r0)
             rb = rep_begin + r0
             chk = _lib.check
-            chk(_lib.lib.dcor_perm_launch(seed_ni, _lib.SITE_PERM, rb, nr, n, k * m, P(perm), sp))
-            chk(_lib.lib.dcor_draws_launch(DRAW_LAPLACE, seed_ni, SITE_NI_LAP_X, rb, nr, k, P(lx), sp))
-            chk(_lib.lib.dcor_draws_launch(DRAW_LAPLACE, seed_ni, SITE_NI_LAP_Y, rb, nr, k, P(ly), sp))
-            chk(_lib.lib.dcor_draws_launch(DRAW_LAPLACE, seed_int, SITE_INT_LOCAL, rb, nr, n, P(ll), sp))
-            chk(_lib.lib.dcor_draws_launch(DRAW_LAPLACE, seed_int, SITE_INT_CENTRAL, rb, nr, 1, P(lc), sp))
-            chk(_lib.lib.dcor_draws_launch(DRAW_NORMAL, seed_int, SITE_MIX_Z, rb, nr, nsim, P(mz), sp))
-            chk(_lib.lib.dcor_draws_launch(DRAW_LAPLACE, seed_int, SITE_MIX_L, rb, nr, nsim, P(ml), sp))
+            if rng == "R":
+                sn, si = r_seeds(eps_idx, nr, rb)
+                I32 = C.POINTER(C.c_int32)
+                chk(_lib.lib.dcor_rstream_hrs_draws(n, k, m, nsim, nr, sn.ctypes.data_as(I32),
+                                                    si.ctypes.data_as(I32), P(perm), P(lx), P(ly),
+                                                    P(ll), P(lc), P(mz), P(ml), sp))
+            else:
+                chk(_lib.lib.dcor_perm_launch(seed_ni, _lib.SITE_PERM, rb, nr, n, k * m, P(perm), sp))
+                chk(_lib.lib.dcor_draws_launch(DRAW_LAPLACE, seed_ni, SITE_NI_LAP_X, rb, nr, k, P(lx), sp))
+                chk(_lib.lib.dcor_draws_launch(DRAW_LAPLACE, seed_ni, SITE_NI_LAP_Y, rb, nr, k, P(ly), sp))
+                chk(_lib.lib.dcor_draws_launch(DRAW_LAPLACE, seed_int, SITE_INT_LOCAL, rb, nr, n, P(ll), sp))
+                chk(_lib.lib.dcor_draws_launch(DRAW_LAPLACE, seed_int, SITE_INT_CENTRAL, rb, nr, 1, P(lc), sp))
+                chk(_lib.lib.dcor_draws_launch(DRAW_NORMAL, seed_int, SITE_MIX_Z, rb, nr, nsim, P(mz), sp))
+                chk(_lib.lib.dcor_draws_launch(DRAW_LAPLACE, seed_int, SITE_MIX_L, rb, nr, nsim, P(ml), sp))
             d = _lib.PrematSubg(n=n, reps=nr, eps1=eps, eps2=eps, eta1=1.0, eta2=1.0, alpha=alpha, hrs=1,
                                 lam_x=lam_age, lam_y=lam_bmi, lam_s=lam_age, lam_o=lam_bmi, lam_r=lam_r,
                                 delta=delta, nsim=nsim, X=X.data_ptr(), Y=Y.data_ptr(), xy_stride=0,
@@ -139,14 +165,16 @@ def _summ(method, eps, hat, lo, hi) -> dict:
             "ci_low_q10": q(lo, 0.10), "ci_high_q90": q(hi, 0.90)}
 
 
-def eps_sweep(age_z, bmi_z, lam_age, lam_bmi, eps_grid=EPS_GRID, reps=R_PER_EPS, nsim=2000):
+def eps_sweep(age_z, bmi_z, lam_age, lam_bmi, eps_grid=EPS_GRID, reps=R_PER_EPS, nsim=2000,
+              rng="philox"):
     """The replicate sweep of real-data-sims.R:345-448: for every eps in seq(.25, 2.5, .1),
     `reps` NI and INT runs (Philox keys 10 + 1000 idx and 20 + 1000 idx, idx 1-based as
-    which(eps_grid == eps)) and the per-eps summaries ni_mean / int_mean."""
+    which(eps_grid == eps); rng='R': the reference's own per-run set.seed streams) and the
+    per-eps summaries ni_mean / int_mean."""
     runs, ni_mean, int_mean = [], [], []
     for idx, eps in enumerate(eps_grid, start=1):
         res = hrs_replicates(age_z, bmi_z, lam_age, lam_bmi, eps, reps, seed_ni=10 + 1000 * idx,
-                             seed_int=20 + 1000 * idx, nsim=nsim)
+                             seed_int=20 + 1000 * idx, nsim=nsim, rng=rng, eps_idx=idx)
         runs.append(res)
         ni_mean.append(_summ("NI", eps, res[:, 0], res[:, 1], res[:, 2]))
         int_mean.append(_summ("INT", eps, res[:, 3], res[:, 4], res[:, 5]))

@@ -161,6 +161,18 @@ int dcor_rstream_draws(const dcor_cell* cell, int64_t reps, const dcor_rs_draws*
 /* The first `count` tempered Mersenne-Twister words after set.seed(seed), from the GPU
  * generator (unif_rand() = fixup(word * 2^-32)). */
 int dcor_rstream_words(int32_t seed, int64_t count, uint32_t* h_out);
+/* The HRS runs' noise on R's streams (real-data-sims.R:355-404), in the explicit-input layout
+ * of dcor_premat_subg (hrs = 1), DEVICE outputs, synchronous on `stream`:
+ *  run r, NI: set.seed(h_ni_seeds[r]); sample.int(n, k*m) -> d_perm[r][k*m] (0-based), then
+ *    rLap(k) twice -> d_lap_x[r][k], d_lap_y[r][k] (unit scale);
+ *  run r, INT: set.seed(h_int_seeds[r]); rLap(n) -> d_lap_local[r][n], rLap(1) ->
+ *    d_lap_central[r], mixquant(nsim) -> d_mix_z[r][nsim], d_mix_l[r][nsim].
+ * The reference seeds run `rep` at eps index idx with 10 + 37 rep + 1000 idx (NI) and
+ * 20 + 41 rep + 1000 idx (INT).  A NULL seed array skips that half.  2 <= n <= 36000. */
+int dcor_rstream_hrs_draws(int64_t n, int64_t k, int64_t m, int64_t nsim, int64_t runs,
+                           const int32_t* h_ni_seeds, const int32_t* h_int_seeds, int32_t* d_perm,
+                           double* d_lap_x, double* d_lap_y, double* d_lap_local,
+                           double* d_lap_central, double* d_mix_z, double* d_mix_l, void* stream);
 
 /* ---- pre-materialised (explicit-input) batch mode: HBM streaming --------- */
 /* Sign family, R replicates.  Per-replicate arrays are laid out rep-major with

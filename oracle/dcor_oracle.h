@@ -164,6 +164,12 @@ int orc_rs_geometry(const void* cell, int64_t* k_out, int* mix_out);
 int orc_rs_draw_rep(orc_rs_state* st, const void* cell, orc_rs_draws* d);
 /* run_sim_one with R's streams: set.seed(cell->seed), B replicates; out B x 6. */
 int orc_rs_sim(const void* cell, int64_t B, double* out);
+/* sample.int(n, k) (0-based) from the stream; the HRS runs' draws after set.seed(seed). */
+void orc_rs_sample_int(orc_rs_state* st, int64_t n, int64_t k, int32_t* out);
+void orc_rs_hrs_ni_draws(int32_t seed, int64_t n, int64_t k, int64_t m, int32_t* perm,
+                         double* lap_x, double* lap_y);
+void orc_rs_hrs_int_draws(int32_t seed, int64_t n, int64_t nsim, double* lap_local,
+                          double* lap_central, double* mix_z, double* mix_l);
 
 #ifdef __cplusplus
 }

@@ -491,3 +491,56 @@ int orc_rs_sim(const void* cellp, int64_t B, double* out) {
   free(d.mix_z); free(d.mix_l);
   return s;
 }
+
+/* ------------------------------------------- HRS runs (real-data-sims.R) --- */
+/* R_unif_index(dn) (R >= 3.6, sample.kind "Rejection"): rbits(ceil(log2(dn))) until < dn;
+ * rbits takes floor(unif_rand() * 65536) per 16 bits. */
+static double rs_unif_index(orc_rs_state* st, double dn) {
+  if (dn <= 0) return 0.0;
+  const int bits = (int)ceil(log2(dn));
+  double dv;
+  do {
+    int64_t v = 0;
+    for (int nn = 0; nn <= bits; nn += 16) {
+      const int v1 = (int)floor(orc_rs_unif(st) * 65536);
+      v = 65536 * v + v1;
+    }
+    dv = (double)(v & (((int64_t)1 << bits) - 1));
+  } while (dn <= dv);
+  return dv;
+}
+
+void orc_rs_sample_int(orc_rs_state* st, int64_t n, int64_t k, int32_t* out) {
+  /* sample.int(n, k) without replacement (do_sample, uniform): 0-based */
+  int32_t* x = (int32_t*)malloc(sizeof(int32_t) * (size_t)n);
+  for (int64_t i = 0; i < n; i++) x[i] = (int32_t)i;
+  int64_t nn = n;
+  for (int64_t i = 0; i < k; i++) {
+    const int64_t j = (int64_t)rs_unif_index(st, (double)nn);
+    out[i] = x[j];
+    x[j] = x[--nn];
+  }
+  free(x);
+}
+
+void orc_rs_hrs_ni_draws(int32_t seed, int64_t n, int64_t k, int64_t m, int32_t* perm,
+                         double* lap_x, double* lap_y) {
+  /* run_NI_once (real-data-sims.R:357-373): set.seed, then correlation_NI_subG's draws:
+   * idx <- sample.int(n, k*m) (:131), rLap(k) X, rLap(k) Y (:136-137; rLap :58-61) */
+  orc_rs_state st;
+  orc_rs_set_seed(&st, seed);
+  orc_rs_sample_int(&st, n, k * m, perm);
+  rs_laplace_n(&st, k, lap_x);
+  rs_laplace_n(&st, k, lap_y);
+}
+
+void orc_rs_hrs_int_draws(int32_t seed, int64_t n, int64_t nsim, double* lap_local,
+                          double* lap_central, double* mix_z, double* mix_l) {
+  /* run_INT_once (real-data-sims.R:375-402): set.seed, then ci_INT_subG's draws: rLap(n)
+   * (:224/:228), rLap(1) (:232), mixquant(nsim = 2000) (:161-164, :240-241) */
+  orc_rs_state st;
+  orc_rs_set_seed(&st, seed);
+  rs_laplace_n(&st, n, lap_local);
+  *lap_central = orc_rs_laplace_unit_word(orc_rs_word(&st));
+  rs_mixquant_draws(&st, nsim, mix_z, mix_l);
+}

@@ -261,6 +261,9 @@ for _n, (_r, _a) in {
     "orc_rs_geometry": (C.c_int, [C.c_void_p, _I64, C.POINTER(C.c_int)]),
     "orc_rs_draw_rep": (C.c_int, [_PS, C.c_void_p, C.POINTER(RsDraws)]),
     "orc_rs_sim": (C.c_int, [C.c_void_p, C.c_int64, _D]),
+    "orc_rs_sample_int": (None, [_PS, C.c_int64, C.c_int64, _I32]),
+    "orc_rs_hrs_ni_draws": (None, [C.c_int32, C.c_int64, C.c_int64, C.c_int64, _I32, _D, _D]),
+    "orc_rs_hrs_int_draws": (None, [C.c_int32, C.c_int64, C.c_int64, _D, _D, _D, _D]),
 }.items():
     _f = getattr(lib, _n)
     _f.restype = _r
@@ -335,3 +338,27 @@ def rs_sim(cell_struct, B: int) -> np.ndarray:
     if st:
         raise RuntimeError(f"oracle status {st}")
     return out
+
+
+def rs_sample_int(seed: int, n: int, k: int) -> np.ndarray:
+    """set.seed(seed); sample.int(n, k) - 1."""
+    st = rs_state(seed)
+    out = np.zeros(k, dtype=np.int32)
+    lib.orc_rs_sample_int(C.byref(st), n, k, out.ctypes.data_as(_I32))
+    return out
+
+
+def rs_hrs_ni_draws(seed: int, n: int, k: int, m: int):
+    perm = np.zeros(k * m, dtype=np.int32)
+    lx, ly = np.zeros(k), np.zeros(k)
+    lib.orc_rs_hrs_ni_draws(seed, n, k, m, perm.ctypes.data_as(_I32), lx.ctypes.data_as(_D),
+                            ly.ctypes.data_as(_D))
+    return perm, lx, ly
+
+
+def rs_hrs_int_draws(seed: int, n: int, nsim: int = 2000):
+    ll, lc = np.zeros(n), np.zeros(1)
+    mz, ml = np.zeros(nsim), np.zeros(nsim)
+    lib.orc_rs_hrs_int_draws(seed, n, nsim, ll.ctypes.data_as(_D), lc.ctypes.data_as(_D),
+                             mz.ctypes.data_as(_D), ml.ctypes.data_as(_D))
+    return ll, float(lc[0]), mz, ml

@@ -94,3 +94,65 @@ def test_panel_pipelined_halves_bitexact(panel):
     piped = hrs.hrs_replicates(*args, chunk=4100)
     np.testing.assert_array_equal(piped.view(np.int64), serial.view(np.int64))
     assert np.isfinite(piped).all()
+
+
+# ------------------------------------------------------- R-stream runs (f4 + a19)
+@pytest.mark.parametrize("eps,idx", [(2.0, 18), (0.35, 2)])
+def test_hrs_r_streams_match_oracle(panel, eps, idx):
+    """rng='R': run rep draws after set.seed(10 + 37 rep + 1000 idx) / set.seed(20 + 41 rep +
+    1000 idx) (real-data-sims.R:404, 423): sample.int, rLap and mixquant bit-exact against the
+    CPU restatement, estimates within 1e-12."""
+    from dcor import hrs
+    from oracle import oracle as orc
+    z = panel
+    n = len(z["age_z"])
+    R, rb = 4, 6
+    res, noise, geo = hrs.hrs_replicates(z["age_z"], z["bmi_z"], z["lambda_age_z"], z["lambda_bmi_z"], eps,
+                                         R, rep_begin=rb, chunk=3, keep_noise=True, rng="R", eps_idx=idx)
+    k, m = geo["k"], geo["m"]
+    sn, si = hrs.r_seeds(idx, R, rb)
+    assert sn[0] == 10 + 37 * (rb + 1) + 1000 * idx and si[0] == 20 + 41 * (rb + 1) + 1000 * idx
+    for r in range(R):
+        perm, lx, ly = orc.rs_hrs_ni_draws(int(sn[r]), n, k, m)
+        np.testing.assert_array_equal(noise["perm"][r], perm)
+        np.testing.assert_array_equal(noise["lap_x"][r], lx)
+        np.testing.assert_array_equal(noise["lap_y"][r], ly)
+        ll, lc, mz, ml = orc.rs_hrs_int_draws(int(si[r]), n, 2000)
+        np.testing.assert_array_equal(noise["lap_local"][r], ll)
+        assert noise["lap_central"][r] == lc
+        np.testing.assert_array_equal(noise["mix_z"][r], mz)
+        np.testing.assert_array_equal(noise["mix_l"][r], ml)
+        st, ni, _ = orc.ni_subg(z["age_z"], z["bmi_z"], eps, eps, hrs=1, lam_x=z["lambda_age_z"],
+                                lam_y=z["lambda_bmi_z"], perm=perm, lap_x=lx, lap_y=ly)
+        st2, it, _ = orc.int_subg(z["age_z"], z["bmi_z"], eps, eps, hrs=1, lam_s=z["lambda_age_z"],
+                                  lam_o=z["lambda_bmi_z"], lam_r=geo["lam_r"], delta=geo["delta"],
+                                  lap_local=ll, lap_central=lc, mix_z=mz, mix_l=ml)
+        assert st == 0 and st2 == 0
+        assert_close(res[r], np.concatenate([ni, it]), what=f"R-stream hrs eps={eps} run {rb + r + 1}")
+
+
+def test_hrs_r_stream_sample_int_is_a_permutation(panel):
+    import ctypes as C
+
+    import torch
+    from dcor import _lib
+    n, k, m, runs = 20000, 9000, 2, 3
+    perm = torch.empty((runs, k * m), dtype=torch.int32, device="cuda")
+    lx = torch.empty((runs, k), dtype=torch.float64, device="cuda")
+    ly = torch.empty_like(lx)
+    seeds = np.array([1, 42, 123], dtype=np.int32)
+    P = lambda t: C.c_void_p(t.data_ptr())
+    _lib.check(_lib.lib.dcor_rstream_hrs_draws(n, k, m, 2000, runs, seeds.ctypes.data_as(C.POINTER(C.c_int32)),
+                                               None, P(perm), P(lx), P(ly), None, None, None, None, None))
+    got = perm.cpu().numpy()
+    from oracle import oracle as orc
+    for r in range(runs):
+        assert len(np.unique(got[r])) == k * m and got[r].min() >= 0 and got[r].max() < n
+        np.testing.assert_array_equal(got[r], orc.rs_sample_int(int(seeds[r]), n, k * m))
+    # R: set.seed(1); sample(10) = 9 4 7 1 2 5 3 10 6 8 (tests/golden/r_known_values.json)
+    p10 = torch.empty((1, 10), dtype=torch.int32, device="cuda")
+    l1 = torch.empty((1, 5), dtype=torch.float64, device="cuda")
+    one = np.array([1], dtype=np.int32)
+    _lib.check(_lib.lib.dcor_rstream_hrs_draws(10, 5, 2, 2000, 1, one.ctypes.data_as(C.POINTER(C.c_int32)),
+                                               None, P(p10), P(l1), P(l1), None, None, None, None, None))
+    assert list(p10.cpu().numpy()[0] + 1) == [9, 4, 7, 1, 2, 5, 3, 10, 6, 8]

@@ -154,3 +154,22 @@ def test_rs_sim_runs_every_family(orc):
         out = orc.rs_sim(_cell(**kw), 4)
         assert out.shape == (4, 6) and np.all(np.isfinite(out))
         assert np.all(out[:, 1] <= out[:, 2]) and np.all(out[:, 4] <= out[:, 5])
+
+
+@pytest.mark.parametrize("case", GOLD["sample"], ids=lambda c: f"sample-{c['seed']}-{c['n']}")
+def test_r_printed_sample(orc, case):
+    """set.seed(seed); sample(n, size): R_unif_index rejection sampling + do_sample."""
+    got = orc.rs_sample_int(case["seed"], case["n"], case["size"]) + 1
+    assert list(got) == case["values"]
+
+
+def test_hrs_run_draws_consume_in_reference_order(orc):
+    """run_NI_once: sample.int then rLap(k) x2; run_INT_once: rLap(n), rLap(1), mixquant."""
+    n, k, m = 101, 25, 4
+    perm, lx, ly = orc.rs_hrs_ni_draws(77, n, k, m)
+    assert sorted(perm) == sorted(set(perm)) and len(perm) == k * m
+    np.testing.assert_array_equal(perm, orc.rs_sample_int(77, n, k * m))
+    ll, lc, mz, ml = orc.rs_hrs_int_draws(78, n, 50)
+    w = orc.rs_stream(78, "word", n + 1)
+    np.testing.assert_array_equal(ll, [orc.lib.orc_rs_laplace_unit_word(int(x)) for x in w[:n]])
+    assert lc == orc.lib.orc_rs_laplace_unit_word(int(w[n]))
