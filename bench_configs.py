@@ -11,6 +11,8 @@ S   sub-G fused, bounded factor, n=1e5, rho=.5, eps=(1,1)
 R1  R-stream mode (R's own Mersenne-Twister streams) on the C1 cell: GPU vs the
     CPU restatement (1 thread)
 RG  R-stream mode on vert-cor.R's own 144-cell sign-family grid, B = 250 (vert-cor.R:486-553)
+RH  R-stream HRS sweep: real-data-sims.R's 23 eps x 200 runs with its own per-run set.seed
+    streams (4,600 NI + 4,600 INT runs) on a stand-in panel n = 19,433
 Run on one GPU: python bench_configs.py [--only C2,C5] > profiles/rNN_configs.jsonl
 """
 import argparse
@@ -266,9 +268,38 @@ def rstream_grid():
          note="R's own streams (set.seed(1e6+i)); cells run side by side, one MT wave each")
 
 
+def rstream_hrs():
+    import numpy as np
+    import torch
+    from dcor import hrs
+    from oracle import oracle as orc
+    age_raw, bmi_raw = hrs.standin_panel(19433, -0.3)
+    z = hrs.standardize_panel(age_raw, bmi_raw, lap=np.zeros(4))
+    args = (z["age_z"], z["bmi_z"], z["lambda_age_z"], z["lambda_bmi_z"])
+    hrs.eps_sweep(*args, eps_grid=hrs.EPS_GRID[:2], reps=20, rng="R")  # warm-up
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    sw = hrs.eps_sweep(*args, rng="R")
+    torch.cuda.synchronize()
+    t = time.perf_counter() - t0
+    runs = len(hrs.EPS_GRID) * hrs.R_PER_EPS
+    # CPU restatement: the draws of 4 NI + 4 INT runs (estimators excluded), scaled
+    n = len(z["age_z"])
+    k, m = 4858, 4  # eps = 1.45 geometry; the draw cost is dominated by sample.int and rLap(n)
+    t0 = time.perf_counter()
+    for r in range(4):
+        orc.rs_hrs_ni_draws(10 + 37 * r, n, k, m)
+        orc.rs_hrs_int_draws(20 + 41 * r, n, 2000)
+    tc = (time.perf_counter() - t0) / 4 * runs
+    line("RH", runs_ni=runs, runs_int=runs, seconds=t, runs_per_s=2 * runs / t,
+         finite=bool(np.isfinite(sw["runs"]).all()), cpu_draws_only_1thread_projected_s=tc,
+         cpu_sample="draws of 4 NI + 4 INT runs (CPU restatement), scaled to the sweep",
+         note="each run replays its own set.seed(10 + 37 rep + 1000 idx) / (20 + 41 rep + 1000 idx)")
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--only", default="C1,C2,C3,C4,C5,C5c,C5e,S,R1,RG")
+    ap.add_argument("--only", default="C1,C2,C3,C4,C5,C5c,C5e,S,R1,RG,RH")
     ap.add_argument("--c3-reps", type=int, default=2000)
     ap.add_argument("--c4-B", type=int, default=1000)
     ap.add_argument("--c5-R", type=int, default=8192)
@@ -287,6 +318,7 @@ def main():
     if "S" in which: subg()
     if "R1" in which: rstream_c1()
     if "RG" in which: rstream_grid()
+    if "RH" in which: rstream_hrs()
 
 
 if __name__ == "__main__":

@@ -181,7 +181,7 @@ struct RsCell {
 #define RS_FAMILY_HRS_INT 2
 int launch_rs_stream(RsCell* d_cells, int ncells, int32_t rc, void* stream);
 // The HRS NI runs: sample.int(n, k*m) and rLap(k) twice after set.seed(seeds[r]); n <= RS_HRS_NMAX.
-#define RS_HRS_NMAX 36000
+#define RS_HRS_NMAX 65536
 size_t rs_hrs_ni_lds_bytes(int64_t n);
 int launch_rs_hrs_ni(const int32_t* d_seeds, int64_t runs, int64_t n, int64_t km, int64_t k,
                      int32_t* perm, double* lx, double* ly, void* stream);

@@ -507,11 +507,12 @@ __global__ __launch_bounds__(64) void k_rs_hrs_ni(const int32_t* __restrict__ se
   extern __shared__ uint32_t rs_sm[];
   uint32_t* mt = rs_sm;
   uint32_t* wb = rs_sm + RS_N;
-  int32_t* x = reinterpret_cast<int32_t*>(rs_sm + 2 * RS_N);
+  uint16_t* x = reinterpret_cast<uint16_t*>(rs_sm + 2 * RS_N);  // n <= 65536: 2 B per index,
+                                                                 // so 3 runs share a CU
   const int lane = threadIdx.x;
   const int64_t r = blockIdx.x;
   rs_seed_mt(mt, seeds[r], lane);
-  for (int64_t i = lane; i < n; i += 64) x[i] = (int32_t)i;
+  for (int64_t i = lane; i < n; i += 64) x[i] = (uint16_t)i;
   int pos = RS_N;                          // set.seed leaves mti = 624: first use regenerates
   auto refill = [&]() {
     __syncthreads();
@@ -522,27 +523,99 @@ __global__ __launch_bounds__(64) void k_rs_hrs_ni(const int32_t* __restrict__ se
   };
   __syncthreads();
   RS_G int32_t* const pr = (RS_G int32_t*)(perm + r * km);
-  int64_t dn = n;
-  for (int64_t i = 0; i < km; ++i, --dn) {
-    dn = rs_u64(dn);
-    const int bits = (dn <= 1) ? 0 : 64 - __builtin_clzll((unsigned long long)(dn - 1));  // ceil(log2 dn)
-    const uint64_t mask = (bits >= 63) ? ~0ull : ((1ull << bits) - 1ull);
-    uint64_t v;
-    do {                                    // R_unif_index: rbits(bits) until < dn
-      v = 0;
-      for (int nn = 0; nn <= bits; nn += 16) {
-        if (pos == RS_N) refill();
-        pos = rs_u(pos);
-        v = 65536ull * v + (wb[pos] >> 16);  // floor(unif_rand() * 65536)
-        ++pos;
-      }
-      v &= mask;
-    } while ((int64_t)v >= dn);
+  // Fast path (one word per attempt, bits <= 15): a window of up to 64 words is evaluated
+  // lane-parallel.  With dn the remaining size, v < dn - W accepts and v >= dn rejects
+  // whatever the window's earlier draws did; any other v sends the window to the exact
+  // in-order path.  The accepted draws' swaps x[j_t] <- x[dn-1-t] then run in parallel
+  // unless two j coincide or a j hits one of the window's tail slots (an LDS bitmap
+  // detects both); otherwise in order.  Both paths give do_sample's exact sequence.
+  uint32_t* mark = reinterpret_cast<uint32_t*>(x + ((n + 1) & ~1ll));
+  for (int64_t q = lane; q < (n + 31) / 32; q += 64) mark[q] = 0u;
+  __syncthreads();
+  int64_t i = 0, dn = n;
+  auto take_one = [&](uint64_t v) {        // accept v as the next index (lane 0 swaps)
     if (lane == 0) {
       const int32_t j = (int32_t)v;
-      pr[i] = x[j];                         // iy[i] = x[j] + 1 (0-based here)
+      pr[i] = (int32_t)x[j];               // iy[i] = x[j] + 1 (0-based here)
       x[j] = x[dn - 1];
     }
+    ++i;
+    --dn;
+  };
+  while (i < km) {
+    i = rs_u64(i); dn = rs_u64(dn);
+    if (pos == RS_N) refill();
+    pos = rs_u(pos);
+    const int bits = (dn <= 1) ? 0 : 64 - __builtin_clzll((unsigned long long)(dn - 1));  // ceil(log2 dn)
+    const int W = (RS_N - pos < 64) ? RS_N - pos : 64;
+    const int bits_lo = (dn - W <= 1) ? 0 : 64 - __builtin_clzll((unsigned long long)(dn - W - 1));
+    if (bits > 15 || bits != bits_lo || dn <= 64) {
+      // exact scalar attempt: R_unif_index = rbits(bits) until < dn
+      const uint64_t mask = (bits >= 63) ? ~0ull : ((1ull << bits) - 1ull);
+      uint64_t v;
+      do {
+        v = 0;
+        for (int nn = 0; nn <= bits; nn += 16) {
+          if (pos == RS_N) refill();
+          pos = rs_u(pos);
+          v = 65536ull * v + (wb[pos] >> 16);  // floor(unif_rand() * 65536)
+          ++pos;
+        }
+        v &= mask;
+      } while ((int64_t)v >= dn);
+      take_one(v);
+      continue;
+    }
+    const uint32_t mask = (1u << bits) - 1u;
+    const bool in = lane < W;
+    const int64_t v = in ? (int64_t)((wb[pos + (in ? lane : 0)] >> 16) & mask) : 0;
+    const bool sure_acc = in && v < dn - W, sure_rej = in && v >= dn;
+    const uint64_t amb = __ballot(in && !sure_acc && !sure_rej);
+    if (amb) {                             // exact, in order through the window
+      int used = 0;
+      for (int l = 0; l < W && i < km; ++l) {
+        const int64_t vl = (int64_t)(uint32_t)rs_rl((int)v, l);
+        used = l + 1;
+        if (vl < dn) take_one((uint64_t)vl);
+      }
+      pos += used;
+      continue;
+    }
+    uint64_t A = __ballot(sure_acc);
+    int used = W;
+    const int64_t need = km - i;
+    if ((int64_t)__builtin_popcountll(A) > need) {   // the sample ends inside this window
+      uint64_t keep = A;
+      for (int64_t c = __builtin_popcountll(A); c > need; --c) keep &= ~(1ull << (63 - __builtin_clzll(keep)));
+      A = keep;
+      used = 64 - __builtin_clzll(A);
+    }
+    const int B = __builtin_popcountll(A);
+    const bool acc = (A >> lane) & 1ull;
+    const int t = __builtin_popcountll(A & ((1ull << lane) - 1ull));
+    const int64_t Lt = dn - 1 - t;
+    bool clash = false;
+    if (acc) clash = (atomicOr(&mark[v >> 5], 1u << (v & 31)) >> (v & 31)) & 1u;
+    __syncthreads();
+    if (acc && Lt != v) clash |= (mark[Lt >> 5] >> (Lt & 31)) & 1u;
+    const bool serial = __ballot(clash) != 0ull;
+    __syncthreads();
+    if (acc) atomicAnd(&mark[v >> 5], ~(1u << (v & 31)));
+    if (!serial) {
+      uint16_t a = 0, b = 0;
+      if (acc) { a = x[v]; b = x[Lt]; }
+      __syncthreads();
+      if (acc) { pr[i + t] = (int32_t)a; x[v] = b; }
+      i += B;
+      dn -= B;
+    } else {
+      for (uint64_t rest = A; rest; rest &= rest - 1ull) {
+        const int l = __builtin_ctzll(rest);
+        take_one((uint64_t)(uint32_t)rs_rl((int)v, l));
+      }
+    }
+    __syncthreads();
+    pos += used;
   }
   // rLap(k) for X, then rLap(k) for Y: the next 2k words
   int64_t t0 = 0;
@@ -561,7 +634,9 @@ __global__ __launch_bounds__(64) void k_rs_hrs_ni(const int32_t* __restrict__ se
   }
 }
 
-size_t rs_hrs_ni_lds_bytes(int64_t n) { return (size_t)(2 * RS_N + n) * 4; }
+size_t rs_hrs_ni_lds_bytes(int64_t n) {
+  return (size_t)(2 * RS_N) * 4 + (size_t)((n + 1) & ~1ll) * 2 + (size_t)((n + 31) / 32) * 4;
+}
 
 int launch_rs_hrs_ni(const int32_t* d_seeds, int64_t runs, int64_t n, int64_t km, int64_t k,
                      int32_t* perm, double* lx, double* ly, void* stream) {

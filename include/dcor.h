@@ -168,7 +168,7 @@ int dcor_rstream_words(int32_t seed, int64_t count, uint32_t* h_out);
  *  run r, INT: set.seed(h_int_seeds[r]); rLap(n) -> d_lap_local[r][n], rLap(1) ->
  *    d_lap_central[r], mixquant(nsim) -> d_mix_z[r][nsim], d_mix_l[r][nsim].
  * The reference seeds run `rep` at eps index idx with 10 + 37 rep + 1000 idx (NI) and
- * 20 + 41 rep + 1000 idx (INT).  A NULL seed array skips that half.  2 <= n <= 36000. */
+ * 20 + 41 rep + 1000 idx (INT).  A NULL seed array skips that half.  2 <= n <= 65536. */
 int dcor_rstream_hrs_draws(int64_t n, int64_t k, int64_t m, int64_t nsim, int64_t runs,
                            const int32_t* h_ni_seeds, const int32_t* h_int_seeds, int32_t* d_perm,
                            double* d_lap_x, double* d_lap_y, double* d_lap_local,
