@@ -76,3 +76,38 @@ def run_grid_distributed(cells, B: int, group=None, stream=None):
             local.extend([_lib.Accum(), _lib.Accum()])
     merged = merge_ranked(gather_accums(local, group))
     return [(merged[2 * i], merged[2 * i + 1]) for i in range(len(cells))]
+
+
+# ------------------------------------------------------ R-stream mode (by cell)
+def cell_shard(costs, world: int) -> List[List[int]]:
+    """Cells of an R-stream grid per rank.  R's stream is sequential within a cell, so the cell
+    is the unit (the reference's mclapply unit); longest-processing-time-first on cost (n * B),
+    ties by cell index, deterministic for a given world size."""
+    order = sorted(range(len(costs)), key=lambda i: (-costs[i], i))
+    load = [0.0] * world
+    out: List[List[int]] = [[] for _ in range(world)]
+    for i in order:
+        g = min(range(world), key=lambda r: (load[r], r))
+        out[g].append(i)
+        load[g] += costs[i]
+    return [sorted(o) for o in out]
+
+
+def run_grid_rstream_distributed(cells, B: int, group=None):
+    """R-stream grid over G ranks: rank g runs its cells of cell_shard() with R's own streams
+    (dcor.rstream); the per-cell accumulators are all-gathered (cells a rank does not own
+    contribute empty accumulators) and merged in rank order.  Returns [(NI, INT)] per cell,
+    identical on all ranks and equal to a single-GPU run."""
+    import torch.distributed as dist
+
+    from .rstream import run_grid
+
+    rank, world = dist.get_rank(group), dist.get_world_size(group)
+    mine = cell_shard([float(c.n) * B for c in cells], world)[rank]
+    local = [_lib.Accum() for _ in range(2 * len(cells))]
+    if mine:
+        res = run_grid([cells[i] for i in mine], B, detail=False)
+        for i, r in zip(mine, res):
+            local[2 * i], local[2 * i + 1] = r["accum"]
+    merged = merge_ranked(gather_accums(local, group))
+    return [(merged[2 * i], merged[2 * i + 1]) for i in range(len(cells))]

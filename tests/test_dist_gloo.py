@@ -76,3 +76,57 @@ def test_gather_merge_two_ranks():
     assert res[0] == [bytes(a) for a in want]
     a0 = _lib.Accum.from_buffer_copy(res[0][0])
     assert a0.n == 10 + 11
+
+
+def test_rstream_cell_shard_balanced_and_covering():
+    from dcor.dist import cell_shard
+    g = np.random.default_rng(3)
+    for ncells in (1, 5, 144, 480):
+        costs = list(g.choice([1e3, 1e4, 1e5, 1e6], ncells) * 250.0)
+        for world in (1, 2, 4, 8):
+            parts = cell_shard(costs, world)
+            flat = sorted(i for p in parts for i in p)
+            assert flat == list(range(ncells))
+            loads = [sum(costs[i] for i in p) for p in parts]
+            # LPT: the heaviest rank exceeds the lightest by at most one cell's cost
+            assert max(loads) - min(loads) <= max(costs) + 1e-9
+            assert parts == cell_shard(costs, world)  # deterministic
+
+
+def _rs_worker(rank, world, port, q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from dcor import _lib
+    from dcor.dist import cell_shard, gather_accums, merge_ranked
+    # cell i's accumulators exist only on its owner; the merge must reproduce them exactly
+    costs = [1.0, 5.0, 2.0, 2.0, 7.0]
+    mine = cell_shard(costs, world)[rank]
+    local = [_lib.Accum() for _ in range(2 * len(costs))]
+    for i in mine:
+        for m in range(2):
+            a = _lib.Accum()
+            a.n = 100 + 10 * i + m
+            a.est[0] = 0.125 * (i + 1) + m
+            a.est[1] = 1e-20 * (i + 1)
+            local[2 * i + m] = a
+    merged = merge_ranked(gather_accums(local))
+    q.put((rank, [(a.n, a.est[0], a.est[1]) for a in merged]))
+    dist.destroy_process_group()
+
+
+def test_rstream_cell_shard_gather_two_ranks():
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_rs_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res[0] == res[1]
+    for i in range(5):
+        for m in range(2):
+            assert res[0][2 * i + m] == (100 + 10 * i + m, 0.125 * (i + 1) + m, 1e-20 * (i + 1))
