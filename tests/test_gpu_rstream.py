@@ -115,3 +115,26 @@ def test_run_sim_one_rng_r(dc, orc):
     ref = orc.rs_sim(_spec(dc).to_c(), 20)
     assert_close(np.stack([res["detail"][k] for k in ("ni_hat", "ni_low", "ni_up", "int_hat",
                                                       "int_low", "int_up")], 1), ref)
+
+
+def test_distributed_rstream_world1_equals_single(dc):
+    """The cell-sharded driver (gloo, world 1 here; the 8-GPU run is the driver's) returns the
+    single-GPU accumulators bit for bit."""
+    import socket
+
+    import torch.distributed as dist
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=0, world_size=1)
+    try:
+        from dcor.dist import run_grid_rstream_distributed
+        specs = [_spec(dc, **CELLS["sign-gauss"]), _spec(dc, **CELLS["subG-bounded"])]
+        got = run_grid_rstream_distributed(specs, 16)
+        ref = dc.rstream.run_grid(specs, 16, detail=False)
+        for (ni, it), r in zip(got, ref):
+            assert bytes(ni) == bytes(r["accum"][0]) and bytes(it) == bytes(r["accum"][1])
+    finally:
+        dist.destroy_process_group()
