@@ -138,3 +138,29 @@ def test_distributed_rstream_world1_equals_single(dc):
             assert bytes(ni) == bytes(r["accum"][0]) and bytes(it) == bytes(r["accum"][1])
     finally:
         dist.destroy_process_group()
+
+
+def test_headline_cell_full_size(dc, orc):
+    """The BASELINE headline cell (n = 1e5) on R's stream: 2 replicates against the CPU
+    restatement (the second one starts where the first one's exp_rand walk ended)."""
+    spec = dc.headline_cell()
+    res = dc.rstream.run_grid([spec], 2)[0]
+    assert_close(res["records"], orc.rs_sim(spec.to_c(), 2))
+
+
+@pytest.mark.parametrize("kw,status", [(dict(n=5, eps1=0.2, eps2=0.2), 2),          # k < 1 (stopifnot)
+                                       (dict(dgp="mix_gaussian"), 1),                 # not replayed
+                                       (dict(seed=2 ** 31), 1)])                      # set.seed range
+def test_rstream_rejects_like_the_reference(dc, kw, status):
+    from dcor import _lib
+    spec = _spec(dc, **kw)
+    with pytest.raises(_lib.DcorError) as e:
+        dc.rstream.run_grid([spec], 2)
+    assert e.value.code == status
+
+
+def test_rstream_extreme_eps_flips_take_no_words(dc, orc):
+    """exp(40)/(exp(40)+1) == 1 in double: rbinom(n, 1, 1) returns 1 without drawing."""
+    spec = _spec(dc, eps1=40.0, eps2=1.0, n=500)
+    res = dc.rstream.run_grid([spec], 3)[0]
+    assert_close(res["records"], orc.rs_sim(spec.to_c(), 3))
