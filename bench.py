@@ -36,22 +36,24 @@ def work_units(cell, m, k):
 
 
 def cpu_baseline(cell, seconds: float = 12.0):
-    """The oracle's fused restatement (C, 1 thread) on a bounded sample of the workload."""
-    import numpy as np
-    from oracle.oracle import sim_reps
+    """The reference's loop restated on the CPU (C, 1 thread) on a bounded sample of the
+    workload: run_sim_one from set.seed(seed) with R's own generators (Mersenne-Twister,
+    inversion rnorm, exp_rand, rbinom, extraDistr rlaplace, mvrnorm's eigen factor) and the
+    R-semantics estimators (oracle/dcor_rstream.c + dcor_oracle.c)."""
+    from oracle.oracle import rs_sim
     c = cell.to_c()
     t0 = time.perf_counter()
-    done = 0
-    while True:
-        sim_reps(c, 10_000_000 + done, 10_000_000 + done + 2, threads=1)
-        done += 2
-        el = time.perf_counter() - t0
-        if el >= seconds or done >= 2000:
-            break
-    return {"value": done / el, "unit": "replicates/s", "cores": 1, "kind": "port",
-            "sample": f"{done} replicates of the headline cell (n={cell.n}) in {el:.1f} s, "
-                      "oracle/dcor_oracle.c fused restatement, 1 thread (mclapply granularity: "
-                      "one core per cell)"}
+    rs_sim(c, 2)
+    per = (time.perf_counter() - t0) / 2
+    B = int(max(2, min(2000, seconds / max(per, 1e-9))))
+    t0 = time.perf_counter()
+    rs_sim(c, B)
+    el = time.perf_counter() - t0
+    return {"value": B / el, "unit": "replicates/s", "cores": 1, "kind": "port",
+            "sample": f"replicates 1..{B} of run_sim_one(seed={cell.seed}) on the headline cell "
+                      f"(n={cell.n}) in {el:.1f} s: oracle/dcor_rstream.c (R's own generators) + "
+                      "dcor_oracle.c (R-semantics estimators), 1 thread (mclapply granularity: one "
+                      "core per cell)"}
 
 
 def pmc_traffic(path=os.path.join(ROOT, "profiles", "r01_headline_summary.json")):
