@@ -114,8 +114,7 @@ dp_sd <- function(x, lo, hi, eps1, eps2) {
 ## dgp: "gaussian"/"bernoulli"/"bounded_factor"/"mix_gaussian" (gen_mix_gaussian, whose
 ## arguments come in `mix`, defaults as ver-cor-subG.R:113-116).
 ## rng: "philox" (counter-based streams, shardable by replicate) or "R" (R's own
-## Mersenne-Twister stream from set.seed(1e6 + i) per cell: the reference's per-seed numbers;
-## gaussian / bernoulli / bounded_factor).
+## Mersenne-Twister stream from set.seed(1e6 + i) per cell: the reference's per-seed numbers).
 dcor_grid <- function(design, B = 250, alpha = 0.05, mu = c(0, 0), sigma = c(1, 1),
                       family = "sign", dgp = "gaussian", ci_mode = "auto", normalise = TRUE,
                       detail = FALSE,

@@ -1098,8 +1098,10 @@ int rs_plan(const dcor_cell& cell, RsPlan& p) {
   if (cell.family != DCOR_FAMILY_SIGN && cell.family != DCOR_FAMILY_SUBG)
     return fail(DCOR_EINVAL, "rstream: bad family");
   if (cell.dgp != DCOR_DGP_GAUSSIAN && cell.dgp != DCOR_DGP_BERNOULLI &&
-      cell.dgp != DCOR_DGP_BOUNDED_FACTOR)
-    return fail(DCOR_EINVAL, "rstream: DGP not available in R-stream mode (gen_mix_gaussian)");
+      cell.dgp != DCOR_DGP_BOUNDED_FACTOR && cell.dgp != DCOR_DGP_MIX_GAUSSIAN)
+    return fail(DCOR_EINVAL, "rstream: bad dgp");
+  if (cell.dgp == DCOR_DGP_MIX_GAUSSIAN && (n > RS_MIX_NMAX || !(cell.mix_pi >= 0.0 && cell.mix_pi <= 1.0)))
+    return fail(DCOR_EINVAL, "rstream: gen_mix_gaussian needs n <= %d and 0 <= pi_mix <= 1", RS_MIX_NMAX);
   if (cell.seed > 0x7fffffffull) return fail(DCOR_EINVAL, "rstream: set.seed takes a 32-bit integer");
   c.n = n; c.nsim = cell.nsim; c.family = cell.family; c.dgp = cell.dgp;
   const bool subg = cell.family == DCOR_FAMILY_SUBG;
@@ -1117,8 +1119,25 @@ int rs_plan(const dcor_cell& cell, RsPlan& p) {
     if (mode == DCOR_MODE_AUTO) mode = (std::sqrt((double)n) * eps_r > 0.5) ? DCOR_MODE_NORMAL : DCOR_MODE_LAPLACE;
     c.has_mix = (mode == DCOR_MODE_NORMAL) ? 1 : 0;
   }
-  // DGP (vert-cor.R:78-98,389-394; ver-cor-subG.R:141-154)
-  if (cell.dgp == DCOR_DGP_GAUSSIAN) {
+  // DGP (vert-cor.R:78-98,389-394; ver-cor-subG.R:113-154)
+  int64_t shuffle_words = 0;
+  if (cell.dgp == DCOR_DGP_MIX_GAUSSIAN) {
+    // labels rbinom(n, 1, pi) (n words unless pi is 0 or 1), 2n normals (4n words), then
+    // sample.int(n): R_unif_index's rejection takes < 2 attempts per draw on average; the
+    // buffer allows 4x that (the walker stops, flagged, rather than overrun it)
+    const double pp = cell.mix_pi;
+    if (pp == 0.0 || pp == 1.0) { c.lab_on = 0; c.lab_const = (pp == 1.0); }
+    else { c.lab_on = 1; c.lab_q = 1. - std::fmin(pp, 1. - pp); c.lab_inv = (pp > 0.5) ? 1 : 0; }
+    c.shuffle = 1;
+    c.dgp_words = (c.lab_on ? n : 0) + 4 * n;
+    c.pre_a = c.dgp_words;
+    const int64_t wpa = (n > 32768) ? 2 : 1;   // words per attempt (16 bits each)
+    shuffle_words = 8 * wpa * n + 4096;
+    rs_mvrnorm_factor(cell.mix_sigma0, cell.rho, c.mA0);
+    rs_mvrnorm_factor(cell.mix_sigma1, cell.rho, c.mA1);
+    c.mmu0[0] = cell.mix_mu0[0]; c.mmu0[1] = cell.mix_mu0[1];
+    c.mmu1[0] = cell.mix_mu1[0]; c.mmu1[1] = cell.mix_mu1[1];
+  } else if (cell.dgp == DCOR_DGP_GAUSSIAN) {
     c.dgp_words = 4 * n;
     rs_mvrnorm_factor(cell.sigma, cell.rho, c.A);
     c.mu[0] = cell.mu[0]; c.mu[1] = cell.mu[1];
@@ -1150,11 +1169,11 @@ int rs_plan(const dcor_cell& cell, RsPlan& p) {
   }
   if (c.has_mix) pre += 2 * c.nsim;
   c.pre = pre;
-  p.rep_max = pre + (c.has_mix ? 18 * c.nsim : 0);
+  p.rep_max = pre + shuffle_words + (c.has_mix ? 18 * c.nsim : 0);
   const int64_t fw = (n + 31) / 32;
   p.per_rep = (size_t)p.rep_max * 4 + (size_t)c.nsim * 8 * 3 + (size_t)n * 16 + 64 +
               (size_t)c.k * 16 + (size_t)fw * 4 + (subg ? (size_t)n * 8 : 0) + 8 + 16 +
-              sizeof(dcor_rep_out) + 256;
+              (c.shuffle ? (size_t)n * 4 + 8 : 0) + sizeof(dcor_rep_out) + 256;
   return DCOR_OK;
 }
 
@@ -1180,6 +1199,9 @@ void rs_carve(RsPlan& p, int32_t rc, char*& base) {
   c.lap_scalar = (double*)take((size_t)rc * 8);
   c.mix_z = (double*)take((size_t)rc * nsim * 8);
   c.mix_l = (double*)take((size_t)rc * nsim * 8);
+  c.shuf = c.shuffle ? (int32_t*)take((size_t)rc * n * 4) : nullptr;
+  c.shuf_end = c.shuffle ? (int64_t*)take((size_t)rc * 8) : nullptr;
+  c.words_cap = (int64_t)rc * p.rep_max + 2 * 624 + 64;
 }
 
 size_t rs_cell_bytes(const RsPlan& p, int32_t rc) {
@@ -1189,7 +1211,8 @@ size_t rs_cell_bytes(const RsPlan& p, int32_t rc) {
          al256((size_t)rc * nsim * 8) + 2 * al256((size_t)rc * n * 8) + 2 * al256((size_t)rc * 32) +
          2 * al256((size_t)rc * k * 8) + al256((size_t)rc * fw * 4) +
          ((c.family == DCOR_FAMILY_SUBG) ? al256((size_t)rc * n * 8) : 0) + al256((size_t)rc * 8) +
-         2 * al256((size_t)rc * nsim * 8);
+         2 * al256((size_t)rc * nsim * 8) +
+         (c.shuffle ? al256((size_t)rc * n * 4) + al256((size_t)rc * 8) : 0);
 }
 
 // The estimators over one chunk of materialised replicates of one cell.
@@ -1278,11 +1301,20 @@ int dcor_rstream_grid_run(const dcor_cell* cells, int ncells, int64_t B, dcor_ac
     }
     HIPCHK(hipMemcpy(dst.p, hst.data(), sizeof(RsState) * (size_t)nb, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(dcells.p, hc.data(), sizeof(RsCell) * (size_t)nb, hipMemcpyHostToDevice));
+    size_t mix_lds = 0;
+    for (int i = 0; i < nb; ++i)
+      if (hc[(size_t)i].shuffle) mix_lds = std::max(mix_lds, rs_mix_lds_bytes(hc[(size_t)i].n));
     for (int64_t done = 0; done < B; done += rc) {
       const int32_t rcc = (int32_t)std::min<int64_t>(rc, B - done);
       int e = launch_rs_stream(dcells.as<RsCell>(), nb, rcc, nullptr);
       if (e) return hip_fail((hipError_t)e, "rstream stream launch");
-      e = launch_rs_materialise(dcells.as<RsCell>(), nb, rcc, nullptr);
+      if (mix_lds) {   // gen_mix_gaussian: sample.int's rejection is unbounded; check the flag
+        HIPCHK(hipMemcpy(hst.data(), dst.p, sizeof(RsState) * (size_t)nb, hipMemcpyDeviceToHost));
+        for (int i = 0; i < nb; ++i)
+          if (hst[(size_t)i].pad[1])
+            return fail(DCOR_ENOMEM, "rstream: cell %d's sample.int ran past its word buffer", i0 + i);
+      }
+      e = launch_rs_materialise(dcells.as<RsCell>(), nb, rcc, nullptr, mix_lds);
       if (e) return hip_fail((hipError_t)e, "rstream materialise launch");
       for (int i = 0; i < nb; ++i)
         if (int st = rs_estimate(cells[i0 + i], hc[(size_t)i], rcc,
@@ -1320,7 +1352,8 @@ int dcor_rstream_draws(const dcor_cell* cell, int64_t reps, const dcor_rs_draws*
   HIPCHK(hipMemcpy(dst.p, &hs, sizeof(hs), hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(dcell.p, &p.c, sizeof(RsCell), hipMemcpyHostToDevice));
   int e = launch_rs_stream(dcell.as<RsCell>(), 1, rc, nullptr);
-  if (!e) e = launch_rs_materialise(dcell.as<RsCell>(), 1, rc, nullptr);
+  if (!e) e = launch_rs_materialise(dcell.as<RsCell>(), 1, rc, nullptr,
+                                    p.c.shuffle ? rs_mix_lds_bytes(p.c.n) : 0);
   if (e) return hip_fail((hipError_t)e, "rstream launch");
   const RsCell& c = p.c;
   const size_t R = (size_t)reps, n = (size_t)c.n, k = (size_t)c.k, ns = (size_t)c.nsim;
@@ -1357,6 +1390,7 @@ int dcor_rstream_words(int32_t seed, int64_t count, uint32_t* h_out) {
   RsState hs;
   rs_seed(seed, hs);
   c.st = dst.as<RsState>(); c.words = words.as<uint32_t>();
+  c.words_cap = count + 2 * 624 + 64;
   c.rep_off = idx.as<int64_t>(); c.exp_end = idx.as<int64_t>() + 1;
   HIPCHK(hipMemcpy(dst.p, &hs, sizeof(hs), hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(dcell.p, &c, sizeof(RsCell), hipMemcpyHostToDevice));
@@ -1415,6 +1449,7 @@ int dcor_rstream_hrs_draws(int64_t n, int64_t k, int64_t m, int64_t nsim, int64_
         c.n = n; c.k = 0; c.nsim = nsim; c.family = RS_FAMILY_HRS_INT; c.has_mix = 1;
         c.pre = pre;
         c.words = (uint32_t*)base; base += words_b;
+        c.words_cap = rep_max + 2 * 624 + 64;
         c.rep_off = (int64_t*)base; base += al256(8);
         c.exp_end = (int64_t*)base; base += al256(8);
         c.expv = (double*)base; base += al256((size_t)nsim * 8);

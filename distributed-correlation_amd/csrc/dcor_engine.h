@@ -176,6 +176,16 @@ struct RsCell {
   double* lap_local;           // [rc][n] (sub-G)
   double* lap_scalar;          // [rc] Z (sign) / central (sub-G)
   double *mix_z, *mix_l;       // [rc][nsim]
+  // gen_mix_gaussian (ver-cor-subG.R:113-136): `pre_a` words of labels + normals, then
+  // sample.int(n) (variable, `shuffle` = 1), then the rest of `pre`
+  int64_t pre_a;
+  int32_t shuffle, lab_on, lab_inv, lab_const;
+  double lab_q;                // rbinom(1, pi_mix): ix = (u >= lab_q)
+  double mA0[4], mA1[4], mmu0[2], mmu1[2];
+  int64_t* shuf_end;           // [rc] first word after each replicate's sample.int
+  int32_t* shuf;               // [rc][n] the shuffled row order (0-based)
+  int64_t words_cap;           // capacity of `words`; the walker stops (RsState.pad[1] = 1)
+                               // rather than overrun it
 };
 // RsCell.family for the HRS INT runs: rLap(n), rLap(1), mixquant (real-data-sims.R:375-402)
 #define RS_FAMILY_HRS_INT 2
@@ -185,6 +195,10 @@ int launch_rs_stream(RsCell* d_cells, int ncells, int32_t rc, void* stream);
 size_t rs_hrs_ni_lds_bytes(int64_t n);
 int launch_rs_hrs_ni(const int32_t* d_seeds, int64_t runs, int64_t n, int64_t km, int64_t k,
                      int32_t* perm, double* lx, double* ly, void* stream);
-int launch_rs_materialise(const RsCell* d_cells, int ncells, int32_t rc, void* stream);
+// lds: dynamic LDS for gen_mix_gaussian cells (rs_mix_lds_bytes(max n)), else 0
+int launch_rs_materialise(const RsCell* d_cells, int ncells, int32_t rc, void* stream,
+                          size_t lds = 0);
+size_t rs_mix_lds_bytes(int64_t n);
+#define RS_MIX_NMAX 65536
 
 }  // namespace dcor

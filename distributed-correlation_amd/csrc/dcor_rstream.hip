@@ -230,8 +230,12 @@ __global__ __launch_bounds__(64) void k_rs_stream(RsCell* cells, int32_t rc) {
   // every field in registers: the kernel's stores could alias the descriptor, and a reload
   // from global memory inside the walk costs an L2 round trip per draw
   const RsCell& cg = cells[blockIdx.x];
-  const int64_t c_pre = cg.pre, c_nsim = cg.nsim;
-  const int c_has_mix = cg.has_mix;
+  const int64_t c_pre = cg.pre, c_nsim = cg.nsim, c_n = cg.n;
+  const int c_has_mix = cg.has_mix, c_shuffle = cg.shuffle;
+  const int64_t c_pre_a = c_shuffle ? cg.pre_a : cg.pre;  // fixed words before sample.int
+  const int64_t c_cap = cg.words_cap;
+  int ovf = 0;
+  RS_G int64_t* const shuf_end = (RS_G int64_t*)cg.shuf_end;
   // global (not flat) stores: a flat store also counts in lgkmcnt, so every LDS wait behind
   // it would wait for the store to reach memory
   RS_G int64_t* const rep_off = (RS_G int64_t*)cg.rep_off;
@@ -271,32 +275,75 @@ __global__ __launch_bounds__(64) void k_rs_stream(RsCell* cells, int32_t rc) {
   };
   constexpr double q[16] = RS_Q_TABLE;
   int32_t r = 0;
-  int phase = 0;                          // 0: fixed words before exp_rand, 1: exp, 2: rbinom
-  int64_t left = c_pre, j = 0;
+  // 0: fixed words before sample.int (gen_mix_gaussian) or before exp_rand; 3: sample.int(n);
+  // 4: fixed words after it; 1: exp_rand; 2: mixquant's rbinom
+  int phase = 0;
+  int64_t left = c_pre_a, j = 0, sdn = 0;
   if (lane == 0) rep_off[0] = 0;
   while (r < rc) {
     // the walk is uniform; say so, or the structurizer keeps it in vector registers under
     // exec masks
-    P = rs_u64(P); Q = rs_u64(Q); j = rs_u64(j); left = rs_u64(left);
+    P = rs_u64(P); Q = rs_u64(Q); j = rs_u64(j); left = rs_u64(left); sdn = rs_u64(sdn);
     r = rs_u(r); phase = rs_u(phase); par = rs_u(par); pslot = rs_u(pslot);
+    if (phase == 3) {
+      // sample.int(n): R_unif_index(dn) for dn = n .. 1, rbits(ceil(log2 dn)) until < dn.  Only
+      // the consumption matters here (k_rs_materialise replays the swaps); a window of words
+      // is classified lane-parallel (v < dn - W accepts, v >= dn rejects whatever came
+      // before), anything else goes attempt by attempt.
+      if (P == Q) { if (Q + RS_N > c_cap) { ovf = 1; break; } next_block(); continue; }
+      const int bits = (sdn <= 1) ? 0 : 64 - __builtin_clzll((unsigned long long)(sdn - 1));
+      const int W = (Q - P < 64) ? (int)(Q - P) : 64;
+      const int bits_lo = (sdn - W <= 1) ? 0 : 64 - __builtin_clzll((unsigned long long)(sdn - W - 1));
+      if (bits > 15 || bits != bits_lo || sdn <= 64) {
+        const int nw = bits / 16 + 1;
+        if (P + nw > Q) { if (Q + RS_N > c_cap) { ovf = 1; break; } next_block(); continue; }
+        uint64_t v = 0;
+        for (int t = 0; t < nw; ++t) v = 65536ull * v + (ring[rs_wrap(pslot + t)] >> 16);
+        v &= (bits >= 63) ? ~0ull : ((1ull << bits) - 1ull);
+        P += nw;
+        pslot = rs_wrap(pslot + nw);
+        if ((int64_t)v < sdn) --sdn;
+      } else {
+        const uint32_t mask = (1u << bits) - 1u;
+        const bool in = lane < W;
+        const int64_t v = in ? (int64_t)((ring[rs_wrap(pslot + lane)] >> 16) & mask) : 0;
+        const bool sure_acc = in && v < sdn - W, sure_rej = in && v >= sdn;
+        if (__ballot(in && !sure_acc && !sure_rej)) {
+          for (int l = 0; l < W; ++l)
+            if ((int64_t)(uint32_t)rs_rl((int)v, l) < sdn) --sdn;
+        } else {
+          sdn -= __builtin_popcountll(__ballot(sure_acc));
+        }
+        P += W;
+        pslot = rs_wrap(pslot + W);
+      }
+      if (sdn == 0) {
+        if (lane == 0) shuf_end[r] = P;
+        phase = 4;
+        left = c_pre - c_pre_a;
+      }
+      continue;
+    }
     if (phase != 1) {
-      if (P == Q) { next_block(); continue; }
+      if (P == Q) { if (Q + RS_N > c_cap) { ovf = 1; break; } next_block(); continue; }
       const int64_t take = (left < Q - P) ? left : Q - P;
       P += take;
       pslot = (int)((pslot + take % (2 * RS_N)) % (2 * RS_N));
       left -= take;
       if (left == 0) {
-        if (phase == 0 && c_has_mix) {
+        if (phase == 0 && c_shuffle) {
+          phase = 3; sdn = c_n;
+        } else if ((phase == 0 || phase == 4) && c_has_mix) {
           phase = 1; j = 0;
         } else {
           ++r;
           if (r < rc && lane == 0) rep_off[r] = P;
-          phase = 0; left = c_pre;
+          phase = 0; left = c_pre_a;
         }
       }
       continue;
     }
-    if (P + RS_EXP_MAXW > Q) { next_block(); continue; }
+    if (P + RS_EXP_MAXW > Q) { if (Q + RS_N > c_cap) { ovf = 1; break; } next_block(); continue; }
     // Window of 64 words at P.  Lane l evaluates "an exp_rand draw starting at P + l": R's
     // doubling loop and the draw's length (1, or 2 + the index i where u <= q[i]) depend on
     // that one word only.  The chain of draw starts is then a scalar walk over a ballot of
@@ -368,6 +415,10 @@ __global__ __launch_bounds__(64) void k_rs_stream(RsCell* cells, int32_t rc) {
       phase = 2; left = c_nsim;
     }
   }
+  if (ovf) {                               // word buffer exhausted (sample.int's rejection
+    if (lane == 0) st->pad[1] = 1;        // sampling ran far past its bound): flag, stop
+    return;
+  }
   // .Random.seed at the consumption point P: in the newest block, just past it, or (after an
   // exp_rand look-ahead) in the previous block, whose raw state is the untempered ring half
   const int64_t o = P + mti0;              // words since the start of the chunk's first block
@@ -386,6 +437,76 @@ __global__ __launch_bounds__(64) void k_rs_stream(RsCell* cells, int32_t rc) {
 }
 
 // -------------------------------------------------------- k_rs_materialise ---
+// sample.int(n) (do_sample's partial Fisher-Yates, R_unif_index rejection) replayed by ONE wave
+// from the words at ws: y[i] = the i-th sampled index (0-based).  x[n] (LDS, = identity on
+// entry) and mark[(n+31)/32] (LDS, zero on entry) are scratch.  Windows of 64 words are
+// classified lane-parallel; the accepted draws' swaps run in parallel unless the bitmap finds
+// two equal indices or an index on one of the window's tail slots.  Returns the words used.
+__device__ int64_t rs_shuffle_wave(const uint32_t* __restrict__ ws, int64_t n, uint16_t* x,
+                                   uint32_t* mark, int32_t* __restrict__ y, int lane) {
+  int64_t p = 0, i = 0, dn = n;
+  auto swap_one = [&](int64_t v) {
+    if (lane == 0) {
+      y[i] = (int32_t)x[v];
+      x[v] = x[dn - 1];
+    }
+    ++i;
+    --dn;
+  };
+  while (i < n) {
+    i = rs_u64(i); dn = rs_u64(dn); p = rs_u64(p);
+    const int bits = (dn <= 1) ? 0 : 64 - __builtin_clzll((unsigned long long)(dn - 1));
+    const int bits_lo = (dn - 64 <= 1) ? 0 : 64 - __builtin_clzll((unsigned long long)(dn - 65));
+    if (bits > 15 || bits != bits_lo || dn <= 64) {
+      const uint64_t mask = (bits >= 63) ? ~0ull : ((1ull << bits) - 1ull);
+      uint64_t v;
+      do {
+        v = 0;
+        for (int nn = 0; nn <= bits; nn += 16) v = 65536ull * v + (ws[p++] >> 16);
+        v &= mask;
+      } while ((int64_t)v >= dn);
+      swap_one((int64_t)v);
+      continue;
+    }
+    const uint32_t mask = (1u << bits) - 1u;
+    const int64_t v = (int64_t)((ws[p + lane] >> 16) & mask);
+    const bool sure_acc = v < dn - 64, sure_rej = v >= dn;
+    p += 64;
+    if (__ballot(!sure_acc && !sure_rej)) {
+      for (int l = 0; l < 64; ++l) {
+        const int64_t vl = (int64_t)(uint32_t)rs_rl((int)v, l);
+        if (vl < dn) swap_one(vl);
+      }
+      continue;
+    }
+    const uint64_t A = __ballot(sure_acc);
+    const int B = __builtin_popcountll(A);
+    const bool acc = sure_acc;
+    const int t = __builtin_popcountll(A & ((1ull << lane) - 1ull));
+    const int64_t Lt = dn - 1 - t;
+    bool clash = false;
+    if (acc) clash = (atomicOr(&mark[v >> 5], 1u << (v & 31)) >> (v & 31)) & 1u;
+    if (acc && Lt != v) clash |= (mark[Lt >> 5] >> (Lt & 31)) & 1u;
+    const bool serial = __ballot(clash) != 0ull;
+    if (acc) atomicAnd(&mark[v >> 5], ~(1u << (v & 31)));
+    if (!serial) {
+      uint16_t a = 0, b = 0;
+      if (acc) { a = x[v]; b = x[Lt]; }
+      if (acc) { y[i + t] = (int32_t)a; x[v] = b; }
+      i += B;
+      dn -= B;
+    } else {
+      for (uint64_t rest = A; rest; rest &= rest - 1ull)
+        swap_one((int64_t)(uint32_t)rs_rl((int)v, __builtin_ctzll(rest)));
+    }
+  }
+  return p;
+}
+
+size_t rs_mix_lds_bytes(int64_t n) {
+  return (size_t)((n + 1) & ~1ll) * 2 + (size_t)((n + 31) / 32) * 4 + 16;
+}
+
 __global__ __launch_bounds__(256) void k_rs_materialise(const RsCell* cells, int32_t rc) {
   const RsCell c = cells[blockIdx.x / rc];  // by value: the stores below cannot alias it
   const int64_t r = blockIdx.x % rc;
@@ -409,7 +530,55 @@ __global__ __launch_bounds__(256) void k_rs_materialise(const RsCell* cells, int
   double* X = c.X + r * n;
   double* Y = c.Y + r * n;
   // 1. DGP
-  if (c.dgp == DCOR_DGP_GAUSSIAN) {
+  int64_t o = c.dgp_words;
+  if (c.dgp == DCOR_DGP_MIX_GAUSSIAN) {
+    // gen_mix_gaussian (ver-cor-subG.R:113-136): labels <- rbinom(n, 1, pi_mix); rows of
+    // rbind(mvrnorm(n0, mu0, S0), mvrnorm(n1, mu1, S1)) in sample.int(n) order; clip to [-1, 1]
+    extern __shared__ uint32_t rs_msm[];
+    __shared__ unsigned long long n0s;
+    uint16_t* xs = reinterpret_cast<uint16_t*>(rs_msm);
+    uint32_t* mark = rs_msm + ((n + 1) & ~1ll) / 2;
+    if (tid == 0) n0s = 0;
+    for (int64_t i = tid; i < n; i += 256) xs[i] = (uint16_t)i;
+    for (int64_t i = tid; i < (n + 31) / 32; i += 256) mark[i] = 0u;
+    __syncthreads();
+    unsigned long long z0 = 0;
+    for (int64_t i = tid; i < n; i += 256) {
+      const uint32_t lab = c.lab_on ? (((rs_unif(w[i]) < c.lab_q) ? 0u : 1u) ^ (uint32_t)c.lab_inv)
+                                    : (uint32_t)c.lab_const;
+      z0 += (lab == 0);
+    }
+    atomicAdd(&n0s, z0);
+    int32_t* y = c.shuf + r * n;
+    const int64_t nlab = c.lab_on ? n : 0;
+    __syncthreads();
+    if (tid < 64) rs_shuffle_wave(w + nlab + 4 * n, n, xs, mark, y, tid);
+    __syncthreads();
+    __threadfence_block();
+    const int64_t n0 = n0s, n1 = n - n0;
+    const uint32_t* wz = w + nlab;      // normals: 2 n0 (component 0) then 2 n1 (component 1)
+    for (int64_t i = tid; i < n; i += 256) {
+      const int64_t src = y[i];
+      double z1, z2, xv, yv;
+      if (src < n0) {
+        z1 = rs_norm(wz[2 * src], wz[2 * src + 1]);
+        z2 = rs_norm(wz[2 * (n0 + src)], wz[2 * (n0 + src) + 1]);
+        xv = c.mmu0[0] + ((0.0 + z1 * c.mA0[0]) + z2 * c.mA0[1]);
+        yv = c.mmu0[1] + ((0.0 + z1 * c.mA0[2]) + z2 * c.mA0[3]);
+      } else {
+        const int64_t t = src - n0, b = 2 * n0;
+        z1 = rs_norm(wz[2 * (b + t)], wz[2 * (b + t) + 1]);
+        z2 = rs_norm(wz[2 * (b + n1 + t)], wz[2 * (b + n1 + t) + 1]);
+        xv = c.mmu1[0] + ((0.0 + z1 * c.mA1[0]) + z2 * c.mA1[1]);
+        yv = c.mmu1[1] + ((0.0 + z1 * c.mA1[2]) + z2 * c.mA1[3]);
+      }
+      xv = (xv > 1.0) ? 1.0 : xv; xv = (xv < -1.0) ? -1.0 : xv;   // pmax(pmin(out, 1), -1)
+      yv = (yv > 1.0) ? 1.0 : yv; yv = (yv < -1.0) ? -1.0 : yv;
+      X[i] = xv;
+      Y[i] = yv;
+    }
+    o = c.shuf_end[r] - c.rep_off[r];
+  } else if (c.dgp == DCOR_DGP_GAUSSIAN) {
     // matrix(rnorm(2n), n): column 1 = draws 0..n-1, column 2 = draws n..2n-1;
     // mu + (V diag(sqrt(ev))) %*% t(Z) in dgemm's order
     for (int64_t i = tid; i < n; i += 256) {
@@ -435,7 +604,6 @@ __global__ __launch_bounds__(256) void k_rs_materialise(const RsCell* cells, int
       Y[i] = U + E2;
     }
   }
-  int64_t o = c.dgp_words;
   double* lx = c.lap_x + r * k;
   double* ly = c.lap_y + r * k;
   if (c.family == DCOR_FAMILY_SIGN) {
@@ -658,8 +826,17 @@ int launch_rs_stream(RsCell* d_cells, int ncells, int32_t rc, void* stream) {
   return (int)hipGetLastError();
 }
 
-int launch_rs_materialise(const RsCell* d_cells, int ncells, int32_t rc, void* stream) {
-  hipLaunchKernelGGL(k_rs_materialise, dim3((unsigned)(ncells * rc)), dim3(256), 0,
+int launch_rs_materialise(const RsCell* d_cells, int ncells, int32_t rc, void* stream, size_t lds) {
+  if (lds > 64 * 1024) {
+    static bool attr = false;
+    if (!attr) {
+      const hipError_t e = hipFuncSetAttribute((const void*)k_rs_materialise,
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
+      if (e != hipSuccess) return (int)e;
+      attr = true;
+    }
+  }
+  hipLaunchKernelGGL(k_rs_materialise, dim3((unsigned)(ncells * rc)), dim3(256), lds,
                      (hipStream_t)stream, d_cells, rc);
   return (int)hipGetLastError();
 }

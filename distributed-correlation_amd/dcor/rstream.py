@@ -21,7 +21,7 @@ from ._lib import lib
 from .api import batch_geometry
 from .sim import CellSpec, detail_frame, finalize
 
-R_DGPS = ("gaussian", "bernoulli", "bounded_factor")
+R_DGPS = ("gaussian", "bernoulli", "bounded_factor", "mix_gaussian")
 
 
 def run_grid(cells, B: int, detail: bool = True) -> list:

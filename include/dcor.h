@@ -142,8 +142,8 @@ int dcor_grid_run(const dcor_cell* cells, int ncells, int64_t B, dcor_accum* h_a
  * SURVEY.md Appendix A): mvrnorm / gen_bernoulli / gen_bounded_factor, priv_standardize and
  * batch Laplace (extraDistr::rlaplace), rbinom flips, mixquant's rnorm / rexp / rbinom.
  * Replicate b of a cell therefore equals the reference's replicate b for that seed, up to
- * libm rounding of log.  seed must fit set.seed's 32-bit integer; DGPs:
- * Gaussian, Bernoulli, bounded factor.  Synchronous, host buffers, like dcor_grid_run. */
+ * libm rounding of log.  seed must fit set.seed's 32-bit integer; every DGP
+ * (gen_mix_gaussian: n <= 65536).  Synchronous, host buffers, like dcor_grid_run. */
 int dcor_rstream_grid_run(const dcor_cell* cells, int ncells, int64_t B, dcor_accum* h_acc,
                           dcor_rep_out* h_detail);
 /* The explicit inputs R-stream replicates 0 .. reps-1 of one cell consume (HOST buffers,

@@ -416,8 +416,43 @@ int orc_rs_draw_rep(orc_rs_state* st, const void* cellp, orc_rs_draws* d) {
     for (int64_t i = 0; i < n; ++i) d->X[i] = U[i] + orc_rs_runif(st, -cE, cE);
     for (int64_t i = 0; i < n; ++i) d->Y[i] = U[i] + orc_rs_runif(st, -cE, cE);
     free(U);
+  } else if (c->dgp == DCOR_DGP_MIX_GAUSSIAN) {
+    /* gen_mix_gaussian (ver-cor-subG.R:113-136): labels <- rbinom(n, 1, pi_mix);
+     * rbind(mvrnorm(n0, mu0, S0), mvrnorm(n1, mu1, S1))[sample.int(n), ], clipped to [-1, 1] */
+    uint8_t* lab = (uint8_t*)malloc((size_t)n);
+    int64_t n0 = 0;
+    for (int64_t i = 0; i < n; ++i) {
+      lab[i] = (uint8_t)orc_rs_rbinom1(st, c->mix_pi);
+      n0 += (lab[i] == 0);
+    }
+    const int64_t n1 = n - n0;
+    double A0[4], A1[4];
+    orc_rs_mvrnorm_factor(c->mix_sigma0, c->rho, A0);
+    orc_rs_mvrnorm_factor(c->mix_sigma1, c->rho, A1);
+    double* z = (double*)malloc(sizeof(double) * (size_t)(2 * n + 1));
+    for (int64_t i = 0; i < 2 * n; ++i) z[i] = orc_rs_norm(st);  /* 2 n0 then 2 n1 normals */
+    double* rx = (double*)malloc(sizeof(double) * (size_t)(n + 1));
+    double* ry = (double*)malloc(sizeof(double) * (size_t)(n + 1));
+    for (int64_t r = 0; r < n0; ++r) {
+      rx[r] = c->mix_mu0[0] + ((0.0 + z[r] * A0[0]) + z[n0 + r] * A0[1]);
+      ry[r] = c->mix_mu0[1] + ((0.0 + z[r] * A0[2]) + z[n0 + r] * A0[3]);
+    }
+    const double* z1 = z + 2 * n0;
+    for (int64_t r = 0; r < n1; ++r) {
+      rx[n0 + r] = c->mix_mu1[0] + ((0.0 + z1[r] * A1[0]) + z1[n1 + r] * A1[1]);
+      ry[n0 + r] = c->mix_mu1[1] + ((0.0 + z1[r] * A1[2]) + z1[n1 + r] * A1[3]);
+    }
+    int32_t* perm = (int32_t*)malloc(sizeof(int32_t) * (size_t)n);
+    orc_rs_sample_int(st, n, n, perm);
+    for (int64_t i = 0; i < n; ++i) {     /* pmax(pmin(out, 1), -1) */
+      double x = rx[perm[i]], y = ry[perm[i]];
+      x = (x > 1.0) ? 1.0 : x; x = (x < -1.0) ? -1.0 : x;
+      y = (y > 1.0) ? 1.0 : y; y = (y < -1.0) ? -1.0 : y;
+      d->X[i] = x; d->Y[i] = y;
+    }
+    free(lab); free(z); free(rx); free(ry); free(perm);
   } else {
-    return DCOR_EINVAL; /* gen_mix_gaussian: not in the R-stream mode */
+    return DCOR_EINVAL;
   }
   d->has_mix = mix;
   d->k = k;

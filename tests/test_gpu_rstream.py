@@ -44,6 +44,11 @@ CELLS = {
     "subG-bounded-rho0": dict(family="subG", dgp="bounded_factor", rho=0.0, n=512, mu=(0, 0), sigma=(1, 1)),
     "subG-gauss": dict(family="subG", dgp="gaussian", rho=0.8, n=2048, mu=(0, 0), sigma=(1, 1),
                        eps1=0.2, eps2=0.2, seed=1_000_300),
+    "subG-mix": dict(family="subG", dgp="mix_gaussian", rho=0.5, n=3001, mu=(0, 0), sigma=(1, 1),
+                     seed=1_000_400),
+    "sign-mix-pi.3": dict(dgp="mix_gaussian", rho=-0.4, n=2000, pi_mix=0.3, seed=1_000_401),
+    "subG-mix-pi1": dict(family="subG", dgp="mix_gaussian", rho=0.2, n=700, pi_mix=1.0, seed=1_000_402),
+    "subG-mix-40000": dict(family="subG", dgp="mix_gaussian", rho=0.3, n=40000, seed=1_000_403),
 }
 
 
@@ -149,7 +154,7 @@ def test_headline_cell_full_size(dc, orc):
 
 
 @pytest.mark.parametrize("kw,status", [(dict(n=5, eps1=0.2, eps2=0.2), 2),          # k < 1 (stopifnot)
-                                       (dict(dgp="mix_gaussian"), 1),                 # not replayed
+                                       (dict(dgp="mix_gaussian", n=70000), 1),        # LDS bound
                                        (dict(seed=2 ** 31), 1)])                      # set.seed range
 def test_rstream_rejects_like_the_reference(dc, kw, status):
     from dcor import _lib
