@@ -6,14 +6,18 @@
 // that contract and puts the parallelism where R's stream allows it:
 //   k_rs_stream       one wave per grid cell: MT19937 blocks of 624 words (the recurrence
 //                     is wave-parallel: every dependency is >= 227 words back), tempered
-//                     words streamed to HBM, and the only data-dependent consumption --
-//                     exp_rand inside mixquant -- walked in order, so every replicate's
-//                     offset in the stream is known.  The MT state is persistent across
-//                     chunks of replicates (.Random.seed semantics).
+//                     words streamed to HBM, and the data-dependent consumption --
+//                     exp_rand inside mixquant, sample.int's rejection in gen_mix_gaussian --
+//                     walked in order, so every replicate's offset in the stream is known.
+//                     The MT state is persistent across chunks of replicates
+//                     (.Random.seed semantics).
 //   k_rs_materialise  one workgroup per (cell, replicate): words -> R's variates (inversion
 //                     rnorm with AS241 qnorm, mvrnorm's eigen factor, runif, rbinom,
-//                     extraDistr rlaplace), written in the explicit-input layout.
+//                     extraDistr rlaplace, the sample.int row shuffle), written in the
+//                     explicit-input layout.
 //   then the pre-materialised estimator kernels (dcor_premat.hip) per cell.
+//   k_rs_hrs_ni       the HRS NI runs (real-data-sims.R): sample.int(n, k*m) and rLap(k) x2
+//                     after each run's own set.seed.
 // Every transform uses IEEE basic operations, explicit fma and R's operation order
 // (-ffp-contract=off); log is the accurate double-double rs_log (csrc/dcor_tables.h), so the
 // GPU matches the CPU restatement oracle/dcor_rstream.c bit for bit.
@@ -346,9 +350,8 @@ __global__ __launch_bounds__(64) void k_rs_stream(RsCell* cells, int32_t rc) {
     if (P + RS_EXP_MAXW > Q) { if (Q + RS_N > c_cap) { ovf = 1; break; } next_block(); continue; }
     // Window of 64 words at P.  Lane l evaluates "an exp_rand draw starting at P + l": R's
     // doubling loop and the draw's length (1, or 2 + the index i where u <= q[i]) depend on
-    // that one word only.  The chain of draw starts is then a scalar walk over a ballot of
-    // the one-word draws (a run of them is one count-trailing-zeros), visiting only the long
-    // draws one by one; finally every start lane computes and stores its own value.
+    // that one word only.  The chain of draw starts from P follows by pointer doubling over
+    // the lengths; finally every start lane computes and stores its own value.
     const int64_t pos = P + lane;
     double a = 0., eu = 0.;
     int len = 1;
