@@ -1,0 +1,68 @@
+"""Randomised GPU-vs-oracle sweep over the cell space (both families, every DGP, both RNG
+modes): small and ragged n, rho at and near +-1, eps from 0.1 to 5, normalise on/off, every
+ci_mode.  Bar as elsewhere: 1e-12 relative (1e-13 absolute floor); a status the oracle
+returns (k < 1) must be the status the engine returns."""
+import numpy as np
+import pytest
+
+from helpers import close
+
+pytestmark = pytest.mark.gpu
+
+DGPS = ("gaussian", "bernoulli", "bounded_factor", "mix_gaussian")
+
+
+def _cells(seed, count):
+    from dcor import CellSpec
+    g = np.random.default_rng(seed)
+    out = []
+    for i in range(count):
+        fam = "sign" if g.random() < 0.5 else "subG"
+        dgp = DGPS[g.integers(0, 4)]
+        rho = float(g.choice([-1.0, -0.999, 1.0, 0.0, g.uniform(-1, 1)]))
+        if dgp == "bounded_factor":
+            rho = abs(rho)
+        n = int(g.choice([2, 3, 7, 31, 64, 65, 100, 257, 1000, 4099]))
+        e1, e2 = float(np.exp(g.uniform(np.log(0.1), np.log(5)))), float(np.exp(g.uniform(np.log(0.1), np.log(5))))
+        out.append(CellSpec(n=n, rho=rho, eps1=e1, eps2=e2, family=fam, dgp=dgp,
+                            mu=(float(g.normal()), float(g.normal())),
+                            sigma=(float(g.uniform(0.5, 3)), float(g.uniform(0.5, 3))),
+                            normalise=bool(g.random() < 0.8),
+                            ci_mode=str(g.choice(["auto", "normal", "laplace"])),
+                            seed=int(g.integers(1, 2 ** 31 - 1))))
+    return out
+
+
+def _agree(got, ref):
+    return close(got, ref, 1e-12, 1e-13)
+
+
+@pytest.mark.parametrize("block", range(4))
+def test_fused_engine_fuzz(block):
+    from dcor import _lib
+    from dcor.sim import simulate
+    from oracle import oracle as orc
+    for cell in _cells(100 + block, 12):
+        try:
+            ref = orc.sim_reps(cell.to_c(), 5, 8)
+        except RuntimeError as e:
+            with pytest.raises(_lib.DcorError):
+                simulate(cell, 3, 5).cpu()
+            continue
+        got = simulate(cell, 3, 5).cpu().numpy()
+        assert _agree(got, ref), (cell, got, ref)
+
+
+@pytest.mark.parametrize("block", range(4))
+def test_rstream_fuzz(block):
+    from dcor import _lib, rstream
+    from oracle import oracle as orc
+    for cell in _cells(200 + block, 10):
+        try:
+            ref = orc.rs_sim(cell.to_c(), 3)
+        except RuntimeError:
+            with pytest.raises(_lib.DcorError):
+                rstream.run_grid([cell], 3)
+            continue
+        got = rstream.run_grid([cell], 3)[0]["records"]
+        assert _agree(got, ref), (cell, got, ref)
