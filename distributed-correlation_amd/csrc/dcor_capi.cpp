@@ -712,7 +712,9 @@ static int premat_subg_run(const dcor_premat_subg* d, const dcor_panel* panel, d
   // decides; the packed L2-gather kernel is the fallback).
   const bool dict = p.perm && p.xy_stride == 0 && p.s.n <= DCOR_DICT_NMAX &&
                     premat_dict_lds_bytes(p.s.n) <= 150 * 1024 && panel == nullptr;
-  const size_t part_b = ((size_t)d->reps * 80 + 255) & ~(size_t)255;
+  // partials: 80 B per replicate slice (a prepared coded panel slices each replicate)
+  const int64_t pslots = (panel != nullptr && panel->coded) ? DCOR_DICT_SLICES : 1;
+  const size_t part_b = ((size_t)d->reps * 80 * pslots + 255) & ~(size_t)255;
   const size_t pack_b = pack ? (size_t)p.s.n * 32 : 0;
   const size_t codes_b = dict ? (((size_t)p.s.n * 2 + 255) & ~(size_t)255) : 0;
   const size_t dict_b = dict ? 2 * 256 * sizeof(double) + 256 : 0;
@@ -739,9 +741,11 @@ static int premat_subg_run(const dcor_premat_subg* d, const dcor_panel* panel, d
   }
   int rc = 0;
   const char* pv = std::getenv("DCOR_PREMAT_PIPELINE");
-  if (panel != nullptr && panel->coded && p.perm && d->reps >= 4096 && !(pv && std::strcmp(pv, "0") == 0)) {
-    // two replicate halves: the first half's (latency-bound) mixquant epilogue runs on the
-    // auxiliary stream beside the second half's (HBM-bound) streaming kernel
+  if (panel != nullptr && panel->coded && p.perm && d->reps >= 4096 && pv && std::strcmp(pv, "1") == 0) {
+    // DCOR_PREMAT_PIPELINE=1: two replicate halves, the first half's mixquant epilogue on the
+    // auxiliary stream beside the second half's streaming kernel.  Off by default: the
+    // streaming kernel already reads at ~5.8 TB/s, and the epilogue's workgroups beside it
+    // cost more than they hide (r01 A/B: 12.5e6 piped vs 13.0e6 serial replicates/s).
     Pipe* pp = nullptr;
     if (int st = pipe_get(&pp)) { (void)hipFreeAsync(part, (hipStream_t)stream); return st; }
     const int64_t half = d->reps / 2;
@@ -756,7 +760,7 @@ static int premat_subg_run(const dcor_premat_subg* d, const dcor_panel* panel, d
       q.lap_central = p.lap_central + r0;
       q.mix_z = p.mix_z + r0 * ns;
       q.mix_l = p.mix_l + r0 * ns;
-      rc = launch_premat_subg(q, nr, (char*)part + r0 * 80, d_out + r0, stream, h ? nullptr : pp->s,
+      rc = launch_premat_subg(q, nr, (char*)part + r0 * 80 * pslots, d_out + r0, stream, h ? nullptr : pp->s,
                               pp->fork);
     }
     if (!rc && hipEventRecord(pp->join, pp->s) != hipSuccess) rc = (int)hipGetLastError();

@@ -21,6 +21,40 @@ __device__ __forceinline__ int sgn_raw(double a, bool& bad) {
   return (a > 0) - (a < 0);
 }
 
+// mixquant over keys already in registers: zv[s], lv[s] = z[i], l[i] for i = tid + s*DCOR_BLOCK
+// (a caller can issue these loads before c is known).
+__device__ __forceinline__ double mixquant_regs(const MixConst& mx, double c,
+                                                const double (&zv)[SEL_VPT],
+                                                const double (&lv)[SEL_VPT], SelScratch* sc) {
+  if (threadIdx.x == 0) sc->nan_cnt = 0;
+  __syncthreads();
+  double val[SEL_VPT];
+  int nn = 0;
+#pragma unroll
+  for (int s = 0; s < SEL_VPT; ++s) {
+    const int i = threadIdx.x + s * DCOR_BLOCK;
+    val[s] = dnan();
+    if (i < mx.nsim) {
+      val[s] = zv[s] + c * lv[s];
+      nn += (val[s] != val[s]);
+    }
+  }
+  if (nn) atomicAdd(&sc->nan_cnt, nn);
+  __syncthreads();
+  return value_select(val, mx.pos, mx.nsim - sc->nan_cnt, sc);
+}
+
+__device__ __forceinline__ void mixquant_prefetch(const MixConst& mx, const double* z,
+                                                  const double* l, double (&zv)[SEL_VPT],
+                                                  double (&lv)[SEL_VPT]) {
+#pragma unroll
+  for (int s = 0; s < SEL_VPT; ++s) {
+    const int i = threadIdx.x + s * DCOR_BLOCK;
+    zv[s] = i < mx.nsim ? z[i] : 0.0;
+    lv[s] = i < mx.nsim ? l[i] : 0.0;
+  }
+}
+
 __device__ __forceinline__ double mixquant_loaded(const MixConst& mx, double c, const double* z,
                                                   const double* l, SelScratch* sc) {
   if (threadIdx.x == 0) sc->nan_cnt = 0;

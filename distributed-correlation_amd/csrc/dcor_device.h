@@ -268,7 +268,7 @@ __device__ __forceinline__ void block_sum(double (&v)[NV], double* scratch) {
   __syncthreads();
 }
 
-template <int NV>
+template <int NV, int NW = DCOR_WAVES>
 __device__ __forceinline__ void block_sum_dd(DD (&v)[NV], double* scratch) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
 #pragma unroll
@@ -276,17 +276,17 @@ __device__ __forceinline__ void block_sum_dd(DD (&v)[NV], double* scratch) {
   if (lane == 0) {
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
-      scratch[(2 * i) * DCOR_WAVES + wv] = v[i].hi;
-      scratch[(2 * i + 1) * DCOR_WAVES + wv] = v[i].lo;
+      scratch[(2 * i) * NW + wv] = v[i].hi;
+      scratch[(2 * i + 1) * NW + wv] = v[i].lo;
     }
   }
   __syncthreads();
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
-    DD s{scratch[(2 * i) * DCOR_WAVES], scratch[(2 * i + 1) * DCOR_WAVES]};
+    DD s{scratch[(2 * i) * NW], scratch[(2 * i + 1) * NW]};
 #pragma unroll
-    for (int w = 1; w < DCOR_WAVES; ++w)
-      s = dd_add(s, DD{scratch[(2 * i) * DCOR_WAVES + w], scratch[(2 * i + 1) * DCOR_WAVES + w]});
+    for (int w = 1; w < NW; ++w)
+      s = dd_add(s, DD{scratch[(2 * i) * NW + w], scratch[(2 * i + 1) * NW + w]});
     v[i] = s;
   }
   __syncthreads();

@@ -96,8 +96,15 @@ struct PrematSubgConst {
   // per launch (k_panel_dict).  dict_ok is set by the device: 1 -> the coded kernel runs,
   // 0 (more than 256 distinct values in a column, or a NaN) -> the L2-gather kernel runs.
   uint16_t* dict_codes; double* dict_vals; int* dict_ok;
+  // Coded-panel kernel only: each replicate's sums are split over `slices` work items (0 or 1:
+  // one), whose partials part[rep * slices + t] the epilogue merges in slice order.
+  int32_t slices, pad_;
 };
 #define DCOR_DICT_NMAX 65536
+// Slices per replicate in the prepared coded-panel kernel (partials: 80 B each).  1: measured
+// best -- 2 slices even out a persistent grid's last round but cost 25 % in per-item start-up
+// and reduction (r01 A/B: 590-605 us vs 735-760 us per 8192 replicates).
+#define DCOR_DICT_SLICES 1
 size_t premat_dict_lds_bytes(int64_t n);
 // codes: n u16 (16-B padded), dict: 512 doubles, ok: 1 int (device).
 int launch_panel_dict(const double* X, const double* Y, int64_t n, uint16_t* codes, double* dict,

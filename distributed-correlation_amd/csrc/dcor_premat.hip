@@ -351,6 +351,21 @@ __device__ __forceinline__ void premat_subg_finish(const PrematSubgConst& p, int
   }, threadIdx.x == 0, out);
 }
 
+// The five sums of replicate `rep`: its p.slices partials merged in slice order.
+__device__ __forceinline__ void load_partials(const PrematSubgConst& p,
+                                              const SubgPartial* __restrict__ part, int64_t rep,
+                                              DD (&d5)[5]) {
+  const int S = p.slices > 1 ? p.slices : 1;
+  const SubgPartial q = part[rep * S];
+#pragma unroll
+  for (int v = 0; v < 5; ++v) d5[v] = two_sum(q.s[2 * v], q.s[2 * v + 1]);
+  for (int t = 1; t < S; ++t) {
+    const SubgPartial r = part[rep * S + t];
+#pragma unroll
+    for (int v = 0; v < 5; ++v) d5[v] = dd_add(d5[v], DD{r.s[2 * v], r.s[2 * v + 1]});
+  }
+}
+
 // Wave-per-replicate epilogue (four replicates per workgroup, no workgroup barriers): the
 // mixquant keys z + c l are loaded VPL per lane and selected with wave_select.
 template <int VPL>
@@ -361,10 +376,8 @@ __global__ __launch_bounds__(DCOR_BLOCK) void k_premat_subg_epilogue_w(PrematSub
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int64_t rep = (int64_t)blockIdx.x * DCOR_WAVES + wv;
   if (rep >= reps) return;  // whole waves only
-  const SubgPartial q = part[rep];
   DD d5[5];
-#pragma unroll
-  for (int v = 0; v < 5; ++v) d5[v] = two_sum(q.s[2 * v], q.s[2 * v + 1]);
+  load_partials(p, part, rep, d5);
   const MixConst& mx = p.s.mix;
   const double* z = p.mix_z + rep * mx.nsim;
   const double* l = p.mix_l + rep * mx.nsim;
@@ -385,11 +398,13 @@ __global__ __launch_bounds__(DCOR_BLOCK) void k_premat_subg_epilogue(PrematSubgC
                                                                      dcor_rep_out* out) {
   __shared__ SelScratch sel;
   const int64_t rep = blockIdx.x;
-  const SubgPartial q = part[rep];
+  const MixConst& mx = p.s.mix;
+  double zv[SEL_VPT], lv[SEL_VPT];  // the mixquant draws do not depend on c*: load them first
+  mixquant_prefetch(mx, p.mix_z + rep * mx.nsim, p.mix_l + rep * mx.nsim, zv, lv);
   DD d5[5];
-#pragma unroll
-  for (int v = 0; v < 5; ++v) d5[v] = two_sum(q.s[2 * v], q.s[2 * v + 1]);
-  premat_subg_finish(p, rep, d5, &sel, out);
+  load_partials(p, part, rep, d5);
+  premat_subg_finish_q(p, rep, d5, [&](double cs) { return mixquant_regs(mx, cs, zv, lv, &sel); },
+                       threadIdx.x == 0, out);
 }
 
 // ------------------------------------------- dictionary-coded shared panel (HRS) ---
@@ -503,42 +518,60 @@ __global__ __launch_bounds__(DICT_THREADS) void k_panel_dict(const double* __res
   if (tid == 0) *ok = 1;
 }
 
-// Streaming kernel over the dictionary-coded panel: persistent workgroups (the coded panel is
-// loaded into LDS once per workgroup), replicates grid-strided.  Dynamic LDS layout: four
+// Streaming kernel over the dictionary-coded panel: persistent workgroups of DICT_NT threads
+// (the coded panel is loaded into LDS once per workgroup; 47 KB of LDS at n = 19,433 leaves
+// three workgroups = 24 waves per CU to keep HBM loads in flight), work items grid-strided.
+// A work item is one slice of one replicate: slice t of S takes the t-th share of the INT
+// sample pairs and of the NI batch pairs, and writes its five compensated sums to
+// part[rep * S + t]; the epilogue merges the S partials in slice order.  Slicing evens out the
+// last round of a persistent grid (replicate counts rarely divide by the workgroup count).  The noise /
+// permutation streams are read once, 16 B per lane, non-temporal.  Dynamic LDS layout: four
 // clipped dictionaries dX, dY (NI clips), dS, dO (INT sender / other clips), the reduction
 // scratch, then the n codes.
-__global__ __launch_bounds__(DCOR_BLOCK) void k_premat_subg_dict(PrematSubgConst p,
-                                                                 const uint16_t* __restrict__ codes_g,
-                                                                 const double* __restrict__ dict_g,
-                                                                 const int* __restrict__ dict_ok,
-                                                                 int64_t reps,
-                                                                 SubgPartial* __restrict__ part) {
+#define DICT_NT 512
+#define DICT_NW (DICT_NT / 64)
+typedef double dv2 __attribute__((ext_vector_type(2)));
+typedef int iv4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ int64_t share(int64_t total, int t, int S) { return total * t / S; }
+
+template <int DUNR, int WPE>  // 16-B loads in flight per thread; waves per SIMD
+__global__ __launch_bounds__(DICT_NT, WPE) void k_premat_subg_dict(PrematSubgConst p,
+                                                             const uint16_t* __restrict__ codes_g,
+                                                             const double* __restrict__ dict_g,
+                                                             const int* __restrict__ dict_ok,
+                                                             int64_t reps,
+                                                             SubgPartial* __restrict__ part) {
   extern __shared__ double dsm[];
   if (*dict_ok == 0) return;  // the L2-gather kernel owns this launch
   const SubgConst& c = p.s;
   const int tid = threadIdx.x;
+  const int S = p.slices > 1 ? p.slices : 1;
   double* dX = dsm;
   double* dY = dsm + DICT_MAX;
   double* dS = dsm + 2 * DICT_MAX;
   double* dO = dsm + 3 * DICT_MAX;
   double* red = dsm + 4 * DICT_MAX;
-  uint16_t* cod = reinterpret_cast<uint16_t*>(dsm + 4 * DICT_MAX + 16 * DCOR_WAVES);
-  {
-    const double x = dict_g[tid], y = dict_g[DICT_MAX + tid];  // DCOR_BLOCK == DICT_MAX
+  uint16_t* cod = reinterpret_cast<uint16_t*>(dsm + 4 * DICT_MAX + 20 * DICT_NW);
+  if (tid < DICT_MAX) {
+    const double x = dict_g[tid], y = dict_g[DICT_MAX + tid];
     dX[tid] = rclip(x, c.l1);                                   // real-data-sims.R:126-127
     dY[tid] = rclip(y, c.l2);
     const double sv = c.sender_is_X ? x : y, ov = c.sender_is_X ? y : x;
     dS[tid] = rclip(sv, c.ls);                                  // real-data-sims.R:222-227
     dO[tid] = p.hrs ? rclip(ov, p.lo_) : ov;
+  }
+  {
     const int64_t nv = (c.n * 2 + 15) / 16;                      // 16-B words of codes
     const uint4* src = reinterpret_cast<const uint4*>(codes_g);
     uint4* dst = reinterpret_cast<uint4*>(cod);
-    for (int64_t w = tid; w < nv; w += DCOR_BLOCK) dst[w] = src[w];
+    for (int64_t w = tid; w < nv; w += DICT_NT) dst[w] = src[w];
   }
   __syncthreads();
-#define DUNR 8  // loads in flight per thread: ~48 KB per CU at 3 workgroups / CU
-  const int64_t step = (int64_t)DCOR_BLOCK * DUNR;
-  for (int64_t rep = blockIdx.x; rep < reps; rep += gridDim.x) {
+  const int64_t items = reps * S;
+  for (int64_t it = blockIdx.x; it < items; it += gridDim.x) {
+    const int64_t rep = it / S;
+    const int t = (int)(it - rep * S);
     const double* __restrict__ lx = p.lap_ni_x + rep * c.k;
     const double* __restrict__ ly = p.lap_ni_y + rep * c.k;
     const double* __restrict__ ll = p.lap_local + rep * c.n;
@@ -549,19 +582,50 @@ __global__ __launch_bounds__(DCOR_BLOCK) void k_premat_subg_dict(PrematSubgConst
       ks_acc(sU, Uc);
       ks_acc(sU2, Uc * Uc);
     };
-    int64_t i = tid;
-    for (; i + (DUNR - 1) * DCOR_BLOCK < c.n; i += step) {
-      double l[DUNR];
+    // INT stream: sample pairs (h + 2q, h + 2q + 1); h = 1 when the replicate's noise row
+    // starts off a 16-B boundary (odd n).  Slice 0 takes the head sample, slice S-1 the tail.
+    {
+      const int64_t h = (reinterpret_cast<uintptr_t>(ll) & 15) ? 1 : 0;
+      const int64_t np = (c.n - h) >> 1;
+      const int64_t q0 = share(np, t, S), q1 = share(np, t + 1, S);
+      const dv2* l2 = reinterpret_cast<const dv2*>(ll + h);
+      int64_t q = q0 + tid;
+      for (; q + (DUNR - 1) * DICT_NT < q1; q += DUNR * DICT_NT) {
+        dv2 v[DUNR];
 #pragma unroll
-      for (int u = 0; u < DUNR; ++u) l[u] = ll[i + u * DCOR_BLOCK];
+        for (int u = 0; u < DUNR; ++u) v[u] = __builtin_nontemporal_load(l2 + q + u * DICT_NT);
 #pragma unroll
-      for (int u = 0; u < DUNR; ++u) uterm(cod[i + u * DCOR_BLOCK], l[u]);
+        for (int u = 0; u < DUNR; ++u) {
+          const int64_t i = h + 2 * (q + u * DICT_NT);
+          uterm(cod[i], v[u].x);
+          uterm(cod[i + 1], v[u].y);
+        }
+      }
+      for (; q < q1; q += DICT_NT) {
+        const dv2 v = __builtin_nontemporal_load(l2 + q);
+        const int64_t i = h + 2 * q;
+        uterm(cod[i], v.x);
+        uterm(cod[i + 1], v.y);
+      }
+      if (tid == 0 && t == 0 && h) uterm(cod[0], ll[0]);
+      if (tid == DICT_NT - 1 && t == S - 1 && h + 2 * np < c.n) uterm(cod[c.n - 1], ll[c.n - 1]);
     }
-    for (; i < c.n; i += DCOR_BLOCK) uterm(cod[i], ll[i]);
+    // workgroup sums: wave sums into a scratch half alternating per item (a wave can run at
+    // most one barrier ahead), then lane v < 5 folds sum v over the waves in wave order.  The
+    // INT sums are wave-reduced here, so they are not live across the NI loop.
+    double* rb = red + (((it - blockIdx.x) / gridDim.x) & 1) * (10 * DICT_NW);
+    auto wave_put = [&](int v, DD a) {
+      a = wave_sum_dd(a);
+      if ((tid & 63) == 0) {
+        rb[(2 * v) * DICT_NW + (tid >> 6)] = a.hi;
+        rb[(2 * v + 1) * DICT_NW + (tid >> 6)] = a.lo;
+      }
+    };
+    wave_put(3, sU);
+    wave_put(4, sU2);
     if (c.m == 2) {  // real-data-sims.R:131-137 with the exact two-value batch mean
-      int64_t j = tid;
-      auto pair = [&](int2 pr, double lxj, double lyj) {
-        const uint32_t a = cod[pr.x], b = cod[pr.y];
+      auto pair = [&](int a0, int b0, double lxj, double lyj) {
+        const uint32_t a = cod[a0], b = cod[b0];
         const double xt = (dX[a & 255u] + dX[b & 255u]) * 0.5 + c.bx * lxj;
         const double yt = (dY[a >> 8] + dY[b >> 8]) * 0.5 + c.by * lyj;
         ks_acc(sP, xt * yt);
@@ -569,22 +633,44 @@ __global__ __launch_bounds__(DCOR_BLOCK) void k_premat_subg_dict(PrematSubgConst
         ks_acc(sT, T);
         ks_acc(sT2, T * T);
       };
-      for (; j + (DUNR - 1) * DCOR_BLOCK < c.k; j += step) {
-        int2 pr[DUNR];
-        double ax[DUNR], ay[DUNR];
+      const bool al = ((reinterpret_cast<uintptr_t>(pm) | reinterpret_cast<uintptr_t>(lx) |
+                        reinterpret_cast<uintptr_t>(ly)) & 15) == 0;
+      if (al) {  // two batches per lane: int4 of indices, double2 of each noise row
+        const int64_t np = c.k >> 1;
+        const int64_t q0 = share(np, t, S), q1 = share(np, t + 1, S);
+        const iv4* p4 = reinterpret_cast<const iv4*>(pm);
+        const dv2* x2 = reinterpret_cast<const dv2*>(lx);
+        const dv2* y2 = reinterpret_cast<const dv2*>(ly);
+        int64_t q = q0 + tid;
+        for (; q + (DUNR / 2 - 1) * DICT_NT < q1; q += (DUNR / 2) * DICT_NT) {
+          iv4 pr[DUNR / 2];
+          dv2 ax[DUNR / 2], ay[DUNR / 2];
 #pragma unroll
-        for (int u = 0; u < DUNR; ++u) {
-          const int64_t jj = j + u * DCOR_BLOCK;
-          pr[u] = *reinterpret_cast<const int2*>(pm + 2 * jj);
-          ax[u] = lx[jj]; ay[u] = ly[jj];
+          for (int u = 0; u < DUNR / 2; ++u) {
+            pr[u] = __builtin_nontemporal_load(p4 + q + u * DICT_NT);
+            ax[u] = __builtin_nontemporal_load(x2 + q + u * DICT_NT);
+            ay[u] = __builtin_nontemporal_load(y2 + q + u * DICT_NT);
+          }
+#pragma unroll
+          for (int u = 0; u < DUNR / 2; ++u) {
+            pair(pr[u].x, pr[u].y, ax[u].x, ay[u].x);
+            pair(pr[u].z, pr[u].w, ax[u].y, ay[u].y);
+          }
         }
-#pragma unroll
-        for (int u = 0; u < DUNR; ++u) pair(pr[u], ax[u], ay[u]);
+        for (; q < q1; q += DICT_NT) {
+          const iv4 pr = __builtin_nontemporal_load(p4 + q);
+          const dv2 ax = __builtin_nontemporal_load(x2 + q), ay = __builtin_nontemporal_load(y2 + q);
+          pair(pr.x, pr.y, ax.x, ay.x);
+          pair(pr.z, pr.w, ax.y, ay.y);
+        }
+        if (tid == DICT_NT - 1 && t == S - 1 && (c.k & 1))
+          pair(pm[2 * (c.k - 1)], pm[2 * (c.k - 1) + 1], lx[c.k - 1], ly[c.k - 1]);
+      } else {
+        for (int64_t j = share(c.k, t, S) + tid; j < share(c.k, t + 1, S); j += DICT_NT)
+          pair(pm[2 * j], pm[2 * j + 1], lx[j], ly[j]);
       }
-      for (; j < c.k; j += DCOR_BLOCK)
-        pair(*reinterpret_cast<const int2*>(pm + 2 * j), lx[j], ly[j]);
     } else {
-      for (int64_t j = tid; j < c.k; j += DCOR_BLOCK) {
+      for (int64_t j = share(c.k, t, S) + tid; j < share(c.k, t + 1, S); j += DICT_NT) {
         DD bx{0, 0}, by{0, 0};
         for (int r = 0; r < c.m; ++r) {
           const uint32_t a = cod[pm[j * c.m + r]];
@@ -600,13 +686,17 @@ __global__ __launch_bounds__(DCOR_BLOCK) void k_premat_subg_dict(PrematSubgConst
         ks_acc(sT2, T * T);
       }
     }
-    DD d5[5] = {sP, sT, sT2, sU, sU2};
-    block_sum_dd<5>(d5, red);
-    if (tid == 0) {
-      SubgPartial q;
+    wave_put(0, sP);
+    wave_put(1, sT);
+    wave_put(2, sT2);
+    __syncthreads();
+    if (tid < 5) {
+      DD a{rb[(2 * tid) * DICT_NW], rb[(2 * tid + 1) * DICT_NW]};
 #pragma unroll
-      for (int v = 0; v < 5; ++v) { q.s[2 * v] = d5[v].hi; q.s[2 * v + 1] = d5[v].lo; }
-      part[rep] = q;
+      for (int w = 1; w < DICT_NW; ++w)
+        a = dd_add(a, DD{rb[(2 * tid) * DICT_NW + w], rb[(2 * tid + 1) * DICT_NW + w]});
+      part[it].s[2 * tid] = a.hi;
+      part[it].s[2 * tid + 1] = a.lo;
     }
   }
 }
@@ -830,37 +920,67 @@ int launch_panel_dict(const double* X, const double* Y, int64_t n, uint16_t* cod
 }
 
 size_t premat_dict_lds_bytes(int64_t n) {
-  return (size_t)(4 * DICT_MAX + 16 * DCOR_WAVES) * sizeof(double) + (size_t)((n * 2 + 15) / 16) * 16;
+  return (size_t)(4 * DICT_MAX + 20 * DICT_NW) * sizeof(double) + (size_t)((n * 2 + 15) / 16) * 16;
 }
 
-int launch_premat_subg(const PrematSubgConst& c, int64_t reps, void* part, dcor_rep_out* out,
+typedef void (*DictKernel)(PrematSubgConst, const uint16_t*, const double*, const int*, int64_t,
+                           SubgPartial*);
+// Coded-panel kernel variant: (16-B loads in flight per thread, waves per SIMD).  The kernel
+// reads at ~5.8 TB/s in every variant (r01 A/B: 590-605 us per 8192 replicates); the default
+// keeps two 512-thread workgroups per CU.  DCOR_DICT_VARIANT=1..3 selects the others for A/B.
+static DictKernel dict_kernel() {
+  static const DictKernel ks[4] = {k_premat_subg_dict<4, 4>, k_premat_subg_dict<4, 6>,
+                                   k_premat_subg_dict<8, 4>, k_premat_subg_dict<6, 6>};
+  static const int v = [] {
+    const char* e = std::getenv("DCOR_DICT_VARIANT");
+    const int x = e ? std::atoi(e) : 0;
+    return (x >= 0 && x < 4) ? x : 0;
+  }();
+  return ks[v];
+}
+
+// Workgroup slots of the coded-panel kernel (CUs x resident workgroups at this LDS size).
+static int premat_dict_slots(int64_t n, int* slots) {
+  const size_t lds = premat_dict_lds_bytes(n);
+  static bool attr_set = false;
+  if (!attr_set) {
+    if (hipFuncSetAttribute((const void*)dict_kernel(),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024) != hipSuccess)
+      return last_err();
+    attr_set = true;
+  }
+  int dev = 0, cus = 0, per_cu = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return last_err();
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    return last_err();
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, dict_kernel(), DICT_NT, lds) !=
+      hipSuccess)
+    return last_err();
+  *slots = cus * (per_cu < 1 ? 1 : per_cu);
+  return 0;
+}
+
+int launch_premat_subg(const PrematSubgConst& c0, int64_t reps, void* part, dcor_rep_out* out,
                        void* stream, void* epi_stream, void* ev) {
   if (reps <= 0) return 0;
+  PrematSubgConst c = c0;
+  c.slices = 1;
   if (c.dict_codes != nullptr) {
-    static_assert(DCOR_BLOCK == DICT_MAX, "dictionary fill assumes one entry per thread");
+    static_assert(DICT_NT >= DICT_MAX, "dictionary fill assumes one entry per thread");
     if (!c.dict_built)
       hipLaunchKernelGGL(k_panel_dict, dim3(1), dim3(DICT_THREADS), 0, (hipStream_t)stream, c.X,
                          c.Y, c.s.n, c.dict_codes, c.dict_vals, c.dict_ok);
-    const size_t lds = premat_dict_lds_bytes(c.s.n);
-    static bool attr_set = false;
-    if (!attr_set) {
-      if (hipFuncSetAttribute((const void*)k_premat_subg_dict,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024) != hipSuccess)
-        return last_err();
-      attr_set = true;
-    }
-    int dev = 0, cus = 0, per_cu = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return last_err();
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-      return last_err();
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_premat_subg_dict, DCOR_BLOCK, lds) !=
-        hipSuccess)
-      return last_err();
-    if (per_cu < 1) per_cu = 1;
-    const int64_t grid = reps < (int64_t)cus * per_cu ? reps : (int64_t)cus * per_cu;
-    hipLaunchKernelGGL(k_premat_subg_dict, dim3((unsigned)grid), dim3(DCOR_BLOCK), lds,
-                       (hipStream_t)stream, c, c.dict_codes, c.dict_vals, c.dict_ok, reps,
-                       (SubgPartial*)part);
+    int slots = 0;
+    if (int e = premat_dict_slots(c.s.n, &slots)) return e;
+    // a prepared coded panel: no L2-gather kernel shares the partials, so replicates are
+    // sliced.  The slice count is fixed (not sized to the launch), so a replicate's sums do
+    // not depend on how replicates are split over launches or GPUs.
+    if (c.dict_built == 2) c.slices = DCOR_DICT_SLICES;
+    const int64_t items = reps * c.slices;
+    const int64_t grid = items < (int64_t)slots ? items : (int64_t)slots;
+    hipLaunchKernelGGL(dict_kernel(), dim3((unsigned)grid), dim3(DICT_NT),
+                       premat_dict_lds_bytes(c.s.n), (hipStream_t)stream, c, c.dict_codes,
+                       c.dict_vals, c.dict_ok, reps, (SubgPartial*)part);
   }
   if (c.xyc != nullptr)
     hipLaunchKernelGGL(k_premat_xy_pack, dim3((unsigned)((c.s.n + DCOR_BLOCK - 1) / DCOR_BLOCK)),

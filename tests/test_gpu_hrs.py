@@ -86,12 +86,12 @@ def test_panel_pipelined_halves_bitexact(panel):
     from dcor import hrs
     z = panel
     args = (z["age_z"], z["bmi_z"], z["lambda_age_z"], z["lambda_bmi_z"], 2.0, 4100)
-    os.environ["DCOR_PREMAT_PIPELINE"] = "0"
+    serial = hrs.hrs_replicates(*args, chunk=4100)
+    os.environ["DCOR_PREMAT_PIPELINE"] = "1"
     try:
-        serial = hrs.hrs_replicates(*args, chunk=4100)
+        piped = hrs.hrs_replicates(*args, chunk=4100)
     finally:
         del os.environ["DCOR_PREMAT_PIPELINE"]
-    piped = hrs.hrs_replicates(*args, chunk=4100)
     np.testing.assert_array_equal(piped.view(np.int64), serial.view(np.int64))
     assert np.isfinite(piped).all()
 
