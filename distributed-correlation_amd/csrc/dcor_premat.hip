@@ -878,29 +878,40 @@ __device__ __forceinline__ uint32_t feistel_f(uint32_t r, uint32_t k, uint32_t m
   return t & mask;
 }
 
-__device__ __forceinline__ uint32_t feistel_perm(uint32_t x, uint32_t n, int a, int c,
-                                                 const U4& kk) {
+// One pass of the four rounds on (c + a)-bit x.
+__device__ __forceinline__ uint32_t feistel_pass(uint32_t x, int a, int c, const U4& kk) {
   const uint32_t ma = (1u << a) - 1u, mc = (1u << c) - 1u;
-  do {
-    uint32_t H = x >> a, L = x & ma;              // (c bits, a bits)
-    uint32_t t;
-    t = H ^ feistel_f(L, kk.w0, mc); H = L; L = t;  // (a, c)
-    t = H ^ feistel_f(L, kk.w1, ma); H = L; L = t;  // (c, a)
-    t = H ^ feistel_f(L, kk.w2, mc); H = L; L = t;  // (a, c)
-    t = H ^ feistel_f(L, kk.w3, ma); H = L; L = t;  // (c, a)
-    x = (H << a) | L;
-  } while (x >= n);
-  return x;
+  uint32_t H = x >> a, L = x & ma;              // (c bits, a bits)
+  uint32_t t;
+  t = H ^ feistel_f(L, kk.w0, mc); H = L; L = t;  // (a, c)
+  t = H ^ feistel_f(L, kk.w1, ma); H = L; L = t;  // (c, a)
+  t = H ^ feistel_f(L, kk.w2, mc); H = L; L = t;  // (a, c)
+  t = H ^ feistel_f(L, kk.w3, ma); H = L; L = t;  // (c, a)
+  return (H << a) | L;
 }
 
+// P_r(t) = the first of pass(t), pass(pass(t)), ... inside [0, n).  Each lane owns the strided
+// sequence t, t + stride, ... and applies one pass per loop trip, moving to its next t as soon
+// as the current one lands: lanes stay busy while their walks differ in length (a loop per t
+// would run every lane of a wave to the longest of its 64 walks, ~3.4x the mean for n just
+// above a power of two).  The launcher gives every lane about 16 values of t.
 __global__ __launch_bounds__(DCOR_BLOCK) void k_perm(uint32_t k0, uint32_t k1, uint32_t site,
                                                      int64_t rep_begin, uint32_t n, int a, int c,
                                                      int64_t count, int32_t* out) {
   const int64_t r = blockIdx.y;
   const U4 kk = draw(0u, (uint32_t)(rep_begin + r), site, k0, k1);
-  for (int64_t t = (int64_t)blockIdx.x * DCOR_BLOCK + threadIdx.x; t < count;
-       t += (int64_t)gridDim.x * DCOR_BLOCK)
-    out[r * count + t] = (int32_t)feistel_perm((uint32_t)t, n, a, c, kk);
+  int32_t* __restrict__ o = out + r * count;
+  const int64_t stride = (int64_t)gridDim.x * DCOR_BLOCK;
+  int64_t t = (int64_t)blockIdx.x * DCOR_BLOCK + threadIdx.x;
+  uint32_t x = (uint32_t)t;
+  while (t < count) {
+    x = feistel_pass(x, a, c, kk);
+    if (x < n) {
+      o[t] = (int32_t)x;
+      t += stride;
+      x = (uint32_t)t;
+    }
+  }
 }
 
 // ============================================================ launchers ===
@@ -1067,7 +1078,7 @@ int launch_perm(uint32_t k0, uint32_t k1, uint32_t site, int64_t rep_begin, int6
   int bits = 1;
   while ((1ll << bits) < n) ++bits;
   const int a = bits / 2, c = bits - a;
-  int64_t gx = (count + DCOR_BLOCK - 1) / DCOR_BLOCK;
+  int64_t gx = (count + 16 * DCOR_BLOCK - 1) / (16 * DCOR_BLOCK);  // ~16 values of t per lane
   if (gx > 4096) gx = 4096;
   hipLaunchKernelGGL(k_perm, dim3((unsigned)gx, (unsigned)reps), dim3(DCOR_BLOCK), 0,
                      (hipStream_t)stream, k0, k1, site, rep_begin, (uint32_t)n, a, c, count, out);
