@@ -901,15 +901,15 @@ __global__ __launch_bounds__(DCOR_BLOCK) void k_perm(uint32_t k0, uint32_t k1, u
   const int64_t r = blockIdx.y;
   const U4 kk = draw(0u, (uint32_t)(rep_begin + r), site, k0, k1);
   int32_t* __restrict__ o = out + r * count;
-  const int64_t stride = (int64_t)gridDim.x * DCOR_BLOCK;
-  int64_t t = (int64_t)blockIdx.x * DCOR_BLOCK + threadIdx.x;
-  uint32_t x = (uint32_t)t;
-  while (t < count) {
+  const uint32_t stride = gridDim.x * DCOR_BLOCK, cnt = (uint32_t)count;  // count <= n < 2^31
+  uint32_t t = blockIdx.x * DCOR_BLOCK + threadIdx.x;
+  uint32_t x = t;
+  while (t < cnt) {
     x = feistel_pass(x, a, c, kk);
     if (x < n) {
       o[t] = (int32_t)x;
       t += stride;
-      x = (uint32_t)t;
+      x = t;
     }
   }
 }
@@ -1078,7 +1078,7 @@ int launch_perm(uint32_t k0, uint32_t k1, uint32_t site, int64_t rep_begin, int6
   int bits = 1;
   while ((1ll << bits) < n) ++bits;
   const int a = bits / 2, c = bits - a;
-  int64_t gx = (count + 16 * DCOR_BLOCK - 1) / (16 * DCOR_BLOCK);  // ~16 values of t per lane
+  int64_t gx = (count + 16 * DCOR_BLOCK - 1) / (16 * DCOR_BLOCK);  // ~16 values of t per lane (8: 479 us, 32: 491 us, 16: 445-452 us)
   if (gx > 4096) gx = 4096;
   hipLaunchKernelGGL(k_perm, dim3((unsigned)gx, (unsigned)reps), dim3(DCOR_BLOCK), 0,
                      (hipStream_t)stream, k0, k1, site, rep_begin, (uint32_t)n, a, c, count, out);
