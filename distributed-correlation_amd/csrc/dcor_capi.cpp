@@ -609,6 +609,13 @@ static int premat_subg_const(const dcor_premat_subg* d, PrematSubgConst& p) {
                          d->lam_y, d->lam_s, d->lam_o, d->lam_r, d->delta, d->nsim, p.s, &p.lo_,
                          &p.crit_sqrt2_s)) return st;
   p.hrs = d->hrs ? 1 : 0;
+  // element-aligned arrays (the streaming kernels read 16 B at a time from the first 16-B
+  // boundary of each row)
+  const uintptr_t mis8 = ((uintptr_t)d->X | (uintptr_t)d->Y | (uintptr_t)d->lap_ni_x |
+                          (uintptr_t)d->lap_ni_y | (uintptr_t)d->lap_local |
+                          (uintptr_t)d->lap_central | (uintptr_t)d->mix_z | (uintptr_t)d->mix_l) & 7;
+  if (mis8 || ((uintptr_t)d->perm & 3))
+    return fail(DCOR_EINVAL, "premat_subg: arrays must be aligned to their element size");
   p.X = d->X; p.Y = d->Y; p.xy_stride = d->xy_stride; p.perm = d->perm;
   p.lap_ni_x = d->lap_ni_x; p.lap_ni_y = d->lap_ni_y; p.lap_local = d->lap_local;
   p.lap_central = d->lap_central; p.mix_z = d->mix_z; p.mix_l = d->mix_l;

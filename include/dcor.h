@@ -196,7 +196,8 @@ typedef struct dcor_premat_sign {
 } dcor_premat_sign;
 
 /* Sub-Gaussian family (simulation variant, hrs = 0, ver-cor-subG.R:25-108) or the
- * HRS variant (hrs = 1, real-data-sims.R:115-147,176-252). */
+ * HRS variant (hrs = 1, real-data-sims.R:115-147,176-252).  Every array must be aligned to
+ * its element size (8 B; perm 4 B), else DCOR_EINVAL. */
 typedef struct dcor_premat_subg {
   int64_t n, reps;
   double eps1, eps2, eta1, eta2, alpha;

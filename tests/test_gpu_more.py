@@ -132,6 +132,7 @@ def _hrs_panel(kind, n, g):
 
 @pytest.mark.parametrize("kind,n,eps", [("continuous", 19433, 2.0), ("coded", 19433, 2.0),
                                         ("coded", 19433, 0.5), ("coded", 1001, 2.0),
+                                        ("coded", 1002, 2.0), ("coded", 1003, 2.0),
                                         ("d256", 5000, 2.0), ("d257", 5000, 2.0),
                                         ("continuous", 3000, 0.5)])
 def test_premat_subg_hrs_shared_panel(dc, orc, kind, n, eps):
@@ -173,6 +174,10 @@ def test_premat_subg_hrs_shared_panel(dc, orc, kind, n, eps):
     _lib.check(_lib.lib.dcor_premat_subg_panel_launch(C.byref(d), pn, C.c_void_p(out2.data_ptr()), None))
     _lib.check(_lib.lib.dcor_panel_destroy(pn))
     np.testing.assert_array_equal(out2.cpu().numpy().view(np.int64), got.view(np.int64))
+    if kind == "coded" and n == 1003:  # misaligned noise rows are refused, not misread
+        d.lap_local = T["ll"].data_ptr() + 4
+        assert _lib.lib.dcor_premat_subg_launch(C.byref(d), C.c_void_p(out.data_ptr()), None) == \
+            _lib.DCOR_EINVAL
     for r in range(R):
         st, ni, km = orc.ni_subg(age, bmi, eps, eps, hrs=1, lam_x=2.22, lam_y=2.60, perm=perms[r],
                                  lap_x=lx[r], lap_y=ly[r])
