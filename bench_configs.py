@@ -221,6 +221,26 @@ def c5_e2e(R):
               "D2H copy of all replicate records")
 
 
+def c5_fused(R):
+    """C5 with the noise drawn inside the streaming kernel (dcor_hrs_fused_launch): the same
+    Philox streams as C5-e2e, no HBM noise arrays; R NI + INT replicates, results to host."""
+    import numpy as np
+    import torch
+    from dcor import hrs
+    age_raw, bmi_raw = hrs.standin_panel(19433, -0.3)
+    z = hrs.standardize_panel(age_raw, bmi_raw, lap=np.zeros(4))
+    args = (z["age_z"], z["bmi_z"], z["lambda_age_z"], z["lambda_bmi_z"], 2.0)
+    hrs.hrs_replicates(*args, 8192, mode="fused")  # warm-up
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    res = hrs.hrs_replicates(*args, R, chunk=65536, mode="fused")
+    torch.cuda.synchronize()
+    t = time.perf_counter() - t0
+    line("C5-fused", reps=R, seconds=t, reps_per_s=R / t, finite=bool(np.isfinite(res).all()),
+         note="HRS replicates with in-kernel Philox noise (k_hrs_fused + epilogue), the D2H copy "
+              "of all replicate records included")
+
+
 def subg():
     from dcor.sim import CellSpec, simulate
     cell = CellSpec(n=100_000, rho=0.5, eps1=1.0, eps2=1.0, family="subG", dgp="bounded_factor", seed=5)
@@ -299,7 +319,7 @@ def rstream_hrs():
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--only", default="C1,C2,C3,C4,C5,C5c,C5e,S,R1,RG,RH")
+    ap.add_argument("--only", default="C1,C2,C3,C4,C5,C5c,C5e,C5f,S,R1,RG,RH")
     ap.add_argument("--c3-reps", type=int, default=2000)
     ap.add_argument("--c4-B", type=int, default=1000)
     ap.add_argument("--c5-R", type=int, default=8192)
@@ -315,6 +335,7 @@ def main():
     if "C5" in which: c5(a.c5_R)
     if "C5c" in which: c5(a.c5_R, panel="continuous")
     if "C5e" in which: c5_e2e(a.c5e_R)
+    if "C5f" in which: c5_fused(a.c5e_R)
     if "S" in which: subg()
     if "R1" in which: rstream_c1()
     if "RG" in which: rstream_grid()

@@ -698,6 +698,38 @@ int dcor_premat_subg_launch(const dcor_premat_subg* d, dcor_rep_out* d_out, void
   return premat_subg_run(d, nullptr, d_out, stream);
 }
 
+int dcor_hrs_fused_launch(const dcor_premat_subg* d, const dcor_panel* panel, uint64_t seed_ni,
+                          uint64_t seed_int, int64_t rep_begin, dcor_rep_out* d_out, void* stream) {
+  if (!d || !panel || d->reps < 0 || (d->reps > 0 && !d_out))
+    return fail(DCOR_EINVAL, "hrs_fused: null argument");
+  if (d->X != panel->X || d->Y != panel->Y || d->xy_stride != 0 || d->n != panel->n)
+    return fail(DCOR_EINVAL, "hrs_fused: X, Y, n must be the panel's and xy_stride 0");
+  if (!d->hrs) return fail(DCOR_EINVAL, "hrs_fused: the HRS variant only (hrs = 1)");
+  if (!panel->coded)
+    return fail(DCOR_EINVAL, "hrs_fused: needs a dictionary-coded panel (<= 256 distinct values "
+                             "per column, no NaN)");
+  if (rep_begin < 0 || rep_begin + d->reps > 0xffffffffLL)
+    return fail(DCOR_EINVAL, "hrs_fused: replicate range exceeds 2^32");
+  if (int st = need_device()) return st;
+  PrematSubgConst p;
+  if (int st = premat_subg_const(d, p)) return st;
+  p.perm = nullptr; p.lap_ni_x = p.lap_ni_y = p.lap_local = p.lap_central = nullptr;
+  p.mix_z = p.mix_l = nullptr;
+  p.dict_codes = panel->codes(); p.dict_vals = panel->dict(); p.dict_ok = panel->ok();
+  p.dict_built = 2;
+  if (d->reps == 0) return DCOR_OK;
+  const size_t bytes = ((size_t)d->reps * 80 + 255) & ~(size_t)255;
+  void* part = nullptr;
+  if (hipMallocAsync(&part, bytes, (hipStream_t)stream) != hipSuccess) {
+    (void)hipGetLastError();
+    return fail(DCOR_ENOMEM, "hrs_fused: cannot allocate %zu scratch bytes", bytes);
+  }
+  const int rc = launch_hrs_fused(p, seed_ni, seed_int, rep_begin, d->reps, part, d_out, stream);
+  (void)hipFreeAsync(part, (hipStream_t)stream);
+  if (rc) return hip_fail((hipError_t)rc, "hrs_fused launch");
+  return DCOR_OK;
+}
+
 }  // extern "C" (reopened below)
 
 static int premat_subg_run(const dcor_premat_subg* d, const dcor_panel* panel, dcor_rep_out* d_out,

@@ -137,6 +137,10 @@ int launch_premat_sign(const PrematSignConst& c, int64_t reps, dcor_rep_out* out
 // part: reps * 80 B scratch (stream -> epilogue partial sums).
 // epi_stream / ev: if non-null the epilogue runs on epi_stream after an event recorded on
 // `stream` behind the streaming kernels (chunk pipelining).
+// HRS replicates [rep_begin, rep_begin + reps) with in-kernel Philox noise over a coded panel
+// (c.dict_codes / c.dict_vals set); part: reps * 80 B.
+int launch_hrs_fused(const PrematSubgConst& c, uint64_t seed_ni, uint64_t seed_int,
+                     int64_t rep_begin, int64_t reps, void* part, dcor_rep_out* out, void* stream);
 int launch_premat_subg(const PrematSubgConst& c, int64_t reps, void* part, dcor_rep_out* out,
                        void* stream, void* epi_stream = nullptr, void* ev = nullptr);
 int launch_accumulate(const dcor_rep_out* d_out, int64_t count, double rho, dcor_accum* acc,

@@ -316,12 +316,12 @@ __global__ __launch_bounds__(DCOR_BLOCK) void k_premat_subg_stream(PrematSubgCon
 template <class Quant>
 __device__ __forceinline__ void premat_subg_finish_q(const PrematSubgConst& p, int64_t rep,
                                                      const DD (&d5)[5], Quant&& quant, bool writer,
-                                                     dcor_rep_out* out) {
+                                                     dcor_rep_out* out, double lapc) {
   const SubgConst& c = p.s;
   double o[6];
   ni_subg_result(c, d5[0], d5[1], d5[2], o);
   const DD mU = dd_div_d(d5[3], c.nd);
-  const double rho = (mU.hi + mU.lo) + c.s_central * p.lap_central[rep];
+  const double rho = (mU.hi + mU.lo) + c.s_central * lapc;
   const double sd = sqrt(dd_var(d5[3], d5[4], c.nd));
   double width;
   if (!p.hrs) {
@@ -348,7 +348,7 @@ __device__ __forceinline__ void premat_subg_finish(const PrematSubgConst& p, int
   const MixConst& mx = p.s.mix;
   premat_subg_finish_q(p, rep, d5, [&](double cs) {
     return mixquant_loaded(mx, cs, p.mix_z + rep * mx.nsim, p.mix_l + rep * mx.nsim, sel);
-  }, threadIdx.x == 0, out);
+  }, threadIdx.x == 0, out, p.lap_central[rep]);
 }
 
 // The five sums of replicate `rep`: its p.slices partials merged in slice order.
@@ -389,7 +389,7 @@ __global__ __launch_bounds__(DCOR_BLOCK) void k_premat_subg_epilogue_w(PrematSub
       val[s] = i < mx.nsim ? z[i] + cs * l[i] : dnan();  // NaN keys are dropped (R's sort)
     }
     return wave_select<VPL>(val, mx.pos, &wsel[wv]);
-  }, lane == 0, out);
+  }, lane == 0, out, p.lap_central[rep]);
 }
 
 // Epilogue of the streaming kernels that hand their sums over through SubgPartial.
@@ -404,7 +404,7 @@ __global__ __launch_bounds__(DCOR_BLOCK) void k_premat_subg_epilogue(PrematSubgC
   DD d5[5];
   load_partials(p, part, rep, d5);
   premat_subg_finish_q(p, rep, d5, [&](double cs) { return mixquant_regs(mx, cs, zv, lv, &sel); },
-                       threadIdx.x == 0, out);
+                       threadIdx.x == 0, out, p.lap_central[rep]);
 }
 
 // ------------------------------------------- dictionary-coded shared panel (HRS) ---
@@ -912,6 +912,250 @@ __global__ __launch_bounds__(DCOR_BLOCK) void k_perm(uint32_t k0, uint32_t k1, u
       x = t;
     }
   }
+}
+
+// ========================================================= fused HRS ===
+// The HRS replicate of k_premat_subg_dict with its noise drawn in the kernel instead of read
+// from HBM: the same Philox streams the HRS driver materialises (dcor_perm_launch with
+// seed_ni, DCOR_SITE_PERM; dcor_draws_launch Laplace seed_ni sites 11 / 12 for the NI
+// batches, seed_int sites 13 / 14 for the INT local / central noise, normal site 15 and
+// Laplace site 16 for mixquant), so every replicate equals the pre-materialised pipeline's
+// bit for bit.  real-data-sims.R:115-147 (NI) and 176-252 (INT) per replicate.
+struct HrsKeys {
+  uint32_t ni0, ni1, in0, in1;  // Philox keys (seed_ni, seed_int)
+  uint32_t rep_begin;
+  int pa, pc;                   // Feistel split of ceil(log2 n) bits (launch_perm)
+};
+#define HRS_SITE_NI_X 11u
+#define HRS_SITE_NI_Y 12u
+#define HRS_SITE_LOCAL 13u
+#define HRS_SITE_CENTRAL 14u
+#define HRS_SITE_MIX_Z 15u
+#define HRS_SITE_MIX_L 16u
+
+__device__ __forceinline__ uint32_t hrs_walk(uint32_t t, uint32_t n, int a, int c, const U4& kk) {
+  uint32_t x = t;
+  do { x = feistel_pass(x, a, c, kk); } while (x >= n);  // = k_perm's P_r(t)
+  return x;
+}
+
+template <int WPE>
+__global__ __launch_bounds__(DICT_NT, WPE) void k_hrs_fused(PrematSubgConst p, HrsKeys hk,
+                                                           const uint16_t* __restrict__ codes_g,
+                                                           const double* __restrict__ dict_g,
+                                                           int64_t reps,
+                                                           SubgPartial* __restrict__ part) {
+  extern __shared__ double dsm[];
+  const SubgConst& c = p.s;
+  const int tid = threadIdx.x;
+  double* dX = dsm;
+  double* dY = dsm + DICT_MAX;
+  double* dS = dsm + 2 * DICT_MAX;
+  double* dO = dsm + 3 * DICT_MAX;
+  double* red = dsm + 4 * DICT_MAX;
+  uint16_t* cod = reinterpret_cast<uint16_t*>(dsm + 4 * DICT_MAX + 20 * DICT_NW);
+  if (tid < DICT_MAX) {
+    const double x = dict_g[tid], y = dict_g[DICT_MAX + tid];
+    dX[tid] = rclip(x, c.l1);
+    dY[tid] = rclip(y, c.l2);
+    const double sv = c.sender_is_X ? x : y, ov = c.sender_is_X ? y : x;
+    dS[tid] = rclip(sv, c.ls);
+    dO[tid] = rclip(ov, p.lo_);
+  }
+  {
+    const int64_t nv = (c.n * 2 + 15) / 16;
+    const uint4* src = reinterpret_cast<const uint4*>(codes_g);
+    uint4* dst = reinterpret_cast<uint4*>(cod);
+    for (int64_t w = tid; w < nv; w += DICT_NT) dst[w] = src[w];
+  }
+  __syncthreads();
+  const uint32_t n = (uint32_t)c.n;
+  for (int64_t it = blockIdx.x; it < reps; it += gridDim.x) {
+    const uint32_t rep = hk.rep_begin + (uint32_t)it;
+    DD sP{0, 0}, sT{0, 0}, sT2{0, 0}, sU{0, 0}, sU2{0, 0};
+    auto uterm = [&](uint32_t cd, double l) {  // real-data-sims.R:222-232
+      const double Uc = rclip((dS[cd & 255u] + c.bs * l) * dO[cd >> 8], c.lr);
+      ks_acc(sU, Uc);
+      ks_acc(sU2, Uc * Uc);
+    };
+    {  // INT local noise: block b -> samples 2b, 2b+1
+      const int64_t nb = c.n >> 1;
+      for (int64_t b = tid; b < nb; b += DICT_NT) {
+        const U4 w = draw((uint32_t)b, rep, HRS_SITE_LOCAL, hk.in0, hk.in1);
+        uterm(cod[2 * b], unit_laplace(u53(w.w0, w.w1)));
+        uterm(cod[2 * b + 1], unit_laplace(u53(w.w2, w.w3)));
+      }
+      if ((c.n & 1) && tid == DICT_NT - 1) {
+        const U4 w = draw((uint32_t)nb, rep, HRS_SITE_LOCAL, hk.in0, hk.in1);
+        uterm(cod[c.n - 1], unit_laplace(u53(w.w0, w.w1)));
+      }
+    }
+    double* rb = red + (((it - blockIdx.x) / gridDim.x) & 1) * (10 * DICT_NW);
+    auto wave_put = [&](int v, DD a) {
+      a = wave_sum_dd(a);
+      if ((tid & 63) == 0) {
+        rb[(2 * v) * DICT_NW + (tid >> 6)] = a.hi;
+        rb[(2 * v + 1) * DICT_NW + (tid >> 6)] = a.lo;
+      }
+    };
+    wave_put(3, sU);
+    wave_put(4, sU2);
+    const U4 kk = draw(0u, rep, DCOR_SITE_PERM, hk.ni0, hk.ni1);
+    auto nterm = [&](double xt, double yt) {  // real-data-sims.R:133-137
+      ks_acc(sP, xt * yt);
+      const double T = c.md * xt * yt;
+      ks_acc(sT, T);
+      ks_acc(sT2, T * T);
+    };
+    if (c.m == 2) {  // batches 2q, 2q+1 share one Philox block of X noise and one of Y noise
+      auto pair = [&](uint32_t ia, uint32_t ib, double lxj, double lyj) {
+        const uint32_t a = cod[ia], b = cod[ib];
+        nterm((dX[a & 255u] + dX[b & 255u]) * 0.5 + c.bx * lxj,
+              (dY[a >> 8] + dY[b >> 8]) * 0.5 + c.by * lyj);
+      };
+      for (int64_t q = tid; 2 * q < c.k; q += DICT_NT) {
+        // the 4 (or 2) permuted indices P(4q) .. P(4q+3) in ONE loop: a lane starts its next
+        // walk as soon as one lands, so a wave runs to the longest lane's total, not to the
+        // sum of four wave-longest walks; results packed 16 bits each (n <= 65536)
+        const uint32_t t0 = (uint32_t)(4 * q);
+        const int want = (2 * q + 1 < c.k) ? 4 : 2;
+        uint64_t res = 0;
+        int got = 0;
+        uint32_t x = t0;
+        while (got < want) {
+          x = feistel_pass(x, hk.pa, hk.pc, kk);
+          if (x < n) {
+            res |= (uint64_t)x << (16 * got);
+            ++got;
+            x = t0 + (uint32_t)got;
+          }
+        }
+        const U4 wx = draw((uint32_t)q, rep, HRS_SITE_NI_X, hk.ni0, hk.ni1);
+        const U4 wy = draw((uint32_t)q, rep, HRS_SITE_NI_Y, hk.ni0, hk.ni1);
+        pair((uint32_t)(res & 0xFFFFu), (uint32_t)((res >> 16) & 0xFFFFu),
+             unit_laplace(u53(wx.w0, wx.w1)), unit_laplace(u53(wy.w0, wy.w1)));
+        if (want == 4)
+          pair((uint32_t)((res >> 32) & 0xFFFFu), (uint32_t)(res >> 48),
+               unit_laplace(u53(wx.w2, wx.w3)), unit_laplace(u53(wy.w2, wy.w3)));
+      }
+    } else {
+      for (int64_t j = tid; j < c.k; j += DICT_NT) {
+        const U4 wx = draw((uint32_t)(j >> 1), rep, HRS_SITE_NI_X, hk.ni0, hk.ni1);
+        const U4 wy = draw((uint32_t)(j >> 1), rep, HRS_SITE_NI_Y, hk.ni0, hk.ni1);
+        const double lxj = unit_laplace((j & 1) ? u53(wx.w2, wx.w3) : u53(wx.w0, wx.w1));
+        const double lyj = unit_laplace((j & 1) ? u53(wy.w2, wy.w3) : u53(wy.w0, wy.w1));
+        DD bx{0, 0}, by{0, 0};
+        for (int r = 0; r < c.m; ++r) {
+          const uint32_t a = cod[hrs_walk((uint32_t)(j * c.m + r), n, hk.pa, hk.pc, kk)];
+          dd_acc(bx, dX[a & 255u]);
+          dd_acc(by, dY[a >> 8]);
+        }
+        const DD xb = dd_div_d(bx, c.md), yb = dd_div_d(by, c.md);
+        nterm((xb.hi + xb.lo) + c.bx * lxj, (yb.hi + yb.lo) + c.by * lyj);
+      }
+    }
+    wave_put(0, sP);
+    wave_put(1, sT);
+    wave_put(2, sT2);
+    __syncthreads();
+    if (tid < 5) {
+      DD a{rb[(2 * tid) * DICT_NW], rb[(2 * tid + 1) * DICT_NW]};
+#pragma unroll
+      for (int w = 1; w < DICT_NW; ++w)
+        a = dd_add(a, DD{rb[(2 * tid) * DICT_NW + w], rb[(2 * tid + 1) * DICT_NW + w]});
+      part[it].s[2 * tid] = a.hi;
+      part[it].s[2 * tid + 1] = a.lo;
+    }
+  }
+}
+
+// Epilogue of k_hrs_fused: central Laplace and mixquant draws generated here.  Thread t holds
+// the pairs of Philox blocks t + 256 s (order is irrelevant to an order statistic).
+__global__ __launch_bounds__(DCOR_BLOCK) void k_hrs_fused_epilogue(PrematSubgConst p, HrsKeys hk,
+                                                                   const SubgPartial* __restrict__ part,
+                                                                   dcor_rep_out* out) {
+  __shared__ SelScratch sel;
+  const int64_t r = blockIdx.x;
+  const uint32_t rep = hk.rep_begin + (uint32_t)r;
+  const MixConst& mx = p.s.mix;
+  double zv[SEL_VPT], lv[SEL_VPT];
+  bool have[SEL_VPT];
+#pragma unroll
+  for (int s = 0; s < SEL_VPT / 2; ++s) {
+    const int b = threadIdx.x + s * DCOR_BLOCK;
+    have[2 * s] = 2 * b < mx.nsim;
+    have[2 * s + 1] = 2 * b + 1 < mx.nsim;
+    zv[2 * s] = zv[2 * s + 1] = lv[2 * s] = lv[2 * s + 1] = 0.0;
+    if (have[2 * s]) {
+      const U4 wz = draw((uint32_t)b, rep, HRS_SITE_MIX_Z, hk.in0, hk.in1);
+      const U4 wl = draw((uint32_t)b, rep, HRS_SITE_MIX_L, hk.in0, hk.in1);
+      normal_pair(wz, &zv[2 * s], &zv[2 * s + 1]);
+      lv[2 * s] = unit_laplace(u53(wl.w0, wl.w1));
+      lv[2 * s + 1] = unit_laplace(u53(wl.w2, wl.w3));
+    }
+  }
+  const U4 wc = draw(0u, rep, HRS_SITE_CENTRAL, hk.in0, hk.in1);
+  const double lapc = unit_laplace(u53(wc.w0, wc.w1));
+  DD d5[5];
+  load_partials(p, part, r, d5);
+  premat_subg_finish_q(p, r, d5, [&](double cs) {
+    if (threadIdx.x == 0) sel.nan_cnt = 0;
+    __syncthreads();
+    double val[SEL_VPT];
+    int nn = 0;
+#pragma unroll
+    for (int s = 0; s < SEL_VPT; ++s) {
+      val[s] = dnan();
+      if (have[s]) {
+        val[s] = zv[s] + cs * lv[s];
+        nn += (val[s] != val[s]);
+      }
+    }
+    if (nn) atomicAdd(&sel.nan_cnt, nn);
+    __syncthreads();
+    return value_select(val, mx.pos, mx.nsim - sel.nan_cnt, &sel);
+  }, threadIdx.x == 0, out, lapc);
+}
+
+int launch_hrs_fused(const PrematSubgConst& c, uint64_t seed_ni, uint64_t seed_int,
+                     int64_t rep_begin, int64_t reps, void* part, dcor_rep_out* out,
+                     void* stream) {
+  if (reps <= 0) return 0;
+  HrsKeys hk;
+  hk.ni0 = (uint32_t)seed_ni; hk.ni1 = (uint32_t)(seed_ni >> 32);
+  hk.in0 = (uint32_t)seed_int; hk.in1 = (uint32_t)(seed_int >> 32);
+  hk.rep_begin = (uint32_t)rep_begin;
+  int bits = 1;
+  while ((1ll << bits) < c.s.n) ++bits;
+  hk.pa = bits / 2; hk.pc = bits - hk.pa;
+  const size_t lds = premat_dict_lds_bytes(c.s.n);
+  static const int wsel = [] {
+    const char* e = std::getenv("DCOR_HRS_WPE");
+    return (e && std::atoi(e) == 4) ? 4 : 6;
+  }();
+  const auto kern = wsel == 4 ? k_hrs_fused<4> : k_hrs_fused<6>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    if (hipFuncSetAttribute((const void*)kern,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024) != hipSuccess)
+      return (int)hipGetLastError();
+    attr_set = true;
+  }
+  int dev = 0, cus = 0, per_cu = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return (int)hipGetLastError();
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    return (int)hipGetLastError();
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, DICT_NT, lds) !=
+      hipSuccess)
+    return (int)hipGetLastError();
+  const int64_t slots = (int64_t)cus * (per_cu < 1 ? 1 : per_cu);
+  const int64_t grid = reps < slots ? reps : slots;
+  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(DICT_NT), lds,
+                     (hipStream_t)stream, c, hk, c.dict_codes, c.dict_vals, reps,
+                     (SubgPartial*)part);
+  hipLaunchKernelGGL(k_hrs_fused_epilogue, dim3((unsigned)reps), dim3(DCOR_BLOCK), 0,
+                     (hipStream_t)stream, c, hk, (const SubgPartial*)part, out);
+  return (int)hipGetLastError();
 }
 
 // ============================================================ launchers ===

@@ -129,6 +129,8 @@ SIGNATURES = {
     "dcor_panel_coded": (C.c_int, [_P, C.POINTER(C.c_int)]),
     "dcor_panel_destroy": (C.c_int, [_P]),
     "dcor_premat_subg_panel_launch": (C.c_int, [C.POINTER(PrematSubg), _P, _P, _P]),
+    "dcor_hrs_fused_launch": (C.c_int, [C.POINTER(PrematSubg), _P, C.c_uint64, C.c_uint64,
+                                        C.c_int64, _P, _P]),
     "dcor_batch_geometry": (C.c_int, [C.c_int64, C.c_double, C.c_double, C.c_int, C.c_int, _I64]),
     "dcor_ci_ni_signbatch": (C.c_int, [_D, _D, C.c_int64, C.c_double, C.c_double, C.c_double,
                                        C.c_int, _D, _D, _D, _D]),

@@ -77,7 +77,7 @@ def r_seeds(idx: int, reps, rep_begin: int = 0):
 
 def hrs_replicates(age_z, bmi_z, lam_age, lam_bmi, eps, reps, seed_ni=NI_SEED, seed_int=INT_SEED,
                    nsim=2000, rep_begin=0, chunk=8192, alpha=0.05, keep_noise=False, rng="philox",
-                   eps_idx=None):
+                   eps_idx=None, mode="premat"):
     """`reps` NI + INT replicates of the HRS estimators on one standardised panel at one eps:
     correlation_NI_subG(lambda_X = lam_age, lambda_Y = lam_bmi) and ci_INT_subG(AGE sends,
     lambda_receiver_from_noise, delta_clip = 1/n) (real-data-sims.R:357-400).  The panel is
@@ -88,7 +88,12 @@ def hrs_replicates(age_z, bmi_z, lam_age, lam_bmi, eps, reps, seed_ni=NI_SEED, s
     rng='R' replays the reference's own streams instead: run rep (1-based, rep_begin + 1 ..)
     draws its NI noise after set.seed(10 + 37 rep + 1000 eps_idx) and its INT noise after
     set.seed(20 + 41 rep + 1000 eps_idx) (dcor_rstream_hrs_draws), so every run is the
-    reference's run for that seed; seed_ni / seed_int are then unused."""
+    reference's run for that seed; seed_ni / seed_int are then unused.
+
+    mode='fused' (rng='philox' only) draws the same Philox noise inside the streaming kernel
+    (dcor_hrs_fused_launch) instead of materialising it in HBM: the results equal the
+    pre-materialised pipeline's to within its compensated sums' rounding.  Needs a
+    dictionary-coded panel (at most 256 distinct values per column)."""
     import ctypes as C
 
     import torch
@@ -107,6 +112,20 @@ def hrs_replicates(age_z, bmi_z, lam_age, lam_bmi, eps, reps, seed_ni=NI_SEED, s
     _lib.check(_lib.lib.dcor_panel_create(P(X), P(Y), n, sp, C.byref(pn)))
     cr = min(chunk, max(1, reps))
     f64 = dict(dtype=torch.float64, device="cuda")
+    if mode == "fused":
+        out = torch.empty((reps, 6), **f64)
+        try:
+            for r0 in range(0, reps, cr):
+                nr = min(cr, reps - r0)
+                d = _lib.PrematSubg(n=n, reps=nr, eps1=eps, eps2=eps, eta1=1.0, eta2=1.0, alpha=alpha,
+                                    hrs=1, lam_x=lam_age, lam_y=lam_bmi, lam_s=lam_age, lam_o=lam_bmi,
+                                    lam_r=lam_r, delta=delta, nsim=nsim, X=X.data_ptr(), Y=Y.data_ptr(),
+                                    xy_stride=0)
+                _lib.check(_lib.lib.dcor_hrs_fused_launch(C.byref(d), pn, seed_ni, seed_int,
+                                                          rep_begin + r0, P(out[r0:]), sp))
+            return out.cpu().numpy()
+        finally:
+            _lib.lib.dcor_panel_destroy(pn)
     perm = torch.empty((cr, k * m), dtype=torch.int32, device="cuda")
     lx, ly = torch.empty((cr, k), **f64), torch.empty((cr, k), **f64)
     ll, lc = torch.empty((cr, n), **f64), torch.empty((cr,), **f64)
@@ -115,6 +134,10 @@ def hrs_replicates(age_z, bmi_z, lam_age, lam_bmi, eps, reps, seed_ni=NI_SEED, s
     noise = {key: [] for key in ("perm", "lap_x", "lap_y", "lap_local", "lap_central", "mix_z", "mix_l")}
     if rng not in ("philox", "R"):
         raise ValueError(f"rng must be 'philox' or 'R', not {rng!r}")
+    if mode not in ("premat", "fused"):
+        raise ValueError(f"mode must be 'premat' or 'fused', not {mode!r}")
+    if mode == "fused" and (rng != "philox" or keep_noise):
+        raise ValueError("mode='fused' draws Philox noise in the kernel: rng='philox', keep_noise=False")
     if rng == "R" and eps_idx is None:
         raise ValueError("rng='R' needs eps_idx (the 1-based position of eps in the sweep)")
     try:

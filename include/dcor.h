@@ -239,6 +239,17 @@ int dcor_panel_destroy(dcor_panel* panel);
 int dcor_premat_subg_panel_launch(const dcor_premat_subg* d, const dcor_panel* panel,
                                   dcor_rep_out* d_out, void* stream);
 
+/* HRS replicates rep_begin .. rep_begin + d->reps - 1 with the noise drawn inside the kernel
+ * (real-data-sims.R:115-147 NI, 176-252 INT; the replicate loop of 345-448): the Philox
+ * streams the HRS driver otherwise materialises in HBM -- dcor_perm_launch(seed_ni,
+ * DCOR_SITE_PERM), dcor_draws_launch(Laplace, seed_ni, 11 / 12) for the NI batches,
+ * (Laplace, seed_int, 13) local and (Laplace, seed_int, 14, count 1) central INT noise,
+ * (normal, seed_int, 15) and (Laplace, seed_int, 16) for mixquant.  Results equal
+ * dcor_premat_subg_panel_launch on those arrays to within the compensated sums' rounding.
+ * d->hrs must be 1 and the panel dictionary-coded; d's noise pointers are ignored. */
+int dcor_hrs_fused_launch(const dcor_premat_subg* d, const dcor_panel* panel, uint64_t seed_ni,
+                          uint64_t seed_int, int64_t rep_begin, dcor_rep_out* d_out, void* stream);
+
 int dcor_premat_sign_launch(const dcor_premat_sign* d, dcor_rep_out* d_out, void* stream);
 int dcor_premat_subg_launch(const dcor_premat_subg* d, dcor_rep_out* d_out, void* stream);
 

@@ -156,3 +156,55 @@ def test_hrs_r_stream_sample_int_is_a_permutation(panel):
     _lib.check(_lib.lib.dcor_rstream_hrs_draws(10, 5, 2, 2000, 1, one.ctypes.data_as(C.POINTER(C.c_int32)),
                                                None, P(p10), P(l1), P(l1), None, None, None, None, None))
     assert list(p10.cpu().numpy()[0] + 1) == [9, 4, 7, 1, 2, 5, 3, 10, 6, 8]
+
+
+# ------------------------------------------------ fused HRS (noise drawn in the kernel)
+@pytest.mark.parametrize("n,eps,reps,rb", [(2501, 2.0, 37, 0), (2501, 2.0, 9, 1001), (2501, 0.55, 11, 5),
+                                           (2501, 1.05, 7, 0), (2500, 2.0, 6, 2), (19433, 2.0, 5, 17)])
+def test_hrs_fused_equals_premat(n, eps, reps, rb):
+    """dcor_hrs_fused_launch draws the HRS driver's Philox streams in the kernel: every
+    replicate equals the pre-materialised pipeline's (whose noise the other tests pin
+    bit-exact against the oracle) within the estimator tolerance; odd / even n, m = 2 and
+    m > 2 batches, a replicate offset."""
+    from dcor import hrs
+    age, bmi = hrs.standin_panel(n, -0.3, seed=5)
+    z = hrs.standardize_panel(age, bmi, lap=np.array([0.3, -0.2, 0.1, 0.4]))
+    args = (z["age_z"], z["bmi_z"], z["lambda_age_z"], z["lambda_bmi_z"], eps, reps)
+    pm = hrs.hrs_replicates(*args, rep_begin=rb)
+    fu = hrs.hrs_replicates(*args, rep_begin=rb, mode="fused")
+    assert np.isfinite(fu).all()
+    for r in range(reps):
+        assert_close(fu[r], pm[r], what=f"fused vs premat n={n} eps={eps} rep {rb + r}")
+
+
+def test_hrs_fused_split_invariant(panel):
+    from dcor import hrs
+    z = panel
+    args = (z["age_z"], z["bmi_z"], z["lambda_age_z"], z["lambda_bmi_z"], 2.0)
+    whole = hrs.hrs_replicates(*args, 10, chunk=10, mode="fused")
+    parts = np.concatenate([hrs.hrs_replicates(*args, 3, chunk=3, mode="fused"),
+                            hrs.hrs_replicates(*args, 7, rep_begin=3, chunk=4, mode="fused")])
+    np.testing.assert_array_equal(whole.view(np.int64), parts.view(np.int64))
+
+
+def test_hrs_fused_refuses_uncoded_panel():
+    import ctypes as C
+
+    import torch
+    from dcor import _lib
+    n = 3000
+    g = np.random.default_rng(1)
+    X = torch.as_tensor(g.standard_normal(n), device="cuda")  # every value distinct: not codable
+    Y = torch.as_tensor(g.standard_normal(n), device="cuda")
+    pn = C.c_void_p()
+    _lib.check(_lib.lib.dcor_panel_create(C.c_void_p(X.data_ptr()), C.c_void_p(Y.data_ptr()), n, None,
+                                          C.byref(pn)))
+    try:
+        d = _lib.PrematSubg(n=n, reps=2, eps1=2.0, eps2=2.0, eta1=1.0, eta2=1.0, alpha=0.05, hrs=1,
+                            lam_x=2.2, lam_y=2.6, lam_s=2.2, lam_o=2.6, lam_r=math.nan, delta=math.nan,
+                            nsim=2000, X=X.data_ptr(), Y=Y.data_ptr(), xy_stride=0)
+        out = torch.empty((2, 6), dtype=torch.float64, device="cuda")
+        st = _lib.lib.dcor_hrs_fused_launch(C.byref(d), pn, 1, 2, 0, C.c_void_p(out.data_ptr()), None)
+        assert st == _lib.DCOR_EINVAL
+    finally:
+        _lib.lib.dcor_panel_destroy(pn)
