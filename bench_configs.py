@@ -187,17 +187,39 @@ def c5(R, panel="coded"):
               reps=5, inner=8)
     per_rep = 8 * n + 4 * k * m + 16 * k + 8 * nsim    # SURVEY §8d pinned: 404,648 B
     read_rep = 8 * n + 4 * k * m + 16 * k + 8 + 16 * nsim  # bytes the ABI actually reads (z, l apart)
+    cpu = c5_cpu(age, bmi, lam, eps, nsim, perm, lx, ly, ll, lc, mz, ml) if panel == "coded" else {}
     ok = C.c_int(-1)
     _lib.check(_lib.lib.dcor_panel_coded(pn, C.byref(ok)))
     _lib.check(_lib.lib.dcor_panel_destroy(pn))
     line("C5" if panel == "coded" else "C5-continuous", reps=R, seconds=t, reps_per_s=R / t,
          algorithmic_bytes_per_rep=per_rep, input_bytes_per_rep=read_rep,
          hbm_gbps=per_rep * R / t / 1e9, hbm_frac=per_rep * R / t / HBM_PEAK,
-         input_gbps=read_rep * R / t / 1e9, panel=panel,
+         input_gbps=read_rep * R / t / 1e9, panel=panel, **cpu,
          kernel="dictionary-coded LDS panel" if ok.value else "L2-gather packed panel",
          note="synthetic stand-in panel; noise pre-generated on device (dcor_draws_launch / "
               "dcor_perm_launch); timed = one dcor_premat_subg_panel_launch (stream + epilogue) over a panel "
               "encoded once by dcor_panel_create")
+
+
+def c5_cpu(age, bmi, lam, eps, nsim, perm, lx, ly, ll, lc, mz, ml, seconds=3.0):
+    """CPU baseline for C5: the HRS NI + INT estimators (real-data-sims.R:115-147, 176-252)
+    restated in C (oracle/dcor_oracle.c, R semantics), 1 thread, on the same panel and the
+    first replicates' noise copied to the host; about `seconds` of work."""
+    from oracle import oracle as orc
+    host = [t[:64].cpu().numpy() for t in (perm, lx, ly, ll, lc, mz, ml)]
+    done, t0 = 0, time.perf_counter()
+    while done < 2000 and (done < 2 or time.perf_counter() - t0 < seconds):
+        r = done % host[0].shape[0]  # the first (up to) 64 replicates' noise, cycled
+        orc.ni_subg(age, bmi, eps, eps, hrs=1, lam_x=lam[0], lam_y=lam[1], perm=host[0][r],
+                    lap_x=host[1][r], lap_y=host[2][r])
+        orc.int_subg(age, bmi, eps, eps, hrs=1, lam_s=lam[0], lam_o=lam[1], lap_local=host[3][r],
+                     lap_central=float(host[4][r]), mix_z=host[5][r], mix_l=host[6][r])
+        done += 1
+    el = time.perf_counter() - t0
+    return {"cpu_1thread_reps_per_s": done / el,
+            "cpu_sample": f"{done} NI + INT replicates of the HRS estimators on the same panel and noise "
+                          f"(the first {host[0].shape[0]} replicates' noise, cycled) "
+                          f"in {el:.2f} s: oracle/dcor_oracle.c (R semantics), 1 thread"}
 
 
 def c5_e2e(R):
