@@ -1134,13 +1134,10 @@ int launch_hrs_fused(const PrematSubgConst& c, uint64_t seed_ni, uint64_t seed_i
     return (e && std::atoi(e) == 4) ? 4 : 6;
   }();
   const auto kern = wsel == 4 ? k_hrs_fused<4> : k_hrs_fused<6>;
-  static bool attr_set = false;
-  if (!attr_set) {
-    if (hipFuncSetAttribute((const void*)kern,
-                            hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024) != hipSuccess)
-      return (int)hipGetLastError();
-    attr_set = true;
-  }
+  // per call: the attribute is per device, and one process may drive several GPUs
+  if (hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          150 * 1024) != hipSuccess)
+    return (int)hipGetLastError();
   int dev = 0, cus = 0, per_cu = 0;
   if (hipGetDevice(&dev) != hipSuccess) return (int)hipGetLastError();
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
@@ -1197,13 +1194,10 @@ static DictKernel dict_kernel() {
 // Workgroup slots of the coded-panel kernel (CUs x resident workgroups at this LDS size).
 static int premat_dict_slots(int64_t n, int* slots) {
   const size_t lds = premat_dict_lds_bytes(n);
-  static bool attr_set = false;
-  if (!attr_set) {
-    if (hipFuncSetAttribute((const void*)dict_kernel(),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024) != hipSuccess)
-      return last_err();
-    attr_set = true;
-  }
+  // per call: the attribute is per device, and one process may drive several GPUs
+  if (hipFuncSetAttribute((const void*)dict_kernel(), hipFuncAttributeMaxDynamicSharedMemorySize,
+                          150 * 1024) != hipSuccess)
+    return last_err();
   int dev = 0, cus = 0, per_cu = 0;
   if (hipGetDevice(&dev) != hipSuccess) return last_err();
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)

@@ -812,13 +812,10 @@ size_t rs_hrs_ni_lds_bytes(int64_t n) {
 int launch_rs_hrs_ni(const int32_t* d_seeds, int64_t runs, int64_t n, int64_t km, int64_t k,
                      int32_t* perm, double* lx, double* ly, void* stream) {
   const size_t lds = rs_hrs_ni_lds_bytes(n);
-  static bool attr = false;
-  if (!attr) {
-    const hipError_t e = hipFuncSetAttribute((const void*)k_rs_hrs_ni,
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
-    if (e != hipSuccess) return (int)e;
-    attr = true;
-  }
+  // per call: the attribute is per device, and one process may drive several GPUs
+  const hipError_t e = hipFuncSetAttribute((const void*)k_rs_hrs_ni,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
+  if (e != hipSuccess) return (int)e;
   hipLaunchKernelGGL(k_rs_hrs_ni, dim3((unsigned)runs), dim3(64), lds, (hipStream_t)stream, d_seeds,
                      n, km, k, perm, lx, ly);
   return (int)hipGetLastError();
@@ -831,13 +828,10 @@ int launch_rs_stream(RsCell* d_cells, int ncells, int32_t rc, void* stream) {
 
 int launch_rs_materialise(const RsCell* d_cells, int ncells, int32_t rc, void* stream, size_t lds) {
   if (lds > 64 * 1024) {
-    static bool attr = false;
-    if (!attr) {
-      const hipError_t e = hipFuncSetAttribute((const void*)k_rs_materialise,
-                                               hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
-      if (e != hipSuccess) return (int)e;
-      attr = true;
-    }
+    // per call: the attribute is per device, and one process may drive several GPUs
+    const hipError_t e = hipFuncSetAttribute((const void*)k_rs_materialise,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
+    if (e != hipSuccess) return (int)e;
   }
   hipLaunchKernelGGL(k_rs_materialise, dim3((unsigned)(ncells * rc)), dim3(256), lds,
                      (hipStream_t)stream, d_cells, rc);
