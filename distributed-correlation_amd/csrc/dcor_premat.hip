@@ -933,18 +933,14 @@ struct HrsKeys {
 #define HRS_SITE_MIX_Z 15u
 #define HRS_SITE_MIX_L 16u
 
-__device__ __forceinline__ uint32_t hrs_walk(uint32_t t, uint32_t n, int a, int c, const U4& kk) {
-  uint32_t x = t;
-  do { x = feistel_pass(x, a, c, kk); } while (x >= n);  // = k_perm's P_r(t)
-  return x;
-}
-
 template <int WPE>
 __global__ __launch_bounds__(DICT_NT, WPE) void k_hrs_fused(PrematSubgConst p, HrsKeys hk,
                                                            const uint16_t* __restrict__ codes_g,
                                                            const double* __restrict__ dict_g,
                                                            int64_t reps,
-                                                           SubgPartial* __restrict__ part) {
+                                                           SubgPartial* __restrict__ part,
+                                                           uint16_t* __restrict__ scr,
+                                                           int64_t scr_stride) {
   extern __shared__ double dsm[];
   const SubgConst& c = p.s;
   const int tid = threadIdx.x;
@@ -978,6 +974,24 @@ __global__ __launch_bounds__(DICT_NT, WPE) void k_hrs_fused(PrematSubgConst p, H
       ks_acc(sU, Uc);
       ks_acc(sU2, Uc * Uc);
     };
+    // Phase A: the panel codes at the permuted batch slots, gs[t] = code[P(t)], t < k m, into
+    // this workgroup's scratch row (L2-resident, reused by every replicate of the workgroup).
+    // Each lane walks its strided run of t and moves to the next t as soon as a walk lands,
+    // so lanes stay busy while walk lengths differ.  Phase B reads the row after a barrier.
+    const U4 kk = draw(0u, rep, DCOR_SITE_PERM, hk.ni0, hk.ni1);
+    uint16_t* __restrict__ gs = scr + (int64_t)blockIdx.x * scr_stride;
+    {
+      const uint32_t km = (uint32_t)(c.k * c.m);
+      uint32_t t = (uint32_t)tid, x = t;
+      while (t < km) {
+        x = feistel_pass(x, hk.pa, hk.pc, kk);
+        if (x < n) {
+          gs[t] = cod[x];
+          t += DICT_NT;
+          x = t;
+        }
+      }
+    }
     {  // INT local noise: block b -> samples 2b, 2b+1
       const int64_t nb = c.n >> 1;
       for (int64_t b = tid; b < nb; b += DICT_NT) {
@@ -1000,7 +1014,7 @@ __global__ __launch_bounds__(DICT_NT, WPE) void k_hrs_fused(PrematSubgConst p, H
     };
     wave_put(3, sU);
     wave_put(4, sU2);
-    const U4 kk = draw(0u, rep, DCOR_SITE_PERM, hk.ni0, hk.ni1);
+    __syncthreads();  // phase A's scratch row is complete
     auto nterm = [&](double xt, double yt) {  // real-data-sims.R:133-137
       ks_acc(sP, xt * yt);
       const double T = c.md * xt * yt;
@@ -1008,35 +1022,18 @@ __global__ __launch_bounds__(DICT_NT, WPE) void k_hrs_fused(PrematSubgConst p, H
       ks_acc(sT2, T * T);
     };
     if (c.m == 2) {  // batches 2q, 2q+1 share one Philox block of X noise and one of Y noise
-      auto pair = [&](uint32_t ia, uint32_t ib, double lxj, double lyj) {
-        const uint32_t a = cod[ia], b = cod[ib];
+      const uint32_t* __restrict__ g2 = reinterpret_cast<const uint32_t*>(gs);  // batch j's codes
+      auto pair = [&](uint32_t ab, double lxj, double lyj) {
+        const uint32_t a = ab & 0xFFFFu, b = ab >> 16;
         nterm((dX[a & 255u] + dX[b & 255u]) * 0.5 + c.bx * lxj,
               (dY[a >> 8] + dY[b >> 8]) * 0.5 + c.by * lyj);
       };
       for (int64_t q = tid; 2 * q < c.k; q += DICT_NT) {
-        // the 4 (or 2) permuted indices P(4q) .. P(4q+3) in ONE loop: a lane starts its next
-        // walk as soon as one lands, so a wave runs to the longest lane's total, not to the
-        // sum of four wave-longest walks; results packed 16 bits each (n <= 65536)
-        const uint32_t t0 = (uint32_t)(4 * q);
-        const int want = (2 * q + 1 < c.k) ? 4 : 2;
-        uint64_t res = 0;
-        int got = 0;
-        uint32_t x = t0;
-        while (got < want) {
-          x = feistel_pass(x, hk.pa, hk.pc, kk);
-          if (x < n) {
-            res |= (uint64_t)x << (16 * got);
-            ++got;
-            x = t0 + (uint32_t)got;
-          }
-        }
         const U4 wx = draw((uint32_t)q, rep, HRS_SITE_NI_X, hk.ni0, hk.ni1);
         const U4 wy = draw((uint32_t)q, rep, HRS_SITE_NI_Y, hk.ni0, hk.ni1);
-        pair((uint32_t)(res & 0xFFFFu), (uint32_t)((res >> 16) & 0xFFFFu),
-             unit_laplace(u53(wx.w0, wx.w1)), unit_laplace(u53(wy.w0, wy.w1)));
-        if (want == 4)
-          pair((uint32_t)((res >> 32) & 0xFFFFu), (uint32_t)(res >> 48),
-               unit_laplace(u53(wx.w2, wx.w3)), unit_laplace(u53(wy.w2, wy.w3)));
+        pair(g2[2 * q], unit_laplace(u53(wx.w0, wx.w1)), unit_laplace(u53(wy.w0, wy.w1)));
+        if (2 * q + 1 < c.k)
+          pair(g2[2 * q + 1], unit_laplace(u53(wx.w2, wx.w3)), unit_laplace(u53(wy.w2, wy.w3)));
       }
     } else {
       for (int64_t j = tid; j < c.k; j += DICT_NT) {
@@ -1046,7 +1043,7 @@ __global__ __launch_bounds__(DICT_NT, WPE) void k_hrs_fused(PrematSubgConst p, H
         const double lyj = unit_laplace((j & 1) ? u53(wy.w2, wy.w3) : u53(wy.w0, wy.w1));
         DD bx{0, 0}, by{0, 0};
         for (int r = 0; r < c.m; ++r) {
-          const uint32_t a = cod[hrs_walk((uint32_t)(j * c.m + r), n, hk.pa, hk.pc, kk)];
+          const uint32_t a = gs[j * c.m + r];
           dd_acc(bx, dX[a & 255u]);
           dd_acc(by, dY[a >> 8]);
         }
@@ -1147,9 +1144,14 @@ int launch_hrs_fused(const PrematSubgConst& c, uint64_t seed_ni, uint64_t seed_i
     return (int)hipGetLastError();
   const int64_t slots = (int64_t)cus * (per_cu < 1 ? 1 : per_cu);
   const int64_t grid = reps < slots ? reps : slots;
+  const int64_t stride = (c.s.k * c.s.m + 63) & ~(int64_t)63;  // u16 codes per scratch row
+  void* scr = nullptr;
+  if (hipMallocAsync(&scr, (size_t)(grid * stride * 2), (hipStream_t)stream) != hipSuccess)
+    return (int)hipGetLastError();
   hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(DICT_NT), lds,
                      (hipStream_t)stream, c, hk, c.dict_codes, c.dict_vals, reps,
-                     (SubgPartial*)part);
+                     (SubgPartial*)part, (uint16_t*)scr, stride);
+  (void)hipFreeAsync(scr, (hipStream_t)stream);
   hipLaunchKernelGGL(k_hrs_fused_epilogue, dim3((unsigned)reps), dim3(DCOR_BLOCK), 0,
                      (hipStream_t)stream, c, hk, (const SubgPartial*)part, out);
   return (int)hipGetLastError();
