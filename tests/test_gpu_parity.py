@@ -173,3 +173,34 @@ def test_fused_split_invariance(dc):
     a = simulate(cell, 96).cpu().numpy()
     b = np.concatenate([simulate(cell, 40, 0).cpu().numpy(), simulate(cell, 56, 40).cpu().numpy()])
     assert np.array_equal(a, b)
+
+
+# C3 size (n = 1e6, the grids' largest n): every fused kernel family
+# against the oracle fed the same Philox streams, replicates 7 and 8 of each cell.
+C3_CELLS = [
+    dict(rho=0.5, eps1=1.0, eps2=1.0, family="sign", dgp="gaussian", mu=(0.5, 0.5), sigma=(2.0, 2.0)),
+    dict(rho=0.8, eps1=1.5, eps2=0.5, family="sign", dgp="gaussian", mu=(0.5, 0.5), sigma=(2.0, 2.0)),
+    dict(rho=0.3, eps1=1.0, eps2=1.0, family="sign", dgp="bernoulli"),
+    dict(rho=0.65, eps1=0.5, eps2=1.5, family="subG", dgp="bounded_factor"),
+    dict(rho=0.6, eps1=1.0, eps2=1.0, family="subG", dgp="mix_gaussian"),
+]
+
+
+@pytest.mark.parametrize("spec", C3_CELLS)
+def test_fused_vs_oracle_n1e6(dc, orc, spec):
+    from dcor.sim import CellSpec, simulate
+    cell = CellSpec(n=1_000_000, seed=1_000_211, **spec)
+    got = simulate(cell, 2, rep_begin=7).cpu().numpy()
+    ref = orc.sim_reps(cell.to_c(), 7, 9)
+    assert_close(got, ref, what=f"fused n=1e6 {spec}")
+
+
+def test_fused_split_invariance_n1e6(dc):
+    """At n = 1e6 a replicate's result is the same alone or inside a larger launch."""
+    from dcor.sim import headline_cell, simulate
+    cell = headline_cell(1_000_000)
+    a = simulate(cell, 12).cpu().numpy()
+    b = np.concatenate([simulate(cell, 5, 0).cpu().numpy(), simulate(cell, 7, 5).cpu().numpy()])
+    assert np.array_equal(a, b)
+    assert np.all(np.isfinite(a))
+    assert np.all((a[:, 1] <= a[:, 2]) & (a[:, 4] <= a[:, 5]))
