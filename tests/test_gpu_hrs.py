@@ -53,6 +53,33 @@ def test_hrs_replicates_match_oracle(panel, eps):
         assert_close(res[r], np.concatenate([ni, it]), what=f"hrs eps={eps} rep {rep}")
 
 
+def test_hrs_replicates_match_oracle_c5_size():
+    """C5's geometry (n = 19,433, eps = 2 -> m = 2, k = 9,716): the on-device noise and both
+    estimators against the oracle, replicates 40 and 41."""
+    from dcor import hrs
+    from oracle import oracle as orc
+    age, bmi = hrs.standin_panel(19_433, -0.3, seed=11)
+    z = hrs.standardize_panel(age, bmi, lap=np.array([-0.1, 0.25, 0.05, -0.3]))
+    n, eps, rb = 19_433, 2.0, 40
+    res, noise, geo = hrs.hrs_replicates(z["age_z"], z["bmi_z"], z["lambda_age_z"], z["lambda_bmi_z"], eps,
+                                         2, seed_ni=77, seed_int=78, rep_begin=rb, keep_noise=True)
+    k, m = geo["k"], geo["m"]
+    assert (k, m) == (9716, 2)
+    for r in range(2):
+        rep = rb + r
+        np.testing.assert_array_equal(noise["perm"][r], orc.perm(77, 8, rep, n, k * m))
+        np.testing.assert_array_equal(noise["lap_local"][r], orc.gen_laplace(78, rep, hrs.SITE_INT_LOCAL, n))
+        st, ni, _ = orc.ni_subg(z["age_z"], z["bmi_z"], eps, eps, hrs=1, lam_x=z["lambda_age_z"],
+                                lam_y=z["lambda_bmi_z"], perm=noise["perm"][r], lap_x=noise["lap_x"][r],
+                                lap_y=noise["lap_y"][r])
+        st2, it, _ = orc.int_subg(z["age_z"], z["bmi_z"], eps, eps, hrs=1, lam_s=z["lambda_age_z"],
+                                  lam_o=z["lambda_bmi_z"], lam_r=geo["lam_r"], delta=geo["delta"],
+                                  lap_local=noise["lap_local"][r], lap_central=noise["lap_central"][r],
+                                  mix_z=noise["mix_z"][r], mix_l=noise["mix_l"][r])
+        assert st == 0 and st2 == 0
+        assert_close(res[r], np.concatenate([ni, it]), what=f"hrs C5 size rep {rep}")
+
+
 def test_hrs_replicates_split_invariant(panel):
     from dcor import hrs
     z = panel
