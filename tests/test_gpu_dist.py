@@ -1,0 +1,88 @@
+"""GPU tests of the replicate-sharding path (dcor.dist; replaces mclapply over cells,
+vert-cor.R:534-553): the RCCL all-gather at world size 1 on this box's one GPU, and two
+ranks sharing cuda:0 over gloo -- each rank simulates its shard on the GPU, the merged
+summaries equal the rank-ordered merge of the same shards computed in one process."""
+import os
+import socket
+
+import pytest
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+B = 37  # odd: the two shards differ in size
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _cells():
+    from dcor.sim import CellSpec, headline_cell
+    return [headline_cell(5000),
+            CellSpec(n=3001, rho=0.65, eps1=1.5, eps2=0.5, family="subG", dgp="bounded_factor", seed=1_000_007),
+            CellSpec(n=2000, rho=0.3, eps1=1.0, eps2=1.0, family="sign", dgp="bernoulli", seed=1_000_008)]
+
+
+def _expected(world):
+    """Per-rank shard accumulators computed in this process, merged in rank order."""
+    from dcor.dist import merge_ranked, shard
+    from dcor.sim import accum_from_bytes, accumulate, simulate
+    per_rank = []
+    for r in range(world):
+        b0, nb = shard(B, r, world)
+        local = []
+        for cell in _cells():
+            out = simulate(cell, nb, b0)
+            local.extend(accum_from_bytes(accumulate(out, cell.rho).cpu().numpy().tobytes()))
+        per_rank.append(local)
+    return [bytes(a) for a in merge_ranked(per_rank)]
+
+
+def _flat(merged):
+    return [bytes(a) for pair in merged for a in pair]
+
+
+def test_run_grid_distributed_rccl_world1():
+    import torch
+    import torch.distributed as dist
+    from dcor.dist import run_grid_distributed
+    assert torch.cuda.is_available()
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        assert dist.get_backend() == "nccl"
+        got = _flat(run_grid_distributed(_cells(), B))
+    finally:
+        dist.destroy_process_group()
+    assert got == _expected(1)
+
+
+def _worker(rank, world, port, q):
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from dcor.dist import run_grid_distributed
+    q.put((rank, _flat(run_grid_distributed(_cells(), B))))
+    dist.destroy_process_group()
+
+
+def test_run_grid_distributed_two_ranks_on_gpu():
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=100) for _ in range(world))
+    for p in procs:
+        p.join(timeout=30)
+        assert p.exitcode == 0
+    assert res[0] == res[1]
+    assert res[0] == _expected(world)
