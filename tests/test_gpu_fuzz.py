@@ -66,3 +66,31 @@ def test_rstream_fuzz(block):
             continue
         got = rstream.run_grid([cell], 3)[0]["records"]
         assert _agree(got, ref), (cell, got, ref)
+
+
+def test_degenerate_cells_and_empty_launches():
+    """n = 1 (no full batch: the oracle's status must be the engine's), zero-replicate
+    launches on every kernel family, and cells the C-ABI must refuse (n = 0, eps = 0,
+    alpha = 1, gen_bounded_factor with rho < 0) -- refused, never launched."""
+    from dcor import CellSpec, _lib
+    from dcor.sim import simulate
+    from oracle import oracle as orc
+    for fam, dgp in (("sign", "gaussian"), ("sign", "bernoulli"), ("subG", "bounded_factor"),
+                     ("subG", "mix_gaussian")):
+        cell = CellSpec(n=1, rho=0.5, eps1=1.0, eps2=1.0, family=fam, dgp=dgp, seed=9)
+        try:
+            ref = orc.sim_reps(cell.to_c(), 0, 2)
+        except RuntimeError:
+            with pytest.raises(_lib.DcorError):
+                simulate(cell, 2).cpu()
+        else:
+            assert _agree(simulate(cell, 2).cpu().numpy(), ref), (cell, ref)
+        empty = simulate(CellSpec(n=1000, rho=0.5, eps1=1.0, eps2=1.0, family=fam, dgp=dgp, seed=9), 0)
+        assert tuple(empty.shape) == (0, 6)
+    bad = (dict(n=0), dict(eps1=0.0), dict(eps2=-1.0), dict(alpha=1.0),
+           dict(family="subG", dgp="bounded_factor", rho=-0.2))
+    for kw in bad:
+        base = dict(n=1000, rho=0.5, eps1=1.0, eps2=1.0, family="sign", dgp="gaussian", seed=9)
+        base.update(kw)
+        with pytest.raises(_lib.DcorError):
+            simulate(CellSpec(**base), 4).cpu()
