@@ -111,10 +111,22 @@ void mvrnorm_factor(const double sigma[2], double rho, double A[4]) {
   A[2] = v1 * a1; A[3] = v0 * a2;
 }
 
+// MASS::mvrnorm's check: stop("'Sigma' is not positive definite") unless every eigenvalue
+// ev >= -tol * |ev[1]| with tol = 1e-6 (ev decreasing).  False for |rho| > 1 (beyond tol).
+bool mvrnorm_pd(const double sigma[2], double rho) {
+  const double s11 = sigma[0] * sigma[0], s12 = sigma[0] * sigma[1] * rho, s22 = sigma[1] * sigma[1];
+  const double mid = (s11 + s22) / 2.0, hd = (s11 - s22) / 2.0;
+  const double d = std::sqrt(hd * hd + s12 * s12);
+  const double l1 = mid + d, l2 = mid - d;
+  return !std::isnan(l2) && l1 >= -1e-6 * std::fabs(l1) && l2 >= -1e-6 * std::fabs(l1);
+}
+
 int make_dgp(const dcor_cell& c, DgpConst& g) {
   std::memset(&g, 0, sizeof(g));
   g.dgp = c.dgp;
   if (c.dgp == DCOR_DGP_GAUSSIAN) {
+    if (!mvrnorm_pd(c.sigma, c.rho))
+      return fail(DCOR_EINVAL, "mvrnorm: 'Sigma' is not positive definite (|rho| > 1; MASS::mvrnorm, vert-cor.R:394)");
     double A[4];
     mvrnorm_factor(c.sigma, c.rho, A);
     g.mu0 = c.mu[0]; g.mu1 = c.mu[1];
@@ -127,11 +139,15 @@ int make_dgp(const dcor_cell& c, DgpConst& g) {
     g.T0_24 = (uint32_t)std::ceil(g.thr0 * 16777216.0);  // thr <= 1: exact scaling, <= 2^24
     g.T1_24 = (uint32_t)std::ceil(g.thr1 * 16777216.0);
   } else if (c.dgp == DCOR_DGP_BOUNDED_FACTOR) {
-    if (!(c.rho >= 0 && c.rho <= 1)) return fail(DCOR_EINVAL, "gen_bounded_factor: rho in [0,1] required");
     g.cU = std::sqrt(3.0 * c.rho); g.cE = std::sqrt(3.0 * (1.0 - c.rho));  // ver-cor-subG.R:148-149
     g.cU2 = g.cU - -g.cU; g.cE2 = g.cE - -g.cE;
+    // rho outside [0, 1]: R's sqrt gives NaN (a warning) and runif(n, NaN, NaN) NaN draws, so the
+    // replicate's estimates are all NaN; the launch writes those without generating anything.
+    g.nan_dgp = (std::isnan(g.cU) || std::isnan(g.cE)) ? 1 : 0;
   } else if (c.dgp == DCOR_DGP_MIX_GAUSSIAN) {
     if (!(c.mix_pi >= 0 && c.mix_pi <= 1)) return fail(DCOR_EINVAL, "gen_mix_gaussian: pi_mix in [0,1] required");
+    if (!mvrnorm_pd(c.mix_sigma0, c.rho) || !mvrnorm_pd(c.mix_sigma1, c.rho))
+      return fail(DCOR_EINVAL, "gen_mix_gaussian: mvrnorm 'Sigma' is not positive definite (|rho| > 1)");
     mvrnorm_factor(c.mix_sigma0, c.rho, g.xa[0]);   // ver-cor-subG.R:119-122
     mvrnorm_factor(c.mix_sigma1, c.rho, g.xa[1]);
     g.xmu[0][0] = c.mix_mu0[0]; g.xmu[0][1] = c.mix_mu0[1];
@@ -148,7 +164,12 @@ int check_common(int64_t n, double eps1, double eps2, double alpha) {
   if (n < 1 || n > 0x7fffffffLL) return fail(DCOR_EINVAL, "n must be in [1, 2^31) (got %lld)", (long long)n);
   if (!(eps1 > 0) || !(eps2 > 0) || !std::isfinite(eps1) || !std::isfinite(eps2))
     return fail(DCOR_EINVAL, "eps1 > 0 and eps2 > 0 required (vert-cor.R:264)");
-  if (!(alpha > 0 && alpha < 1)) return fail(DCOR_EINVAL, "alpha must be in (0,1)");
+  // The reference never checks alpha: qnorm(1 - alpha/2) and mixquant's
+  // sort(x)[ceiling((1 - alpha/2) nsim)] are evaluated as they come (alpha = 1: a zero-width
+  // CI; alpha < 0: NaN).  alpha >= 2 makes the mixquant index < 1, where R's x[0] is
+  // numeric(0) and run_sim_one's detail assignment fails, so it is refused here.
+  if (std::isnan(alpha) || !(alpha < 2))
+    return fail(DCOR_EINVAL, "alpha must be < 2 (R's mixquant index ceiling((1-alpha/2)*nsim) >= 1)");
   return DCOR_OK;
 }
 
@@ -431,6 +452,21 @@ int dcor_sim_launch(const dcor_cell* cell, int64_t rep_begin, int64_t rep_count,
   const dcor_cell& c = *cell;
   DgpConst g;
   if (int st = make_dgp(c, g)) return st;
+  if (g.nan_dgp) {  // every estimate NaN (see make_dgp); the estimators' own checks still apply
+    if (c.family == DCOR_FAMILY_SIGN) {
+      SignConst k;
+      if (int st = make_sign(c.n, c.eps1, c.eps2, c.alpha, c.normalise, c.ci_mode, c.nsim, false, k)) return st;
+    } else if (c.family == DCOR_FAMILY_SUBG) {
+      SubgConst k;
+      if (int st = make_subg(c.n, c.eps1, c.eps2, c.eta1, c.eta2, c.alpha, 0, NAN, NAN, NAN, NAN,
+                             NAN, NAN, c.nsim, k, nullptr, nullptr)) return st;
+    } else {
+      return fail(DCOR_EINVAL, "unknown family %d", c.family);
+    }
+    if (rep_count > 0)
+      HIPCHK(hipMemsetAsync(d_out, 0xFF, sizeof(dcor_rep_out) * (size_t)rep_count, (hipStream_t)stream));
+    return DCOR_OK;
+  }
   int rc;
   if (c.family == DCOR_FAMILY_SIGN) {
     SignConst k;
@@ -484,7 +520,7 @@ int dcor_sim_launch(const dcor_cell* cell, int64_t rep_begin, int64_t rep_count,
       if (nch == 1 && rep_count >= 512) nch = 2;  // two chunks at least: pass 2 of one beside pass 1 of the other
       const int64_t chunk = (rep_count + nch - 1) / nch;
       const size_t slab_b = ((size_t)chunk * per_rep + 255) / 256 * 256;
-      const size_t sums_b = ((size_t)chunk * (4 * sizeof(double) + 48) + 255) / 256 * 256;
+      const size_t sums_b = ((size_t)chunk * (8 * sizeof(double) + 48) + 255) / 256 * 256;
       const int nbuf = nch > 1 ? 2 : 1;
       void* scratch = nullptr;
       if (int st = arena_get(nbuf * (slab_b + sums_b), &scratch)) return st;
@@ -1146,6 +1182,13 @@ int rs_plan(const dcor_cell& cell, RsPlan& p) {
   if (cell.dgp == DCOR_DGP_MIX_GAUSSIAN && (n > RS_MIX_NMAX || !(cell.mix_pi >= 0.0 && cell.mix_pi <= 1.0)))
     return fail(DCOR_EINVAL, "rstream: gen_mix_gaussian needs n <= %d and 0 <= pi_mix <= 1", RS_MIX_NMAX);
   if (cell.seed > 0x7fffffffull) return fail(DCOR_EINVAL, "rstream: set.seed takes a 32-bit integer");
+  if ((cell.dgp == DCOR_DGP_GAUSSIAN && !mvrnorm_pd(cell.sigma, cell.rho)) ||
+      (cell.dgp == DCOR_DGP_MIX_GAUSSIAN &&
+       (!mvrnorm_pd(cell.mix_sigma0, cell.rho) || !mvrnorm_pd(cell.mix_sigma1, cell.rho))))
+    return fail(DCOR_EINVAL, "rstream: mvrnorm 'Sigma' is not positive definite (|rho| > 1)");
+  if (cell.dgp == DCOR_DGP_BERNOULLI && !(std::fabs(cell.rho) <= 1))
+    return fail(DCOR_EINVAL, "rstream: gen_bernoulli needs |rho| <= 1 (vert-cor.R:79)");
+  if (int st = check_common(n, cell.eps1, cell.eps2, cell.alpha)) return st;
   c.n = n; c.nsim = cell.nsim; c.family = cell.family; c.dgp = cell.dgp;
   const bool subg = cell.family == DCOR_FAMILY_SUBG;
   c.normalise = (!subg && cell.normalise) ? 1 : 0;

@@ -80,10 +80,11 @@ __device__ __forceinline__ double mixquant_loaded(const MixConst& mx, double c, 
 // ------------------------------------------------- sign-family epilogues
 struct SignStd { double muNx, sdNx, muNy, sdNy, muIx, sdIx, muIy, sdIy; };
 
-__device__ __forceinline__ void priv_std_from_sums(const SignConst& c, const double v[4],
-                                                   const double lap[8], SignStd& s) {
-  // vert-cor.R:335-344 with mean(xc) = sum/n (R: LD mean, agrees to rounding)
-  const double mx = v[0] / c.nd, m2x = v[1] / c.nd, my = v[2] / c.nd, m2y = v[3] / c.nd;
+// vert-cor.R:335-344 from mean(xc), mean(xc^2), mean(yc), mean(yc^2): NI thresholds with
+// draws lap[0..3], INT thresholds (fresh noise, :271-272) with lap[4..7].
+__device__ __forceinline__ void priv_std_from_means(const SignConst& c, double mx, double m2x,
+                                                    double my, double m2y, const double lap[8],
+                                                    SignStd& s) {
   s.muNx = mx + c.s_mu_x * lap[0];
   s.sdNx = sqrt(rmax((m2x + c.s_m2_x * lap[1]) - s.muNx * s.muNx, 1e-12));
   s.muNy = my + c.s_mu_y * lap[2];
@@ -92,6 +93,12 @@ __device__ __forceinline__ void priv_std_from_sums(const SignConst& c, const dou
   s.sdIx = sqrt(rmax((m2x + c.s_m2_x * lap[5]) - s.muIx * s.muIx, 1e-12));
   s.muIy = my + c.s_mu_y * lap[6];
   s.sdIy = sqrt(rmax((m2y + c.s_m2_y * lap[7]) - s.muIy * s.muIy, 1e-12));
+}
+
+__device__ __forceinline__ void priv_std_from_sums(const SignConst& c, const double v[4],
+                                                   const double lap[8], SignStd& s) {
+  // mean(xc) = sum/n (R: LD mean, agrees to rounding)
+  priv_std_from_means(c, v[0] / c.nd, v[1] / c.nd, v[2] / c.nd, v[3] / c.nd, lap, s);
 }
 
 __device__ __forceinline__ void ni_sign_result(const SignConst& c, DD sT, DD sT2, bool bad,

@@ -13,7 +13,9 @@ namespace dcor {
 
 struct DgpConst {
   int32_t dgp;
-  int32_t pad;
+  int32_t nan_dgp;                      // gen_bounded_factor with rho outside [0, 1]: sqrt(3 rho)
+                                        // or sqrt(3 (1 - rho)) is NaN, runif(n, NaN, NaN) gives
+                                        // NaN, so every estimate of the replicate is NaN
   double mu0, mu1, a00, a01, a10, a11;  // Gaussian: X = mu + A z  (MASS::mvrnorm)
   double thr0, thr1;                    // Bernoulli: p01/0.5, p11/0.5
   uint64_t T0, T1;                      // ceil(thr*2^32): u32*2^-32 < thr  <=>  u32 < T

@@ -304,16 +304,21 @@ __device__ __forceinline__ void exact_signs(const SignConst& c, const SignStd& s
   iy = sgn_std(yc, s.muIy, s.sdIy, bad_int);
 }
 
-// Pass 1: replicate r of the chunk -> slab r (n records) and its 4 clipped sums.
+// Pass 1: replicate `rep` -> its slab (n records) and its clipped sums (SIGN_SUMS doubles:
+// sum clip(x) as double-double {hi, lo}, sum clip(x)^2, the same for y).  The sums of clip(x),
+// clip(y) decide the private centres, hence every sign (vert-cor.R:335-347), so they are
+// compensated: each thread adds its group of 4 samples plainly and folds the group sum into a
+// TwoSum accumulator; the workgroup reduction is double-double.  The second moments only set
+// sd > 0, which never changes a sign, and stay plain sums.
+#define SIGN_SUMS 8
 template <int DGP>
-__global__ __launch_bounds__(DCOR_BLOCK) void k_sign_pass1(SignConst c,
-                                                           uint32_t* __restrict__ scratch,
-                                                           double* __restrict__ sums) {
+__device__ __forceinline__ void sign_pass1_body(const SignConst& c, uint32_t rep,
+                                                uint32_t* __restrict__ slab,
+                                                double* __restrict__ sums_out) {
   __shared__ double red[16 * DCOR_WAVES];
   const int tid = threadIdx.x;
-  const uint32_t rep = (uint32_t)(c.rep_begin + blockIdx.x);
-  uint32_t* slab = scratch + (size_t)blockIdx.x * (size_t)c.n;
-  double v[4] = {0.0, 0.0, 0.0, 0.0};
+  DD sx{0.0, 0.0}, sy{0.0, 0.0};
+  double v[2] = {0.0, 0.0};
   const int64_t ngrp = (c.n + 3) / 4;
   for (int64_t g4 = tid; g4 < ngrp; g4 += DCOR_BLOCK) {
     const uint32_t i0 = (uint32_t)(4 * g4);
@@ -331,23 +336,48 @@ __global__ __launch_bounds__(DCOR_BLOCK) void k_sign_pass1(SignConst c,
       for (int q = 0; q < 4; ++q) fl[q] = ((uint64_t)word(fw, q) < c.flipT) ? 1u : 0u;
     }
     uint32_t rec[4];
+    double gx = 0.0, gy = 0.0;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const double xc = rclip_fin(x[q], c.L), yc = rclip_fin(y[q], c.L);
-      if ((int64_t)(i0 + q) < c.n) { v[0] += xc; v[1] += xc * xc; v[2] += yc; v[3] += yc * yc; }
+      if ((int64_t)(i0 + q) < c.n) { gx += xc; v[0] += xc * xc; gy += yc; v[1] += yc * yc; }
       const uint32_t qx = code16(xc, c.cinv_xf, c.cnb_xf, 65535.0f);
       const uint32_t qy = code16(yc, c.cinv_yf, c.cnb_yf, 32767.0f);
       const uint32_t f = fl[q];
       rec[q] = qx | (qy << 16) | (f << 31);
     }
+    ks_acc(sx, gx);
+    ks_acc(sy, gy);
     if ((int64_t)i0 + 3 < c.n) {
       *reinterpret_cast<uint4*>(slab + i0) = make_uint4(rec[0], rec[1], rec[2], rec[3]);
     } else {
       for (int q = 0; q < 4; ++q) if ((int64_t)(i0 + q) < c.n) slab[i0 + q] = rec[q];
     }
   }
-  block_sum<4>(v, red);
-  if (tid < 4) sums[4 * (size_t)blockIdx.x + tid] = v[tid];
+  DD d2[2] = {sx, sy};
+  block_sum_dd<2>(d2, red);
+  block_sum<2>(v, red + 4 * DCOR_WAVES);
+  if (tid == 0) {
+    sums_out[0] = d2[0].hi; sums_out[1] = d2[0].lo; sums_out[2] = v[0];
+    sums_out[3] = d2[1].hi; sums_out[4] = d2[1].lo; sums_out[5] = v[1];
+  }
+}
+
+template <int DGP>
+__global__ __launch_bounds__(DCOR_BLOCK) void k_sign_pass1(SignConst c,
+                                                           uint32_t* __restrict__ scratch,
+                                                           double* __restrict__ sums) {
+  sign_pass1_body<DGP>(c, (uint32_t)(c.rep_begin + blockIdx.x),
+                       scratch + (size_t)blockIdx.x * (size_t)c.n, sums + SIGN_SUMS * (size_t)blockIdx.x);
+}
+
+// The private centres and scales from pass 1's sums (vert-cor.R:335-344): mean(xc) is the
+// double-double sum divided by n, rounded once.
+__device__ __forceinline__ void sign_std_from_pass1(const SignConst& c, const double* sums,
+                                                    const double lap[8], SignStd& s) {
+  const double mx = dd_div_d(DD{sums[0], sums[1]}, c.nd).hi;
+  const double my = dd_div_d(DD{sums[3], sums[4]}, c.nd).hi;
+  priv_std_from_means(c, mx, sums[2] / c.nd, my, sums[5] / c.nd, lap, s);
 }
 
 // Per-replicate partial results handed from pass 2 to the epilogue.
@@ -360,26 +390,22 @@ struct SignPartial {
 // Pass 2: signs from the codes (exact regeneration on a code tie), batch counts, NI
 // Laplace, T sums and the INT flip sum.  Lean: the mixquant/CI epilogue is its own kernel.
 template <int DGP>
-__global__ __launch_bounds__(DCOR_BLOCK) void k_sign_pass2(SignConst c,
-                                                           const uint32_t* __restrict__ scratch,
-                                                           const double* __restrict__ sums,
-                                                           SignPartial* __restrict__ part) {
+__device__ __forceinline__ void sign_pass2_body(const SignConst& c, uint32_t rep,
+                                                const uint32_t* __restrict__ slab,
+                                                const double* __restrict__ sums_in,
+                                                SignPartial* __restrict__ part_out) {
   __shared__ double red[16 * DCOR_WAVES];
   __shared__ long long redi[DCOR_WAVES];
   __shared__ double lap[10];
   const int tid = threadIdx.x;
-  const uint32_t rep = (uint32_t)(c.rep_begin + blockIdx.x);
-  const uint32_t* slab = scratch + (size_t)blockIdx.x * (size_t)c.n;
   scalar_laplace(rep, c.k0, c.k1, lap);
   __syncthreads();
   SignStd s;
   {
-    double v[4], l8[8];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) v[q] = sums[4 * (size_t)blockIdx.x + q];
+    double l8[8];
 #pragma unroll
     for (int q = 0; q < 8; ++q) l8[q] = lap[q];
-    priv_std_from_sums(c, v, l8, s);
+    sign_std_from_pass1(c, sums_in, l8, s);
   }
   const bool thr_nan = (s.muNx != s.muNx) || (s.muNy != s.muNy) || (s.muIx != s.muIx) ||
                        (s.muIy != s.muIy) || (s.sdNx != s.sdNx) || (s.sdNy != s.sdNy) ||
@@ -492,8 +518,18 @@ __global__ __launch_bounds__(DCOR_BLOCK) void k_sign_pass2(SignConst c,
     p.sT[0] = d2[0].hi; p.sT[1] = d2[0].lo; p.sT2[0] = d2[1].hi; p.sT2[1] = d2[1].lo;
     p.core = core;
     p.flags = ((nbad & 0xFFFFF) ? 1 : 0) | ((nbad >> 20) ? 2 : 0);
-    part[blockIdx.x] = p;
+    *part_out = p;
   }
+}
+
+template <int DGP>
+__global__ __launch_bounds__(DCOR_BLOCK) void k_sign_pass2(SignConst c,
+                                                           const uint32_t* __restrict__ scratch,
+                                                           const double* __restrict__ sums,
+                                                           SignPartial* __restrict__ part) {
+  sign_pass2_body<DGP>(c, (uint32_t)(c.rep_begin + blockIdx.x),
+                       scratch + (size_t)blockIdx.x * (size_t)c.n,
+                       sums + SIGN_SUMS * (size_t)blockIdx.x, part + blockIdx.x);
 }
 
 // Wave-per-replicate epilogue (four replicates per workgroup, no workgroup barriers):
@@ -823,27 +859,35 @@ __global__ __launch_bounds__(DCOR_BLOCK) void k_sign_fused(SignConst c, dcor_rep
   const uint32_t rep = (uint32_t)(c.rep_begin + blockIdx.x);
   const int tid = threadIdx.x;
   scalar_laplace(rep, c.k0, c.k1, lap);
-  double v[4] = {0.0, 0.0, 0.0, 0.0};
+  // the same compensated sums as k_sign_pass1 (groups of 4, TwoSum, double-double reduction)
+  DD sx{0.0, 0.0}, sy{0.0, 0.0};
+  double v[2] = {0.0, 0.0};
   if (c.normalise) {
     for (int64_t g4 = tid; 4 * g4 < c.n; g4 += DCOR_BLOCK) {
       double x[4], y[4];
       Dgp<DGP>::quad(c.g, (uint32_t)(4 * g4), rep, c.k0, c.k1, x, y);
+      double gx = 0.0, gy = 0.0;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         if (4 * g4 + q < c.n) {
           const double xc = rclip_fin(x[q], c.L), yc = rclip_fin(y[q], c.L);
-          v[0] += xc; v[1] += xc * xc; v[2] += yc; v[3] += yc * yc;
+          gx += xc; v[0] += xc * xc; gy += yc; v[1] += yc * yc;
         }
       }
+      ks_acc(sx, gx);
+      ks_acc(sy, gy);
     }
   }
-  block_sum<4>(v, red);
+  DD d2s[2] = {sx, sy};
+  block_sum_dd<2>(d2s, red);
+  block_sum<2>(v, red + 4 * DCOR_WAVES);
   SignStd s;
   {
     double l8[8];
 #pragma unroll
     for (int q = 0; q < 8; ++q) l8[q] = lap[q];
-    priv_std_from_sums(c, v, l8, s);
+    const double sums[6] = {d2s[0].hi, d2s[0].lo, v[0], d2s[1].hi, d2s[1].lo, v[1]};
+    sign_std_from_pass1(c, sums, l8, s);
   }
   FlipGen fl;
   fl.cidx = 0xffffffffu;
@@ -1006,7 +1050,7 @@ static int launch_codes_t(SignConst c, int64_t reps, int64_t chunk, const CodesB
     const int64_t nr = (reps - r < chunk) ? reps - r : chunk;
     const int b = two ? (int)(t & 1) : 0;
     c.rep_begin = rep0 + r;
-    SignPartial* part = reinterpret_cast<SignPartial*>(bf.sums[b] + 4 * chunk);
+    SignPartial* part = reinterpret_cast<SignPartial*>(bf.sums[b] + SIGN_SUMS * chunk);
     hipLaunchKernelGGL(k_sign_pass1<DGP>, dim3((unsigned)nr), dim3(DCOR_BLOCK), 0, st[b], c,
                        bf.slab[b], bf.sums[b]);
     hipLaunchKernelGGL(k_sign_pass2<DGP>, dim3((unsigned)nr), dim3(DCOR_BLOCK), 0, st[b], c,

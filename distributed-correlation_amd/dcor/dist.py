@@ -66,14 +66,16 @@ def run_grid_distributed(cells, B: int, group=None, stream=None):
     rank, world = dist.get_rank(group), dist.get_world_size(group)
     b0, nb = shard(B, rank, world)
     local = []
-    buf = torch.empty((max(nb, 1), 6), dtype=torch.float64, device="cuda")
-    for cell in cells:
-        if nb > 0:
-            simulate(cell, nb, b0, out=buf, stream=stream)
-            acc = accumulate(buf[:nb], cell.rho, stream=stream)
-            local.extend(accum_from_bytes(acc.cpu().numpy().tobytes()))
-        else:
-            local.extend([_lib.Accum(), _lib.Accum()])
+    s = torch.cuda.current_stream() if stream is None else stream
+    with torch.cuda.stream(s):   # torch's D2H copies run on the current stream
+        buf = torch.empty((max(nb, 1), 6), dtype=torch.float64, device="cuda")
+        for cell in cells:
+            if nb > 0:
+                simulate(cell, nb, b0, out=buf, stream=s)
+                acc = accumulate(buf[:nb], cell.rho, stream=s)
+                local.extend(accum_from_bytes(acc.cpu().numpy().tobytes()))
+            else:
+                local.extend([_lib.Accum(), _lib.Accum()])
     merged = merge_ranked(gather_accums(local, group))
     return [(merged[2 * i], merged[2 * i + 1]) for i in range(len(cells))]
 

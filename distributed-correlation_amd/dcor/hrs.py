@@ -24,7 +24,9 @@ AGE_LO, AGE_HI = 45.0, 90.0
 BMI_LO, BMI_HI = 15.0, 35.0
 EPS_MEAN, EPS_M2 = 0.10, 0.10
 EPS_CORR = 2.0
-EPS_GRID = tuple(round(0.25 + 0.1 * i, 10) for i in range(23))  # seq(0.25, 2.5, by = 0.1)
+# seq(0.25, 2.5, by = 0.1): R's seq.default computes from + (0:n) * by without rounding, so
+# e.g. the 7th value is 0.8500000000000001 (R prints 0.85); which(eps_grid == eps) matches these.
+EPS_GRID = tuple(0.25 + i * 0.1 for i in range(23))
 R_PER_EPS = 200
 NI_SEED, INT_SEED = 231, 322                                     # set.seed (:289, :312)
 
@@ -99,6 +101,14 @@ def hrs_replicates(age_z, bmi_z, lam_age, lam_bmi, eps, reps, seed_ni=NI_SEED, s
     import torch
 
     from . import _lib, api
+    if rng not in ("philox", "R"):
+        raise ValueError(f"rng must be 'philox' or 'R', not {rng!r}")
+    if mode not in ("premat", "fused"):
+        raise ValueError(f"mode must be 'premat' or 'fused', not {mode!r}")
+    if mode == "fused" and (rng != "philox" or keep_noise):
+        raise ValueError("mode='fused' draws Philox noise in the kernel: rng='philox', keep_noise=False")
+    if rng == "R" and eps_idx is None:
+        raise ValueError("rng='R' needs eps_idx (the 1-based position of eps in the sweep)")
     X = torch.as_tensor(np.ascontiguousarray(age_z, dtype=np.float64), device="cuda")
     Y = torch.as_tensor(np.ascontiguousarray(bmi_z, dtype=np.float64), device="cuda")
     n = int(X.shape[0])
@@ -132,14 +142,6 @@ def hrs_replicates(age_z, bmi_z, lam_age, lam_bmi, eps, reps, seed_ni=NI_SEED, s
     mz, ml = torch.empty((cr, nsim), **f64), torch.empty((cr, nsim), **f64)
     out = torch.empty((reps, 6), **f64)
     noise = {key: [] for key in ("perm", "lap_x", "lap_y", "lap_local", "lap_central", "mix_z", "mix_l")}
-    if rng not in ("philox", "R"):
-        raise ValueError(f"rng must be 'philox' or 'R', not {rng!r}")
-    if mode not in ("premat", "fused"):
-        raise ValueError(f"mode must be 'premat' or 'fused', not {mode!r}")
-    if mode == "fused" and (rng != "philox" or keep_noise):
-        raise ValueError("mode='fused' draws Philox noise in the kernel: rng='philox', keep_noise=False")
-    if rng == "R" and eps_idx is None:
-        raise ValueError("rng='R' needs eps_idx (the 1-based position of eps in the sweep)")
     try:
         for r0 in range(0, reps, cr):
             nr = min(cr, reps - r0)

@@ -126,6 +126,20 @@ def finalize(acc: _lib.Accum, rho: float) -> dict:
     return {"mse": s.mse, "bias": s.bias, "var": s.var, "coverage": s.coverage, "ci_length": s.ci_length}
 
 
+def r_cover(rho: float, lo, up) -> np.ndarray:
+    """R's `rho >= lo && rho <= up` (vert-cor.R:405) / vectorised `&` (ver-cor-subG.R:203) with
+    three-valued logic: FALSE if either comparison is FALSE, NA (NaN) if neither is FALSE and one
+    is NA, else TRUE -- the rule the device accumulator applies (k_accumulate)."""
+    lo = np.asarray(lo, dtype=np.float64)
+    up = np.asarray(up, dtype=np.float64)
+    with np.errstate(invalid="ignore"):
+        f1 = ~np.isnan(lo) & ~(rho >= lo)
+        f2 = ~np.isnan(up) & ~(rho <= up)
+    cov = np.where(np.isnan(lo) | np.isnan(up), np.nan, 1.0)
+    cov[f1 | f2] = 0.0
+    return cov
+
+
 def detail_frame(rec: np.ndarray, rho: float) -> dict:
     """run_sim_one's `detail` (vert-cor.R:367-417) from the six per-replicate numbers."""
     rec = np.asarray(rec, dtype=np.float64).reshape(-1, 6)
@@ -135,28 +149,28 @@ def detail_frame(rec: np.ndarray, rho: float) -> dict:
     for m in ("ni", "int"):
         lo, up, hat = d[f"{m}_low"], d[f"{m}_up"], d[f"{m}_hat"]
         d[f"{m}_se2"] = (hat - rho) ** 2
-        with np.errstate(invalid="ignore"):
-            cov = (rho >= lo) & (rho <= up)
-        cov = cov.astype(float)
-        cov[np.isnan(lo) | np.isnan(up)] = np.nan
-        d[f"{m}_cover"] = cov
+        d[f"{m}_cover"] = r_cover(rho, lo, up)
         d[f"{m}_ci_len"] = up - lo
     return d
 
 
 def run_cell(cell: CellSpec, B: int, detail: bool = True, chunk: int = 1 << 16, stream=None) -> dict:
-    """All B replicates of one cell on the current GPU -> {'detail', 'summary'}."""
+    """All B replicates of one cell on the current GPU -> {'detail', 'summary'}.  With a
+    `stream`, buffers are allocated, filled and copied back on that stream (torch's D2H copy
+    runs on the current stream, so the loop runs with `stream` current)."""
     torch = _torch()
     recs = []
     accs = []
-    buf = torch.empty((min(B, chunk), 6), dtype=torch.float64, device="cuda")
-    for r0 in range(0, B, chunk):
-        nr = min(chunk, B - r0)
-        simulate(cell, nr, r0, out=buf, stream=stream)
-        a = accumulate(buf[:nr], cell.rho, stream=stream)
-        accs.extend(accum_from_bytes(a.cpu().numpy().tobytes()))
-        if detail:
-            recs.append(buf[:nr].cpu().numpy().copy())
+    s = torch.cuda.current_stream() if stream is None else stream
+    with torch.cuda.stream(s):
+        buf = torch.empty((min(B, chunk), 6), dtype=torch.float64, device="cuda")
+        for r0 in range(0, B, chunk):
+            nr = min(chunk, B - r0)
+            simulate(cell, nr, r0, out=buf, stream=s)
+            a = accumulate(buf[:nr], cell.rho, stream=s)
+            accs.extend(accum_from_bytes(a.cpu().numpy().tobytes()))
+            if detail:
+                recs.append(buf[:nr].cpu().numpy().copy())
     ni = merge(accs[0::2])
     it = merge(accs[1::2])
     summary = {"NI": finalize(ni, cell.rho), "INT": finalize(it, cell.rho)}

@@ -416,6 +416,30 @@ void orc_mvrnorm_factor(const double mu[2], const double sigma[2], double rho, d
   A[2] = v1 * a1;   A[3] = v0 * a2;
 }
 
+/* MASS::mvrnorm: stop("'Sigma' is not positive definite") unless all(ev >= -tol*abs(ev[1]))
+ * with tol = 1e-6 and ev = eigen(Sigma)$values (decreasing). */
+static int mvrnorm_pd(const double sigma[2], double rho) {
+  const double s11 = sigma[0] * sigma[0], s12 = sigma[0] * sigma[1] * rho, s22 = sigma[1] * sigma[1];
+  const double mid = (s11 + s22) / 2.0, hd = (s11 - s22) / 2.0;
+  const double d = sqrt(hd * hd + s12 * s12);
+  const double l1 = mid + d, l2 = mid - d;
+  return !isnan(l2) && l1 >= -1e-6 * fabs(l1) && l2 >= -1e-6 * fabs(l1);
+}
+
+/* The argument errors R raises for a cell before any draw: mvrnorm's positive-definite check
+ * (vert-cor.R:394, ver-cor-subG.R:131-132), gen_bernoulli's stopifnot(abs(rho) <= 1)
+ * (vert-cor.R:79), and alpha >= 2, where mixquant's index ceiling((1-alpha/2)*nsim) < 1 makes
+ * sort(x)[.] numeric(0) and the replicate's detail assignment fails. */
+int orc_cell_check(const void* cellp) {
+  const dcor_cell* c = (const dcor_cell*)cellp;
+  if (isnan(c->alpha) || !(c->alpha < 2)) return DCOR_EINVAL;
+  if (c->dgp == DCOR_DGP_GAUSSIAN && !mvrnorm_pd(c->sigma, c->rho)) return DCOR_EINVAL;
+  if (c->dgp == DCOR_DGP_MIX_GAUSSIAN &&
+      (!mvrnorm_pd(c->mix_sigma0, c->rho) || !mvrnorm_pd(c->mix_sigma1, c->rho))) return DCOR_EINVAL;
+  if (c->dgp == DCOR_DGP_BERNOULLI && !(fabs(c->rho) <= 1)) return DCOR_EINVAL;
+  return DCOR_OK;
+}
+
 void orc_mvrnorm_apply(const double* z1, const double* z2, int64_t n, const double mu[2],
                        const double A[4], double* X, double* Y) {
   for (int64_t i = 0; i < n; ++i) {
@@ -620,6 +644,7 @@ int orc_sim_rep(const void* cellp, int64_t rep, double out[6]) {
   const dcor_cell* c = (const dcor_cell*)cellp;
   const int64_t n = c->n;
   if (n < 1 || !(c->eps1 > 0) || !(c->eps2 > 0)) return DCOR_EINVAL;
+  if (orc_cell_check(c)) return DCOR_EINVAL;
   const int64_t nsim = c->nsim;
   const int subg = (c->family == DCOR_FAMILY_SUBG);
   double* X = (double*)malloc(sizeof(double) * (size_t)n);

@@ -118,6 +118,9 @@ void   orc_normal_pair(const uint32_t w[4], double* z1, double* z2);
  * the GPU engine draws them, then fed through the estimators above.
  * cell layout = dcor_cell in include/dcor.h.  out = {ni_hat, ni_lo, ni_hi,
  * int_hat, int_lo, int_hi}.  Returns status. */
+/* R's argument errors for a cell (mvrnorm's positive-definite check, gen_bernoulli's
+ * |rho| <= 1, alpha >= 2): DCOR_EINVAL, else DCOR_OK. */
+int orc_cell_check(const void* cell);
 int orc_sim_rep(const void* cell, int64_t rep, double out[6]);
 /* Replicates [r0, r1) on `threads` host threads (pthreads). */
 int orc_sim_reps(const void* cell, int64_t r0, int64_t r1, int threads, double* out);

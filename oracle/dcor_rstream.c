@@ -485,6 +485,7 @@ int orc_rs_sim(const void* cellp, int64_t B, double* out) {
   const dcor_cell* c = (const dcor_cell*)cellp;
   const int64_t n = c->n, nsim = c->nsim;
   if (n < 1 || !(c->eps1 > 0) || !(c->eps2 > 0) || c->seed > 0x7fffffffull) return DCOR_EINVAL;
+  if (orc_cell_check(c)) return DCOR_EINVAL;
   int64_t k;
   int mix;
   int s = orc_rs_geometry(cellp, &k, &mix);

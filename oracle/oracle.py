@@ -58,6 +58,7 @@ _sigs = {
     "orc_log": (C.c_double, [C.c_double]),
     "orc_sincospi": (None, [C.c_double, _D, _D]),
     "orc_unit_laplace": (C.c_double, [C.c_double]),
+    "orc_cell_check": (C.c_int, [C.c_void_p]),
     "orc_sim_rep": (C.c_int, [C.c_void_p, C.c_int64, _D]),
     "orc_sim_reps": (C.c_int, [C.c_void_p, C.c_int64, C.c_int64, C.c_int, _D]),
     "orc_gen_normals": (None, [C.c_uint64, C.c_int64, C.c_int, C.c_int64, _D]),

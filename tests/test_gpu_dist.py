@@ -60,6 +60,7 @@ def test_run_grid_distributed_rccl_world1():
     finally:
         dist.destroy_process_group()
     assert got == _expected(1)
+    _assert_equals_world1(got)
 
 
 def _worker(rank, world, port, q):
@@ -86,3 +87,39 @@ def test_run_grid_distributed_two_ranks_on_gpu():
         assert p.exitcode == 0
     assert res[0] == res[1]
     assert res[0] == _expected(world)
+    _assert_equals_world1(res[0])
+
+
+def _world1():
+    """The unsharded run: every replicate of each cell in one launch, one accumulation."""
+    from dcor.sim import accum_from_bytes, accumulate, simulate
+    out = []
+    for cell in _cells():
+        rec = simulate(cell, B, 0)
+        out.extend(accum_from_bytes(accumulate(rec, cell.rho).cpu().numpy().tobytes()))
+    return out
+
+
+def _assert_equals_world1(flat):
+    """Merged world-2 accumulators vs the world-1 run: counts exactly, every double-double sum
+    within 1e-15 relative, and the finalized summaries (mse, bias, var, coverage, ci_length;
+    vert-cor.R:422-430) within 1e-13 relative -- bias and var cancel (mean - rho,
+    E[x^2] - E[x]^2), which magnifies the sums' last-bit differences."""
+    import math
+
+    from dcor import _lib
+    from dcor.sim import finalize
+    ref = _world1()
+    cells = _cells()
+    for i, (raw, r) in enumerate(zip(flat, ref)):
+        a = _lib.Accum.from_buffer_copy(raw)
+        for f in ("n", "n_cover", "n_cover_na", "n_na_est", "n_na_ci"):
+            assert getattr(a, f) == getattr(r, f), (i, f)
+        for f in ("est", "est2", "se2", "len", "lo", "hi"):
+            x, y = getattr(a, f)[0] + getattr(a, f)[1], getattr(r, f)[0] + getattr(r, f)[1]
+            assert abs(x - y) <= 1e-15 * max(abs(x), abs(y), 1e-300) or x == y, (i, f, x, y)
+        rho = cells[i // 2].rho
+        sa, sr = finalize(a, rho), finalize(r, rho)
+        for k in sa:
+            x, y = sa[k], sr[k]
+            assert (math.isnan(x) and math.isnan(y)) or abs(x - y) <= 1e-13 * max(abs(x), abs(y)) + 1e-300, (i, k, x, y)

@@ -70,8 +70,10 @@ def test_rstream_fuzz(block):
 
 def test_degenerate_cells_and_empty_launches():
     """n = 1 (no full batch: the oracle's status must be the engine's), zero-replicate
-    launches on every kernel family, and cells the C-ABI must refuse (n = 0, eps = 0,
-    alpha = 1, gen_bounded_factor with rho < 0) -- refused, never launched."""
+    launches on every kernel family, and cells R itself refuses (n = 0, eps = 0: stopifnot;
+    mvrnorm's non-positive-definite Sigma at |rho| > 1; gen_bernoulli's |rho| <= 1;
+    alpha >= 2, where mixquant's index ceiling((1-alpha/2)*nsim) < 1) -- refused, never
+    launched."""
     from dcor import CellSpec, _lib
     from dcor.sim import simulate
     from oracle import oracle as orc
@@ -87,10 +89,38 @@ def test_degenerate_cells_and_empty_launches():
             assert _agree(simulate(cell, 2).cpu().numpy(), ref), (cell, ref)
         empty = simulate(CellSpec(n=1000, rho=0.5, eps1=1.0, eps2=1.0, family=fam, dgp=dgp, seed=9), 0)
         assert tuple(empty.shape) == (0, 6)
-    bad = (dict(n=0), dict(eps1=0.0), dict(eps2=-1.0), dict(alpha=1.0),
-           dict(family="subG", dgp="bounded_factor", rho=-0.2))
+    bad = (dict(n=0), dict(eps1=0.0), dict(eps2=-1.0), dict(alpha=2.0), dict(alpha=float("nan")),
+           dict(rho=1.5), dict(dgp="bernoulli", rho=-1.5), dict(family="subG", dgp="mix_gaussian", rho=2.0))
     for kw in bad:
         base = dict(n=1000, rho=0.5, eps1=1.0, eps2=1.0, family="sign", dgp="gaussian", seed=9)
         base.update(kw)
+        with pytest.raises(RuntimeError):
+            orc.sim_reps(CellSpec(**base).to_c(), 0, 1)
         with pytest.raises(_lib.DcorError):
             simulate(CellSpec(**base), 4).cpu()
+
+
+@pytest.mark.parametrize("kw", [
+    dict(alpha=1.0),                      # qnorm(.5) = 0, log(1/alpha) = 0: zero-width CIs
+    dict(alpha=1.0, ci_mode="laplace"),
+    dict(alpha=0.0),                      # qnorm(1) = Inf: CIs clipped to [-1, 1] (or NaN at se = 0)
+    dict(alpha=1.5),                      # inverted intervals, mixquant element ceiling(.25 nsim)
+    dict(alpha=-0.1),                     # qnorm(1.05) = NaN, mixquant index past nsim: NA CIs
+    dict(family="subG", dgp="bounded_factor", rho=-0.2),   # sqrt(3 rho) = NaN: runif NaN draws
+    dict(family="sign", dgp="bounded_factor", rho=1.3),    # sqrt(3 (1 - rho)) = NaN
+    dict(family="subG", alpha=1.0),
+])
+def test_r_semantics_edge_cells(kw):
+    """Cells R evaluates without error although they are degenerate: the engine returns R's
+    values (the oracle's), not a refusal (ver-cor-subG.R:57,101,148-152; vert-cor.R:242,302-308)."""
+    from dcor import CellSpec
+    from dcor.sim import simulate
+    from oracle import oracle as orc
+    base = dict(n=1000, rho=0.5, eps1=1.0, eps2=1.0, family="sign", dgp="gaussian", seed=9)
+    base.update(kw)
+    cell = CellSpec(**base)
+    ref = orc.sim_reps(cell.to_c(), 3, 7)
+    got = simulate(cell, 4, 3).cpu().numpy()
+    assert _agree(got, ref), (kw, got, ref)
+    if cell.dgp == "bounded_factor":
+        assert np.all(np.isnan(got))

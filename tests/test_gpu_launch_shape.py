@@ -1,0 +1,97 @@
+"""Oracle parity on the exact launch shapes the benchmarks time.
+
+bench.py launches 8192 headline replicates per step (n = 1e5): dcor_sim_launch splits them
+into 4 chunks of 2048 that alternate between the caller's stream and the library's
+auxiliary stream, each chunk with its own code slab (dcor_capi.cpp, launch_codes_t).  These
+tests run that same call -- same cell, same replicate count, a reused output buffer and the
+bench's replicate offsets -- and compare the replicates at every chunk and stream boundary
+with the CPU oracle fed the same Philox streams (orc_sim_reps; vert-cor.R:392-419).  The
+same is done for BASELINE config C2 (Bernoulli, n = 1e4, 1e4 replicates in one launch of
+k_sign_bern_w) and for the sub-G line S (bounded factor, n = 1e5, 4096 replicates).
+Tolerance: 1e-12 relative, 1e-13 absolute floor (tests/helpers.py)."""
+import numpy as np
+import pytest
+
+from helpers import assert_close
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def dc():
+    import torch
+    assert torch.cuda.is_available()
+    import dcor
+    return dcor
+
+
+@pytest.fixture(scope="module")
+def orc():
+    from oracle import oracle
+    return oracle
+
+
+def _oracle_at(orc, cell, r0, idx):
+    c = cell.to_c()
+    return np.stack([orc.sim_reps(c, r0 + int(i), r0 + int(i) + 1)[0] for i in idx])
+
+
+HEADLINE_IDX = [0, 1, 2047, 2048, 4095, 4096, 6143, 6144, 8190, 8191]
+
+
+@pytest.mark.parametrize("step", [0, 19])
+def test_headline_bench_shape(dc, orc, step):
+    """bench.py's step `step` at N = 1 (r0 = step * 8192) after a warm-up launch at another
+    offset into the same buffer: 4 chunks, 2 streams, the chunk boundaries vs the oracle."""
+    import torch
+    from dcor.sim import headline_cell, simulate
+    cell = headline_cell()
+    R = 8192
+    stream = torch.cuda.current_stream()
+    buf = torch.empty((R, 6), dtype=torch.float64, device="cuda")
+    simulate(cell, R, (20 + step) * R, out=buf, stream=stream)   # a warm-up step's replicates
+    simulate(cell, R, step * R, out=buf, stream=stream)
+    got = buf.cpu().numpy()[HEADLINE_IDX]
+    ref = _oracle_at(orc, cell, step * R, HEADLINE_IDX)
+    assert_close(got, ref, what=f"headline bench shape, step {step}")
+    assert np.all(np.isfinite(got))
+
+
+def test_headline_bench_shape_side_stream(dc, orc):
+    """The same launch on a non-default torch stream: the library's fork/join events order
+    its auxiliary stream after, and the caller's stream behind, every chunk."""
+    import torch
+    from dcor.sim import headline_cell, simulate
+    cell = headline_cell()
+    R = 8192
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        buf = torch.full((R, 6), float("nan"), dtype=torch.float64, device="cuda")
+        simulate(cell, R, 3 * R, out=buf, stream=s)
+        got = buf[HEADLINE_IDX].cpu().numpy()
+    ref = _oracle_at(orc, cell, 3 * R, HEADLINE_IDX)
+    assert_close(got, ref, what="headline on a side stream")
+
+
+@pytest.mark.parametrize("rho,eps", [(0.5, (1.0, 1.0)), (0.65, (1.5, 0.5)), (0.0, (0.5, 0.5))])
+def test_c2_bernoulli_launch_shape(dc, orc, rho, eps):
+    """C2: one cell of the Bernoulli grid, n = 1e4, all 1e4 replicates in one launch
+    (bench_configs.run_grid_gpu) -- wave-per-replicate k_sign_bern_w, four replicates per
+    workgroup, the last workgroup partial."""
+    from dcor.sim import expand_grid, simulate
+    cells = expand_grid([10_000], [0, 0.15, 0.3, 0.4, 0.5, 0.65, 0.8, 0.9],
+                        [(0.5, 0.5), (1.0, 1.0), (1.5, 0.5)], family="sign", dgp="bernoulli")
+    cell = next(c for c in cells if c.rho == rho and (c.eps1, c.eps2) == eps)
+    B = 10_000
+    got_all = simulate(cell, B).cpu().numpy()
+    idx = [0, 1, 3, 4, 5, 4095, 4096, 9995, 9996, 9999]
+    assert_close(got_all[idx], _oracle_at(orc, cell, 0, idx), what=f"C2 rho={rho} eps={eps}")
+
+
+def test_s_subg_launch_shape(dc, orc):
+    """S: sub-G bounded factor, n = 1e5, 4096 replicates in one k_subg_fused launch."""
+    from dcor.sim import CellSpec, simulate
+    cell = CellSpec(n=100_000, rho=0.5, eps1=1.0, eps2=1.0, family="subG", dgp="bounded_factor", seed=5)
+    got_all = simulate(cell, 4096).cpu().numpy()
+    idx = [0, 1, 2047, 2048, 4094, 4095]
+    assert_close(got_all[idx], _oracle_at(orc, cell, 0, idx), what="S launch shape")
