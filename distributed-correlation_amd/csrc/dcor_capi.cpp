@@ -6,7 +6,11 @@
 // device every compute entry fails with DCOR_ENODEV.
 #include <hip/hip_runtime.h>
 
+#include <unistd.h>
+
 #include <algorithm>
+#include <atomic>
+#include <mutex>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -17,10 +21,12 @@
 
 #include "../../include/dcor.h"
 #include "dcor_engine.h"
+#include "dcor_host.h"
 
 using namespace dcor;
 
-namespace {
+namespace dcor {
+namespace host {
 
 thread_local char g_err[512] = "";
 
@@ -36,13 +42,25 @@ int hip_fail(hipError_t e, const char* what) {
   return fail(DCOR_EHIP, "%s: %s", what, hipGetErrorString(e));
 }
 
-#define HIPCHK(expr)                                   \
-  do {                                                 \
-    hipError_t e_ = (expr);                            \
-    if (e_ != hipSuccess) return hip_fail(e_, #expr);  \
-  } while (0)
+
+// The process that first reached the device.  A process forked from it afterwards (R's
+// mclapply children) inherits no usable HIP state: every entry there fails with DCOR_EFORK
+// before touching HIP.
+std::atomic<int> g_owner_pid{0};
+
+int fork_guard() {
+  const int me = (int)getpid();
+  int owner = g_owner_pid.load();
+  if (owner == 0 && g_owner_pid.compare_exchange_strong(owner, me)) owner = me;
+  if (owner != me)
+    return fail(DCOR_EFORK, "the dcor engine was used in process %d before this process (%d) was "
+                            "forked (mclapply?): HIP does not survive fork(); run the grid from the "
+                            "parent with one dcor_grid_run call (R: dcor_grid)", owner, me);
+  return DCOR_OK;
+}
 
 int need_device() {
+  if (int st = fork_guard()) return st;
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) {
     (void)hipGetLastError();
@@ -293,19 +311,66 @@ int make_subg(int64_t n, double eps1, double eps2, double eta1, double eta2, dou
   return DCOR_OK;
 }
 
-// Per-device scratch arena for the one-pass sign kernel (grid * n * 4 B); owned by the
-// library, grown on demand outside any kernel, released by dcor_shutdown().
-struct Arena { void* p = nullptr; size_t bytes = 0; };
-Arena g_arena[64];
-// per-device auxiliary stream + fork/join events of the two-stream chunk pipeline
-struct Pipe { hipStream_t s = nullptr; hipEvent_t fork = nullptr, join = nullptr; };
-Pipe g_pipe[64];
+// Library-owned device state of one (host thread, device): the scratch arenas (the one-pass
+// sign kernel's code slabs, the batched grid's tables and partials, the R-stream buffers), the
+// auxiliary stream with the fork/join events of the two-stream chunk pipeline, and a pinned
+// staging buffer for the grid tables.  One per calling thread and device, so two host threads
+// never share scratch or streams; every context is registered for dcor_shutdown(), and the grid's
+// worker threads release theirs when they finish.
+std::mutex g_ctx_mu;
+std::vector<Ctx*> g_ctxs;            // every live context (guarded by g_ctx_mu)
+std::atomic<uint64_t> g_ctx_gen{1};  // bumped by dcor_shutdown: older thread caches are stale
+struct ThreadCtx { Ctx* c[64] = {}; uint64_t gen = 0; };
+thread_local ThreadCtx t_ctx;
 
-int pipe_get(Pipe** out) {
+void ctx_free(Ctx* c) {
+  if (c->pipe.s) {
+    (void)hipStreamSynchronize(c->pipe.s);
+    (void)hipStreamDestroy(c->pipe.s);
+    (void)hipEventDestroy(c->pipe.fork);
+    (void)hipEventDestroy(c->pipe.join);
+  }
+  if (c->staging_free) { (void)hipEventSynchronize(c->staging_free); (void)hipEventDestroy(c->staging_free); }
+  if (c->staging) (void)hipHostFree(c->staging);
+  for (Arena* a : {&c->codes, &c->rs, &c->grid})
+    if (a->p) (void)hipFree(a->p);
+  delete c;
+}
+
+int ctx_get(Ctx** out) {
   int dev = 0;
   HIPCHK(hipGetDevice(&dev));
   if (dev < 0 || dev >= 64) return fail(DCOR_EINVAL, "device id out of range");
-  Pipe& p = g_pipe[dev];
+  const uint64_t gen = g_ctx_gen.load();
+  if (t_ctx.gen != gen) { t_ctx = ThreadCtx(); t_ctx.gen = gen; }
+  if (!t_ctx.c[dev]) {
+    Ctx* c = new Ctx();
+    c->dev = dev;
+    std::lock_guard<std::mutex> lk(g_ctx_mu);
+    g_ctxs.push_back(c);
+    t_ctx.c[dev] = c;
+  }
+  *out = t_ctx.c[dev];
+  return DCOR_OK;
+}
+
+void ctx_release_thread() {
+  if (t_ctx.gen != g_ctx_gen.load()) { t_ctx = ThreadCtx(); return; }
+  for (Ctx*& c : t_ctx.c) {
+    if (!c) continue;
+    {
+      std::lock_guard<std::mutex> lk(g_ctx_mu);
+      g_ctxs.erase(std::remove(g_ctxs.begin(), g_ctxs.end(), c), g_ctxs.end());
+    }
+    ctx_free(c);
+    c = nullptr;
+  }
+}
+
+int pipe_get(Pipe** out) {
+  Ctx* c = nullptr;
+  if (int st = ctx_get(&c)) return st;
+  Pipe& p = c->pipe;
   if (!p.s) {
     HIPCHK(hipStreamCreateWithFlags(&p.s, hipStreamNonBlocking));
     HIPCHK(hipEventCreateWithFlags(&p.fork, hipEventDisableTiming));
@@ -315,15 +380,9 @@ int pipe_get(Pipe** out) {
   return DCOR_OK;
 }
 
-// R-stream mode's arena (words, draws, replicate records): same lifetime rules.
-Arena g_rs_arena[64];
-
-int arena_get_in(Arena* arenas, size_t bytes, void** out) {
-  int dev = 0;
-  HIPCHK(hipGetDevice(&dev));
-  if (dev < 0 || dev >= 64) return fail(DCOR_EINVAL, "device id out of range");
-  Arena& a = arenas[dev];
+int arena_grow(Arena& a, size_t bytes, void** out) {
   if (a.bytes < bytes) {
+    // the old block may still be read by work queued earlier: wait for the device
     if (a.p) { HIPCHK(hipDeviceSynchronize()); HIPCHK(hipFree(a.p)); a.p = nullptr; a.bytes = 0; }
     if (hipMalloc(&a.p, bytes) != hipSuccess) {
       (void)hipGetLastError();
@@ -336,7 +395,17 @@ int arena_get_in(Arena* arenas, size_t bytes, void** out) {
   return DCOR_OK;
 }
 
-int arena_get(size_t bytes, void** out) { return arena_get_in(g_arena, bytes, out); }
+int arena_get(size_t bytes, void** out) {
+  Ctx* c = nullptr;
+  if (int st = ctx_get(&c)) return st;
+  return arena_grow(c->codes, bytes, out);
+}
+
+int rs_arena_get(size_t bytes, void** out) {
+  Ctx* c = nullptr;
+  if (int st = ctx_get(&c)) return st;
+  return arena_grow(c->rs, bytes, out);
+}
 
 // Monotone code map of clip(v): base + [0, 2R) -> [0, levels).  Only affects speed (how many
 // samples tie a threshold's code), never results.
@@ -347,7 +416,62 @@ void code_map(double center, double R, double levels, double* base, double* inv)
   *inv = levels / (2.0 * R);
 }
 
-}  // namespace
+// Every data-independent constant of one fused cell (R operation order) and the kernel family
+// that runs it.  The status is the one the reference raises for the cell (stopifnot, k < 1).
+int prepare_cell(const dcor_cell& c, CellPlan& p) {
+  std::memset(&p, 0, sizeof(p));
+  DgpConst g;
+  if (int st = make_dgp(c, g)) return st;
+  p.dgp = c.dgp;
+  p.nan_dgp = g.nan_dgp != 0;
+  const char* var = std::getenv("DCOR_SIGN_KERNEL");
+  const bool force_regen = var && std::strcmp(var, "regen") == 0;
+  if (c.family == DCOR_FAMILY_SIGN) {
+    SignConst& k = p.sign;
+    if (int st = make_sign(c.n, c.eps1, c.eps2, c.alpha, c.normalise, c.ci_mode, c.nsim, false, k)) return st;
+    k.g = g;
+    k.k0 = (uint32_t)c.seed; k.k1 = (uint32_t)(c.seed >> 32);
+    // code windows centred on the DGP's location (speed only)
+    double cx = 0.0, cy = 0.0, rx = 1.0, ry = 1.0;
+    if (c.dgp == DCOR_DGP_GAUSSIAN) {
+      cx = r_min(r_max(c.mu[0], -k.L), k.L); cy = r_min(r_max(c.mu[1], -k.L), k.L);
+      rx = 2.0 * std::sqrt(g.a00 * g.a00 + g.a01 * g.a01);
+      ry = 2.0 * std::sqrt(g.a10 * g.a10 + g.a11 * g.a11);
+    } else if (c.dgp == DCOR_DGP_BERNOULLI) {
+      cx = cy = 0.5; rx = ry = 1.0;
+    } else if (c.dgp == DCOR_DGP_MIX_GAUSSIAN) {
+      cx = cy = 0.0; rx = ry = 1.0;       // clipped to [-1, 1]
+    } else {
+      cx = cy = 0.0; rx = ry = 2.0;
+    }
+    code_map(cx, rx, 65536.0, &k.cbase_x, &k.cinv_x);
+    code_map(cy, ry, 32768.0, &k.cbase_y, &k.cinv_y);
+    k.cinv_xf = (float)k.cinv_x; k.cnb_xf = (float)(-k.cbase_x * k.cinv_x);
+    k.cinv_yf = (float)k.cinv_y; k.cnb_yf = (float)(-k.cbase_y * k.cinv_y);
+    if (c.dgp == DCOR_DGP_BERNOULLI && !force_regen)
+      p.kind = c.n <= GRID_BERN_W_NMAX ? GK_SIGN_BERN_W : GK_SIGN_BERN;
+    else if (force_regen || !c.normalise)
+      p.kind = GK_SIGN_REGEN;
+    else
+      p.kind = GK_SIGN_CODES;
+    p.vpl32 = k.mix.nsim > 1024 ? 1 : 0;
+  } else if (c.family == DCOR_FAMILY_SUBG) {
+    SubgConst& k = p.subg;
+    if (int st = make_subg(c.n, c.eps1, c.eps2, c.eta1, c.eta2, c.alpha, 0, NAN, NAN, NAN, NAN,
+                           NAN, NAN, c.nsim, k, nullptr, nullptr)) return st;
+    k.g = g;
+    k.k0 = (uint32_t)c.seed; k.k1 = (uint32_t)(c.seed >> 32);
+    p.kind = GK_SUBG;
+  } else {
+    return fail(DCOR_EINVAL, "unknown family %d", c.family);
+  }
+  return DCOR_OK;
+}
+
+}  // namespace host
+}  // namespace dcor
+
+using namespace dcor::host;
 
 // ===================================================================== ABI
 extern "C" {
@@ -363,6 +487,7 @@ int dcor_last_error(char* buf, size_t len) {
 }
 
 int dcor_device_count(void) {
+  if (fork_guard()) return 0;
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess) { (void)hipGetLastError(); return 0; }
   return n;
@@ -382,8 +507,8 @@ double dcor_lambda_receiver_from_noise(double lam_s, double lam_o, double eps_s,
   return (lam_s + b_s * std::log(1.0 / delta)) * lam_o;
 }
 
-double dcor_lambda_from_priv(double lo, double hi, double mean, double sd) {
-  const double sig = r_max(sd, 1e-8);  // real-data-sims.R:104
+double dcor_lambda_from_priv(double lo, double hi, double mean, double sd, double eps_sd) {
+  const double sig = r_max(sd, eps_sd);  // real-data-sims.R:104
   return r_max(std::fabs((lo - mean) / sig), std::fabs((hi - mean) / sig));
 }
 
@@ -450,49 +575,22 @@ int dcor_sim_launch(const dcor_cell* cell, int64_t rep_begin, int64_t rep_count,
   if (rep_count > 0x7fffffffLL) return fail(DCOR_EINVAL, "rep_count too large for one launch");
   if (int st = need_device()) return st;
   const dcor_cell& c = *cell;
-  DgpConst g;
-  if (int st = make_dgp(c, g)) return st;
-  if (g.nan_dgp) {  // every estimate NaN (see make_dgp); the estimators' own checks still apply
-    if (c.family == DCOR_FAMILY_SIGN) {
-      SignConst k;
-      if (int st = make_sign(c.n, c.eps1, c.eps2, c.alpha, c.normalise, c.ci_mode, c.nsim, false, k)) return st;
-    } else if (c.family == DCOR_FAMILY_SUBG) {
-      SubgConst k;
-      if (int st = make_subg(c.n, c.eps1, c.eps2, c.eta1, c.eta2, c.alpha, 0, NAN, NAN, NAN, NAN,
-                             NAN, NAN, c.nsim, k, nullptr, nullptr)) return st;
-    } else {
-      return fail(DCOR_EINVAL, "unknown family %d", c.family);
-    }
+  CellPlan cp;
+  if (int st = prepare_cell(c, cp)) return st;
+  if (cp.nan_dgp) {  // every estimate NaN (see make_dgp); the estimators' own checks applied
     if (rep_count > 0)
       HIPCHK(hipMemsetAsync(d_out, 0xFF, sizeof(dcor_rep_out) * (size_t)rep_count, (hipStream_t)stream));
     return DCOR_OK;
   }
   int rc;
-  if (c.family == DCOR_FAMILY_SIGN) {
-    SignConst k;
-    if (int st = make_sign(c.n, c.eps1, c.eps2, c.alpha, c.normalise, c.ci_mode, c.nsim, false, k)) return st;
-    k.g = g; k.rep_begin = rep_begin;
-    k.k0 = (uint32_t)c.seed; k.k1 = (uint32_t)(c.seed >> 32);
-    // code windows centred on the DGP's location (speed only)
-    double cx = 0.0, cy = 0.0, rx = 1.0, ry = 1.0;
-    if (c.dgp == DCOR_DGP_GAUSSIAN) {
-      cx = r_min(r_max(c.mu[0], -k.L), k.L); cy = r_min(r_max(c.mu[1], -k.L), k.L);
-      rx = 2.0 * std::sqrt(g.a00 * g.a00 + g.a01 * g.a01);
-      ry = 2.0 * std::sqrt(g.a10 * g.a10 + g.a11 * g.a11);
-    } else if (c.dgp == DCOR_DGP_BERNOULLI) {
-      cx = cy = 0.5; rx = ry = 1.0;
-    } else if (c.dgp == DCOR_DGP_MIX_GAUSSIAN) {
-      cx = cy = 0.0; rx = ry = 1.0;       // clipped to [-1, 1]
-    } else {
-      cx = cy = 0.0; rx = ry = 2.0;
-    }
-    code_map(cx, rx, 65536.0, &k.cbase_x, &k.cinv_x);
-    code_map(cy, ry, 32768.0, &k.cbase_y, &k.cinv_y);
-    k.cinv_xf = (float)k.cinv_x; k.cnb_xf = (float)(-k.cbase_x * k.cinv_x);
-    k.cinv_yf = (float)k.cinv_y; k.cnb_yf = (float)(-k.cbase_y * k.cinv_y);
-    const char* var = std::getenv("DCOR_SIGN_KERNEL");
-    const bool regen = (var && std::strcmp(var, "regen") == 0) || !c.normalise;
-    if (c.dgp == DCOR_DGP_BERNOULLI && !(var && std::strcmp(var, "regen") == 0) && rep_count > 0) {
+  if (cp.kind == GK_SUBG) {
+    SubgConst k = cp.subg;
+    k.rep_begin = rep_begin;
+    rc = launch_subg_fused(k, rep_count, d_out, stream);
+  } else {
+    SignConst k = cp.sign;
+    k.rep_begin = rep_begin;
+    if ((cp.kind == GK_SIGN_BERN_W || cp.kind == GK_SIGN_BERN) && rep_count > 0) {
       // two-valued samples: bit-plane kernel (normalise = TRUE or FALSE)
       const size_t per_rep = (size_t)3 * 4 * (size_t)((c.n + 255) / 256) * sizeof(uint64_t) + 64;
       size_t budget = (size_t)1 << 30;
@@ -505,7 +603,7 @@ int dcor_sim_launch(const dcor_cell* cell, int64_t rep_begin, int64_t rep_count,
       if (int st = arena_get(plane_bytes + (size_t)chunk * 64, &scratch)) return st;
       rc = launch_sign_bern(k, rep_count, chunk, (uint64_t*)scratch,
                             (SignPartial*)((char*)scratch + plane_bytes), d_out, stream);
-    } else if (regen || rep_count == 0) {
+    } else if (cp.kind != GK_SIGN_CODES || rep_count == 0) {
       rc = launch_sign_fused(k, rep_count, d_out, stream);
     } else {
       // two slabs (two-stream chunk pipeline), each within a budget of >= 1 GiB and
@@ -540,15 +638,6 @@ int dcor_sim_launch(const dcor_cell* cell, int64_t rep_begin, int64_t rep_count,
       }
       rc = launch_sign_fused_codes(k, rep_count, chunk, bf, d_out, stream);
     }
-  } else if (c.family == DCOR_FAMILY_SUBG) {
-    SubgConst k;
-    if (int st = make_subg(c.n, c.eps1, c.eps2, c.eta1, c.eta2, c.alpha, 0, NAN, NAN, NAN, NAN,
-                           NAN, NAN, c.nsim, k, nullptr, nullptr)) return st;
-    k.g = g; k.rep_begin = rep_begin;
-    k.k0 = (uint32_t)c.seed; k.k1 = (uint32_t)(c.seed >> 32);
-    rc = launch_subg_fused(k, rep_count, d_out, stream);
-  } else {
-    return fail(DCOR_EINVAL, "unknown family %d", c.family);
   }
   if (rc) return hip_fail((hipError_t)rc, "sim kernel launch");
   return DCOR_OK;
@@ -599,25 +688,6 @@ void dcor_accum_finalize(const dcor_accum* a, double rho, dcor_summary* out) {
   out->var = (nae || a->n < 2) ? NAN : (double)((est2 - est * est / n) / (n - 1));
   out->coverage = (a->n_cover_na > 0 || a->n == 0) ? NAN : (double)a->n_cover / n;
   out->ci_length = nac || a->n == 0 ? NAN : (double)(((long double)a->len[0] + a->len[1]) / n);
-}
-
-int dcor_grid_run(const dcor_cell* cells, int ncells, int64_t B, dcor_accum* h_acc,
-                  dcor_rep_out* h_detail) {
-  if (!cells || ncells < 0 || B < 1 || !h_acc) return fail(DCOR_EINVAL, "bad grid arguments");
-  if (int st = need_device()) return st;
-  DevBuf out, acc;
-  HIPCHK(out.alloc(sizeof(dcor_rep_out) * (size_t)B));
-  HIPCHK(acc.alloc(sizeof(dcor_accum) * 2));
-  for (int i = 0; i < ncells; ++i) {
-    if (int st = dcor_sim_launch(&cells[i], 0, B, out.as<dcor_rep_out>(), nullptr)) return st;
-    if (int st = dcor_accumulate_launch(out.as<dcor_rep_out>(), B, cells[i].rho,
-                                        acc.as<dcor_accum>(), nullptr)) return st;
-    HIPCHK(hipMemcpy(h_acc + 2 * i, acc.p, sizeof(dcor_accum) * 2, hipMemcpyDeviceToHost));
-    if (h_detail)
-      HIPCHK(hipMemcpy(h_detail + (size_t)i * B, out.p, sizeof(dcor_rep_out) * (size_t)B,
-                       hipMemcpyDeviceToHost));
-  }
-  return DCOR_OK;
 }
 
 int dcor_premat_sign_launch(const dcor_premat_sign* d, dcor_rep_out* d_out, void* stream) {
@@ -1066,22 +1136,13 @@ int dcor_perm_launch(uint64_t seed, int site, int64_t rep_begin, int64_t reps, i
 }
 
 int dcor_shutdown(void) {
-  for (auto& a : g_arena) {
-    if (a.p) { (void)hipFree(a.p); a.p = nullptr; a.bytes = 0; }
+  std::vector<Ctx*> all;
+  {
+    std::lock_guard<std::mutex> lk(g_ctx_mu);
+    all.swap(g_ctxs);
+    g_ctx_gen.fetch_add(1);
   }
-  for (auto& a : g_rs_arena) {
-    if (a.p) { (void)hipFree(a.p); a.p = nullptr; a.bytes = 0; }
-  }
-  for (auto& p : g_pipe) {
-    if (p.s) {
-      (void)hipStreamSynchronize(p.s);
-      (void)hipStreamDestroy(p.s);
-      (void)hipEventDestroy(p.fork);
-      (void)hipEventDestroy(p.join);
-      p = Pipe();
-    }
-  }
-
+  for (Ctx* c : all) ctx_free(c);
   return DCOR_OK;
 }
 
@@ -1371,7 +1432,7 @@ int dcor_rstream_grid_run(const dcor_cell* cells, int ncells, int64_t B, dcor_ac
     const size_t off_out = off_cells + al256(sizeof(RsCell) * (size_t)nb);
     const size_t off_acc = off_out + al256(sizeof(dcor_rep_out) * (size_t)B * (size_t)nb);
     void* arena = nullptr;
-    if (int st = arena_get_in(g_rs_arena, off_acc + al256(sizeof(dcor_accum) * 2 * (size_t)nb), &arena))
+    if (int st = rs_arena_get(off_acc + al256(sizeof(dcor_accum) * 2 * (size_t)nb), &arena))
       return st;
     const View buf{arena}, dst{(char*)arena + off_st}, dcells{(char*)arena + off_cells},
         dout{(char*)arena + off_out}, acc{(char*)arena + off_acc};
@@ -1525,7 +1586,7 @@ int dcor_rstream_hrs_draws(int64_t n, int64_t k, int64_t m, int64_t nsim, int64_
       const size_t off_st = (size_t)nr * (words_b + 2 * al256(8) + al256((size_t)nsim * 8));
       const size_t off_cells = off_st + al256(sizeof(RsState) * (size_t)nr);
       void* arena = nullptr;
-      if (int st = arena_get_in(g_rs_arena, off_cells + al256(sizeof(RsCell) * (size_t)nr), &arena))
+      if (int st = rs_arena_get(off_cells + al256(sizeof(RsCell) * (size_t)nr), &arena))
         return st;
       char* base = (char*)arena;
       RsState* dst = (RsState*)((char*)arena + off_st);
@@ -1556,6 +1617,155 @@ int dcor_rstream_hrs_draws(int64_t n, int64_t k, int64_t m, int64_t nsim, int64_
     }
   }
   return DCOR_OK;
+}
+
+}  // extern "C"
+
+// ============================================== R-surface helpers (R/dcor*.R) ===
+extern "C" {
+
+int dcor_int_subg_sd_uc(const double* X, const double* Y, int64_t n, double eps1, double eps2,
+                        double eta1, double eta2, int hrs, double lam_s, double lam_o,
+                        double lam_r, double delta, const double* lap_local, double* sd_uc) {
+  if (!X || !Y || !lap_local || !sd_uc) return fail(DCOR_EINVAL, "int_subg_sd_uc: null argument");
+  if (int st = need_device()) return st;
+  dcor_premat_subg d;
+  std::memset(&d, 0, sizeof(d));
+  d.n = n; d.reps = 1; d.eps1 = eps1; d.eps2 = eps2; d.eta1 = eta1; d.eta2 = eta2; d.alpha = 0.05;
+  d.hrs = hrs; d.lam_x = d.lam_y = NAN; d.lam_s = lam_s; d.lam_o = lam_o; d.lam_r = lam_r;
+  d.delta = delta; d.nsim = 1;
+  PrematSubgConst p;
+  if (int st = premat_subg_const(&d, p)) return st;
+  DevBuf bX, bY, bl, bo;
+  if (int st = upload(bX, X, (size_t)n)) return st;
+  if (int st = upload(bY, Y, (size_t)n)) return st;
+  if (int st = upload(bl, lap_local, (size_t)n)) return st;
+  HIPCHK(bo.alloc(sizeof(double)));
+  p.X = bX.as<double>(); p.Y = bY.as<double>(); p.lap_local = bl.as<double>();
+  const int rc = launch_uc_sd(p, bo.as<double>(), nullptr);
+  if (rc) return hip_fail((hipError_t)rc, "uc_sd launch");
+  HIPCHK(hipMemcpy(sd_uc, bo.p, sizeof(double), hipMemcpyDeviceToHost));
+  return DCOR_OK;
+}
+
+int dcor_dp_mean(const double* x, int64_t n, double lo, double hi, double eps, double lap,
+                 double* out) {
+  if (!x || !out || n < 1) return fail(DCOR_EINVAL, "dp_mean: bad argument");
+  if (int st = need_device()) return st;
+  const double s_mu = (hi - lo) / ((double)n * eps);  // real-data-sims.R:69
+  const double lap2[2] = {lap, 0.0};
+  DevBuf bx, bl, bo;
+  if (int st = upload(bx, x, (size_t)n)) return st;
+  if (int st = upload(bl, lap2, 2)) return st;
+  HIPCHK(bo.alloc(sizeof(double) * 2));
+  const int rc = launch_dp_sd(bx.as<double>(), n, lo, hi, s_mu, 0.0, bl.as<double>(),
+                              bo.as<double>(), nullptr);
+  if (rc) return hip_fail((hipError_t)rc, "dp_mean launch");
+  HIPCHK(hipMemcpy(out, bo.p, sizeof(double), hipMemcpyDeviceToHost));
+  return DCOR_OK;
+}
+
+int dcor_standardize_dp(const double* x, int64_t n, double lo, double hi, double mean, double sd,
+                        double eps, double* out) {
+  if ((n > 0 && (!x || !out)) || n < 0) return fail(DCOR_EINVAL, "standardize_dp: bad argument");
+  if (n == 0) return DCOR_OK;
+  if (int st = need_device()) return st;
+  const double den = r_max(sd, eps);  // max(priv$sd, eps), real-data-sims.R:89
+  DevBuf bx, bo;
+  if (int st = upload(bx, x, (size_t)n)) return st;
+  HIPCHK(bo.alloc(sizeof(double) * (size_t)n));
+  const int rc = launch_standardize_dp(bx.as<double>(), n, lo, hi, mean, den, bo.as<double>(), nullptr);
+  if (rc) return hip_fail((hipError_t)rc, "standardize_dp launch");
+  HIPCHK(hipMemcpy(out, bo.p, sizeof(double) * (size_t)n, hipMemcpyDeviceToHost));
+  return DCOR_OK;
+}
+
+int dcor_gen_bernoulli(const double* u, const double* v, int64_t n, double rho, double* X,
+                       double* Y) {
+  if (n < 0 || (n > 0 && (!u || !v || !X || !Y))) return fail(DCOR_EINVAL, "gen_bernoulli: bad argument");
+  if (!(std::fabs(rho) <= 1)) return fail(DCOR_EINVAL, "gen_bernoulli: abs(rho) <= 1 is not TRUE (vert-cor.R:79)");
+  if (n == 0) return DCOR_OK;
+  if (int st = need_device()) return st;
+  const double p11 = 0.25 + rho / 4, p10 = 0.25 - rho / 4, p01 = p10;  // vert-cor.R:80-82
+  DevBuf bu, bv, bX, bY;
+  if (int st = upload(bu, u, (size_t)n)) return st;
+  if (int st = upload(bv, v, (size_t)n)) return st;
+  HIPCHK(bX.alloc(sizeof(double) * (size_t)n));
+  HIPCHK(bY.alloc(sizeof(double) * (size_t)n));
+  const int rc = launch_gen_bernoulli(bu.as<double>(), bv.as<double>(), n, p01 / 0.5, p11 / 0.5,
+                                      bX.as<double>(), bY.as<double>(), nullptr);
+  if (rc) return hip_fail((hipError_t)rc, "gen_bernoulli launch");
+  HIPCHK(hipMemcpy(X, bX.p, sizeof(double) * (size_t)n, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(Y, bY.p, sizeof(double) * (size_t)n, hipMemcpyDeviceToHost));
+  return DCOR_OK;
+}
+
+int dcor_gen_bounded_factor(const double* U, const double* E1, const double* E2, int64_t n,
+                            double* X, double* Y) {
+  if (n < 0 || (n > 0 && (!U || !E1 || !E2 || !X || !Y)))
+    return fail(DCOR_EINVAL, "gen_bounded_factor: bad argument");
+  if (n == 0) return DCOR_OK;
+  if (int st = need_device()) return st;
+  DevBuf bU, b1, b2, bX, bY;
+  if (int st = upload(bU, U, (size_t)n)) return st;
+  if (int st = upload(b1, E1, (size_t)n)) return st;
+  if (int st = upload(b2, E2, (size_t)n)) return st;
+  HIPCHK(bX.alloc(sizeof(double) * (size_t)n));
+  HIPCHK(bY.alloc(sizeof(double) * (size_t)n));
+  const int rc = launch_gen_bounded_factor(bU.as<double>(), b1.as<double>(), b2.as<double>(), n,
+                                           bX.as<double>(), bY.as<double>(), nullptr);
+  if (rc) return hip_fail((hipError_t)rc, "gen_bounded_factor launch");
+  HIPCHK(hipMemcpy(X, bX.p, sizeof(double) * (size_t)n, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(Y, bY.p, sizeof(double) * (size_t)n, hipMemcpyDeviceToHost));
+  return DCOR_OK;
+}
+
+static int mvn_run(const double* z0, int64_t n0, const double* z1, int64_t n1, const int32_t* perm,
+                   const MvnConst& m, double* X, double* Y) {
+  const int64_t n = n0 + n1;
+  if (n == 0) return DCOR_OK;
+  if (int st = need_device()) return st;
+  DevBuf b0, b1, bp, bX, bY;
+  if (int st = upload(b0, z0, (size_t)(2 * n0))) return st;
+  if (int st = upload(b1, z1, (size_t)(2 * n1))) return st;
+  if (perm) { if (int st = upload(bp, perm, (size_t)n)) return st; }
+  HIPCHK(bX.alloc(sizeof(double) * (size_t)n));
+  HIPCHK(bY.alloc(sizeof(double) * (size_t)n));
+  const int rc = launch_mvrnorm_apply(b0.as<double>(), n0, b1.as<double>(), n1,
+                                      perm ? bp.as<int32_t>() : nullptr, m, bX.as<double>(),
+                                      bY.as<double>(), nullptr);
+  if (rc) return hip_fail((hipError_t)rc, "mvrnorm launch");
+  HIPCHK(hipMemcpy(X, bX.p, sizeof(double) * (size_t)n, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(Y, bY.p, sizeof(double) * (size_t)n, hipMemcpyDeviceToHost));
+  return DCOR_OK;
+}
+
+int dcor_mvrnorm(const double* z, int64_t n, const double mu[2], const double sigma[2],
+                 double rho, double* X, double* Y) {
+  if (n < 0 || !mu || !sigma || (n > 0 && (!z || !X || !Y))) return fail(DCOR_EINVAL, "mvrnorm: bad argument");
+  if (!mvrnorm_pd(sigma, rho)) return fail(DCOR_EINVAL, "mvrnorm: 'Sigma' is not positive definite");
+  MvnConst m;
+  std::memset(&m, 0, sizeof(m));
+  rs_mvrnorm_factor(sigma, rho, m.A0);
+  m.mu0[0] = mu[0]; m.mu0[1] = mu[1];
+  return mvn_run(z, n, nullptr, 0, nullptr, m, X, Y);
+}
+
+int dcor_mix_gaussian(const double* z0, int64_t n0, const double* z1, int64_t n1,
+                      const int32_t* perm, double rho, const double mu0[2], const double sigma0[2],
+                      const double mu1[2], const double sigma1[2], double* X, double* Y) {
+  if (n0 < 0 || n1 < 0 || !mu0 || !sigma0 || !mu1 || !sigma1 ||
+      (n0 + n1 > 0 && (!perm || !X || !Y || (n0 && !z0) || (n1 && !z1))))
+    return fail(DCOR_EINVAL, "gen_mix_gaussian: bad argument");
+  for (int64_t i = 0; i < n0 + n1; ++i)
+    if (perm[i] < 0 || perm[i] >= n0 + n1) return fail(DCOR_EINVAL, "gen_mix_gaussian: perm out of range");
+  if (!mvrnorm_pd(sigma0, rho) || !mvrnorm_pd(sigma1, rho))
+    return fail(DCOR_EINVAL, "gen_mix_gaussian: mvrnorm 'Sigma' is not positive definite");
+  MvnConst m;
+  rs_mvrnorm_factor(sigma0, rho, m.A0);
+  rs_mvrnorm_factor(sigma1, rho, m.A1);
+  m.mu0[0] = mu0[0]; m.mu0[1] = mu0[1]; m.mu1[0] = mu1[0]; m.mu1[1] = mu1[1];
+  return mvn_run(z0, n0, z1, n1, perm, m, X, Y);
 }
 
 }  // extern "C"

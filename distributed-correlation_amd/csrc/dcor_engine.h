@@ -135,6 +135,42 @@ struct CodesBufs {
 int launch_sign_fused_codes(const SignConst& c, int64_t reps, int64_t chunk, const CodesBufs& bf,
                             dcor_rep_out* out, void* stream);
 int launch_subg_fused(const SubgConst& c, int64_t reps, dcor_rep_out* out, void* stream);
+
+// ---- batched grid launches (dcor_grid_launch): many cells' replicates per launch ----------
+// One work item = one replicate: the cell's constants come from a device table, so a launch
+// covers any mix of cells of one kernel family and DGP (no per-cell launches, no per-cell
+// occupancy cliff at the reference grids' B = 250).
+struct GridItem {
+  uint32_t cell;      // index into the launch's constant table
+  uint32_t rep;       // replicate index: the Philox counter
+  uint64_t scratch;   // first element of the replicate's scratch (codes: u32 records; Bernoulli
+                      // planes: u64 words)
+  uint64_t out;       // index of its output record
+};
+enum GridKind { GK_SIGN_CODES = 0, GK_SIGN_REGEN = 1, GK_SIGN_BERN_W = 2, GK_SIGN_BERN = 3, GK_SUBG = 4 };
+// per-item scratch of the kinds that use it
+#define GRID_BERN_W_NMAX 16384
+// doubles per replicate handed from the one-pass sign kernel's pass 1 to pass 2
+#define SIGN_SUMS 8
+// Pass 1 + pass 2 over `nitems` items (scratch: the items' code slabs; sums: SIGN_SUMS doubles per
+// item; part: per-item SignPartial), then the wave epilogue writing out[item.out].
+int launch_grid_sign_codes(int dgp, const SignConst* cells, const GridItem* items, int64_t nitems,
+                           uint32_t* scratch, double* sums, SignPartial* part, int vpl32,
+                           dcor_rep_out* out, void* stream);
+int launch_grid_sign_regen(int dgp, const SignConst* cells, const GridItem* items, int64_t nitems,
+                           dcor_rep_out* out, void* stream);
+int launch_grid_sign_bern(bool wave, const SignConst* cells, const GridItem* items, int64_t nitems,
+                          uint64_t* scratch, SignPartial* part, int vpl32, dcor_rep_out* out,
+                          void* stream);
+int launch_grid_subg(int dgp, const SubgConst* cells, const GridItem* items, int64_t nitems,
+                     dcor_rep_out* out, void* stream);
+// Accumulators of ncells cell segments of `rec` (segment i: seg_off[i], seg_cnt[i] records, rho[i])
+// into acc[2 i], acc[2 i + 1]; byte-identical to launch_accumulate on each segment.  part: scratch
+// of 512 * 2 accumulators per cell (cells with more than 2048 records).
+int launch_accumulate_seg(const dcor_rep_out* rec, int ncells, const int64_t* seg_off,
+                          const int64_t* seg_cnt, const double* rho, int max_nb, dcor_accum* part,
+                          dcor_accum* acc, void* stream);
+int accumulate_blocks(int64_t count);   // launch_accumulate's partition of `count` records
 int launch_premat_sign(const PrematSignConst& c, int64_t reps, dcor_rep_out* out, void* stream);
 // part: reps * 80 B scratch (stream -> epilogue partial sums).
 // epi_stream / ev: if non-null the epilogue runs on epi_stream after an event recorded on
@@ -157,6 +193,21 @@ int launch_perm(uint32_t k0, uint32_t k1, uint32_t site, int64_t rep_begin, int6
                 int64_t n, int64_t count, int32_t* out, void* stream);
 int launch_dp_sd(const double* x, int64_t n, double lo, double hi, double s_mu, double s_m2,
                  const double* lap2, double* out2, void* stream);
+// R-surface transforms (dcor_premat.hip): the arithmetic half of the R wrappers' DGPs and DP
+// helpers, whose random draws the wrappers take with R's own RNG.
+struct MvnConst {          // MASS::mvrnorm factors A = V diag(sqrt(ev)) (row-major 2x2) and means
+  double A0[4], mu0[2];    // component 0 (the only one for a plain mvrnorm)
+  double A1[4], mu1[2];    // component 1 (gen_mix_gaussian)
+};
+int launch_uc_sd(const PrematSubgConst& p, double* out, void* stream);
+int launch_standardize_dp(const double* x, int64_t n, double lo, double hi, double mean, double den,
+                          double* out, void* stream);
+int launch_gen_bernoulli(const double* u, const double* v, int64_t n, double t0, double t1,
+                         double* X, double* Y, void* stream);
+int launch_gen_bounded_factor(const double* U, const double* E1, const double* E2, int64_t n,
+                              double* X, double* Y, void* stream);
+int launch_mvrnorm_apply(const double* z0, int64_t n0, const double* z1, int64_t n1,
+                         const int32_t* perm, const MvnConst& m, double* X, double* Y, void* stream);
 
 // R-stream mode (dcor_rstream.hip): R's Mersenne-Twister state as set.seed leaves it.
 struct RsState {

@@ -310,7 +310,6 @@ __device__ __forceinline__ void exact_signs(const SignConst& c, const SignStd& s
 // compensated: each thread adds its group of 4 samples plainly and folds the group sum into a
 // TwoSum accumulator; the workgroup reduction is double-double.  The second moments only set
 // sd > 0, which never changes a sign, and stay plain sums.
-#define SIGN_SUMS 8
 template <int DGP>
 __device__ __forceinline__ void sign_pass1_body(const SignConst& c, uint32_t rep,
                                                 uint32_t* __restrict__ slab,
@@ -535,31 +534,37 @@ __global__ __launch_bounds__(DCOR_BLOCK) void k_sign_pass2(SignConst c,
 // Wave-per-replicate epilogue (four replicates per workgroup, no workgroup barriers):
 // NI estimate/CI, INT estimate, mixquant, INT CI (vert-cor.R:233-254, 186-194, 281-313).
 template <int VPL>
-__global__ __launch_bounds__(DCOR_BLOCK) void k_sign_epilogue_w(SignConst c, int64_t nreps,
-                                                                const SignPartial* __restrict__ part,
-                                                                dcor_rep_out* out) {
-  __shared__ WaveSel wsel[DCOR_WAVES];
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int64_t r = (int64_t)blockIdx.x * DCOR_WAVES + wv;
-  if (r >= nreps) return;  // whole waves only
-  const uint32_t rep = (uint32_t)(c.rep_begin + r);
+__device__ __forceinline__ void sign_epilogue_wave(const SignConst& c, uint32_t rep,
+                                                   const SignPartial& p, dcor_rep_out* dst,
+                                                   WaveSel* ws) {
+  const int lane = threadIdx.x & 63;
   const U4 wz = draw(4u, rep, DCOR_SITE_SCALAR, c.k0, c.k1);  // SCALAR block 4: Z (vert-cor.R:188)
   const double lapz = unit_laplace(u53(wz.w0, wz.w1));
-  const SignPartial p = part[r];
   double o[6];
   ni_sign_result(c, DD{p.sT[0], p.sT[1]}, DD{p.sT2[0], p.sT2[1]}, (p.flags & 1) != 0, o);
   double rho, eta, se, cstar;
   int_sign_point(c, p.core, lapz, rho, eta, se, cstar);
   double w;
   if (c.mode_normal)
-    w = wave_mixquant_fused<VPL>(c.mix, cstar, rep, c.k0, c.k1, &wsel[wv]) * se;
+    w = wave_mixquant_fused<VPL>(c.mix, cstar, rep, c.k0, c.k1, ws) * se;
   else
     w = c.w_laplace;
   o[3] = rho;
   o[4] = sin(M_PI / 2.0 * rmax(eta - w, -1.0));
   o[5] = sin(M_PI / 2.0 * rmin(eta + w, 1.0));
   if (p.flags & 2) o[3] = o[4] = o[5] = dnan();
-  if (lane == 0) out[r] = dcor_rep_out{o[0], o[1], o[2], o[3], o[4], o[5]};
+  if (lane == 0) *dst = dcor_rep_out{o[0], o[1], o[2], o[3], o[4], o[5]};
+}
+
+template <int VPL>
+__global__ __launch_bounds__(DCOR_BLOCK) void k_sign_epilogue_w(SignConst c, int64_t nreps,
+                                                                const SignPartial* __restrict__ part,
+                                                                dcor_rep_out* out) {
+  __shared__ WaveSel wsel[DCOR_WAVES];
+  const int wv = threadIdx.x >> 6;
+  const int64_t r = (int64_t)blockIdx.x * DCOR_WAVES + wv;
+  if (r >= nreps) return;  // whole waves only
+  sign_epilogue_wave<VPL>(c, (uint32_t)(c.rep_begin + r), part[r], out + r, &wsel[wv]);
 }
 
 // Epilogue: NI estimate/CI, INT estimate, mixquant, INT CI (vert-cor.R:233-254, 186-194, 281-313).
@@ -729,15 +734,14 @@ __device__ __forceinline__ void bern_batch(const SignConst& c, const BernSigns& 
   dd_acc(sT2, T * T);
 }
 
-__global__ __launch_bounds__(DCOR_BLOCK) void k_sign_bern(SignConst c, uint64_t* __restrict__ scratch,
-                                                          SignPartial* __restrict__ part) {
+__device__ __forceinline__ void sign_bern_body(const SignConst& c, uint32_t rep,
+                                               uint64_t* __restrict__ planes,
+                                               SignPartial* __restrict__ part_out) {
   __shared__ double red[16 * DCOR_WAVES];
   __shared__ long long redi[8 * DCOR_WAVES];
   __shared__ double lap[10];
   const int tid = threadIdx.x, lane = tid & 63;
-  const uint32_t rep = (uint32_t)(c.rep_begin + blockIdx.x);
   const int64_t nw = 4 * ((c.n + 255) / 256);  // plane words per replicate
-  uint64_t* planes = scratch + (size_t)blockIdx.x * 3 * (size_t)nw;
   scalar_laplace(rep, c.k0, c.k1, lap);
   // ---- pass A: generate, ballot into plane words, count (wave-uniform counters)
   BernCounts t{0, 0, 0, 0, 0, 0, 0};
@@ -786,8 +790,15 @@ __global__ __launch_bounds__(DCOR_BLOCK) void k_sign_bern(SignConst c, uint64_t*
     p.sT[0] = d2[0].hi; p.sT[1] = d2[0].lo; p.sT2[0] = d2[1].hi; p.sT2[1] = d2[1].lo;
     p.core = sg.core;
     p.flags = (nbad ? 1 : 0) | (sg.bad_int ? 2 : 0);
-    part[blockIdx.x] = p;
+    *part_out = p;
   }
+}
+
+__global__ __launch_bounds__(DCOR_BLOCK) void k_sign_bern(SignConst c, uint64_t* __restrict__ scratch,
+                                                          SignPartial* __restrict__ part) {
+  const int64_t nw = 4 * ((c.n + 255) / 256);
+  sign_bern_body(c, (uint32_t)(c.rep_begin + blockIdx.x),
+                 scratch + (size_t)blockIdx.x * 3 * (size_t)nw, part + blockIdx.x);
 }
 
 // Wave-per-replicate form for n <= BERN_W_NMAX: the planes of a replicate (3 x n/8 B) stay
@@ -796,13 +807,10 @@ __global__ __launch_bounds__(DCOR_BLOCK) void k_sign_bern(SignConst c, uint64_t*
 // thresholds, reductions -- is latency that the other waves hide).
 #define BERN_W_NMAX 16384
 #define BERN_W_WORDS (4 * (BERN_W_NMAX / 256))
-__global__ __launch_bounds__(DCOR_BLOCK) void k_sign_bern_w(SignConst c, int64_t nreps,
-                                                            SignPartial* __restrict__ part) {
-  __shared__ uint64_t pls[DCOR_WAVES][3][BERN_W_WORDS];
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int64_t r = (int64_t)blockIdx.x * DCOR_WAVES + wv;
-  if (r >= nreps) return;  // whole waves only
-  const uint32_t rep = (uint32_t)(c.rep_begin + r);
+__device__ __forceinline__ void sign_bern_wave(const SignConst& c, uint32_t rep,
+                                               uint64_t (*pls)[BERN_W_WORDS],
+                                               SignPartial* __restrict__ part_out) {
+  const int lane = threadIdx.x & 63;
   const int64_t nw = 4 * ((c.n + 255) / 256);
   // scalar Laplace blocks 0..3 (NI / INT mu, m2 of X, Y): lane q < 4 draws block q
   double la = 0.0, lb = 0.0;
@@ -826,14 +834,14 @@ __global__ __launch_bounds__(DCOR_BLOCK) void k_sign_bern_w(SignConst c, int64_t
     const int64_t w0 = g0 / 16;
     if (lane < 12 && w0 + (lane & 3) < nw) {
       const int q = lane & 3, pl = lane >> 2;
-      pls[wv][pl][w0 + q] = pl == 0 ? interleave4(BX, q) : (pl == 1 ? interleave4(BY, q) : interleave4(BF, q));
+      pls[pl][w0 + q] = pl == 0 ? interleave4(BX, q) : (pl == 1 ? interleave4(BY, q) : interleave4(BF, q));
     }
   }
   wave_sync();  // plane words written by lanes 0..11 are read by every lane below
   const BernSigns sg = bern_signs(c, t, l8);
   bool bad_ni = sg.bad_ni;
   DD sT{0.0, 0.0}, sT2{0.0, 0.0};
-  for (int64_t j = lane; j < c.k; j += 64) bern_batch(c, sg, pls[wv][0], pls[wv][1], j, rep, sT, sT2, bad_ni);
+  for (int64_t j = lane; j < c.k; j += 64) bern_batch(c, sg, pls[0], pls[1], j, rep, sT, sT2, bad_ni);
   sT = wave_sum_dd(sT);
   sT2 = wave_sum_dd(sT2);
   const bool any_bad = __ballot(bad_ni) != 0;
@@ -842,8 +850,17 @@ __global__ __launch_bounds__(DCOR_BLOCK) void k_sign_bern_w(SignConst c, int64_t
     p.sT[0] = sT.hi; p.sT[1] = sT.lo; p.sT2[0] = sT2.hi; p.sT2[1] = sT2.lo;
     p.core = sg.core;
     p.flags = (any_bad ? 1 : 0) | (sg.bad_int ? 2 : 0);
-    part[r] = p;
+    *part_out = p;
   }
+}
+
+__global__ __launch_bounds__(DCOR_BLOCK) void k_sign_bern_w(SignConst c, int64_t nreps,
+                                                            SignPartial* __restrict__ part) {
+  __shared__ uint64_t pls[DCOR_WAVES][3][BERN_W_WORDS];
+  const int wv = threadIdx.x >> 6;
+  const int64_t r = (int64_t)blockIdx.x * DCOR_WAVES + wv;
+  if (r >= nreps) return;  // whole waves only
+  sign_bern_wave(c, (uint32_t)(c.rep_begin + r), pls[wv], part + r);
 }
 
 // ============================= fused sign family, regenerate (two-pass, A/B) ===
@@ -851,12 +868,11 @@ __global__ __launch_bounds__(DCOR_BLOCK) void k_sign_bern_w(SignConst c, int64_t
 // normalise = FALSE (signs against 0: pass 1 is skipped, so it is one pass) and as the
 // A/B reference for k_sign_fused_codes (DCOR_SIGN_KERNEL=regen).
 template <int DGP>
-__global__ __launch_bounds__(DCOR_BLOCK) void k_sign_fused(SignConst c, dcor_rep_out* out) {
+__device__ __forceinline__ void sign_fused_body(const SignConst& c, uint32_t rep, dcor_rep_out* dst) {
   __shared__ double red[16 * DCOR_WAVES];
   __shared__ long long redi[DCOR_WAVES];
   __shared__ double lap[10];
   __shared__ SelScratch sel;
-  const uint32_t rep = (uint32_t)(c.rep_begin + blockIdx.x);
   const int tid = threadIdx.x;
   scalar_laplace(rep, c.k0, c.k1, lap);
   // the same compensated sums as k_sign_pass1 (groups of 4, TwoSum, double-double reduction)
@@ -945,19 +961,22 @@ __global__ __launch_bounds__(DCOR_BLOCK) void k_sign_fused(SignConst c, dcor_rep
   block_sum_dd<2>(d2, red);
   core = block_sum_i(core, redi);
   const long long nbad = block_sum_i((bad_ni ? 1LL : 0LL) + (bad_int ? (1LL << 20) : 0LL), redi);
-  sign_finish(c, rep, d2[0], d2[1], core, (nbad & 0xFFFFF) != 0, (nbad >> 20) != 0, lap, &sel,
-              out + blockIdx.x);
+  sign_finish(c, rep, d2[0], d2[1], core, (nbad & 0xFFFFF) != 0, (nbad >> 20) != 0, lap, &sel, dst);
+}
+
+template <int DGP>
+__global__ __launch_bounds__(DCOR_BLOCK) void k_sign_fused(SignConst c, dcor_rep_out* out) {
+  sign_fused_body<DGP>(c, (uint32_t)(c.rep_begin + blockIdx.x), out + blockIdx.x);
 }
 
 // ===================================================== fused sub-G family ===
 // correlation_NI_subG + ci_INT_subG (ver-cor-subG.R:25-108): single pass (the clip
 // thresholds are data-independent).  Each thread owns whole contiguous batches.
 template <int DGP>
-__global__ __launch_bounds__(DCOR_BLOCK) void k_subg_fused(SubgConst c, dcor_rep_out* out) {
+__device__ __forceinline__ void subg_fused_body(const SubgConst& c, uint32_t rep, dcor_rep_out* dst) {
   __shared__ double red[16 * DCOR_WAVES];
   __shared__ double lapz;
   __shared__ SelScratch sel;
-  const uint32_t rep = (uint32_t)(c.rep_begin + blockIdx.x);
   const int tid = threadIdx.x;
   if (tid == 0) {
     const U4 w = draw(4u, rep, DCOR_SITE_SCALAR, c.k0, c.k1);
@@ -1009,11 +1028,172 @@ __global__ __launch_bounds__(DCOR_BLOCK) void k_subg_fused(SubgConst c, dcor_rep
   o[3] = rho;
   o[4] = rmax(rho - width, -1.0);
   o[5] = rmin(rho + width, 1.0);
-  if (tid == 0) out[blockIdx.x] = dcor_rep_out{o[0], o[1], o[2], o[3], o[4], o[5]};
+  if (tid == 0) *dst = dcor_rep_out{o[0], o[1], o[2], o[3], o[4], o[5]};
+}
+
+template <int DGP>
+__global__ __launch_bounds__(DCOR_BLOCK) void k_subg_fused(SubgConst c, dcor_rep_out* out) {
+  subg_fused_body<DGP>(c, (uint32_t)(c.rep_begin + blockIdx.x), out + blockIdx.x);
+}
+
+// ================================================== batched grid kernels ===
+// The same bodies over a work-item table (dcor_grid_launch): workgroup (or wave) w runs item
+// items[w] with the constants of cells[item.cell].  Both index loads are uniform, so the
+// constants are scalar loads as with a kernel argument.
+template <int DGP>
+__global__ __launch_bounds__(DCOR_BLOCK) void k_grid_sign_pass1(const SignConst* __restrict__ cells,
+                                                                const GridItem* __restrict__ items,
+                                                                uint32_t* __restrict__ scratch,
+                                                                double* __restrict__ sums) {
+  const GridItem it = items[blockIdx.x];
+  sign_pass1_body<DGP>(cells[it.cell], it.rep, scratch + it.scratch, sums + SIGN_SUMS * (size_t)blockIdx.x);
+}
+
+template <int DGP>
+__global__ __launch_bounds__(DCOR_BLOCK) void k_grid_sign_pass2(const SignConst* __restrict__ cells,
+                                                                const GridItem* __restrict__ items,
+                                                                const uint32_t* __restrict__ scratch,
+                                                                const double* __restrict__ sums,
+                                                                SignPartial* __restrict__ part) {
+  const GridItem it = items[blockIdx.x];
+  sign_pass2_body<DGP>(cells[it.cell], it.rep, scratch + it.scratch,
+                       sums + SIGN_SUMS * (size_t)blockIdx.x, part + blockIdx.x);
+}
+
+// wave w of the launch = item w; the index is made wave-uniform (SGPR) for the table loads
+__device__ __forceinline__ int64_t wave_item() {
+  return (int64_t)blockIdx.x * DCOR_WAVES + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+}
+
+template <int VPL>
+__global__ __launch_bounds__(DCOR_BLOCK) void k_grid_sign_epilogue(const SignConst* __restrict__ cells,
+                                                                   const GridItem* __restrict__ items,
+                                                                   int64_t nitems,
+                                                                   const SignPartial* __restrict__ part,
+                                                                   dcor_rep_out* out) {
+  __shared__ WaveSel wsel[DCOR_WAVES];
+  const int64_t r = wave_item();
+  if (r >= nitems) return;  // whole waves only
+  const GridItem it = items[r];
+  sign_epilogue_wave<VPL>(cells[it.cell], it.rep, part[r], out + it.out, &wsel[threadIdx.x >> 6]);
+}
+
+template <int DGP>
+__global__ __launch_bounds__(DCOR_BLOCK) void k_grid_sign_regen(const SignConst* __restrict__ cells,
+                                                                const GridItem* __restrict__ items,
+                                                                dcor_rep_out* out) {
+  const GridItem it = items[blockIdx.x];
+  sign_fused_body<DGP>(cells[it.cell], it.rep, out + it.out);
+}
+
+__global__ __launch_bounds__(DCOR_BLOCK) void k_grid_sign_bern(const SignConst* __restrict__ cells,
+                                                               const GridItem* __restrict__ items,
+                                                               uint64_t* __restrict__ scratch,
+                                                               SignPartial* __restrict__ part) {
+  const GridItem it = items[blockIdx.x];
+  sign_bern_body(cells[it.cell], it.rep, scratch + it.scratch, part + blockIdx.x);
+}
+
+__global__ __launch_bounds__(DCOR_BLOCK) void k_grid_sign_bern_w(const SignConst* __restrict__ cells,
+                                                                 const GridItem* __restrict__ items,
+                                                                 int64_t nitems,
+                                                                 SignPartial* __restrict__ part) {
+  __shared__ uint64_t pls[DCOR_WAVES][3][BERN_W_WORDS];
+  const int64_t r = wave_item();
+  if (r >= nitems) return;
+  const GridItem it = items[r];
+  sign_bern_wave(cells[it.cell], it.rep, pls[threadIdx.x >> 6], part + r);
+}
+
+template <int DGP>
+__global__ __launch_bounds__(DCOR_BLOCK) void k_grid_subg(const SubgConst* __restrict__ cells,
+                                                          const GridItem* __restrict__ items,
+                                                          dcor_rep_out* out) {
+  const GridItem it = items[blockIdx.x];
+  subg_fused_body<DGP>(cells[it.cell], it.rep, out + it.out);
 }
 
 // ============================================================ launchers ===
 static inline int last_err() { return (int)hipGetLastError(); }
+
+static inline unsigned wave_groups(int64_t n) { return (unsigned)((n + DCOR_WAVES - 1) / DCOR_WAVES); }
+
+static void launch_grid_epilogue(const SignConst* cells, const GridItem* items, int64_t nitems,
+                                 const SignPartial* part, int vpl32, dcor_rep_out* out, hipStream_t st) {
+  if (vpl32)
+    hipLaunchKernelGGL(k_grid_sign_epilogue<32>, dim3(wave_groups(nitems)), dim3(DCOR_BLOCK), 0, st,
+                       cells, items, nitems, part, out);
+  else
+    hipLaunchKernelGGL(k_grid_sign_epilogue<16>, dim3(wave_groups(nitems)), dim3(DCOR_BLOCK), 0, st,
+                       cells, items, nitems, part, out);
+}
+
+template <int DGP>
+static void grid_codes_t(const SignConst* cells, const GridItem* items, int64_t nitems,
+                         uint32_t* scratch, double* sums, SignPartial* part, hipStream_t st) {
+  hipLaunchKernelGGL(k_grid_sign_pass1<DGP>, dim3((unsigned)nitems), dim3(DCOR_BLOCK), 0, st, cells,
+                     items, scratch, sums);
+  hipLaunchKernelGGL(k_grid_sign_pass2<DGP>, dim3((unsigned)nitems), dim3(DCOR_BLOCK), 0, st, cells,
+                     items, scratch, sums, part);
+}
+
+int launch_grid_sign_codes(int dgp, const SignConst* cells, const GridItem* items, int64_t nitems,
+                           uint32_t* scratch, double* sums, SignPartial* part, int vpl32,
+                           dcor_rep_out* out, void* stream) {
+  if (nitems <= 0) return 0;
+  const hipStream_t st = (hipStream_t)stream;
+  switch (dgp) {
+    case DCOR_DGP_GAUSSIAN: grid_codes_t<DCOR_DGP_GAUSSIAN>(cells, items, nitems, scratch, sums, part, st); break;
+    case DCOR_DGP_BERNOULLI: grid_codes_t<DCOR_DGP_BERNOULLI>(cells, items, nitems, scratch, sums, part, st); break;
+    case DCOR_DGP_MIX_GAUSSIAN: grid_codes_t<DCOR_DGP_MIX_GAUSSIAN>(cells, items, nitems, scratch, sums, part, st); break;
+    default: grid_codes_t<DCOR_DGP_BOUNDED_FACTOR>(cells, items, nitems, scratch, sums, part, st);
+  }
+  launch_grid_epilogue(cells, items, nitems, part, vpl32, out, st);
+  return last_err();
+}
+
+int launch_grid_sign_regen(int dgp, const SignConst* cells, const GridItem* items, int64_t nitems,
+                           dcor_rep_out* out, void* stream) {
+  if (nitems <= 0) return 0;
+  const dim3 g((unsigned)nitems), b(DCOR_BLOCK);
+  const hipStream_t st = (hipStream_t)stream;
+  switch (dgp) {
+    case DCOR_DGP_GAUSSIAN: hipLaunchKernelGGL(k_grid_sign_regen<DCOR_DGP_GAUSSIAN>, g, b, 0, st, cells, items, out); break;
+    case DCOR_DGP_BERNOULLI: hipLaunchKernelGGL(k_grid_sign_regen<DCOR_DGP_BERNOULLI>, g, b, 0, st, cells, items, out); break;
+    case DCOR_DGP_MIX_GAUSSIAN: hipLaunchKernelGGL(k_grid_sign_regen<DCOR_DGP_MIX_GAUSSIAN>, g, b, 0, st, cells, items, out); break;
+    default: hipLaunchKernelGGL(k_grid_sign_regen<DCOR_DGP_BOUNDED_FACTOR>, g, b, 0, st, cells, items, out);
+  }
+  return last_err();
+}
+
+int launch_grid_sign_bern(bool wave, const SignConst* cells, const GridItem* items, int64_t nitems,
+                          uint64_t* scratch, SignPartial* part, int vpl32, dcor_rep_out* out,
+                          void* stream) {
+  if (nitems <= 0) return 0;
+  const hipStream_t st = (hipStream_t)stream;
+  if (wave)
+    hipLaunchKernelGGL(k_grid_sign_bern_w, dim3(wave_groups(nitems)), dim3(DCOR_BLOCK), 0, st, cells,
+                       items, nitems, part);
+  else
+    hipLaunchKernelGGL(k_grid_sign_bern, dim3((unsigned)nitems), dim3(DCOR_BLOCK), 0, st, cells, items,
+                       scratch, part);
+  launch_grid_epilogue(cells, items, nitems, part, vpl32, out, st);
+  return last_err();
+}
+
+int launch_grid_subg(int dgp, const SubgConst* cells, const GridItem* items, int64_t nitems,
+                     dcor_rep_out* out, void* stream) {
+  if (nitems <= 0) return 0;
+  const dim3 g((unsigned)nitems), b(DCOR_BLOCK);
+  const hipStream_t st = (hipStream_t)stream;
+  switch (dgp) {
+    case DCOR_DGP_GAUSSIAN: hipLaunchKernelGGL(k_grid_subg<DCOR_DGP_GAUSSIAN>, g, b, 0, st, cells, items, out); break;
+    case DCOR_DGP_BERNOULLI: hipLaunchKernelGGL(k_grid_subg<DCOR_DGP_BERNOULLI>, g, b, 0, st, cells, items, out); break;
+    case DCOR_DGP_MIX_GAUSSIAN: hipLaunchKernelGGL(k_grid_subg<DCOR_DGP_MIX_GAUSSIAN>, g, b, 0, st, cells, items, out); break;
+    default: hipLaunchKernelGGL(k_grid_subg<DCOR_DGP_BOUNDED_FACTOR>, g, b, 0, st, cells, items, out);
+  }
+  return last_err();
+}
 
 template <int DGP>
 static int launch_sign_t(const SignConst& c, int64_t reps, dcor_rep_out* out, void* stream) {

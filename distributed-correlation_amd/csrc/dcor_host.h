@@ -1,0 +1,61 @@
+// dcor_host.h -- host-side internals shared by the C-ABI translation units (dcor_capi.cpp,
+// dcor_grid.cpp): error reporting, the per-(thread, device) library context, and the per-cell
+// constant builder.  Not part of the ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdint>
+
+#include "../../include/dcor.h"
+#include "dcor_engine.h"
+
+namespace dcor {
+struct SignPartial;
+namespace host {
+
+// Record the message of a failure for dcor_last_error() (thread-local) and return `code`.
+int fail(int code, const char* fmt, ...);
+int hip_fail(hipError_t e, const char* what);
+#define HIPCHK(expr)                                   \
+  do {                                                 \
+    hipError_t e_ = (expr);                            \
+    if (e_ != hipSuccess) return hip_fail(e_, #expr);  \
+  } while (0)
+
+// DCOR_EFORK in a process forked after its parent used the engine, DCOR_ENODEV without a GPU.
+int need_device();
+double r_min(double a, double b);
+double r_max(double a, double b);
+
+struct Arena { void* p = nullptr; size_t bytes = 0; };
+struct Pipe { hipStream_t s = nullptr; hipEvent_t fork = nullptr, join = nullptr; };
+// The library's state for one (host thread, device): scratch arenas, the auxiliary stream of the
+// two-stream chunk pipeline, and a pinned staging buffer (the grid's tables) with the event that
+// marks the end of its last upload.
+struct Ctx {
+  int dev = -1;
+  Arena codes, rs, grid;
+  Pipe pipe;
+  void* staging = nullptr;
+  size_t staging_bytes = 0;
+  hipEvent_t staging_free = nullptr;
+};
+int ctx_get(Ctx** out);          // the calling thread's context on the current device
+void ctx_release_thread();       // free every context of the calling thread
+int pipe_get(Pipe** out);
+int arena_grow(Arena& a, size_t bytes, void** out);
+
+// All constants of one fused cell and the kernel family that runs it.
+struct CellPlan {
+  int kind;        // GridKind
+  int dgp;         // DCOR_DGP_*
+  bool nan_dgp;    // gen_bounded_factor with rho outside [0, 1]: every estimate NaN
+  int vpl32;       // the sign epilogue's wave-select width (nsim > 1024)
+  SignConst sign;  // family SIGN (rep_begin 0)
+  SubgConst subg;  // family SUBG (rep_begin 0)
+};
+int prepare_cell(const dcor_cell& c, CellPlan& p);
+
+}  // namespace host
+}  // namespace dcor

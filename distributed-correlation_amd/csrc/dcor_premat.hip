@@ -785,6 +785,76 @@ __global__ __launch_bounds__(DCOR_BLOCK) void k_accumulate_merge(const dcor_accu
   }
 }
 
+// Segmented form for the batched grid: block (b, i) runs block b of cell segment i's partition
+// (accumulate_blocks), exactly the work k_accumulate's block b does on that segment alone; a
+// one-block segment writes its accumulators directly, the others through `part` and the merge.
+__global__ __launch_bounds__(DCOR_BLOCK) void k_accumulate_seg(const dcor_rep_out* rec,
+                                                               const int64_t* __restrict__ seg_off,
+                                                               const int64_t* __restrict__ seg_cnt,
+                                                               const double* __restrict__ rho,
+                                                               int max_nb, dcor_accum* part,
+                                                               dcor_accum* acc) {
+  __shared__ double red[16 * DCOR_WAVES];
+  __shared__ long long redi[DCOR_WAVES];
+  const int cell = blockIdx.y;
+  const int64_t count = seg_cnt[cell];
+  int64_t nb = (count + 2047) / 2048;
+  if (nb < 1) nb = 1;
+  if (nb > 512) nb = 512;
+  if ((int64_t)blockIdx.x >= nb) return;
+  const int64_t per = (count + nb - 1) / nb > 0 ? (count + nb - 1) / nb : 1;
+  const int64_t b0 = (int64_t)blockIdx.x * per;
+  const int64_t b1 = (b0 + per < count) ? b0 + per : count;
+  const dcor_rep_out* r0 = rec + seg_off[cell];
+  dcor_accum* dst = nb == 1 ? acc + 2 * cell : part + ((size_t)cell * max_nb + blockIdx.x) * 2;
+  for (int meth = 0; meth < 2; ++meth) {
+    DD s[6] = {{0, 0}, {0, 0}, {0, 0}, {0, 0}, {0, 0}, {0, 0}};
+    long long cnt[4] = {0, 0, 0, 0};
+    for (int64_t b = b0 + threadIdx.x; b < b1; b += DCOR_BLOCK) {
+      const double* r = &r0[b].ni_hat + 3 * meth;
+      acc_record(r[0], r[1], r[2], rho[cell], s, cnt);
+    }
+    block_sum_dd<6>(s, red);
+    long long tot[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) tot[q] = block_sum_i(cnt[q], redi);
+    if (threadIdx.x == 0) acc_write(dst + meth, b1 > b0 ? b1 - b0 : 0, s, tot);
+  }
+}
+
+__global__ __launch_bounds__(DCOR_BLOCK) void k_accumulate_seg_merge(const int64_t* __restrict__ seg_cnt,
+                                                                     int max_nb,
+                                                                     const dcor_accum* part,
+                                                                     dcor_accum* acc) {
+  __shared__ double red[16 * DCOR_WAVES];
+  __shared__ long long redi[DCOR_WAVES];
+  const int cell = blockIdx.x;
+  const int64_t count = seg_cnt[cell];
+  int64_t nb = (count + 2047) / 2048;
+  if (nb > 512) nb = 512;
+  if (nb <= 1) return;
+  const dcor_accum* p = part + (size_t)cell * max_nb * 2;
+  for (int meth = 0; meth < 2; ++meth) {
+    DD s[6] = {{0, 0}, {0, 0}, {0, 0}, {0, 0}, {0, 0}, {0, 0}};
+    long long cnt[4] = {0, 0, 0, 0};
+    for (int b = threadIdx.x; b < nb; b += DCOR_BLOCK) {
+      const dcor_accum& a = p[2 * b + meth];
+      s[0] = dd_add(s[0], DD{a.est[0], a.est[1]});
+      s[1] = dd_add(s[1], DD{a.est2[0], a.est2[1]});
+      s[2] = dd_add(s[2], DD{a.se2[0], a.se2[1]});
+      s[3] = dd_add(s[3], DD{a.len[0], a.len[1]});
+      s[4] = dd_add(s[4], DD{a.lo[0], a.lo[1]});
+      s[5] = dd_add(s[5], DD{a.hi[0], a.hi[1]});
+      cnt[0] += a.n_cover; cnt[1] += a.n_cover_na; cnt[2] += a.n_na_est; cnt[3] += a.n_na_ci;
+    }
+    block_sum_dd<6>(s, red);
+    long long tot[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) tot[q] = block_sum_i(cnt[q], redi);
+    if (threadIdx.x == 0) acc_write(acc + 2 * cell + meth, count, s, tot);
+  }
+}
+
 // ================================================== single-call helpers ===
 __global__ __launch_bounds__(DCOR_BLOCK) void k_mixquant(const double* z, const double* l,
                                                          MixConst mx, double c, double* out) {
@@ -834,6 +904,89 @@ __global__ __launch_bounds__(DCOR_BLOCK) void k_dp_sd(const double* x, int64_t n
     out[0] = mu;
     out[1] = sqrt(rmax(m2p - mu * mu, 0.0));
   }
+}
+
+// ================================================ R-surface transforms ===
+// The elementwise halves of the R wrappers' DGP and DP helpers: the wrapper draws with R's own
+// RNG calls (so .Random.seed advances exactly as in the reference) and the GPU does the
+// arithmetic, in R's operation order.
+
+// sd(Uc) of ci_INT_subG's clipped products (ver-cor-subG.R:88-99; real-data-sims.R:221-236),
+// one workgroup: the HRS wrapper's test of the sd(Uc) == 0 branch (real-data-sims.R:237).
+__global__ __launch_bounds__(DCOR_BLOCK) void k_uc_sd(PrematSubgConst p, double* out) {
+  __shared__ double red[16 * DCOR_WAVES];
+  const SubgConst& c = p.s;
+  const double* S = c.sender_is_X ? p.X : p.Y;
+  const double* O = c.sender_is_X ? p.Y : p.X;
+  DD a[2] = {{0, 0}, {0, 0}};
+  for (int64_t i = threadIdx.x; i < c.n; i += DCOR_BLOCK) {
+    const double ov = p.hrs ? rclip(O[i], p.lo_) : O[i];
+    const double Uc = rclip((rclip(S[i], c.ls) + c.bs * p.lap_local[i]) * ov, c.lr);
+    ks_acc(a[0], Uc);
+    ks_acc(a[1], Uc * Uc);
+  }
+  block_sum_dd<2>(a, red);
+  if (threadIdx.x == 0) out[0] = sqrt(dd_var(a[0], a[1], c.nd));
+}
+
+// standardize_dp (real-data-sims.R:87-90): (pmin(pmax(x, lo), hi) - mean) / max(sd, eps).
+__global__ __launch_bounds__(DCOR_BLOCK) void k_standardize_dp(const double* x, int64_t n, double lo,
+                                                               double hi, double mean, double den,
+                                                               double* out) {
+  const int64_t i = (int64_t)blockIdx.x * DCOR_BLOCK + threadIdx.x;
+  if (i < n) out[i] = (rclip_lohi(x[i], lo, hi) - mean) / den;
+}
+
+// gen_bernoulli from its uniforms u, v (vert-cor.R:85-97).
+__global__ __launch_bounds__(DCOR_BLOCK) void k_gen_bernoulli(const double* u, const double* v,
+                                                              int64_t n, double t0, double t1,
+                                                              double* X, double* Y) {
+  const int64_t i = (int64_t)blockIdx.x * DCOR_BLOCK + threadIdx.x;
+  if (i >= n) return;
+  const double x = (u[i] < 0.5) ? 1.0 : 0.0;                           // :88
+  X[i] = x;
+  Y[i] = (x == 0.0) ? (v[i] < t0 ? 1.0 : 0.0) : (v[i] < t1 ? 1.0 : 0.0);  // :92-96
+}
+
+// cbind(U + E1, U + E2) of gen_bounded_factor (ver-cor-subG.R:153).
+__global__ __launch_bounds__(DCOR_BLOCK) void k_gen_bounded_factor(const double* U, const double* E1,
+                                                                   const double* E2, int64_t n,
+                                                                   double* X, double* Y) {
+  const int64_t i = (int64_t)blockIdx.x * DCOR_BLOCK + threadIdx.x;
+  if (i >= n) return;
+  X[i] = U[i] + E1[i];
+  Y[i] = U[i] + E2[i];
+}
+
+// MASS::mvrnorm's transform of Z = matrix(rnorm(2n), n) (column 1 = z[0..n), column 2 =
+// z[n..2n)): mu + (V diag(sqrt(ev))) %*% t(Z) in dgemm's order, transposed back.  With `perm`
+// (gen_mix_gaussian, ver-cor-subG.R:127-135): rows of rbind(mvrnorm(n0), mvrnorm(n1)) taken in
+// sample.int(n) order and clipped to [-1, 1]; z1 holds component 1's 2 n1 normals.
+__global__ __launch_bounds__(DCOR_BLOCK) void k_mvrnorm_apply(const double* z0, int64_t n0,
+                                                              const double* z1, int64_t n1,
+                                                              const int32_t* perm, MvnConst m,
+                                                              double* X, double* Y) {
+  const int64_t n = n0 + n1;
+  const int64_t i = (int64_t)blockIdx.x * DCOR_BLOCK + threadIdx.x;
+  if (i >= n) return;
+  const int64_t src = perm ? (int64_t)perm[i] : i;
+  double xv, yv;
+  if (src < n0) {
+    const double a = z0[src], b = z0[n0 + src];
+    xv = m.mu0[0] + ((0.0 + a * m.A0[0]) + b * m.A0[1]);
+    yv = m.mu0[1] + ((0.0 + a * m.A0[2]) + b * m.A0[3]);
+  } else {
+    const int64_t t = src - n0;
+    const double a = z1[t], b = z1[n1 + t];
+    xv = m.mu1[0] + ((0.0 + a * m.A1[0]) + b * m.A1[1]);
+    yv = m.mu1[1] + ((0.0 + a * m.A1[2]) + b * m.A1[3]);
+  }
+  if (perm) {   // pmax(pmin(out, 1), -1)
+    xv = rclip_lohi(xv, -1.0, 1.0);
+    yv = rclip_lohi(yv, -1.0, 1.0);
+  }
+  X[i] = xv;
+  Y[i] = yv;
 }
 
 // ============================================================== draws ===
@@ -1263,6 +1416,26 @@ int launch_premat_subg(const PrematSubgConst& c0, int64_t reps, void* part, dcor
                        (hipStream_t)stream, c, reps, (const SubgPartial*)part, out);
   return last_err();
 }
+int accumulate_blocks(int64_t count) {
+  int64_t nb = (count + 2047) / 2048;
+  if (nb < 1) nb = 1;
+  if (nb > 512) nb = 512;
+  return (int)nb;
+}
+
+int launch_accumulate_seg(const dcor_rep_out* rec, int ncells, const int64_t* seg_off,
+                          const int64_t* seg_cnt, const double* rho, int max_nb, dcor_accum* part,
+                          dcor_accum* acc, void* stream) {
+  if (ncells <= 0) return 0;
+  const hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(k_accumulate_seg, dim3((unsigned)max_nb, (unsigned)ncells), dim3(DCOR_BLOCK), 0,
+                     st, rec, seg_off, seg_cnt, rho, max_nb, part, acc);
+  if (max_nb > 1)
+    hipLaunchKernelGGL(k_accumulate_seg_merge, dim3((unsigned)ncells), dim3(DCOR_BLOCK), 0, st, seg_cnt,
+                       max_nb, part, acc);
+  return last_err();
+}
+
 int launch_accumulate(const dcor_rep_out* d_out, int64_t count, double rho, dcor_accum* acc,
                       void* stream) {
   // ~2048 records per block, at most 512 blocks; 1 block writes acc directly.
@@ -1328,6 +1501,41 @@ int launch_dp_sd(const double* x, int64_t n, double lo, double hi, double s_mu, 
                  const double* lap2, double* out2, void* stream) {
   hipLaunchKernelGGL(k_dp_sd, dim3(1), dim3(DCOR_BLOCK), 0, (hipStream_t)stream, x, n, lo, hi,
                      s_mu, s_m2, lap2, out2);
+  return last_err();
+}
+
+static inline dim3 elem_grid(int64_t n) { return dim3((unsigned)((n + DCOR_BLOCK - 1) / DCOR_BLOCK)); }
+
+int launch_uc_sd(const PrematSubgConst& p, double* out, void* stream) {
+  hipLaunchKernelGGL(k_uc_sd, dim3(1), dim3(DCOR_BLOCK), 0, (hipStream_t)stream, p, out);
+  return last_err();
+}
+int launch_standardize_dp(const double* x, int64_t n, double lo, double hi, double mean, double den,
+                          double* out, void* stream) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(k_standardize_dp, elem_grid(n), dim3(DCOR_BLOCK), 0, (hipStream_t)stream, x, n,
+                     lo, hi, mean, den, out);
+  return last_err();
+}
+int launch_gen_bernoulli(const double* u, const double* v, int64_t n, double t0, double t1,
+                         double* X, double* Y, void* stream) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(k_gen_bernoulli, elem_grid(n), dim3(DCOR_BLOCK), 0, (hipStream_t)stream, u, v,
+                     n, t0, t1, X, Y);
+  return last_err();
+}
+int launch_gen_bounded_factor(const double* U, const double* E1, const double* E2, int64_t n,
+                              double* X, double* Y, void* stream) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(k_gen_bounded_factor, elem_grid(n), dim3(DCOR_BLOCK), 0, (hipStream_t)stream,
+                     U, E1, E2, n, X, Y);
+  return last_err();
+}
+int launch_mvrnorm_apply(const double* z0, int64_t n0, const double* z1, int64_t n1,
+                         const int32_t* perm, const MvnConst& m, double* X, double* Y, void* stream) {
+  if (n0 + n1 <= 0) return 0;
+  hipLaunchKernelGGL(k_mvrnorm_apply, elem_grid(n0 + n1), dim3(DCOR_BLOCK), 0, (hipStream_t)stream,
+                     z0, n0, z1, n1, perm, m, X, Y);
   return last_err();
 }
 

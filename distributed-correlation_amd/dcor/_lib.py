@@ -12,7 +12,7 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libdcor.so")
 
-DCOR_OK, DCOR_EINVAL, DCOR_EKLT1, DCOR_EHIP, DCOR_ENOMEM, DCOR_ENODEV = 0, 1, 2, 3, 4, 5
+DCOR_OK, DCOR_EINVAL, DCOR_EKLT1, DCOR_EHIP, DCOR_ENOMEM, DCOR_ENODEV, DCOR_EFORK = 0, 1, 2, 3, 4, 5, 6
 FAMILY_SIGN, FAMILY_SUBG = 0, 1
 DGP_GAUSSIAN, DGP_BERNOULLI, DGP_BOUNDED_FACTOR, DGP_MIX_GAUSSIAN = 0, 1, 2, 3
 MODE_AUTO, MODE_NORMAL, MODE_LAPLACE = 0, 1, 2
@@ -108,13 +108,16 @@ SIGNATURES = {
     "dcor_lambda_n": (C.c_double, [C.c_double, C.c_double]),
     "dcor_lambda_int_n": (None, [C.c_double, C.c_double, C.c_double, C.c_double, _D]),
     "dcor_lambda_receiver_from_noise": (C.c_double, [C.c_double] * 4),
-    "dcor_lambda_from_priv": (C.c_double, [C.c_double] * 4),
+    "dcor_lambda_from_priv": (C.c_double, [C.c_double] * 5),
     "dcor_qnorm": (C.c_double, [C.c_double]),
     "dcor_sim_launch": (C.c_int, [C.POINTER(Cell), C.c_int64, C.c_int64, _P, _P]),
     "dcor_accumulate_launch": (C.c_int, [_P, C.c_int64, C.c_double, _P, _P]),
     "dcor_accum_merge": (None, [C.POINTER(Accum), C.POINTER(Accum)]),
     "dcor_accum_finalize": (None, [C.POINTER(Accum), C.c_double, C.POINTER(Summary)]),
     "dcor_grid_run": (C.c_int, [C.POINTER(Cell), C.c_int, C.c_int64, C.POINTER(Accum), C.POINTER(RepOut)]),
+    "dcor_grid_launch": (C.c_int, [C.POINTER(Cell), C.c_int, _I64, _I64, _P, _P, _P]),
+    "dcor_grid_run_multi": (C.c_int, [C.POINTER(Cell), C.c_int, C.c_int64, C.POINTER(C.c_int), C.c_int,
+                                      C.POINTER(Accum), C.POINTER(RepOut)]),
     "dcor_rstream_grid_run": (C.c_int, [C.POINTER(Cell), C.c_int, C.c_int64, C.POINTER(Accum),
                                         C.POINTER(RepOut)]),
     "dcor_rstream_draws": (C.c_int, [C.POINTER(Cell), C.c_int64, C.POINTER(RsDraws)]),
@@ -150,6 +153,18 @@ SIGNATURES = {
     "dcor_perm_launch": (C.c_int, [C.c_uint64, C.c_int, C.c_int64, C.c_int64, C.c_int64, C.c_int64,
                                    _P, _P]),
     "dcor_dp_sd": (C.c_int, [_D, C.c_int64, C.c_double, C.c_double, C.c_double, C.c_double, _D, _D]),
+    # R-surface helpers (R/dcor*.R): the GPU half of wrappers that draw with R's own RNG
+    "dcor_int_subg_sd_uc": (C.c_int, [_D, _D, C.c_int64, C.c_double, C.c_double, C.c_double,
+                                      C.c_double, C.c_int, C.c_double, C.c_double, C.c_double,
+                                      C.c_double, _D, _D]),
+    "dcor_dp_mean": (C.c_int, [_D, C.c_int64, C.c_double, C.c_double, C.c_double, C.c_double, _D]),
+    "dcor_standardize_dp": (C.c_int, [_D, C.c_int64, C.c_double, C.c_double, C.c_double, C.c_double,
+                                      C.c_double, _D]),
+    "dcor_gen_bernoulli": (C.c_int, [_D, _D, C.c_int64, C.c_double, _D, _D]),
+    "dcor_gen_bounded_factor": (C.c_int, [_D, _D, _D, C.c_int64, _D, _D]),
+    "dcor_mvrnorm": (C.c_int, [_D, C.c_int64, _D, _D, C.c_double, _D, _D]),
+    "dcor_mix_gaussian": (C.c_int, [_D, C.c_int64, _D, C.c_int64, C.POINTER(C.c_int32), C.c_double,
+                                    _D, _D, _D, _D, _D, _D]),
 }
 
 

@@ -79,7 +79,8 @@ def lambda_receiver_from_noise(lambda_sender, lambda_other, eps_sender, delta_pe
 
 def lambda_from_priv(lo, hi, priv, eps_sd=1e-8) -> float:
     """real-data-sims.R:103-106 (priv = {'mean', 'sd'})."""
-    return lib.dcor_lambda_from_priv(float(lo), float(hi), float(priv["mean"]), float(priv["sd"]))
+    return lib.dcor_lambda_from_priv(float(lo), float(hi), float(priv["mean"]), float(priv["sd"]),
+                                     float(eps_sd))
 
 
 def qnorm(p) -> float:
@@ -130,15 +131,66 @@ def dp_sd(x, lo, hi, eps1, eps2, lap=None, rng=None) -> dict:
 
 
 def dp_mean(x, lo, hi, eps, lap=None, rng=None) -> float:
-    """dp_mean (real-data-sims.R:64-70)."""
+    """dp_mean (real-data-sims.R:64-70) (NA dropped like x[!is.na(x)])."""
+    v = _f64(x)
+    v = np.ascontiguousarray(v[~np.isnan(v)])
+    if v.size == 0:
+        return math.nan
     lap1 = unit_laplace(1, rng)[0] if lap is None else float(np.ravel(lap)[0])
-    return dp_sd(x, lo, hi, eps, 1.0, lap=[lap1, 0.0])["mean"]
+    out = C.c_double()
+    check(lib.dcor_dp_mean(_dp(v), len(v), float(lo), float(hi), float(eps), float(lap1), C.byref(out)))
+    return out.value
 
 
 def standardize_dp(x, priv, lo, hi, eps=1e-8) -> np.ndarray:
-    """standardize_dp (real-data-sims.R:87-90): once-per-dataset host preprocessing."""
-    xc = np.minimum(np.maximum(np.asarray(x, dtype=np.float64), lo), hi)
-    return (xc - priv["mean"]) / max(priv["sd"], eps)
+    """standardize_dp (real-data-sims.R:87-90): (pmin(pmax(x, lo), hi) - mean) / max(sd, eps)."""
+    v = _f64(x)
+    out = np.empty_like(v)
+    check(lib.dcor_standardize_dp(_dp(v), len(v), float(lo), float(hi), float(priv["mean"]),
+                                  float(priv["sd"]), float(eps), _dp(out)))
+    return out
+
+
+# ----------------------------------------------- DGPs from explicit (R) draws
+# The arithmetic half of the R wrappers' generators (R/dcor*.R): the caller supplies the draws R
+# would make, in R's order; the GPU returns (X, Y) as R computes them.
+def gen_bernoulli(u, v, rho):
+    """gen_bernoulli (vert-cor.R:78-98) from u = runif(n), v = runif(n) -> (X, Y)."""
+    u, v = _f64(u), _f64(v)
+    X, Y = np.empty_like(u), np.empty_like(u)
+    check(lib.dcor_gen_bernoulli(_dp(u), _dp(v), len(u), float(rho), _dp(X), _dp(Y)))
+    return X, Y
+
+
+def gen_bounded_factor(U, E1, E2):
+    """gen_bounded_factor (ver-cor-subG.R:141-154): (U + E1, U + E2) from its runif draws."""
+    U, E1, E2 = _f64(U), _f64(E1), _f64(E2)
+    X, Y = np.empty_like(U), np.empty_like(U)
+    check(lib.dcor_gen_bounded_factor(_dp(U), _dp(E1), _dp(E2), len(U), _dp(X), _dp(Y)))
+    return X, Y
+
+
+def mvrnorm(z, mu, sigma, rho):
+    """MASS::mvrnorm(n, mu, Sigma(sigma, rho)) (vert-cor.R:389-394) from z = rnorm(2n)."""
+    z = _f64(z)
+    n = len(z) // 2
+    mu_, sg = _f64(mu), _f64(sigma)
+    X, Y = np.empty(n), np.empty(n)
+    check(lib.dcor_mvrnorm(_dp(z), n, _dp(mu_), _dp(sg), float(rho), _dp(X), _dp(Y)))
+    return X, Y
+
+
+def mix_gaussian(z0, z1, perm, rho, mu0=(0, 0), sigma0=(1, 1), mu1=(3, 3), sigma1=(2, 0.5)):
+    """gen_mix_gaussian (ver-cor-subG.R:115-136) from z0 = rnorm(2 n0), z1 = rnorm(2 n1) and the
+    0-based row order perm = sample.int(n) - 1."""
+    z0, z1 = _f64(z0), _f64(z1)
+    n0, n1 = len(z0) // 2, len(z1) // 2
+    pm = np.ascontiguousarray(np.asarray(perm, dtype=np.int32))
+    a = [_f64(v) for v in (mu0, sigma0, mu1, sigma1)]
+    X, Y = np.empty(n0 + n1), np.empty(n0 + n1)
+    check(lib.dcor_mix_gaussian(_dp(z0), n0, _dp(z1), n1, pm.ctypes.data_as(C.POINTER(C.c_int32)),
+                                float(rho), *[_dp(v) for v in a], _dp(X), _dp(Y)))
+    return X, Y
 
 
 # ---------------------------------------------------------------- sign family

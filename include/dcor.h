@@ -37,6 +37,9 @@ extern "C" {
 #define DCOR_EHIP 3    /* HIP runtime error                                            */
 #define DCOR_ENOMEM 4
 #define DCOR_ENODEV 5  /* no gfx950 device visible                                     */
+#define DCOR_EFORK 6   /* called in a process forked (mclapply) after its parent had used the
+                          engine: HIP does not survive fork(); run the grid from the parent
+                          with one dcor_grid_run call instead            */
 
 enum { DCOR_FAMILY_SIGN = 0, DCOR_FAMILY_SUBG = 1 };
 enum { DCOR_DGP_GAUSSIAN = 0, DCOR_DGP_BERNOULLI = 1, DCOR_DGP_BOUNDED_FACTOR = 2,
@@ -95,10 +98,10 @@ const char* dcor_version(void);
 int dcor_last_error(char* buf, size_t len);
 /* Number of visible HIP devices (0 on a host without GPU; never fails). */
 int dcor_device_count(void);
-/* Release the library-owned per-device scratch arenas (the one-pass sign kernel keeps a
- * chunk x n x 4 B slab of per-sample codes, reused by every dcor_sim_launch on that
- * device: launches on different streams of one device must be ordered by the caller).
- * Safe to call at any time from the host. */
+/* Release the library-owned scratch: per (host thread, device) the one-pass sign kernel's
+ * chunk x n x 4 B slab of per-sample codes, the grid tables and the auxiliary stream.  Each host
+ * thread has its own, so threads never share scratch; launches of ONE thread on different
+ * streams of one device must be ordered by the caller.  Call when no work is in flight. */
 int dcor_shutdown(void);
 
 /* ---- calibration scalars (host closed forms) ----------------------------- */
@@ -108,8 +111,8 @@ double dcor_lambda_n(double n, double eta);
 void dcor_lambda_int_n(double n, double eta_s, double eta_r, double eps_s, double out[2]);
 /* lambda_receiver_from_noise, real-data-sims.R:170-174. */
 double dcor_lambda_receiver_from_noise(double lam_s, double lam_o, double eps_s, double delta);
-/* lambda_from_priv, real-data-sims.R:103-106. */
-double dcor_lambda_from_priv(double lo, double hi, double mean, double sd);
+/* lambda_from_priv(lo, hi, priv, eps_sd), real-data-sims.R:103-106 (priv = {mean, sd}). */
+double dcor_lambda_from_priv(double lo, double hi, double mean, double sd, double eps_sd);
 /* qnorm(p) (R's qnorm, used as qnorm(1 - alpha/2)). */
 double dcor_qnorm(double p);
 
@@ -129,11 +132,32 @@ int dcor_accumulate_launch(const dcor_rep_out* d_out, int64_t count, double rho,
 /* Host helpers over accumulators. */
 void dcor_accum_merge(dcor_accum* dst, const dcor_accum* src);
 void dcor_accum_finalize(const dcor_accum* acc, double rho, dcor_summary* out);
-/* Whole grid on the current device, synchronous, host buffers: the one `.Call`
- * that replaces the mclapply grid (vert-cor.R:534-553; ver-cor-subG.R:294-295).
- * h_acc: 2*ncells accumulators (NI, INT per cell); h_detail: NULL or ncells*B. */
+/* Whole grid on the current device, synchronous, host buffers (dcor_grid_run_multi with the
+ * current device).  h_acc: 2*ncells accumulators (NI, INT per cell); h_detail: NULL or ncells*B
+ * records, cell-major. */
 int dcor_grid_run(const dcor_cell* cells, int ncells, int64_t B, dcor_accum* h_acc,
                   dcor_rep_out* h_detail);
+
+/* The batched grid on the CURRENT device, asynchronous on `stream`: replicates
+ * [rep_begin[i], rep_begin[i] + rep_count[i]) of every cell i.  The replicates of all cells of one
+ * kernel family run in the same launches (one workgroup or wave per replicate, each cell's
+ * constants from a device table), so a grid of small cells -- the reference grids' B = 250 --
+ * fills the GPU like one large cell.  d_out: sum(rep_count) records, cell-major (cell i's first at
+ * sum_{j<i} rep_count[j]); d_acc: 2*ncells accumulators (NI, INT per cell) of those records,
+ * byte-identical to dcor_accumulate_launch on each cell's records.  Per-replicate results equal
+ * dcor_sim_launch's.  The scratch and tables are the calling thread's (one set per thread and
+ * device); ncells <= 65535. */
+int dcor_grid_launch(const dcor_cell* cells, int ncells, const int64_t* rep_begin,
+                     const int64_t* rep_count, dcor_rep_out* d_out, dcor_accum* d_acc,
+                     void* stream);
+/* The grid over several GPUs of one node, synchronous, host buffers: every cell's B replicates are
+ * split into contiguous ranges, shard g = [g B / G, (g+1) B / G) on device_ids[g] from its own host
+ * thread (a device may appear more than once); accumulators are merged in device-list order, so
+ * the summary is deterministic for a given list, and per-replicate records do not depend on it.
+ * device_ids = NULL / ndev = 0: every visible device.  Replaces mclapply over cells
+ * (vert-cor.R:534-553; ver-cor-subG.R:294-295). */
+int dcor_grid_run_multi(const dcor_cell* cells, int ncells, int64_t B, const int* device_ids,
+                        int ndev, dcor_accum* h_acc, dcor_rep_out* h_detail);
 
 /* ---- R-stream mode ------------------------------------- */
 /* The same grid as dcor_grid_run, but every replicate consumes R's OWN random stream: cell
@@ -289,6 +313,42 @@ int dcor_priv_standardize(const double* v, int64_t n, double eps_norm, double L_
 /* dp_sd (real-data-sims.R:73-84): out = {mean, sd}; lap = {mean, m2} unit draws. */
 int dcor_dp_sd(const double* x, int64_t n, double lo, double hi, double eps1, double eps2,
                const double lap[2], double out[2]);
+
+/* ---- R-surface helpers: the arithmetic half of R wrappers that draw with R's RNG ----------
+ * The R wrappers (R/dcor*.R) make the reference's own RNG calls in the reference's order, so
+ * .Random.seed advances exactly as it does under the reference, and hand the draws to these
+ * entries, which evaluate the rest on the GPU in R's operation order.  Host pointers,
+ * synchronous. */
+/* sd(Uc) of ci_INT_subG's clipped products for given X, Y and unit local noise
+ * (ver-cor-subG.R:87-99; hrs: real-data-sims.R:221-236): the HRS wrapper needs it to take the
+ * sd(Uc) == 0 branch (real-data-sims.R:237-238), which draws no mixquant values, before drawing
+ * anything.  Same lambda rules as dcor_ci_int_subg. */
+int dcor_int_subg_sd_uc(const double* X, const double* Y, int64_t n, double eps1, double eps2,
+                        double eta1, double eta2, int hrs, double lam_s, double lam_o,
+                        double lam_r, double delta, const double* lap_local, double* sd_uc);
+/* dp_mean (real-data-sims.R:64-70) of n non-NA values: mean(pmin(pmax(x, lo), hi)) +
+ * (hi - lo)/(n eps) * lap, lap a unit Laplace draw. */
+int dcor_dp_mean(const double* x, int64_t n, double lo, double hi, double eps, double lap,
+                 double* out);
+/* standardize_dp (real-data-sims.R:87-90): (pmin(pmax(x, lo), hi) - mean) / max(sd, eps). */
+int dcor_standardize_dp(const double* x, int64_t n, double lo, double hi, double mean, double sd,
+                        double eps, double* out);
+/* gen_bernoulli (vert-cor.R:78-98) from u = runif(n), v = runif(n); |rho| <= 1. */
+int dcor_gen_bernoulli(const double* u, const double* v, int64_t n, double rho, double* X,
+                       double* Y);
+/* gen_bounded_factor (ver-cor-subG.R:141-154): cbind(U + E1, U + E2) from its three runif draws. */
+int dcor_gen_bounded_factor(const double* U, const double* E1, const double* E2, int64_t n,
+                            double* X, double* Y);
+/* MASS::mvrnorm(n, mu, Sigma) with Sigma = [[s1^2, s1 s2 rho], [s1 s2 rho, s2^2]]
+ * (vert-cor.R:389-394) from z = rnorm(2n): LAPACK's eigenvectors (dsyevr / dlaev2) and dgemm's
+ * summation order, so X, Y equal R's.  DCOR_EINVAL if Sigma is not positive definite. */
+int dcor_mvrnorm(const double* z, int64_t n, const double mu[2], const double sigma[2],
+                 double rho, double* X, double* Y);
+/* gen_mix_gaussian (ver-cor-subG.R:115-136) from its draws: n0 labels 0 (rbinom), z0 = rnorm(2 n0),
+ * z1 = rnorm(2 n1), perm = sample.int(n) - 1 (0-based); rows clipped to [-1, 1]. */
+int dcor_mix_gaussian(const double* z0, int64_t n0, const double* z1, int64_t n1,
+                      const int32_t* perm, double rho, const double mu0[2], const double sigma0[2],
+                      const double mu1[2], const double sigma1[2], double* X, double* Y);
 
 /* On-device unit draws from the engine's Philox streams (pre-materialised inputs
  * generated in HBM, e.g. the HRS noise of BASELINE config C5).  kind: 0 unit Laplace,

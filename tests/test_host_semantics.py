@@ -71,3 +71,33 @@ def test_oracle_cell_check(kw, ok):
     c = CellSpec(**base).to_c()
     st = orc.lib.orc_cell_check(C.cast(C.pointer(c), C.c_void_p))
     assert (st == 0) == ok
+
+
+def test_fork_guard():
+    """A process forked after its parent reached the engine (R's mclapply children) gets
+    DCOR_EFORK from every compute entry, before any HIP call; the parent keeps working."""
+    import ctypes as C
+    import os
+
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("fork is only exercised on a host without a GPU")
+    from dcor import _lib
+    z = np.zeros(4)
+    P = C.POINTER(C.c_double)
+    out = C.c_double()
+    st = _lib.lib.dcor_mixquant(z.ctypes.data_as(P), z.ctypes.data_as(P), 4, 1.0, 0.5, C.byref(out))
+    assert st == _lib.DCOR_ENODEV          # the parent now owns the engine
+    r, w = os.pipe()
+    pid = os.fork()
+    if pid == 0:
+        code = _lib.lib.dcor_mixquant(z.ctypes.data_as(P), z.ctypes.data_as(P), 4, 1.0, 0.5, C.byref(out))
+        os.write(w, bytes([code]) + _lib.last_error().encode()[:200])
+        os._exit(0)
+    os.close(w)
+    msg = os.read(r, 256)
+    os.waitpid(pid, 0)
+    assert msg[0] == _lib.DCOR_EFORK, msg
+    assert b"fork" in msg
+    st = _lib.lib.dcor_mixquant(z.ctypes.data_as(P), z.ctypes.data_as(P), 4, 1.0, 0.5, C.byref(out))
+    assert st == _lib.DCOR_ENODEV
