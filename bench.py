@@ -35,11 +35,29 @@ def work_units(cell, m, k):
     return W_SAMPLE[cell.dgp] * cell.n + W_BATCH * k + W_REP
 
 
+def _cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(cell, seconds: float = 12.0):
-    """The reference's loop restated on the CPU (C, 1 thread) on a bounded sample of the
-    workload: run_sim_one from set.seed(seed) with R's own generators (Mersenne-Twister,
-    inversion rnorm, exp_rand, rbinom, extraDistr rlaplace, mvrnorm's eigen factor) and the
-    R-semantics estimators (oracle/dcor_rstream.c + dcor_oracle.c)."""
+    """The reference's loop restated on the CPU on a bounded sample of the workload:
+    run_sim_one from set.seed(seed) with R's own generators (Mersenne-Twister, inversion rnorm,
+    exp_rand, rbinom, extraDistr rlaplace, mvrnorm's eigen factor) and the R-semantics
+    estimators (oracle/dcor_rstream.c + dcor_oracle.c).
+
+    Two granularities: (i) one core, run_sim_one's own loop; (ii) the mclapply
+    grid equivalent -- mc.cores = detectCores() - 1 workers, each running its own cell (seed
+    1e6 + i, vert-cor.R:513,534-552), here threads calling the C restatement (ctypes releases
+    the GIL), capped at this box's CPU share.  Runs before the GPU is touched."""
+    import concurrent.futures as cf
+
     from oracle.oracle import rs_sim
     c = cell.to_c()
     t0 = time.perf_counter()
@@ -49,14 +67,43 @@ def cpu_baseline(cell, seconds: float = 12.0):
     t0 = time.perf_counter()
     rs_sim(c, B)
     el = time.perf_counter() - t0
+    nproc = os.cpu_count() or 1
+    usable = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else nproc
+    share = int(os.environ.get("OMP_NUM_THREADS", usable) or usable)
+    workers = max(1, min(usable, share, nproc) - 1)
+    Bw = max(2, int(B * 0.8))
+
+    def one(i):
+        ci = cell.to_c()
+        ci.seed = 1_000_000 + 1 + i
+        rs_sim(ci, Bw)
+        return Bw
+
+    t0 = time.perf_counter()
+    with cf.ThreadPoolExecutor(max_workers=workers) as ex:
+        done = sum(ex.map(one, range(workers)))
+    elm = time.perf_counter() - t0
     return {"value": B / el, "unit": "replicates/s", "cores": 1, "kind": "port",
             "sample": f"replicates 1..{B} of run_sim_one(seed={cell.seed}) on the headline cell "
                       f"(n={cell.n}) in {el:.1f} s: oracle/dcor_rstream.c (R's own generators) + "
                       "dcor_oracle.c (R-semantics estimators), 1 thread (mclapply granularity: one "
-                      "core per cell)"}
+                      "core per cell); faster than R, whose batch loop is interpreted",
+            "nproc": nproc, "usable_cores": usable, "cpu_model": _cpu_model(),
+            "multi_core_value": done / elm, "multi_core_cores": workers,
+            "multi_core_sample": f"{workers} threads x {Bw} replicates, each its own headline-config "
+                                 f"cell (seed 1e6 + i), in {elm:.1f} s: the mclapply grid's "
+                                 "detectCores() - 1 workers, capped at this box's CPU share"}
 
 
-def pmc_traffic(path=os.path.join(ROOT, "profiles", "r01_headline_summary.json")):
+def _profile(name):
+    for tag in ("r02", "r01"):
+        p = os.path.join(ROOT, "profiles", f"{tag}_{name}_summary.json")
+        if os.path.exists(p):
+            return p
+    return None
+
+
+def pmc_traffic(path=_profile("headline")):
     """HBM bytes per simulate() call from the committed rocprofv3 PMC passes (FETCH_SIZE x2
     for gfx950's half-count of wide reads, + WRITE_SIZE; scripts/summarize_prof.py), summed
     over the sign kernels of one call.  None if the profile is absent."""
@@ -70,15 +117,23 @@ def pmc_traffic(path=os.path.join(ROOT, "profiles", "r01_headline_summary.json")
         return None
 
 
-def issue_util(path=os.path.join(ROOT, "profiles", "r01_serial_summary.json")):
-    """Measured VALU issue utilisation of the sign kernels (rocprofv3 PMC, chunks profiled
-    serially: SQ_INSTS_VALU / (256 CUs x GRBM_GUI_ACTIVE/8)), or None."""
+def issue_frac(path=_profile("serial")):
+    """Physically grounded VALU roofline of the sign kernels from the committed rocprofv3 profile
+    (chunks profiled serially): each instruction class of the measured mix (SQ_INSTS_VALU_*)
+    weighted by its measured gfx950 issue cost (profiles/r02_issue_costs.json,
+    scripts/ubench_issue.hip), over the dispatch's SIMD-cycles (1024 x GRBM_GUI_ACTIVE / 8).
+    -> (time-weighted fraction over pass 1 + pass 2 + epilogue, per kernel, source) or Nones."""
     try:
         ks = json.load(open(path))["kernels"]
-        return {name.split("::")[1].split("<")[0]: round(v["valu_issue_util"], 3)
-                for name, v in ks.items() if "k_sign_pass" in name and "valu_issue_util" in v}
-    except (OSError, KeyError, ValueError, IndexError):
-        return None
+        per, num, den = {}, 0.0, 0.0
+        for name, v in ks.items():
+            if "k_sign_" in name and "valu_time_frac" in v:
+                per[name.split("::")[1].split("(")[0]] = round(v["valu_time_frac"], 3)
+                num += v["valu_time_frac"] * v["avg_ns"] * v["calls"]
+                den += v["avg_ns"] * v["calls"]
+        return (num / den if den else None), (per or None), os.path.relpath(path, ROOT)
+    except (OSError, KeyError, ValueError, IndexError, TypeError):
+        return None, None, None
 
 
 def main():
@@ -98,6 +153,10 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    cpu = None
+    if world == 1 and not args.no_cpu_baseline:   # before the GPU is touched (the pool forks nothing)
+        from dcor.sim import headline_cell as _hc
+        cpu = cpu_baseline(_hc(args.n), args.cpu_seconds)
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -158,6 +217,7 @@ def main():
     achieved = R * W * 2.0 / (kern_ms * 1e-3) / 1e12  # fp64-equivalent TFLOP/s per GPU
     summ = {"NI": finalize(merged[0], cell.rho), "INT": finalize(merged[1], cell.rho)}
 
+    ifrac, iper, isrc = issue_frac()
     if rank == 0:
         res = {
             "metric": METRIC, "value": value, "unit": "replicates/s", "n_gpus": world,
@@ -169,21 +229,26 @@ def main():
                        "n": cell.n, "m": m, "k": k, "replicates_per_gpu_per_step": R,
                        "parallelism": f"replicate-shard x{world}"},
             "roofline": {"bound": "valu_fp64", "achieved": achieved, "peak": FP64_PEAK_TFLOPS,
-                         "unit": "TFLOP/s", "frac": achieved / FP64_PEAK_TFLOPS, "traffic": pmc_traffic(),
-                         "traffic_unit": "B per simulate() call (rocprofv3 PMC, profiles/r01_headline_summary.json)",
-                         "kernel": "k_sign_pass1 + k_sign_pass2 (one simulate() call)",
+                         "unit": "TFLOP/s", "frac": achieved / FP64_PEAK_TFLOPS,
+                         "frac_convention": achieved / FP64_PEAK_TFLOPS,
+                         "frac_kind": "pinned-convention: SURVEY §8d work weights (fp64-FMA units) per "
+                                      "replicate x replicates / kernel time over the fp64 peak; > 1 means "
+                                      "the kernels issue fewer instructions than the weights assume",
+                         "issue_frac": ifrac, "issue_frac_per_kernel": iper,
+                         "issue_frac_kind": "measured: VALU instruction mix (rocprofv3 PMC) x measured "
+                                            "gfx950 issue cost per class / SIMD-cycles, time-weighted "
+                                            "over the sign kernels",
+                         "issue_source": isrc,
+                         "traffic": pmc_traffic(),
+                         "traffic_unit": "HBM B per simulate() call (rocprofv3 PMC, FETCH_SIZE x2 + WRITE_SIZE)",
+                         "kernel": "k_sign_pass1 + k_sign_pass2 + k_sign_epilogue_w (one simulate() call)",
                          "kernel_ms_avg": kern_ms,
-                         "work_units_per_rep": W,
-                         "valu_issue_util": issue_util(),
-                         "note": "achieved = R * W_rep(SURVEY §8d pinned weights) * 2 / kernel time; "
-                                 "frac > 1 means fewer instructions than the pinned weights assume; "
-                                 "valu_issue_util = measured fraction of the VALU issue ceiling "
-                                 "(profiles/r01_serial_summary.json)"},
+                         "work_units_per_rep": W},
             "summary": {"coverage_NI": summ["NI"]["coverage"], "coverage_INT": summ["INT"]["coverage"],
                         "ci_len_NI": summ["NI"]["ci_length"], "ci_len_INT": summ["INT"]["ci_length"]},
         }
-        if world == 1 and not args.no_cpu_baseline:
-            res["cpu_baseline"] = cpu_baseline(cell, args.cpu_seconds)
+        if cpu is not None:
+            res["cpu_baseline"] = cpu
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()

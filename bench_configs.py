@@ -8,6 +8,9 @@ C4  legacy paper sweep: {sign: gaussian, bernoulli; sub-G: gaussian, bounded fac
 C5  HRS BMI-vs-Age pre-materialised streaming (synthetic stand-in panel n=19,433, eps=2): noise
     generated on device into HBM, then the streaming kernel is timed -> replicates/s and HBM GB/s
 S   sub-G fused, bounded factor, n=1e5, rho=.5, eps=(1,1)
+VG  vert-cor.R's own 144-cell sign grid (vert-cor.R:486-499) at its B = 250, Philox mode, batched
+    launches (dcor_grid_run_multi) vs the per-cell launch loop
+SG  ver-cor-subG.R's own 120-cell sub-G grid (ver-cor-subG.R:245-258) at B = 250, likewise
 R1  R-stream mode (R's own Mersenne-Twister streams) on the C1 cell: GPU vs the
     CPU restatement (1 thread)
 RG  R-stream mode on vert-cor.R's own 144-cell sign-family grid, B = 250 (vert-cor.R:486-553)
@@ -59,7 +62,15 @@ def grid_units(cells, B):
     return tot
 
 
+def run_grid_batched(cells, B):
+    """The grid through dcor_grid_run_multi on GPU 0: batched launches, accumulators to the host."""
+    from dcor.sim import run_grid
+    return run_grid(cells, B, devices=[0])
+
+
 def run_grid_gpu(cells, B, chunk=1 << 15):
+    """The per-cell launch loop (dcor_sim_launch + dcor_accumulate_launch per cell): the A/B
+    reference for the batched grid."""
     import torch
     from dcor.sim import simulate, accumulate
     buf = torch.empty((min(B, chunk), 6), dtype=torch.float64, device="cuda")
@@ -100,7 +111,7 @@ def c2():
     cells = expand_grid([10_000], [0, 0.15, 0.3, 0.4, 0.5, 0.65, 0.8, 0.9],
                         [(0.5, 0.5), (1.0, 1.0), (1.5, 0.5)], family="sign", dgp="bernoulli")
     B = 10_000
-    t = timed(lambda: run_grid_gpu(cells, B), reps=2)
+    t = timed(lambda: run_grid_batched(cells, B), reps=2)
     u = grid_units(cells, B)
     line("C2", cells=len(cells), reps_per_cell=B, seconds=t, reps_per_s=len(cells) * B / t,
          roofline_frac=u / t / FP64_PEAK_UNITS)
@@ -111,7 +122,7 @@ def c3(reps):
     cells = expand_grid([1_000_000], [0, 0.15, 0.3, 0.4, 0.5, 0.65, 0.8, 0.9],
                         [(0.5, 0.5), (1.0, 1.0), (1.5, 0.5)], family="sign", dgp="gaussian",
                         mu=(0.5, 0.5), sigma=(2.0, 2.0))
-    t = timed(lambda: run_grid_gpu(cells, reps), reps=1)
+    t = timed(lambda: run_grid_batched(cells, reps), reps=1)
     u = grid_units(cells, reps)
     rps = len(cells) * reps / t
     line("C3", cells=len(cells), reps_per_cell=reps, seconds=t, reps_per_s=rps,
@@ -129,10 +140,25 @@ def c4(B):
         if c.family == "sign" and c.n // m < 1:
             continue
         ok.append(c)
-    t = timed(lambda: run_grid_gpu(ok, B), reps=1)
+    t = timed(lambda: run_grid_batched(ok, B), reps=1)
+    tl = timed(lambda: run_grid_gpu(ok, B), reps=1)
     u = grid_units(ok, B)
     line("C4", cells=len(ok), cells_skipped_k_lt_1=len(cells) - len(ok), reps_per_cell=B, seconds=t,
-         reps_per_s=len(ok) * B / t, roofline_frac=u / t / FP64_PEAK_UNITS)
+         reps_per_s=len(ok) * B / t, roofline_frac=u / t / FP64_PEAK_UNITS,
+         per_cell_loop_seconds=tl, per_cell_loop_reps_per_s=len(ok) * B / tl)
+
+
+def ref_grid(name, cells, B=250):
+    """A reference grid at its own B: batched (one dcor_grid_run_multi call, accumulators on the
+    host) vs the per-cell launch loop."""
+    t = timed(lambda: run_grid_batched(cells, B), reps=3)
+    tl = timed(lambda: run_grid_gpu(cells, B), reps=3)
+    u = grid_units(cells, B)
+    line(name, cells=len(cells), reps_per_cell=B, seconds=t, reps_per_s=len(cells) * B / t,
+         roofline_frac=u / t / FP64_PEAK_UNITS, per_cell_loop_seconds=tl,
+         per_cell_loop_reps_per_s=len(cells) * B / tl, speedup_vs_per_cell_loop=tl / t,
+         note="Philox mode; seconds include the planning, the table upload and the host copy of "
+              "every cell's accumulators")
 
 
 def c5(R, panel="coded"):
@@ -341,7 +367,7 @@ def rstream_hrs():
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--only", default="C1,C2,C3,C4,C5,C5c,C5e,C5f,S,R1,RG,RH")
+    ap.add_argument("--only", default="C1,C2,C3,C4,VG,SG,C5,C5c,C5e,C5f,S,R1,RG,RH")
     ap.add_argument("--c3-reps", type=int, default=2000)
     ap.add_argument("--c4-B", type=int, default=1000)
     ap.add_argument("--c5-R", type=int, default=8192)
@@ -354,6 +380,12 @@ def main():
     if "C2" in which: c2()
     if "C3" in which: c3(a.c3_reps)
     if "C4" in which: c4(a.c4_B)
+    if "VG" in which:
+        from dcor.sim import vert_cor_grid
+        ref_grid("VG", vert_cor_grid())
+    if "SG" in which:
+        from dcor.sim import subg_grid
+        ref_grid("SG", subg_grid())
     if "C5" in which: c5(a.c5_R)
     if "C5c" in which: c5(a.c5_R, panel="continuous")
     if "C5e" in which: c5_e2e(a.c5e_R)

@@ -4,7 +4,11 @@ Copies the kernel-trace stats CSV and writes <tag>_summary.json / .md with, per 
 average duration, PMC counters per dispatch (FETCH_SIZE doubled for gfx950's 1/2 under-
 report of wide streaming reads, MI355X_MICROARCH.md §HBM), effective clock, VALU
 activity and the fp64 instruction mix.
-Usage: python scripts/summarize_prof.py <tag> [gpurun_out]
+VALU time: each instruction class of the mix weighted by its measured issue cost on gfx950
+(SIMD cycles per wave64 instruction, scripts/ubench_issue.hip -> profiles/<costs>.json), over
+the SIMD-cycles the dispatch had (1024 SIMDs x GRBM_GUI_ACTIVE / 8): the physically grounded
+roofline fraction of a VALU-bound kernel.
+Usage: python scripts/summarize_prof.py <tag> [gpurun_out] [issue-costs json]
 """
 import collections
 import csv
@@ -18,6 +22,21 @@ src = sys.argv[2] if len(sys.argv) > 2 else "gpurun_out"
 root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 dst = os.path.join(root, "profiles")
 os.makedirs(dst, exist_ok=True)
+costs_path = sys.argv[3] if len(sys.argv) > 3 else os.path.join(dst, "r02_issue_costs.json")
+COSTS = json.load(open(costs_path))["cycles_per_wave_instruction"] if os.path.exists(costs_path) else None
+# instruction class of the mix counters -> the measured instruction that represents it
+CLASS_COST = {"SQ_INSTS_VALU_ADD_F64": "v_add_f64", "SQ_INSTS_VALU_MUL_F64": "v_mul_f64",
+              "SQ_INSTS_VALU_FMA_F64": "v_fma_f64", "SQ_INSTS_VALU_TRANS_F64": "v_rsq_f64",
+              "SQ_INSTS_VALU_INT32": "v_add_u32", "SQ_INSTS_VALU_INT64": "v_mad_u64_u32",
+              "SQ_INSTS_VALU_CVT": "v_cvt_f64_i32"}
+OTHER_COST = "v_bitop3_b32"   # the rest: bit ops, moves, selects, fp32 (single-issue class)
+
+
+def valu_cycles(avg):
+    """SIMD cycles the dispatch's VALU instructions take at their measured issue costs."""
+    mix = {c: avg.get(c, 0.0) for c in CLASS_COST}
+    rest = max(0.0, avg["SQ_INSTS_VALU"] - sum(mix.values()))
+    return sum(v * COSTS[CLASS_COST[c]] for c, v in mix.items()) + rest * COSTS[OTHER_COST]
 
 
 def short(name):
@@ -66,6 +85,10 @@ for kname, cs in counters.items():
         # per CU (256 CUs); meaningful for kernels profiled without overlap (PIPE=0 runs)
         if "SQ_INSTS_VALU" in avg:
             k["valu_issue_util"] = avg["SQ_INSTS_VALU"] / (256 * avg["GRBM_GUI_ACTIVE"] / 8)
+            if COSTS and all(c in avg for c in CLASS_COST):
+                # VALU time over the SIMD-cycles of the dispatch (1024 SIMDs)
+                k["valu_time_frac"] = valu_cycles(avg) / (1024 * avg["GRBM_GUI_ACTIVE"] / 8)
+                k["valu_cycles_per_dispatch"] = valu_cycles(avg)
     mix = {c: avg[c] for c in avg if c.startswith("SQ_INSTS_VALU_")}
     if mix:
         k["valu_mix_wave_instructions"] = mix
@@ -91,14 +114,15 @@ if os.path.exists(trace):
 
 json.dump(out, open(os.path.join(dst, f"{tag}_summary.json"), "w"), indent=1, sort_keys=True)
 lines = [f"# rocprofv3 summary `{tag}`", "",
-         "| kernel | calls | avg µs | % time | VGPR | HBM read B (corr.) | HBM write B | VALU active / wave-cycles | VALU issue util | clock GHz |",
-         "|---|---|---|---|---|---|---|---|---|---|"]
+         "| kernel | calls | avg µs | % time | VGPR | HBM read B (corr.) | HBM write B | VALU active / wave-cycles | VALU instr / CU-cycle | VALU time / SIMD-cycles | clock GHz |",
+         "|---|---|---|---|---|---|---|---|---|---|---|"]
 for kname, k in sorted(out["kernels"].items(), key=lambda kv: -kv[1].get("pct_time", 0)):
     def f(x, fmt="{:.3g}"):
         return fmt.format(x) if isinstance(x, (int, float)) else "—"
     lines.append(f"| {kname} | {k.get('calls', '—')} | {f(k.get('avg_ns', 0) / 1e3)} | {f(k.get('pct_time'))} | "
                  f"{f(k.get('vgpr'))} | {f(k.get('hbm_read_bytes_corrected'))} | {f(k.get('hbm_write_bytes'))} | "
                  f"{f(k.get('valu_active_frac_of_wave_cycles'))} | {f(k.get('valu_issue_util'))} | "
+                 f"{f(k.get('valu_time_frac'))} | "
                  f"{f(k.get('effective_clock_ghz'))} |")
 if "simulate_call_span_ms" in out:
     sp = out["simulate_call_span_ms"]
