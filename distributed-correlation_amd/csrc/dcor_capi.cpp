@@ -332,7 +332,8 @@ void ctx_free(Ctx* c) {
   }
   if (c->staging_free) { (void)hipEventSynchronize(c->staging_free); (void)hipEventDestroy(c->staging_free); }
   if (c->staging) (void)hipHostFree(c->staging);
-  for (Arena* a : {&c->codes, &c->rs, &c->grid})
+  if (c->work) { (void)hipStreamSynchronize(c->work); (void)hipStreamDestroy(c->work); }
+  for (Arena* a : {&c->codes, &c->rs, &c->grid, &c->out})
     if (a->p) (void)hipFree(a->p);
   delete c;
 }

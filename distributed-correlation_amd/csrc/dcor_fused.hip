@@ -8,6 +8,7 @@
 
 #include <cstdlib>
 #include <cstring>
+#include <type_traits>
 
 #include "dcor_common.h"
 
@@ -318,8 +319,9 @@ __device__ __forceinline__ void sign_pass1_body(const SignConst& c, uint32_t rep
   const int tid = threadIdx.x;
   DD sx{0.0, 0.0}, sy{0.0, 0.0};
   double v[2] = {0.0, 0.0};
-  const int64_t ngrp = (c.n + 3) / 4;
-  for (int64_t g4 = tid; g4 < ngrp; g4 += DCOR_BLOCK) {
+  // group g4 = samples 4 g4 .. 4 g4 + 3; FULL: all four exist (the hot loop has no guards)
+  auto group = [&](int64_t g4, auto full_tag) {
+    constexpr bool FULL = decltype(full_tag)::value;
     const uint32_t i0 = (uint32_t)(4 * g4);
     double x[4], y[4];
     uint32_t fl[4];  // INT flip bits (vert-cor.R:175)
@@ -339,20 +341,24 @@ __device__ __forceinline__ void sign_pass1_body(const SignConst& c, uint32_t rep
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const double xc = rclip_fin(x[q], c.L), yc = rclip_fin(y[q], c.L);
-      if ((int64_t)(i0 + q) < c.n) { gx += xc; v[0] += xc * xc; gy += yc; v[1] += yc * yc; }
+      if (FULL || (int64_t)(i0 + q) < c.n) { gx += xc; v[0] += xc * xc; gy += yc; v[1] += yc * yc; }
       const uint32_t qx = code16(xc, c.cinv_xf, c.cnb_xf, 65535.0f);
       const uint32_t qy = code16(yc, c.cinv_yf, c.cnb_yf, 32767.0f);
-      const uint32_t f = fl[q];
-      rec[q] = qx | (qy << 16) | (f << 31);
+      rec[q] = qx | (qy << 16) | (fl[q] << 31);
     }
     ks_acc(sx, gx);
     ks_acc(sy, gy);
-    if ((int64_t)i0 + 3 < c.n) {
+    if (FULL) {
       *reinterpret_cast<uint4*>(slab + i0) = make_uint4(rec[0], rec[1], rec[2], rec[3]);
     } else {
       for (int q = 0; q < 4; ++q) if ((int64_t)(i0 + q) < c.n) slab[i0 + q] = rec[q];
     }
-  }
+  };
+  // each thread runs its groups in increasing order; the partial last group (n % 4) is the last
+  // group of its thread, so the per-thread accumulation order is the same as one guarded loop
+  const int64_t nfull = c.n / 4;
+  for (int64_t g4 = tid; g4 < nfull; g4 += DCOR_BLOCK) group(g4, std::true_type());
+  if ((c.n & 3) && tid == (int)(nfull % DCOR_BLOCK)) group(nfull, std::false_type());
   DD d2[2] = {sx, sy};
   block_sum_dd<2>(d2, red);
   block_sum<2>(v, red + 4 * DCOR_WAVES);
@@ -362,8 +368,15 @@ __device__ __forceinline__ void sign_pass1_body(const SignConst& c, uint32_t rep
   }
 }
 
+// Minimum waves per SIMD the one-pass kernels are compiled for (register budget 512 / w).
+#ifndef DCOR_P1_WPE
+#define DCOR_P1_WPE 1
+#endif
+#ifndef DCOR_P2_WPE
+#define DCOR_P2_WPE 1
+#endif
 template <int DGP>
-__global__ __launch_bounds__(DCOR_BLOCK) void k_sign_pass1(SignConst c,
+__global__ __launch_bounds__(DCOR_BLOCK, DCOR_P1_WPE) void k_sign_pass1(SignConst c,
                                                            uint32_t* __restrict__ scratch,
                                                            double* __restrict__ sums) {
   sign_pass1_body<DGP>(c, (uint32_t)(c.rep_begin + blockIdx.x),
@@ -522,7 +535,7 @@ __device__ __forceinline__ void sign_pass2_body(const SignConst& c, uint32_t rep
 }
 
 template <int DGP>
-__global__ __launch_bounds__(DCOR_BLOCK) void k_sign_pass2(SignConst c,
+__global__ __launch_bounds__(DCOR_BLOCK, DCOR_P2_WPE) void k_sign_pass2(SignConst c,
                                                            const uint32_t* __restrict__ scratch,
                                                            const double* __restrict__ sums,
                                                            SignPartial* __restrict__ part) {

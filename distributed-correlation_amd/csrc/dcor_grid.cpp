@@ -267,32 +267,22 @@ int run_shard(const dcor_cell* cells, int ncells, bool detail, Shard& s) {
   const size_t nrec = (size_t)ncells * (size_t)s.nb;
   if (detail) s.rec.resize(nrec);
   std::vector<int64_t> rb((size_t)ncells, s.b0), rn((size_t)ncells, s.nb);
-  hipStream_t st = nullptr;
-  HIPCHK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
-  void* d_out = nullptr;
-  void* d_acc = nullptr;
-  int rc = DCOR_OK;
-  if (hipMallocAsync(&d_out, std::max<size_t>(nrec, 1) * sizeof(dcor_rep_out), st) != hipSuccess ||
-      hipMallocAsync(&d_acc, (size_t)ncells * 2 * sizeof(dcor_accum), st) != hipSuccess) {
-    (void)hipGetLastError();
-    rc = fail(DCOR_ENOMEM, "grid: cannot allocate the replicate records");
-  }
-  if (rc == DCOR_OK)
-    rc = dcor_grid_launch(cells, ncells, rb.data(), rn.data(), (dcor_rep_out*)d_out,
-                          (dcor_accum*)d_acc, st);
-  if (rc == DCOR_OK &&
-      hipMemcpyAsync(s.acc.data(), d_acc, s.acc.size() * sizeof(dcor_accum), hipMemcpyDeviceToHost, st) != hipSuccess)
-    rc = hip_fail(hipGetLastError(), "grid: accumulator copy");
-  if (rc == DCOR_OK && detail && nrec &&
-      hipMemcpyAsync(s.rec.data(), d_out, nrec * sizeof(dcor_rep_out), hipMemcpyDeviceToHost, st) != hipSuccess)
-    rc = hip_fail(hipGetLastError(), "grid: record copy");
-  const hipError_t se = hipStreamSynchronize(st);
-  if (rc == DCOR_OK && se != hipSuccess) rc = hip_fail(se, "grid: stream synchronize");
-  if (d_out) (void)hipFreeAsync(d_out, st);
-  if (d_acc) (void)hipFreeAsync(d_acc, st);
-  (void)hipStreamSynchronize(st);
-  (void)hipStreamDestroy(st);
-  return rc;
+  // the calling thread's stream and record buffer on this device (kept across calls)
+  Ctx* ctx = nullptr;
+  if (int st = ctx_get(&ctx)) return st;
+  if (!ctx->work) HIPCHK(hipStreamCreateWithFlags(&ctx->work, hipStreamNonBlocking));
+  const hipStream_t st = ctx->work;
+  const size_t rec_b = al256(std::max<size_t>(nrec, 1) * sizeof(dcor_rep_out));
+  void* buf = nullptr;
+  if (int e = arena_grow(ctx->out, rec_b + (size_t)ncells * 2 * sizeof(dcor_accum), &buf)) return e;
+  dcor_rep_out* d_out = (dcor_rep_out*)buf;
+  dcor_accum* d_acc = (dcor_accum*)((char*)buf + rec_b);
+  if (int e = dcor_grid_launch(cells, ncells, rb.data(), rn.data(), d_out, d_acc, st)) return e;
+  HIPCHK(hipMemcpyAsync(s.acc.data(), d_acc, s.acc.size() * sizeof(dcor_accum), hipMemcpyDeviceToHost, st));
+  if (detail && nrec)
+    HIPCHK(hipMemcpyAsync(s.rec.data(), d_out, nrec * sizeof(dcor_rep_out), hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  return DCOR_OK;
 }
 
 }  // namespace

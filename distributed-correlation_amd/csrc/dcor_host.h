@@ -36,6 +36,8 @@ struct Pipe { hipStream_t s = nullptr; hipEvent_t fork = nullptr, join = nullptr
 struct Ctx {
   int dev = -1;
   Arena codes, rs, grid;
+  Arena out;                      // the synchronous grid entries' replicate records + accumulators
+  hipStream_t work = nullptr;     // ... and their stream
   Pipe pipe;
   void* staging = nullptr;
   size_t staging_bytes = 0;

@@ -10,7 +10,8 @@ import math
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libdcor.so")
+# DCOR_LIB: an alternative in-tree build of the same library (A/B runs of compile-time variants)
+LIB_PATH = os.environ.get("DCOR_LIB") or os.path.join(_HERE, "libdcor.so")
 
 DCOR_OK, DCOR_EINVAL, DCOR_EKLT1, DCOR_EHIP, DCOR_ENOMEM, DCOR_ENODEV, DCOR_EFORK = 0, 1, 2, 3, 4, 5, 6
 FAMILY_SIGN, FAMILY_SUBG = 0, 1
