@@ -118,18 +118,18 @@ def pmc_traffic(path=_profile("headline")):
 
 
 def issue_frac(path=_profile("serial")):
-    """Physically grounded VALU roofline of the sign kernels from the committed rocprofv3 profile
-    (chunks profiled serially): each instruction class of the measured mix (SQ_INSTS_VALU_*)
-    weighted by its measured gfx950 issue cost (profiles/r02_issue_costs.json,
-    scripts/ubench_issue.hip), over the dispatch's SIMD-cycles (1024 x GRBM_GUI_ACTIVE / 8).
+    """Hardware-measured VALU roofline of the sign kernels from the committed rocprofv3 profile
+    (chunks profiled serially, so no kernel shares the SIMDs): rocprof's VALUBusy,
+    SQ_ACTIVE_INST_VALU x 4 / (1024 SIMDs x GRBM_GUI_ACTIVE / 8), the fraction of SIMD-cycles the
+    vector ALU was executing (scripts/summarize_prof.py valu_busy; <= 1 by construction).
     -> (time-weighted fraction over pass 1 + pass 2 + epilogue, per kernel, source) or Nones."""
     try:
         ks = json.load(open(path))["kernels"]
         per, num, den = {}, 0.0, 0.0
         for name, v in ks.items():
-            if "k_sign_" in name and "valu_time_frac" in v:
-                per[name.split("::")[1].split("(")[0]] = round(v["valu_time_frac"], 3)
-                num += v["valu_time_frac"] * v["avg_ns"] * v["calls"]
+            if "k_sign_" in name and "valu_busy" in v:
+                per[name.split("::")[1].split("(")[0]] = round(v["valu_busy"], 3)
+                num += v["valu_busy"] * v["avg_ns"] * v["calls"]
                 den += v["avg_ns"] * v["calls"]
         return (num / den if den else None), (per or None), os.path.relpath(path, ROOT)
     except (OSError, KeyError, ValueError, IndexError, TypeError):
@@ -235,9 +235,9 @@ def main():
                                       "replicate x replicates / kernel time over the fp64 peak; > 1 means "
                                       "the kernels issue fewer instructions than the weights assume",
                          "issue_frac": ifrac, "issue_frac_per_kernel": iper,
-                         "issue_frac_kind": "measured: VALU instruction mix (rocprofv3 PMC) x measured "
-                                            "gfx950 issue cost per class / SIMD-cycles, time-weighted "
-                                            "over the sign kernels",
+                         "issue_frac_kind": "measured: rocprofv3 VALUBusy (SQ_ACTIVE_INST_VALU x 4 / "
+                                            "SIMD-cycles), time-weighted over the sign kernels "
+                                            "profiled serially; the VALU-bound kernels' roofline",
                          "issue_source": isrc,
                          "traffic": pmc_traffic(),
                          "traffic_unit": "HBM B per simulate() call (rocprofv3 PMC, FETCH_SIZE x2 + WRITE_SIZE)",

@@ -269,24 +269,33 @@ def c5_e2e(R):
               "D2H copy of all replicate records")
 
 
-def c5_fused(R):
+def c5_fused(R, panel="coded"):
     """C5 with the noise drawn inside the streaming kernel (dcor_hrs_fused_launch): the same
-    Philox streams as C5-e2e, no HBM noise arrays; R NI + INT replicates, results to host."""
+    Philox streams as C5-e2e, no HBM noise arrays; R NI + INT replicates, results to host.
+    panel 'continuous': every value distinct (as c5's), the uncoded kernel k_hrs_fused_l2."""
     import numpy as np
     import torch
     from dcor import hrs
-    age_raw, bmi_raw = hrs.standin_panel(19433, -0.3)
-    z = hrs.standardize_panel(age_raw, bmi_raw, lap=np.zeros(4))
-    args = (z["age_z"], z["bmi_z"], z["lambda_age_z"], z["lambda_bmi_z"], 2.0)
+    if panel == "coded":
+        age_raw, bmi_raw = hrs.standin_panel(19433, -0.3)
+        z = hrs.standardize_panel(age_raw, bmi_raw, lap=np.zeros(4))
+        args = (z["age_z"], z["bmi_z"], z["lambda_age_z"], z["lambda_bmi_z"], 2.0)
+    else:
+        g = np.random.default_rng(2)
+        age = np.clip(g.normal(0.0, 1.0, 19433), -2.22, 2.22)
+        bmi = -0.19 * age + math.sqrt(1 - 0.19 ** 2) * g.normal(0.0, 1.0, 19433)
+        args = (age, bmi, 2.22, 2.60, 2.0)
     hrs.hrs_replicates(*args, 8192, mode="fused")  # warm-up
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     res = hrs.hrs_replicates(*args, R, chunk=65536, mode="fused")
     torch.cuda.synchronize()
     t = time.perf_counter() - t0
-    line("C5-fused", reps=R, seconds=t, reps_per_s=R / t, finite=bool(np.isfinite(res).all()),
-         note="HRS replicates with in-kernel Philox noise (k_hrs_fused + epilogue), the D2H copy "
-              "of all replicate records included")
+    line("C5-fused" if panel == "coded" else "C5-fused-continuous", reps=R, seconds=t, reps_per_s=R / t,
+         finite=bool(np.isfinite(res).all()), panel=panel,
+         kernel="k_hrs_fused (LDS codes)" if panel == "coded" else "k_hrs_fused_l2 (clipped panel in L2)",
+         note="HRS replicates with in-kernel Philox noise (+ epilogue), the D2H copy of all replicate "
+              "records included")
 
 
 def subg():
@@ -367,7 +376,7 @@ def rstream_hrs():
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--only", default="C1,C2,C3,C4,VG,SG,C5,C5c,C5e,C5f,S,R1,RG,RH")
+    ap.add_argument("--only", default="C1,C2,C3,C4,VG,SG,C5,C5c,C5e,C5f,C5fc,S,R1,RG,RH")
     ap.add_argument("--c3-reps", type=int, default=2000)
     ap.add_argument("--c4-B", type=int, default=1000)
     ap.add_argument("--c5-R", type=int, default=8192)
@@ -390,6 +399,7 @@ def main():
     if "C5c" in which: c5(a.c5_R, panel="continuous")
     if "C5e" in which: c5_e2e(a.c5e_R)
     if "C5f" in which: c5_fused(a.c5e_R)
+    if "C5fc" in which: c5_fused(a.c5e_R, panel="continuous")
     if "S" in which: subg()
     if "R1" in which: rstream_c1()
     if "RG" in which: rstream_grid()

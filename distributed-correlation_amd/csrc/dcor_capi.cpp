@@ -747,6 +747,64 @@ struct dcor_panel {
 static int premat_subg_run(const dcor_premat_subg* d, const dcor_panel* panel, dcor_rep_out* d_out,
                            void* stream);
 
+// dcor_hrs_fused_launch on an uncoded panel too large for the LDS index row (n > 65536): the
+// same Philox streams materialised per chunk (dcor_perm_launch / dcor_draws_launch sites), then
+// the pre-materialised panel kernels -- replicate r equals the fused kernel's replicate r within
+// the compensated sums' rounding, as for any panel.
+static int hrs_fused_materialised(const dcor_premat_subg* d, const dcor_panel* panel,
+                                  uint64_t seed_ni, uint64_t seed_int, int64_t rep_begin,
+                                  dcor_rep_out* d_out, void* stream) {
+  int64_t km[2];
+  if (int st = dcor_batch_geometry(d->n, d->eps1, d->eps2, DCOR_FAMILY_SUBG, 1, km)) return st;
+  const int64_t k = km[0], m = km[1], n = d->n, ns = d->nsim;
+  auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+  const size_t per = al((size_t)k * m * 4) + 2 * al((size_t)k * 8) + al((size_t)n * 8) + 256 +
+                     2 * al((size_t)ns * 8);
+  int64_t cr = (int64_t)(((size_t)1 << 30) / per);
+  if (cr < 1) cr = 1;
+  if (cr > 65535) cr = 65535;
+  if (cr > d->reps) cr = d->reps;
+  if (cr == 0) return DCOR_OK;
+  char* buf = nullptr;
+  const hipStream_t st = (hipStream_t)stream;
+  if (hipMallocAsync((void**)&buf, per * (size_t)cr, st) != hipSuccess) {
+    (void)hipGetLastError();
+    return fail(DCOR_ENOMEM, "hrs_fused: cannot allocate %zu noise bytes", per * (size_t)cr);
+  }
+  int32_t* perm = (int32_t*)buf;
+  double* lx = (double*)(buf + al((size_t)cr * k * m * 4));
+  double* ly = lx + (al((size_t)cr * k * 8) / 8);
+  double* ll = ly + (al((size_t)cr * k * 8) / 8);
+  double* lc = ll + (al((size_t)cr * n * 8) / 8);
+  double* mz = lc + (al((size_t)cr * 8) / 8);
+  double* ml = mz + (al((size_t)cr * ns * 8) / 8);
+  const uint32_t n0 = (uint32_t)seed_ni, n1 = (uint32_t)(seed_ni >> 32);
+  const uint32_t i0 = (uint32_t)seed_int, i1 = (uint32_t)(seed_int >> 32);
+  int rc = 0;
+  for (int64_t r0 = 0; r0 < d->reps && !rc; r0 += cr) {
+    const int64_t nr = d->reps - r0 < cr ? d->reps - r0 : cr, rb = rep_begin + r0;
+    rc = launch_perm(n0, n1, DCOR_SITE_PERM, rb, nr, n, k * m, perm, stream);
+    if (!rc) rc = launch_draws(0, n0, n1, 11, rb, nr, k, lx, stream);
+    if (!rc) rc = launch_draws(0, n0, n1, 12, rb, nr, k, ly, stream);
+    if (!rc) rc = launch_draws(0, i0, i1, 13, rb, nr, n, ll, stream);
+    if (!rc) rc = launch_draws(0, i0, i1, 14, rb, nr, 1, lc, stream);
+    if (!rc) rc = launch_draws(1, i0, i1, 15, rb, nr, ns, mz, stream);
+    if (!rc) rc = launch_draws(0, i0, i1, 16, rb, nr, ns, ml, stream);
+    if (rc) break;
+    dcor_premat_subg q = *d;
+    q.reps = nr;
+    q.perm = perm; q.lap_ni_x = lx; q.lap_ni_y = ly; q.lap_local = ll; q.lap_central = lc;
+    q.mix_z = mz; q.mix_l = ml;
+    if (int e = premat_subg_run(&q, panel, d_out + r0, stream)) {
+      (void)hipFreeAsync(buf, st);
+      return e;
+    }
+  }
+  (void)hipFreeAsync(buf, st);
+  if (rc) return hip_fail((hipError_t)rc, "hrs_fused noise launch");
+  return DCOR_OK;
+}
+
 extern "C" {
 
 int dcor_panel_create(const double* d_X, const double* d_Y, int64_t n, void* stream,
@@ -812,24 +870,40 @@ int dcor_hrs_fused_launch(const dcor_premat_subg* d, const dcor_panel* panel, ui
   if (d->X != panel->X || d->Y != panel->Y || d->xy_stride != 0 || d->n != panel->n)
     return fail(DCOR_EINVAL, "hrs_fused: X, Y, n must be the panel's and xy_stride 0");
   if (!d->hrs) return fail(DCOR_EINVAL, "hrs_fused: the HRS variant only (hrs = 1)");
-  if (!panel->coded)
-    return fail(DCOR_EINVAL, "hrs_fused: needs a dictionary-coded panel (<= 256 distinct values "
-                             "per column, no NaN)");
   if (rep_begin < 0 || rep_begin + d->reps > 0xffffffffLL)
     return fail(DCOR_EINVAL, "hrs_fused: replicate range exceeds 2^32");
   if (int st = need_device()) return st;
   PrematSubgConst p;
   if (int st = premat_subg_const(d, p)) return st;
+  // DCOR_HRS_FUSED_L2=1 runs a coded panel through the uncoded kernel (A/B and the tests'
+  // bit-identity check of the two kernels)
+  static const bool force_l2 = [] {
+    const char* e = std::getenv("DCOR_HRS_FUSED_L2");
+    return e && std::strcmp(e, "1") == 0;
+  }();
+  const bool coded = panel->coded && !force_l2;
+  if (!coded && d->n > DCOR_DICT_NMAX)
+    return hrs_fused_materialised(d, panel, seed_ni, seed_int, rep_begin, d_out, stream);
   p.perm = nullptr; p.lap_ni_x = p.lap_ni_y = p.lap_local = p.lap_central = nullptr;
   p.mix_z = p.mix_l = nullptr;
-  p.dict_codes = panel->codes(); p.dict_vals = panel->dict(); p.dict_ok = panel->ok();
-  p.dict_built = 2;
+  if (coded) {
+    p.dict_codes = panel->codes(); p.dict_vals = panel->dict(); p.dict_ok = panel->ok();
+    p.dict_built = 2;
+  } else {
+    p.dict_codes = nullptr; p.dict_vals = nullptr; p.dict_ok = nullptr;
+  }
   if (d->reps == 0) return DCOR_OK;
-  const size_t bytes = ((size_t)d->reps * 80 + 255) & ~(size_t)255;
+  const size_t part_b = ((size_t)d->reps * 80 + 255) & ~(size_t)255;
+  const size_t pack_b = coded ? 0 : (size_t)d->n * 32;  // xyc | soc (uncoded kernel)
+  const size_t bytes = part_b + pack_b;
   void* part = nullptr;
   if (hipMallocAsync(&part, bytes, (hipStream_t)stream) != hipSuccess) {
     (void)hipGetLastError();
     return fail(DCOR_ENOMEM, "hrs_fused: cannot allocate %zu scratch bytes", bytes);
+  }
+  if (!coded) {
+    p.xyc = (const double2*)((char*)part + part_b);
+    p.soc = p.xyc + d->n;
   }
   const int rc = launch_hrs_fused(p, seed_ni, seed_int, rep_begin, d->reps, part, d_out, stream);
   (void)hipFreeAsync(part, (hipStream_t)stream);
@@ -852,8 +926,7 @@ static int premat_subg_run(const dcor_premat_subg* d, const dcor_panel* panel, d
   // launches on different streams.
   // HRS over one shared panel: the packed clipped panel (2 x n x 16 B) follows the partials.
   // a prepared panel's path is known on the host: launch only the kernel that does the work
-  const bool pack = p.hrs && p.perm && p.xy_stride == 0 && p.s.m == 2 &&
-                    !(panel != nullptr && panel->coded);
+  const bool pack = p.hrs && p.perm && p.xy_stride == 0 && !(panel != nullptr && panel->coded);
   // Shared panel + random batches: try the dictionary-coded LDS kernel first (the device
   // decides; the packed L2-gather kernel is the fallback).
   const bool dict = p.perm && p.xy_stride == 0 && p.s.n <= DCOR_DICT_NMAX &&

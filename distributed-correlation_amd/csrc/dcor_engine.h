@@ -44,7 +44,7 @@ struct SignConst {
   double inv_k, crit, sqrt_k;
   double pflip;                               // exp(eps_s)/(exp(eps_s)+1)
   uint64_t flipT;                             // ceil(pflip*2^32): flip <=> u32 < flipT
-  uint32_t flipT24;                           // ceil(pflip*2^24): Gaussian DGP spare-bit flips
+  uint32_t flipT24;                           // ceil(pflip*2^24): Bernoulli DGP spare-bit flips
   int32_t md_pow2;                            // m is a power of two: count / m == count * inv_md
   double inv_md;
   double scale_Z, coefZ, q2, ratio, inv_sqrt_n, eps_r, w_laplace;
@@ -176,7 +176,8 @@ int launch_premat_sign(const PrematSignConst& c, int64_t reps, dcor_rep_out* out
 // epi_stream / ev: if non-null the epilogue runs on epi_stream after an event recorded on
 // `stream` behind the streaming kernels (chunk pipelining).
 // HRS replicates [rep_begin, rep_begin + reps) with in-kernel Philox noise over a coded panel
-// (c.dict_codes / c.dict_vals set); part: reps * 80 B.
+// (c.dict_codes / c.dict_vals set), or over an uncoded one (c.xyc / c.soc: 2 x n double2 of
+// scratch the launch packs; n <= DCOR_DICT_NMAX); part: reps * 80 B.
 int launch_hrs_fused(const PrematSubgConst& c, uint64_t seed_ni, uint64_t seed_int,
                      int64_t rep_begin, int64_t reps, void* part, dcor_rep_out* out, void* stream);
 int launch_premat_subg(const PrematSubgConst& c, int64_t reps, void* part, dcor_rep_out* out,

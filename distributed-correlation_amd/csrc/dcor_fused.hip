@@ -18,34 +18,32 @@ namespace dcor {
 // Sample i of a replicate from the draw-site contract of include/dcor.h.
 template <int DGP> struct Dgp;
 
-template <> struct Dgp<DCOR_DGP_GAUSSIAN> {  // MASS::mvrnorm (vert-cor.R:389-394)
-  // The sample's 24 bits Box-Muller leaves unused (low 12 of w1 and of w3) carry the sign
-  // family's INT flip for this DGP (spare_flip): u24 < ceil(p 2^24) (vert-cor.R:175).
-  static constexpr bool spare_flip = true;
-  static __device__ __forceinline__ void one_u24(const DgpConst& g, uint32_t i, uint32_t rep,
-                                                 uint32_t k0, uint32_t k1, double& x, double& y,
-                                                 uint32_t& u24) {
-    const U4 w = draw(i, rep, DCOR_SITE_DGP_A, k0, k1);
+template <> struct Dgp<DCOR_DGP_GAUSSIAN> {  // MASS::mvrnorm (vert-cor.R:389-394), 2 samples/block
+  // Sample i: words (wa, wb) = (w0, w1) or (w2, w3) of DGP_A block i/2, Box-Muller from the
+  // 32-bit uniforms (wa + 1/2) 2^-32 (radius) and (wb + 1/2) 2^-32 (angle); the sign family's
+  // INT flips come from the FLIP site.  Half a Philox block per sample.
+  static constexpr bool spare_flip = false;
+  static __device__ __forceinline__ void from_words(const DgpConst& g, uint32_t wa, uint32_t wb,
+                                                    double& x, double& y) {
     double r, s, cs;
-    normal_polar(w, &r, &s, &cs);
+    normal_polar32(wa, wb, &r, &s, &cs);
     mvn_polar(r, s, cs, g.mu0, g.mu1, g.a00, g.a01, g.a10, g.a11, &x, &y);
-    u24 = ((w.w1 & 0xFFFu) << 12) | (w.w3 & 0xFFFu);
   }
   static __device__ __forceinline__ void one(const DgpConst& g, uint32_t i, uint32_t rep,
                                              uint32_t k0, uint32_t k1, double& x, double& y) {
-    uint32_t u24;
-    one_u24(g, i, rep, k0, k1, x, y, u24);
+    const U4 w = draw(i >> 1, rep, DCOR_SITE_DGP_A, k0, k1);
+    if (i & 1) from_words(g, w.w2, w.w3, x, y);
+    else from_words(g, w.w0, w.w1, x, y);
   }
-  static __device__ __forceinline__ void quad_u24(const DgpConst& g, uint32_t i0, uint32_t rep,
-                                                  uint32_t k0, uint32_t k1, double* x, double* y,
-                                                  uint32_t* u24) {
-#pragma unroll
-    for (int q = 0; q < 4; ++q) one_u24(g, i0 + q, rep, k0, k1, x[q], y[q], u24[q]);
-  }
+  // i0 even
   static __device__ __forceinline__ void quad(const DgpConst& g, uint32_t i0, uint32_t rep,
                                               uint32_t k0, uint32_t k1, double* x, double* y) {
-#pragma unroll
-    for (int q = 0; q < 4; ++q) one(g, i0 + q, rep, k0, k1, x[q], y[q]);
+    const U4 a = draw(i0 >> 1, rep, DCOR_SITE_DGP_A, k0, k1);
+    const U4 b = draw((i0 >> 1) + 1, rep, DCOR_SITE_DGP_A, k0, k1);
+    from_words(g, a.w0, a.w1, x[0], y[0]);
+    from_words(g, a.w2, a.w3, x[1], y[1]);
+    from_words(g, b.w0, b.w1, x[2], y[2]);
+    from_words(g, b.w2, b.w3, x[3], y[3]);
   }
   static __device__ __forceinline__ double lap(uint32_t i, uint32_t rep, uint32_t k0, uint32_t k1) {
     const U4 v = draw(i, rep, DCOR_SITE_DGP_B, k0, k1);

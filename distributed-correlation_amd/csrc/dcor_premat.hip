@@ -132,9 +132,9 @@ struct SubgPartial { double s[10]; };  // sP, sT, sT2, sU, sU2 as (hi, lo)
 
 #define SUBG_UNR 4
 
-// Pack the shared HRS panel once per launch (same clips as the per-rep path, so the
-// results are identical): halves the NI gather transactions (one 16-B line access per
-// sample instead of two 8-B ones) and removes the per-rep clip work.
+// Pack the shared HRS panel once per launch (the clips of the per-sample paths, so the values
+// are identical) for the uncoded persistent kernels (k_premat_subg_dict<.., true>,
+// k_hrs_fused_l2): one 16-B gather per NI sample instead of two 8-B ones, no per-rep clips.
 __global__ __launch_bounds__(DCOR_BLOCK) void k_premat_xy_pack(PrematSubgConst p,
                                                                double2* __restrict__ xyc,
                                                                double2* __restrict__ soc) {
@@ -178,58 +178,7 @@ __global__ __launch_bounds__(DCOR_BLOCK) void k_premat_subg_stream(PrematSubgCon
     ks_acc(sT, T);
     ks_acc(sT2, T * T);
   };
-  // m = 2: the batch mean of two values is fl(a + b) / 2 exactly (scaling by 1/2 is exact),
-  // which is what the double-double batch mean rounds to.
-  auto pair_term = [&](double xa, double xb, double ya, double yb, double lxj, double lyj) {
-    const double xt = (xa + xb) * 0.5 + c.bx * lxj;
-    const double yt = (ya + yb) * 0.5 + c.by * lyj;
-    ks_acc(sP, xt * yt);
-    const double T = c.md * xt * yt;
-    ks_acc(sT, T);
-    ks_acc(sT2, T * T);
-  };
-  if (p.xyc != nullptr && c.m == 2) {
-    // HRS, shared packed panel (real-data-sims.R:131, 222-232).
-    const double2* __restrict__ so = p.soc;
-    const double2* __restrict__ xy = p.xyc;
-    const int64_t step = (int64_t)DCOR_BLOCK * SUBG_UNR;
-    auto uterm = [&](double2 v, double l) {
-      const double Uc = rclip((v.x + c.bs * l) * v.y, c.lr);
-      ks_acc(sU, Uc);
-      ks_acc(sU2, Uc * Uc);
-    };
-    int64_t i = tid;
-    for (; i + (SUBG_UNR - 1) * DCOR_BLOCK < c.n; i += step) {
-      double l[SUBG_UNR];
-      double2 v[SUBG_UNR];
-#pragma unroll
-      for (int u = 0; u < SUBG_UNR; ++u) { l[u] = ll[i + u * DCOR_BLOCK]; v[u] = so[i + u * DCOR_BLOCK]; }
-#pragma unroll
-      for (int u = 0; u < SUBG_UNR; ++u) uterm(v[u], l[u]);
-    }
-    for (; i < c.n; i += DCOR_BLOCK) uterm(so[i], ll[i]);
-    const int32_t* __restrict__ pm = p.perm + rep * (c.k * c.m);
-    int64_t j = tid;
-    for (; j + (SUBG_UNR - 1) * DCOR_BLOCK < c.k; j += step) {
-      int2 pr[SUBG_UNR];
-      double ax[SUBG_UNR], ay[SUBG_UNR];
-#pragma unroll
-      for (int u = 0; u < SUBG_UNR; ++u) {
-        const int64_t jj = j + u * DCOR_BLOCK;
-        pr[u] = *reinterpret_cast<const int2*>(pm + 2 * jj);
-        ax[u] = lx[jj]; ay[u] = ly[jj];
-      }
-#pragma unroll
-      for (int u = 0; u < SUBG_UNR; ++u) {
-        const double2 a = xy[pr[u].x], b = xy[pr[u].y];
-        pair_term(a.x, b.x, a.y, b.y, ax[u], ay[u]);
-      }
-    }
-    for (; j < c.k; j += DCOR_BLOCK) {
-      const double2 a = xy[pm[2 * j]], b = xy[pm[2 * j + 1]];
-      pair_term(a.x, b.x, a.y, b.y, lx[j], ly[j]);
-    }
-  } else if (p.perm == nullptr) {
+  if (p.perm == nullptr) {
     // contiguous batches: each element read once by its batch owner (NI + INT)
     for (int64_t j = tid; j < c.k; j += DCOR_BLOCK) {
       DD bx{0, 0}, by{0, 0};
@@ -535,7 +484,10 @@ typedef int iv4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ int64_t share(int64_t total, int t, int S) { return total * t / S; }
 
-template <int DUNR, int WPE>  // 16-B loads in flight per thread; waves per SIMD
+// L2 = true: the same kernel for a panel that has no dictionary -- the clipped panel packed in
+// HBM (xyc, soc; 32 B per sample, L2-resident at survey sizes), each INT sample pair read as two
+// coalesced double2, each NI sample gathered from L2.  Only the reduction scratch is in LDS.
+template <int DUNR, int WPE, bool L2>  // 16-B loads in flight per thread; waves per SIMD
 __global__ __launch_bounds__(DICT_NT, WPE) void k_premat_subg_dict(PrematSubgConst p,
                                                              const uint16_t* __restrict__ codes_g,
                                                              const double* __restrict__ dict_g,
@@ -543,7 +495,8 @@ __global__ __launch_bounds__(DICT_NT, WPE) void k_premat_subg_dict(PrematSubgCon
                                                              int64_t reps,
                                                              SubgPartial* __restrict__ part) {
   extern __shared__ double dsm[];
-  if (*dict_ok == 0) return;  // the L2-gather kernel owns this launch
+  // the coded kernel owns a launch whose device probe found a dictionary, else the L2 kernel
+  if (L2 ? (dict_ok != nullptr && *dict_ok != 0) : (*dict_ok == 0)) return;
   const SubgConst& c = p.s;
   const int tid = threadIdx.x;
   const int S = p.slices > 1 ? p.slices : 1;
@@ -551,23 +504,34 @@ __global__ __launch_bounds__(DICT_NT, WPE) void k_premat_subg_dict(PrematSubgCon
   double* dY = dsm + DICT_MAX;
   double* dS = dsm + 2 * DICT_MAX;
   double* dO = dsm + 3 * DICT_MAX;
-  double* red = dsm + 4 * DICT_MAX;
+  double* red = L2 ? dsm : dsm + 4 * DICT_MAX;
   uint16_t* cod = reinterpret_cast<uint16_t*>(dsm + 4 * DICT_MAX + 20 * DICT_NW);
-  if (tid < DICT_MAX) {
-    const double x = dict_g[tid], y = dict_g[DICT_MAX + tid];
-    dX[tid] = rclip(x, c.l1);                                   // real-data-sims.R:126-127
-    dY[tid] = rclip(y, c.l2);
-    const double sv = c.sender_is_X ? x : y, ov = c.sender_is_X ? y : x;
-    dS[tid] = rclip(sv, c.ls);                                  // real-data-sims.R:222-227
-    dO[tid] = p.hrs ? rclip(ov, p.lo_) : ov;
-  }
-  {
+  const double2* __restrict__ xyp = p.xyc;
+  const double2* __restrict__ sop = p.soc;
+  if constexpr (!L2) {
+    if (tid < DICT_MAX) {
+      const double x = dict_g[tid], y = dict_g[DICT_MAX + tid];
+      dX[tid] = rclip(x, c.l1);                                   // real-data-sims.R:126-127
+      dY[tid] = rclip(y, c.l2);
+      const double sv = c.sender_is_X ? x : y, ov = c.sender_is_X ? y : x;
+      dS[tid] = rclip(sv, c.ls);                                  // real-data-sims.R:222-227
+      dO[tid] = p.hrs ? rclip(ov, p.lo_) : ov;
+    }
     const int64_t nv = (c.n * 2 + 15) / 16;                      // 16-B words of codes
     const uint4* src = reinterpret_cast<const uint4*>(codes_g);
     uint4* dst = reinterpret_cast<uint4*>(cod);
     for (int64_t w = tid; w < nv; w += DICT_NT) dst[w] = src[w];
+    __syncthreads();
   }
-  __syncthreads();
+  // the clipped values of sample i: NI (x, y) and INT (sender, other)
+  auto ni_xy = [&](int64_t i) -> double2 {
+    if constexpr (L2) {
+      return xyp[i];
+    } else {
+      const uint32_t a = cod[i];
+      return make_double2(dX[a & 255u], dY[a >> 8]);
+    }
+  };
   const int64_t items = reps * S;
   for (int64_t it = blockIdx.x; it < items; it += gridDim.x) {
     const int64_t rep = it / S;
@@ -577,8 +541,16 @@ __global__ __launch_bounds__(DICT_NT, WPE) void k_premat_subg_dict(PrematSubgCon
     const double* __restrict__ ll = p.lap_local + rep * c.n;
     const int32_t* __restrict__ pm = p.perm + rep * (c.k * c.m);
     DD sP{0, 0}, sT{0, 0}, sT2{0, 0}, sU{0, 0}, sU2{0, 0};
-    auto uterm = [&](uint32_t cd, double l) {  // ver-cor-subG.R:88-90; real-data-sims.R:222-232
-      const double Uc = rclip((dS[cd & 255u] + c.bs * l) * dO[cd >> 8], c.lr);
+    auto uterm = [&](int64_t i, double l) {  // ver-cor-subG.R:88-90; real-data-sims.R:222-232
+      double sv, ov;
+      if constexpr (L2) {
+        const double2 v = sop[i];
+        sv = v.x; ov = v.y;
+      } else {
+        const uint32_t cd = cod[i];
+        sv = dS[cd & 255u]; ov = dO[cd >> 8];
+      }
+      const double Uc = rclip((sv + c.bs * l) * ov, c.lr);
       ks_acc(sU, Uc);
       ks_acc(sU2, Uc * Uc);
     };
@@ -597,18 +569,18 @@ __global__ __launch_bounds__(DICT_NT, WPE) void k_premat_subg_dict(PrematSubgCon
 #pragma unroll
         for (int u = 0; u < DUNR; ++u) {
           const int64_t i = h + 2 * (q + u * DICT_NT);
-          uterm(cod[i], v[u].x);
-          uterm(cod[i + 1], v[u].y);
+          uterm(i, v[u].x);
+          uterm(i + 1, v[u].y);
         }
       }
       for (; q < q1; q += DICT_NT) {
         const dv2 v = __builtin_nontemporal_load(l2 + q);
         const int64_t i = h + 2 * q;
-        uterm(cod[i], v.x);
-        uterm(cod[i + 1], v.y);
+        uterm(i, v.x);
+        uterm(i + 1, v.y);
       }
-      if (tid == 0 && t == 0 && h) uterm(cod[0], ll[0]);
-      if (tid == DICT_NT - 1 && t == S - 1 && h + 2 * np < c.n) uterm(cod[c.n - 1], ll[c.n - 1]);
+      if (tid == 0 && t == 0 && h) uterm(0, ll[0]);
+      if (tid == DICT_NT - 1 && t == S - 1 && h + 2 * np < c.n) uterm(c.n - 1, ll[c.n - 1]);
     }
     // workgroup sums: wave sums into a scratch half alternating per item (a wave can run at
     // most one barrier ahead), then lane v < 5 folds sum v over the waves in wave order.  The
@@ -625,9 +597,9 @@ __global__ __launch_bounds__(DICT_NT, WPE) void k_premat_subg_dict(PrematSubgCon
     wave_put(4, sU2);
     if (c.m == 2) {  // real-data-sims.R:131-137 with the exact two-value batch mean
       auto pair = [&](int a0, int b0, double lxj, double lyj) {
-        const uint32_t a = cod[a0], b = cod[b0];
-        const double xt = (dX[a & 255u] + dX[b & 255u]) * 0.5 + c.bx * lxj;
-        const double yt = (dY[a >> 8] + dY[b >> 8]) * 0.5 + c.by * lyj;
+        const double2 a = ni_xy(a0), b = ni_xy(b0);
+        const double xt = (a.x + b.x) * 0.5 + c.bx * lxj;
+        const double yt = (a.y + b.y) * 0.5 + c.by * lyj;
         ks_acc(sP, xt * yt);
         const double T = c.md * xt * yt;
         ks_acc(sT, T);
@@ -673,9 +645,9 @@ __global__ __launch_bounds__(DICT_NT, WPE) void k_premat_subg_dict(PrematSubgCon
       for (int64_t j = share(c.k, t, S) + tid; j < share(c.k, t + 1, S); j += DICT_NT) {
         DD bx{0, 0}, by{0, 0};
         for (int r = 0; r < c.m; ++r) {
-          const uint32_t a = cod[pm[j * c.m + r]];
-          dd_acc(bx, dX[a & 255u]);
-          dd_acc(by, dY[a >> 8]);
+          const double2 a = ni_xy(pm[j * c.m + r]);
+          dd_acc(bx, a.x);
+          dd_acc(by, a.y);
         }
         const DD xb = dd_div_d(bx, c.md), yb = dd_div_d(by, c.md);
         const double xt = (xb.hi + xb.lo) + c.bx * lx[j];
@@ -1219,6 +1191,124 @@ __global__ __launch_bounds__(DICT_NT, WPE) void k_hrs_fused(PrematSubgConst p, H
   }
 }
 
+// k_hrs_fused for a panel that is not dictionary-codable (continuous values): the same
+// replicate, work split and summation order, with the clipped panel packed once per launch in
+// HBM (xyc = NI clips, soc = INT sender / other clips, k_premat_xy_pack; 32 B per sample, L2-
+// resident at survey sizes) instead of LDS codes.  LDS holds this replicate's permuted batch
+// indices (u16, n <= 65536), written by phase A's Feistel walks; phase B gathers the two
+// samples of each batch from L2.  The clipped values are the coded kernel's dictionary entries,
+// so on a codable panel both kernels return the same bits.
+template <int WPE>
+__global__ __launch_bounds__(DICT_NT, WPE) void k_hrs_fused_l2(PrematSubgConst p, HrsKeys hk,
+                                                              int64_t reps,
+                                                              SubgPartial* __restrict__ part) {
+  extern __shared__ double dsm[];
+  const SubgConst& c = p.s;
+  const int tid = threadIdx.x;
+  double* red = dsm;
+  uint16_t* gs = reinterpret_cast<uint16_t*>(dsm + 20 * DICT_NW);
+  const double2* __restrict__ xy = p.xyc;
+  const double2* __restrict__ so = p.soc;
+  const uint32_t n = (uint32_t)c.n;
+  for (int64_t it = blockIdx.x; it < reps; it += gridDim.x) {
+    const uint32_t rep = hk.rep_begin + (uint32_t)it;
+    DD sP{0, 0}, sT{0, 0}, sT2{0, 0}, sU{0, 0}, sU2{0, 0};
+    auto uterm = [&](double2 v, double l) {  // real-data-sims.R:222-232
+      const double Uc = rclip((v.x + c.bs * l) * v.y, c.lr);
+      ks_acc(sU, Uc);
+      ks_acc(sU2, Uc * Uc);
+    };
+    // Phase A: gs[t] = P(t), t < k m (sample.int(n, k*m) - 1, real-data-sims.R:131); the
+    // previous item's readers are past the barrier that ends its reduction.
+    const U4 kk = draw(0u, rep, DCOR_SITE_PERM, hk.ni0, hk.ni1);
+    {
+      const uint32_t km = (uint32_t)(c.k * c.m);
+      uint32_t t = (uint32_t)tid, x = t;
+      while (t < km) {
+        x = feistel_pass(x, hk.pa, hk.pc, kk);
+        if (x < n) {
+          gs[t] = (uint16_t)x;
+          t += DICT_NT;
+          x = t;
+        }
+      }
+    }
+    {  // INT local noise: block b -> samples 2b, 2b+1
+      const int64_t nb = c.n >> 1;
+      for (int64_t b = tid; b < nb; b += DICT_NT) {
+        const U4 w = draw((uint32_t)b, rep, HRS_SITE_LOCAL, hk.in0, hk.in1);
+        const double2 v0 = so[2 * b], v1 = so[2 * b + 1];
+        uterm(v0, unit_laplace(u53(w.w0, w.w1)));
+        uterm(v1, unit_laplace(u53(w.w2, w.w3)));
+      }
+      if ((c.n & 1) && tid == DICT_NT - 1) {
+        const U4 w = draw((uint32_t)nb, rep, HRS_SITE_LOCAL, hk.in0, hk.in1);
+        uterm(so[c.n - 1], unit_laplace(u53(w.w0, w.w1)));
+      }
+    }
+    double* rb = red + (((it - blockIdx.x) / gridDim.x) & 1) * (10 * DICT_NW);
+    auto wave_put = [&](int v, DD a) {
+      a = wave_sum_dd(a);
+      if ((tid & 63) == 0) {
+        rb[(2 * v) * DICT_NW + (tid >> 6)] = a.hi;
+        rb[(2 * v + 1) * DICT_NW + (tid >> 6)] = a.lo;
+      }
+    };
+    wave_put(3, sU);
+    wave_put(4, sU2);
+    __syncthreads();  // phase A's index row is complete
+    auto nterm = [&](double xt, double yt) {  // real-data-sims.R:133-137
+      ks_acc(sP, xt * yt);
+      const double T = c.md * xt * yt;
+      ks_acc(sT, T);
+      ks_acc(sT2, T * T);
+    };
+    if (c.m == 2) {
+      const uint32_t* __restrict__ g2 = reinterpret_cast<const uint32_t*>(gs);
+      auto pair = [&](uint32_t ab, double lxj, double lyj) {
+        const double2 a = xy[ab & 0xFFFFu], b = xy[ab >> 16];
+        nterm((a.x + b.x) * 0.5 + c.bx * lxj, (a.y + b.y) * 0.5 + c.by * lyj);
+      };
+      for (int64_t q = tid; 2 * q < c.k; q += DICT_NT) {
+        const uint32_t ab0 = g2[2 * q];
+        const uint32_t ab1 = 2 * q + 1 < c.k ? g2[2 * q + 1] : 0u;
+        const U4 wx = draw((uint32_t)q, rep, HRS_SITE_NI_X, hk.ni0, hk.ni1);
+        const U4 wy = draw((uint32_t)q, rep, HRS_SITE_NI_Y, hk.ni0, hk.ni1);
+        pair(ab0, unit_laplace(u53(wx.w0, wx.w1)), unit_laplace(u53(wy.w0, wy.w1)));
+        if (2 * q + 1 < c.k)
+          pair(ab1, unit_laplace(u53(wx.w2, wx.w3)), unit_laplace(u53(wy.w2, wy.w3)));
+      }
+    } else {
+      for (int64_t j = tid; j < c.k; j += DICT_NT) {
+        const U4 wx = draw((uint32_t)(j >> 1), rep, HRS_SITE_NI_X, hk.ni0, hk.ni1);
+        const U4 wy = draw((uint32_t)(j >> 1), rep, HRS_SITE_NI_Y, hk.ni0, hk.ni1);
+        const double lxj = unit_laplace((j & 1) ? u53(wx.w2, wx.w3) : u53(wx.w0, wx.w1));
+        const double lyj = unit_laplace((j & 1) ? u53(wy.w2, wy.w3) : u53(wy.w0, wy.w1));
+        DD bx{0, 0}, by{0, 0};
+        for (int r = 0; r < c.m; ++r) {
+          const double2 v = xy[gs[j * c.m + r]];
+          dd_acc(bx, v.x);
+          dd_acc(by, v.y);
+        }
+        const DD xb = dd_div_d(bx, c.md), yb = dd_div_d(by, c.md);
+        nterm((xb.hi + xb.lo) + c.bx * lxj, (yb.hi + yb.lo) + c.by * lyj);
+      }
+    }
+    wave_put(0, sP);
+    wave_put(1, sT);
+    wave_put(2, sT2);
+    __syncthreads();
+    if (tid < 5) {
+      DD a{rb[(2 * tid) * DICT_NW], rb[(2 * tid + 1) * DICT_NW]};
+#pragma unroll
+      for (int w = 1; w < DICT_NW; ++w)
+        a = dd_add(a, DD{rb[(2 * tid) * DICT_NW + w], rb[(2 * tid + 1) * DICT_NW + w]});
+      part[it].s[2 * tid] = a.hi;
+      part[it].s[2 * tid + 1] = a.lo;
+    }
+  }
+}
+
 // Epilogue of k_hrs_fused: central Laplace and mixquant draws generated here.  Thread t holds
 // the pairs of Philox blocks t + 256 s (order is irrelevant to an order statistic).
 __global__ __launch_bounds__(DCOR_BLOCK) void k_hrs_fused_epilogue(PrematSubgConst p, HrsKeys hk,
@@ -1278,25 +1368,42 @@ int launch_hrs_fused(const PrematSubgConst& c, uint64_t seed_ni, uint64_t seed_i
   int bits = 1;
   while ((1ll << bits) < c.s.n) ++bits;
   hk.pa = bits / 2; hk.pc = bits - hk.pa;
-  const size_t lds = premat_dict_lds_bytes(c.s.n);
   static const int wsel = [] {
     const char* e = std::getenv("DCOR_HRS_WPE");
     return (e && std::atoi(e) == 4) ? 4 : 6;
   }();
-  const auto kern = wsel == 4 ? k_hrs_fused<4> : k_hrs_fused<6>;
+  const bool l2 = c.xyc != nullptr;  // uncoded panel: packed clips in HBM, indices in LDS
+  const size_t lds = l2 ? (size_t)(20 * DICT_NW) * sizeof(double) +
+                              (size_t)((c.s.k * c.s.m * 2 + 15) / 16) * 16
+                        : premat_dict_lds_bytes(c.s.n);
+  if (l2)
+    hipLaunchKernelGGL(k_premat_xy_pack, dim3((unsigned)((c.s.n + DCOR_BLOCK - 1) / DCOR_BLOCK)),
+                       dim3(DCOR_BLOCK), 0, (hipStream_t)stream, c, (double2*)c.xyc,
+                       (double2*)c.soc);
+  typedef void (*FusedK)(PrematSubgConst, HrsKeys, const uint16_t*, const double*, int64_t,
+                         SubgPartial*, uint16_t*, int64_t);
+  typedef void (*FusedL2K)(PrematSubgConst, HrsKeys, int64_t, SubgPartial*);
+  const FusedK kern = wsel == 4 ? k_hrs_fused<4> : k_hrs_fused<6>;
+  const FusedL2K kern_l2 = wsel == 4 ? k_hrs_fused_l2<4> : k_hrs_fused_l2<6>;
+  const void* kf = l2 ? (const void*)kern_l2 : (const void*)kern;
   // per call: the attribute is per device, and one process may drive several GPUs
-  if (hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
-                          150 * 1024) != hipSuccess)
+  if (hipFuncSetAttribute(kf, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024) != hipSuccess)
     return (int)hipGetLastError();
   int dev = 0, cus = 0, per_cu = 0;
   if (hipGetDevice(&dev) != hipSuccess) return (int)hipGetLastError();
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
     return (int)hipGetLastError();
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, DICT_NT, lds) !=
-      hipSuccess)
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kf, DICT_NT, lds) != hipSuccess)
     return (int)hipGetLastError();
   const int64_t slots = (int64_t)cus * (per_cu < 1 ? 1 : per_cu);
   const int64_t grid = reps < slots ? reps : slots;
+  if (l2) {
+    hipLaunchKernelGGL(kern_l2, dim3((unsigned)grid), dim3(DICT_NT), lds, (hipStream_t)stream, c,
+                       hk, reps, (SubgPartial*)part);
+    hipLaunchKernelGGL(k_hrs_fused_epilogue, dim3((unsigned)reps), dim3(DCOR_BLOCK), 0,
+                       (hipStream_t)stream, c, hk, (const SubgPartial*)part, out);
+    return (int)hipGetLastError();
+  }
   const int64_t stride = (c.s.k * c.s.m + 63) & ~(int64_t)63;  // u16 codes per scratch row
   void* scr = nullptr;
   if (hipMallocAsync(&scr, (size_t)(grid * stride * 2), (hipStream_t)stream) != hipSuccess)
@@ -1336,10 +1443,23 @@ typedef void (*DictKernel)(PrematSubgConst, const uint16_t*, const double*, cons
 // reads at ~5.8 TB/s in every variant (r01 A/B: 590-605 us per 8192 replicates); the default
 // keeps two 512-thread workgroups per CU.  DCOR_DICT_VARIANT=1..3 selects the others for A/B.
 static DictKernel dict_kernel() {
-  static const DictKernel ks[4] = {k_premat_subg_dict<4, 4>, k_premat_subg_dict<4, 6>,
-                                   k_premat_subg_dict<8, 4>, k_premat_subg_dict<6, 6>};
+  static const DictKernel ks[4] = {k_premat_subg_dict<4, 4, false>, k_premat_subg_dict<4, 6, false>,
+                                   k_premat_subg_dict<8, 4, false>, k_premat_subg_dict<6, 6, false>};
   static const int v = [] {
     const char* e = std::getenv("DCOR_DICT_VARIANT");
+    const int x = e ? std::atoi(e) : 0;
+    return (x >= 0 && x < 4) ? x : 0;
+  }();
+  return ks[v];
+}
+
+// Uncoded shared-panel kernel variant (16-B loads in flight per thread, waves per SIMD);
+// DCOR_L2_VARIANT=1..3 selects the others for A/B.
+static DictKernel l2_kernel() {
+  static const DictKernel ks[4] = {k_premat_subg_dict<4, 8, true>, k_premat_subg_dict<4, 4, true>,
+                                   k_premat_subg_dict<8, 8, true>, k_premat_subg_dict<8, 4, true>};
+  static const int v = [] {
+    const char* e = std::getenv("DCOR_L2_VARIANT");
     const int x = e ? std::atoi(e) : 0;
     return (x >= 0 && x < 4) ? x : 0;
   }();
@@ -1386,13 +1506,31 @@ int launch_premat_subg(const PrematSubgConst& c0, int64_t reps, void* part, dcor
                        premat_dict_lds_bytes(c.s.n), (hipStream_t)stream, c, c.dict_codes,
                        c.dict_vals, c.dict_ok, reps, (SubgPartial*)part);
   }
-  if (c.xyc != nullptr)
+  if (c.xyc != nullptr) {
+    // shared panel, random batches, no dictionary (or the device probe may find none): the
+    // clipped panel packed once, then the persistent kernel gathering it from L2
     hipLaunchKernelGGL(k_premat_xy_pack, dim3((unsigned)((c.s.n + DCOR_BLOCK - 1) / DCOR_BLOCK)),
                        dim3(DCOR_BLOCK), 0, (hipStream_t)stream, c, (double2*)c.xyc,
                        (double2*)c.soc);
-  if (c.dict_built != 2)  // 2: a prepared panel known to be coded (dcor_panel)
+    if (c.dict_built != 2) {
+      const DictKernel kl = l2_kernel();
+      const size_t lds = (size_t)(20 * DICT_NW) * sizeof(double);
+      int dev = 0, cus = 0, per_cu = 0;
+      if (hipGetDevice(&dev) != hipSuccess) return last_err();
+      if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        return last_err();
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kl, DICT_NT, lds) != hipSuccess)
+        return last_err();
+      const int64_t slots = (int64_t)cus * (per_cu < 1 ? 1 : per_cu);
+      const int64_t grid = reps < slots ? reps : slots;
+      hipLaunchKernelGGL(kl, dim3((unsigned)grid), dim3(DICT_NT), lds, (hipStream_t)stream, c,
+                         (const uint16_t*)nullptr, (const double*)nullptr, (const int*)c.dict_ok,
+                         reps, (SubgPartial*)part);
+    }
+  } else if (c.dict_built != 2) {  // 2: a prepared panel known to be coded (dcor_panel)
     hipLaunchKernelGGL(k_premat_subg_stream, dim3((unsigned)reps), dim3(DCOR_BLOCK), 0,
                        (hipStream_t)stream, c, (const int*)c.dict_ok, (SubgPartial*)part);
+  }
   // workgroup-per-replicate epilogue: measured faster here than the wave-per-replicate form
   // (k_premat_subg_epilogue_w: 2000 loaded keys per wave cost 200+ VGPRs, one wave per SIMD)
   static const int wave_epi = [] {

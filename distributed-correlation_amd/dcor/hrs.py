@@ -94,8 +94,10 @@ def hrs_replicates(age_z, bmi_z, lam_age, lam_bmi, eps, reps, seed_ni=NI_SEED, s
 
     mode='fused' (rng='philox' only) draws the same Philox noise inside the streaming kernel
     (dcor_hrs_fused_launch) instead of materialising it in HBM: the results equal the
-    pre-materialised pipeline's to within its compensated sums' rounding.  Needs a
-    dictionary-coded panel (at most 256 distinct values per column)."""
+    pre-materialised pipeline's to within its compensated sums' rounding.  Any panel: a
+    dictionary-coded one (at most 256 distinct values per column) runs from LDS codes, a
+    continuous one gathers its clipped values from L2 (n <= 65536) or is materialised per
+    chunk (larger n)."""
     import ctypes as C
 
     import torch

@@ -270,7 +270,10 @@ int dcor_premat_subg_panel_launch(const dcor_premat_subg* d, const dcor_panel* p
  * (Laplace, seed_int, 13) local and (Laplace, seed_int, 14, count 1) central INT noise,
  * (normal, seed_int, 15) and (Laplace, seed_int, 16) for mixquant.  Results equal
  * dcor_premat_subg_panel_launch on those arrays to within the compensated sums' rounding.
- * d->hrs must be 1 and the panel dictionary-coded; d's noise pointers are ignored. */
+ * d->hrs must be 1; d's noise pointers are ignored.  Any panel: a dictionary-coded one runs
+ * from LDS codes; an uncoded one (continuous values) with n <= 65536 gathers its clipped
+ * samples from L2 (same results bit for bit as the coded kernel on a codable panel); larger
+ * uncoded panels materialise the same streams per chunk and run the pre-materialised kernels. */
 int dcor_hrs_fused_launch(const dcor_premat_subg* d, const dcor_panel* panel, uint64_t seed_ni,
                           uint64_t seed_int, int64_t rep_begin, dcor_rep_out* d_out, void* stream);
 
@@ -367,7 +370,7 @@ int dcor_perm_launch(uint64_t seed, int site, int64_t rep_begin, int64_t reps, i
 /* Draw-site contract of the fused engine (DESIGN.md "RNG"): Philox4x32-10 with
  * key = (seed lo32, seed hi32), counter = (index, rep, site, 0). */
 enum {
-  DCOR_SITE_DGP_A = 1,   /* Gaussian pair / Bernoulli pair-of-samples / U,E1      */
+  DCOR_SITE_DGP_A = 1,   /* 2 Gaussian samples (32-bit uniforms) / 2 Bernoulli samples / U,E1 */
   DCOR_SITE_DGP_B = 2,   /* bounded-factor E2 (w0,w1) ; sub-G local Laplace (w2,w3) */
   DCOR_SITE_FLIP = 3,    /* sign-family INT flips, 4 samples per block            */
   DCOR_SITE_NI_LAP = 4,  /* batch j: Laplace X (w0,w1), Y (w2,w3)                  */

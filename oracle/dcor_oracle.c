@@ -540,6 +540,15 @@ static void orc_normal_polar(const uint32_t w[4], double* r, double* s, double* 
   orc_sincospi(u2 * 128.0, s, c);
 }
 
+/* The Gaussian DGP's pair from two 32-bit words (dcor_device.h normal_polar32): u1 = (a + 1/2)
+ * 2^-32, u2 = (b + 1/2) 2^-32, both exact. */
+static void orc_normal_polar32(uint32_t a, uint32_t b, double* r, double* s, double* c) {
+  const double u1 = ((double)a + 0.5) * 0x1p-32;
+  const double u2 = ((double)b + 0.5) * 0x1p-32;
+  *r = sqrt(-2.0 * orc_log(u1));
+  orc_sincospi(u2 * 128.0, s, c);
+}
+
 void orc_normal_pair(const uint32_t w[4], double* z1, double* z2) {
   double r, s, c;
   orc_normal_polar(w, &r, &s, &c);
@@ -549,12 +558,16 @@ void orc_normal_pair(const uint32_t w[4], double* z1, double* z2) {
 
 /* mu + A (r c, r s) of MASS::mvrnorm (vert-cor.R:389-394) as the engine fuses it
  * (dcor_device.h mvn_polar). */
+static void orc_mvn_rsc(double r, double s, double c, const double mu[2], const double a[4],
+                        double* x, double* y) {
+  *x = fma(r, fma(a[1], s, a[0] * c), mu[0]);
+  *y = fma(r, fma(a[3], s, a[2] * c), mu[1]);
+}
 static void orc_mvn_polar(const uint32_t w[4], const double mu[2], const double a[4], double* x,
                           double* y) {
   double r, s, c;
   orc_normal_polar(w, &r, &s, &c);
-  *x = fma(r, fma(a[1], s, a[0] * c), mu[0]);
-  *y = fma(r, fma(a[3], s, a[2] * c), mu[1]);
+  orc_mvn_rsc(r, s, c, mu, a, x, y);
 }
 
 static void blk(uint64_t seed, uint32_t idx, uint32_t rep, uint32_t site, uint32_t w[4]) {
@@ -597,8 +610,12 @@ static void gen_xy(const dcor_cell* c, int64_t rep, double* X, double* Y, double
   for (int64_t i = 0; i < n; ++i) {
     uint32_t w[4];
     if (c->dgp == DCOR_DGP_GAUSSIAN) {
-      blk(c->seed, (uint32_t)i, (uint32_t)rep, DCOR_SITE_DGP_A, w);
-      orc_mvn_polar(w, c->mu, A, &X[i], &Y[i]);
+      /* two samples per block: words (w0, w1) for even i, (w2, w3) for odd i */
+      blk(c->seed, (uint32_t)(i >> 1), (uint32_t)rep, DCOR_SITE_DGP_A, w);
+      const int b = 2 * (int)(i & 1);
+      double r, s, cs;
+      orc_normal_polar32(w[b], w[b + 1], &r, &s, &cs);
+      orc_mvn_rsc(r, s, cs, c->mu, A, &X[i], &Y[i]);
     } else if (c->dgp == DCOR_DGP_MIX_GAUSSIAN) {
       /* gen_mix_gaussian (ver-cor-subG.R:113-133): label = rbinom(1, pi_mix) from the 24
        * bits the normal pair leaves unused, u24 < ceil(pi * 2^24); component mvrnorm;
@@ -685,12 +702,7 @@ int orc_sim_rep(const void* cellp, int64_t rep, double out[6]) {
       uint8_t* fl = (uint8_t*)malloc((size_t)n);
       for (int64_t i = 0; i < n; ++i) {
         uint32_t w[4];
-        if (c->dgp == DCOR_DGP_GAUSSIAN) {
-          /* the 24 bits of sample i's normal-pair block that Box-Muller leaves unused */
-          blk(c->seed, (uint32_t)i, (uint32_t)rep, DCOR_SITE_DGP_A, w);
-          const uint32_t u24 = ((w[1] & 0xFFFu) << 12) | (w[3] & 0xFFFu);
-          fl[i] = ((double)u24 * 0x1p-24 < p) ? 1 : 0;
-        } else if (c->dgp == DCOR_DGP_BERNOULLI) {
+        if (c->dgp == DCOR_DGP_BERNOULLI) {
           /* the top 24 bits of the sample's second word */
           blk(c->seed, (uint32_t)(i >> 1), (uint32_t)rep, DCOR_SITE_DGP_A, w);
           const uint32_t u24 = w[2 * (i & 1) + 1] >> 8;

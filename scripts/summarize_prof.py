@@ -4,7 +4,11 @@ Copies the kernel-trace stats CSV and writes <tag>_summary.json / .md with, per 
 average duration, PMC counters per dispatch (FETCH_SIZE doubled for gfx950's 1/2 under-
 report of wide streaming reads, MI355X_MICROARCH.md §HBM), effective clock, VALU
 activity and the fp64 instruction mix.
-VALU time: each instruction class of the mix weighted by its measured issue cost on gfx950
+VALU busy: rocprof's derived VALUBusy, SQ_ACTIVE_INST_VALU x 4 (quad-cycles -> cycles) over the
+SIMD-cycles of the dispatch (1024 SIMDs x GRBM_GUI_ACTIVE / 8 XCDs): the fraction of SIMD time
+the vector ALU was executing, <= 1 by construction -- the hardware-measured roofline fraction
+of a VALU-bound kernel (bench.py roofline.issue_frac).
+VALU time (cross-check): each instruction class of the mix weighted by its measured issue cost on gfx950
 (SIMD cycles per wave64 instruction, scripts/ubench_issue.hip -> profiles/<costs>.json), over
 the SIMD-cycles the dispatch had (1024 SIMDs x GRBM_GUI_ACTIVE / 8): the physically grounded
 roofline fraction of a VALU-bound kernel.
@@ -83,6 +87,8 @@ for kname, cs in counters.items():
         k["effective_clock_ghz"] = avg["GRBM_GUI_ACTIVE"] / 8 / k["avg_ns"]
         # VALU issue ceiling: one wave64 VALU instruction per 4 cycles per SIMD = 1 per cycle
         # per CU (256 CUs); meaningful for kernels profiled without overlap (PIPE=0 runs)
+        if "SQ_ACTIVE_INST_VALU" in avg:
+            k["valu_busy"] = avg["SQ_ACTIVE_INST_VALU"] * 4 / (1024 * avg["GRBM_GUI_ACTIVE"] / 8)
         if "SQ_INSTS_VALU" in avg:
             k["valu_issue_util"] = avg["SQ_INSTS_VALU"] / (256 * avg["GRBM_GUI_ACTIVE"] / 8)
             if COSTS and all(c in avg for c in CLASS_COST):
@@ -114,15 +120,15 @@ if os.path.exists(trace):
 
 json.dump(out, open(os.path.join(dst, f"{tag}_summary.json"), "w"), indent=1, sort_keys=True)
 lines = [f"# rocprofv3 summary `{tag}`", "",
-         "| kernel | calls | avg µs | % time | VGPR | HBM read B (corr.) | HBM write B | VALU active / wave-cycles | VALU instr / CU-cycle | VALU time / SIMD-cycles | clock GHz |",
-         "|---|---|---|---|---|---|---|---|---|---|---|"]
+         "| kernel | calls | avg µs | % time | VGPR | HBM read B (corr.) | HBM write B | VALU active / wave-cycles | VALU instr / CU-cycle | VALU time / SIMD-cycles | VALUBusy | clock GHz |",
+         "|---|---|---|---|---|---|---|---|---|---|---|---|"]
 for kname, k in sorted(out["kernels"].items(), key=lambda kv: -kv[1].get("pct_time", 0)):
     def f(x, fmt="{:.3g}"):
         return fmt.format(x) if isinstance(x, (int, float)) else "—"
     lines.append(f"| {kname} | {k.get('calls', '—')} | {f(k.get('avg_ns', 0) / 1e3)} | {f(k.get('pct_time'))} | "
                  f"{f(k.get('vgpr'))} | {f(k.get('hbm_read_bytes_corrected'))} | {f(k.get('hbm_write_bytes'))} | "
                  f"{f(k.get('valu_active_frac_of_wave_cycles'))} | {f(k.get('valu_issue_util'))} | "
-                 f"{f(k.get('valu_time_frac'))} | "
+                 f"{f(k.get('valu_time_frac'))} | {f(k.get('valu_busy'))} | "
                  f"{f(k.get('effective_clock_ghz'))} |")
 if "simulate_call_span_ms" in out:
     sp = out["simulate_call_span_ms"]

@@ -2,8 +2,10 @@
 // instruction classes the fused kernels issue on gfx950, with 8 waves per SIMD each running 8
 // independent chains (throughput, not latency).  Cycles come from s_memtime (shader clock)
 // around each wave's loop; cost = wave cycles / (waves per SIMD x instructions per wave).
-// These costs turn rocprofv3's instruction-mix counters into a VALU-time roofline
-// (bench.py roofline.issue_frac; scripts/summarize_prof.py).
+// s_memtime does not tick at the shader clock on gfx950 (its per-XCD bases also differ), so the
+// costs are relative: v_fma_f64 costs 2.3x v_fma_f32 and 1.8x v_add_u32.  They weight the
+// instruction-mix cross-check in scripts/summarize_prof.py (valu_time_frac); the roofline
+// fraction the bench line reports is the hardware's own VALUBusy (roofline.issue_frac).
 // Build: hipcc --offload-arch=gfx950 -O3 -o ubench_issue ubench_issue.hip
 #include <hip/hip_runtime.h>
 

@@ -214,24 +214,75 @@ def test_hrs_fused_split_invariant(panel):
     np.testing.assert_array_equal(whole.view(np.int64), parts.view(np.int64))
 
 
-def test_hrs_fused_refuses_uncoded_panel():
-    import ctypes as C
+def _continuous(n, seed=1):
+    """A panel no dictionary codes: every value distinct (standardised normal draws)."""
+    g = np.random.default_rng(seed)
+    x = g.standard_normal(n)
+    y = -0.3 * x + math.sqrt(1 - 0.09) * g.standard_normal(n)
+    return {"age_z": x, "bmi_z": y, "lambda_age_z": 2.2, "lambda_bmi_z": 2.6}
 
-    import torch
-    from dcor import _lib
-    n = 3000
-    g = np.random.default_rng(1)
-    X = torch.as_tensor(g.standard_normal(n), device="cuda")  # every value distinct: not codable
-    Y = torch.as_tensor(g.standard_normal(n), device="cuda")
-    pn = C.c_void_p()
-    _lib.check(_lib.lib.dcor_panel_create(C.c_void_p(X.data_ptr()), C.c_void_p(Y.data_ptr()), n, None,
-                                          C.byref(pn)))
-    try:
-        d = _lib.PrematSubg(n=n, reps=2, eps1=2.0, eps2=2.0, eta1=1.0, eta2=1.0, alpha=0.05, hrs=1,
-                            lam_x=2.2, lam_y=2.6, lam_s=2.2, lam_o=2.6, lam_r=math.nan, delta=math.nan,
-                            nsim=2000, X=X.data_ptr(), Y=Y.data_ptr(), xy_stride=0)
-        out = torch.empty((2, 6), dtype=torch.float64, device="cuda")
-        st = _lib.lib.dcor_hrs_fused_launch(C.byref(d), pn, 1, 2, 0, C.c_void_p(out.data_ptr()), None)
-        assert st == _lib.DCOR_EINVAL
-    finally:
-        _lib.lib.dcor_panel_destroy(pn)
+
+@pytest.mark.parametrize("n,eps,reps,rb", [(3001, 2.0, 9, 0), (3000, 0.55, 5, 11), (19433, 2.0, 4, 40)])
+def test_hrs_fused_continuous_panel_matches_oracle(n, eps, reps, rb):
+    """mode='fused' on a panel with no dictionary (k_hrs_fused_l2): every replicate against the
+    oracle estimators fed the oracle's own Philox restatement of the same streams."""
+    from dcor import api, hrs
+    from oracle import oracle as orc
+    z = _continuous(n)
+    fu = hrs.hrs_replicates(z["age_z"], z["bmi_z"], z["lambda_age_z"], z["lambda_bmi_z"], eps, reps,
+                            seed_ni=1010, seed_int=1020, rep_begin=rb, mode="fused")
+    k, m = api.batch_geometry(n, eps, eps, "subG", hrs=True)
+    delta = 1.0 / n
+    lam_r = api.lambda_receiver_from_noise(z["lambda_age_z"], z["lambda_bmi_z"], eps, delta)
+    for r in range(reps):
+        rep = rb + r
+        st, ni, _ = orc.ni_subg(z["age_z"], z["bmi_z"], eps, eps, hrs=1, lam_x=z["lambda_age_z"],
+                                lam_y=z["lambda_bmi_z"], perm=orc.perm(1010, 8, rep, n, k * m),
+                                lap_x=orc.gen_laplace(1010, rep, hrs.SITE_NI_LAP_X, k),
+                                lap_y=orc.gen_laplace(1010, rep, hrs.SITE_NI_LAP_Y, k))
+        st2, it, _ = orc.int_subg(z["age_z"], z["bmi_z"], eps, eps, hrs=1, lam_s=z["lambda_age_z"],
+                                  lam_o=z["lambda_bmi_z"], lam_r=lam_r, delta=delta,
+                                  lap_local=orc.gen_laplace(1020, rep, hrs.SITE_INT_LOCAL, n),
+                                  lap_central=orc.gen_laplace(1020, rep, hrs.SITE_INT_CENTRAL, 1)[0],
+                                  mix_z=orc.gen_normals(1020, rep, hrs.SITE_MIX_Z, 2000),
+                                  mix_l=orc.gen_laplace(1020, rep, hrs.SITE_MIX_L, 2000))
+        assert st == 0 and st2 == 0
+        assert_close(fu[r], np.concatenate([ni, it]), what=f"fused continuous n={n} eps={eps} rep {rep}")
+
+
+def test_hrs_fused_l2_kernel_equals_coded_kernel(panel):
+    """On a codable panel the uncoded kernel (DCOR_HRS_FUSED_L2=1) gathers the same clipped values
+    the coded kernel reads from its dictionaries, in the same order: identical bits."""
+    import os
+    import subprocess
+    import sys
+    z = panel
+    args = (z["age_z"], z["bmi_z"], z["lambda_age_z"], z["lambda_bmi_z"], 2.0, 23)
+    from dcor import hrs
+    coded = hrs.hrs_replicates(*args, rep_begin=5, mode="fused")
+    # the override is read once per process: run the uncoded kernel in a child
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    paths = [root, os.path.join(root, "distributed-correlation_amd")]
+    code = ("import sys, numpy as np; sys.path[:0] = %r; from dcor import hrs; "
+            "z = np.load(sys.argv[1]); "
+            "r = hrs.hrs_replicates(z['a'], z['b'], float(z['la']), float(z['lb']), 2.0, 23, rep_begin=5, "
+            "mode='fused'); np.save(sys.argv[2], r)") % (paths,)
+    import tempfile
+    with tempfile.TemporaryDirectory() as d:
+        np.savez(os.path.join(d, "p.npz"), a=z["age_z"], b=z["bmi_z"], la=z["lambda_age_z"], lb=z["lambda_bmi_z"])
+        env = dict(os.environ, DCOR_HRS_FUSED_L2="1")
+        subprocess.run([sys.executable, "-c", code, os.path.join(d, "p.npz"), os.path.join(d, "o.npy")],
+                       check=True, env=env, timeout=120)
+        l2 = np.load(os.path.join(d, "o.npy"))
+    np.testing.assert_array_equal(l2.view(np.int64), coded.view(np.int64))
+
+
+def test_hrs_fused_large_uncoded_panel_materialises():
+    """n > 65536 with no dictionary: the fused entry materialises the same streams and runs the
+    pre-materialised kernels, so its replicates equal mode='premat' exactly."""
+    from dcor import hrs
+    z = _continuous(70001, seed=3)
+    args = (z["age_z"], z["bmi_z"], z["lambda_age_z"], z["lambda_bmi_z"], 2.0, 3)
+    fu = hrs.hrs_replicates(*args, rep_begin=2, mode="fused")
+    pm = hrs.hrs_replicates(*args, rep_begin=2)
+    np.testing.assert_array_equal(fu.view(np.int64), pm.view(np.int64))

@@ -334,3 +334,30 @@ def test_perm_uniformity():
     c = np.bincount(np.arange(n) % 8, minlength=8).astype(float)
     exp = (np.outer(c, c) - np.diag(c)).ravel() / (n * (n - 1)) * R
     assert stats.chisquare(pair, exp).pvalue > 1e-4
+
+
+def test_gaussian_dgp_law_two_samples_per_block():
+    """The Gaussian DGP's draw contract (two samples per DGP_A block, Box-Muller on 32-bit
+    uniforms): MASS::mvrnorm's moments (vert-cor.R:389-394), normal quantiles of the
+    standardised marginals, independence of the two samples sharing a block, and the radius
+    cut-off sqrt(-2 ln 2^-33) = 6.76 sd."""
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "distributed-correlation_amd"))
+    from scipy import stats
+    from dcor.sim import CellSpec
+    n = 400_000
+    cell = CellSpec(n=n, rho=0.5, eps1=1.0, eps2=1.0, mu=(0.5, -0.25), sigma=(2.0, 0.5), seed=1234)
+    X, Y = O.gen_xy(cell.to_c(), 3)
+    zx, zy = (X - 0.5) / 2.0, (Y + 0.25) / 0.5
+    se = 1 / math.sqrt(n)
+    assert abs(zx.mean()) < 5 * se and abs(zy.mean()) < 5 * se
+    assert abs(zx.var() - 1) < 5 * math.sqrt(2) * se and abs(zy.var() - 1) < 5 * math.sqrt(2) * se
+    assert abs(np.corrcoef(zx, zy)[0, 1] - 0.5) < 5 * 0.75 * se
+    assert stats.kstest(zx, "norm").pvalue > 1e-4 and stats.kstest(zy, "norm").pvalue > 1e-4
+    # samples 2b and 2b+1 come from one Philox block: uncorrelated, in both coordinates
+    assert abs(np.corrcoef(zx[0::2], zx[1::2])[0, 1]) < 5 * math.sqrt(2) * se
+    assert abs(np.corrcoef(zy[0::2], zx[1::2])[0, 1]) < 5 * math.sqrt(2) * se
+    # radius of the underlying standard pair never exceeds the 32-bit cut-off
+    r = np.hypot(zx, (zy - 0.5 * zx) / math.sqrt(0.75))
+    assert r.max() <= math.sqrt(-2 * math.log(2.0 ** -33)) + 1e-9
