@@ -59,21 +59,19 @@ __device__ __forceinline__ double u53(uint32_t a, uint32_t b) {
 }
 
 // Division-free log for positive normal x (same code as oracle/orc_log): x = 2^k z with
-// z in [0.6875, 1.375), r = fma(z, 1/c, -1) against a 128-entry table, log x = k ln2 +
-// log c + log1p(r) with a degree-8 polynomial (|r| < 2^-7).  ~14 fp64 ops; <= 2.7 ulp.
+// z in [0.6875, 1.375), r = fma(z, 1/c, -1) against a 256-entry table, log x = k ln2 +
+// log c + log1p(r) with a degree-6 polynomial (|r| < 2^-9).  ~12 fp64 ops; <= 2 ulp.
 __device__ __forceinline__ double dlog(double x) {
   // The offset's low word is 0, so the reduction lives in the high word (32-bit ops only).
   const uint64_t ix = (uint64_t)__double_as_longlong(x);
   const uint32_t hi = (uint32_t)(ix >> 32), tmp = hi - 0x3fe60000u;
-  const int i = (int)((tmp >> 13) & 127u);
+  const int i = (int)((tmp >> 12) & 255u);
   const int k = (int)tmp >> 20;
   const double z = __longlong_as_double(
       (long long)(((uint64_t)(hi - (tmp & 0xfff00000u)) << 32) | (uint32_t)ix));
-  const double invc = dcor_log_tab[i][0], logc = dcor_log_tab[i][1];
+  const double invc = dcor_log8_tab[i][0], logc = dcor_log8_tab[i][1];
   const double r = fma(z, invc, -1.0), kd = (double)k, r2 = r * r;
-  double p = fma(r, DCOR_LOG1P_C8, DCOR_LOG1P_C7);
-  p = fma(r, p, DCOR_LOG1P_C6);
-  p = fma(r, p, DCOR_LOG1P_C5);
+  double p = fma(r, DCOR_LOG1P_C6, DCOR_LOG1P_C5);
   p = fma(r, p, DCOR_LOG1P_C4);
   p = fma(r, p, DCOR_LOG1P_C3);
   p = fma(r, p, DCOR_LOG1P_C2);
@@ -83,13 +81,13 @@ __device__ __forceinline__ double dlog(double x) {
 
 // sin(pi t), cos(pi t) for t in [0, 2], given t64 = 64 t (same code as oracle/orc_sincospi):
 // j = rint(t64), d = (t64 - j) pi / 64 (|d| <= pi/128), angle addition with the 129-entry
-// table of sin / cos(pi j / 64) and degree-7 / 8 polynomials in d.  ~19 fp64 ops.
+// table of sin / cos(pi j / 64) and degree-7 / 6 polynomials in d.  ~18 fp64 ops.
 __device__ __forceinline__ void dsincospi64(double t64, double* sp, double* cp) {
   const double jd = rint(t64), r = t64 - jd;
   const int j = (int)jd;
   const double d = fma(r, DCOR_PI64_HI, r * DCOR_PI64_LO), z = d * d;
   const double sd = fma(d * z, fma(z, fma(z, DCOR_SIN_S7, DCOR_SIN_S5), DCOR_SIN_S3), d);
-  const double cm1 = z * fma(z, fma(z, fma(z, DCOR_COS_C8, DCOR_COS_C6), DCOR_COS_C4), DCOR_COS_C2);
+  const double cm1 = z * fma(z, fma(z, DCOR_COS_C6, DCOR_COS_C4), DCOR_COS_C2);
   const double S = dcor_sincospi_tab[j][0], C = dcor_sincospi_tab[j][1];
   *sp = fma(S, cm1, fma(C, sd, S));
   *cp = fma(C, cm1, fma(-S, sd, C));

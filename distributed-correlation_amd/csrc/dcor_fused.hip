@@ -304,11 +304,16 @@ __device__ __forceinline__ void exact_signs(const SignConst& c, const SignStd& s
 }
 
 // Pass 1: replicate `rep` -> its slab (n records) and its clipped sums (SIGN_SUMS doubles:
-// sum clip(x) as double-double {hi, lo}, sum clip(x)^2, the same for y).  The sums of clip(x),
-// clip(y) decide the private centres, hence every sign (vert-cor.R:335-347), so they are
-// compensated: each thread adds its group of 4 samples plainly and folds the group sum into a
-// TwoSum accumulator; the workgroup reduction is double-double.  The second moments only set
-// sd > 0, which never changes a sign, and stay plain sums.
+// sum clip(x) as double-double {hi, lo}, a second-moment slot, the same for y).  The sums of
+// clip(x), clip(y) decide the private centres, hence every sign (vert-cor.R:335-347), so they
+// are compensated: each thread adds its group of 4 samples plainly and folds the group sum into
+// a TwoSum accumulator; the workgroup reduction is double-double.
+// The second moments are not accumulated: mean(clip(x)^2) enters the reference only through
+// sd_priv = sqrt(max(m2 + noise - mu^2, 1e-12)) (vert-cor.R:339-347), and only signs of
+// (clip(x) - mu) / sd_priv are used (:218, :277).  For any finite mean(x^2) in [0, L^2], sd_priv
+// is positive and finite (signs = signs of clip(x) - mu), or +Inf / NaN exactly when the noise
+// terms overflow -- the same for every such value -- so the slot carries 0 and every sign, hence
+// every result, is unchanged.
 template <int DGP>
 __device__ __forceinline__ void sign_pass1_body(const SignConst& c, uint32_t rep,
                                                 uint32_t* __restrict__ slab,
@@ -316,7 +321,6 @@ __device__ __forceinline__ void sign_pass1_body(const SignConst& c, uint32_t rep
   __shared__ double red[16 * DCOR_WAVES];
   const int tid = threadIdx.x;
   DD sx{0.0, 0.0}, sy{0.0, 0.0};
-  double v[2] = {0.0, 0.0};
   // group g4 = samples 4 g4 .. 4 g4 + 3; FULL: all four exist (the hot loop has no guards)
   auto group = [&](int64_t g4, auto full_tag) {
     constexpr bool FULL = decltype(full_tag)::value;
@@ -339,7 +343,7 @@ __device__ __forceinline__ void sign_pass1_body(const SignConst& c, uint32_t rep
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const double xc = rclip_fin(x[q], c.L), yc = rclip_fin(y[q], c.L);
-      if (FULL || (int64_t)(i0 + q) < c.n) { gx += xc; v[0] += xc * xc; gy += yc; v[1] += yc * yc; }
+      if (FULL || (int64_t)(i0 + q) < c.n) { gx += xc; gy += yc; }
       const uint32_t qx = code16(xc, c.cinv_xf, c.cnb_xf, 65535.0f);
       const uint32_t qy = code16(yc, c.cinv_yf, c.cnb_yf, 32767.0f);
       rec[q] = qx | (qy << 16) | (fl[q] << 31);
@@ -359,10 +363,9 @@ __device__ __forceinline__ void sign_pass1_body(const SignConst& c, uint32_t rep
   if ((c.n & 3) && tid == (int)(nfull % DCOR_BLOCK)) group(nfull, std::false_type());
   DD d2[2] = {sx, sy};
   block_sum_dd<2>(d2, red);
-  block_sum<2>(v, red + 4 * DCOR_WAVES);
   if (tid == 0) {
-    sums_out[0] = d2[0].hi; sums_out[1] = d2[0].lo; sums_out[2] = v[0];
-    sums_out[3] = d2[1].hi; sums_out[4] = d2[1].lo; sums_out[5] = v[1];
+    sums_out[0] = d2[0].hi; sums_out[1] = d2[0].lo; sums_out[2] = 0.0;
+    sums_out[3] = d2[1].hi; sums_out[4] = d2[1].lo; sums_out[5] = 0.0;
   }
 }
 
@@ -886,9 +889,9 @@ __device__ __forceinline__ void sign_fused_body(const SignConst& c, uint32_t rep
   __shared__ SelScratch sel;
   const int tid = threadIdx.x;
   scalar_laplace(rep, c.k0, c.k1, lap);
-  // the same compensated sums as k_sign_pass1 (groups of 4, TwoSum, double-double reduction)
+  // the same compensated sums as k_sign_pass1 (groups of 4, TwoSum, double-double reduction;
+  // no second moments, see sign_pass1_body)
   DD sx{0.0, 0.0}, sy{0.0, 0.0};
-  double v[2] = {0.0, 0.0};
   if (c.normalise) {
     for (int64_t g4 = tid; 4 * g4 < c.n; g4 += DCOR_BLOCK) {
       double x[4], y[4];
@@ -897,8 +900,8 @@ __device__ __forceinline__ void sign_fused_body(const SignConst& c, uint32_t rep
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         if (4 * g4 + q < c.n) {
-          const double xc = rclip_fin(x[q], c.L), yc = rclip_fin(y[q], c.L);
-          gx += xc; v[0] += xc * xc; gy += yc; v[1] += yc * yc;
+          gx += rclip_fin(x[q], c.L);
+          gy += rclip_fin(y[q], c.L);
         }
       }
       ks_acc(sx, gx);
@@ -907,13 +910,12 @@ __device__ __forceinline__ void sign_fused_body(const SignConst& c, uint32_t rep
   }
   DD d2s[2] = {sx, sy};
   block_sum_dd<2>(d2s, red);
-  block_sum<2>(v, red + 4 * DCOR_WAVES);
   SignStd s;
   {
     double l8[8];
 #pragma unroll
     for (int q = 0; q < 8; ++q) l8[q] = lap[q];
-    const double sums[6] = {d2s[0].hi, d2s[0].lo, v[0], d2s[1].hi, d2s[1].lo, v[1]};
+    const double sums[6] = {d2s[0].hi, d2s[0].lo, 0.0, d2s[1].hi, d2s[1].lo, 0.0};
     sign_std_from_pass1(c, sums, l8, s);
   }
   FlipGen fl;

@@ -496,16 +496,14 @@ double orc_log(double x) {
   uint64_t ix;
   memcpy(&ix, &x, 8);
   const uint64_t tmp = ix - 0x3fe6000000000000ull;
-  const int i = (int)((tmp >> 45) & 127u);
+  const int i = (int)((tmp >> 44) & 255u);
   const int64_t k = (int64_t)tmp >> 52;
   const uint64_t iz = ix - (tmp & (0xfffull << 52));
   double z;
   memcpy(&z, &iz, 8);
-  const double invc = dcor_log_tab[i][0], logc = dcor_log_tab[i][1];
+  const double invc = dcor_log8_tab[i][0], logc = dcor_log8_tab[i][1];
   const double r = fma(z, invc, -1.0), kd = (double)k, r2 = r * r;
-  double p = fma(r, DCOR_LOG1P_C8, DCOR_LOG1P_C7);
-  p = fma(r, p, DCOR_LOG1P_C6);
-  p = fma(r, p, DCOR_LOG1P_C5);
+  double p = fma(r, DCOR_LOG1P_C6, DCOR_LOG1P_C5);
   p = fma(r, p, DCOR_LOG1P_C4);
   p = fma(r, p, DCOR_LOG1P_C3);
   p = fma(r, p, DCOR_LOG1P_C2);
@@ -519,7 +517,7 @@ void orc_sincospi(double t64, double* sp, double* cp) {
   const int j = (int)jd;
   const double d = fma(r, DCOR_PI64_HI, r * DCOR_PI64_LO), z = d * d;
   const double sd = fma(d * z, fma(z, fma(z, DCOR_SIN_S7, DCOR_SIN_S5), DCOR_SIN_S3), d);
-  const double cm1 = z * fma(z, fma(z, fma(z, DCOR_COS_C8, DCOR_COS_C6), DCOR_COS_C4), DCOR_COS_C2);
+  const double cm1 = z * fma(z, fma(z, DCOR_COS_C6, DCOR_COS_C4), DCOR_COS_C2);
   const double S = dcor_sincospi_tab[j][0], C = dcor_sincospi_tab[j][1];
   *sp = fma(S, cm1, fma(C, sd, S));
   *cp = fma(C, cm1, fma(-S, sd, C));
