@@ -1220,6 +1220,21 @@ int dcor_shutdown(void) {
   return DCOR_OK;
 }
 
+int dcor_dgp_launch(const dcor_cell* cell, int64_t rep_begin, int64_t reps, double* d_X,
+                    double* d_Y, void* stream) {
+  if (!cell || reps < 0 || cell->n < 1 || cell->n > 0x7fffffffLL || (reps > 0 && (!d_X || !d_Y)))
+    return fail(DCOR_EINVAL, "bad dgp arguments");
+  if (reps > 65535) return fail(DCOR_EINVAL, "dgp: at most 65535 replicates per launch");
+  if (rep_begin < 0 || rep_begin + reps > 0xffffffffLL) return fail(DCOR_EINVAL, "dgp: replicate range exceeds 2^32");
+  DgpConst g;
+  if (int st = make_dgp(*cell, g)) return st;
+  if (int st = need_device()) return st;
+  const int rc = launch_dgp(g, (uint32_t)cell->seed, (uint32_t)(cell->seed >> 32), rep_begin, reps,
+                            cell->n, d_X, d_Y, stream);
+  if (rc) return hip_fail((hipError_t)rc, "dgp launch");
+  return DCOR_OK;
+}
+
 int dcor_draws_launch(int kind, uint64_t seed, int site, int64_t rep_begin, int64_t reps,
                       int64_t count, double* d_out, void* stream) {
   if (kind < 0 || kind > 2 || reps < 0 || count < 0 || (reps * count > 0 && !d_out))

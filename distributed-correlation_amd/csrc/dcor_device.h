@@ -11,6 +11,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "../../include/dcor.h"
+
 #define DCOR_TABLE_ATTR __device__
 #include "dcor_tables.h"
 
@@ -132,6 +134,67 @@ __device__ __forceinline__ void normal_polar32(uint32_t a, uint32_t b, double* r
   const double t64 = fma((double)b, 0x1p-25, 0x1p-26);
   *r = sqrt_pos(-2.0 * dlog(u1));
   dsincospi64(t64, s, c);
+}
+
+// ------------------------------------------------------------- ziggurat
+// The Gaussian DGP's normals (Marsaglia & Tsang's ziggurat, 512 layers, tables in
+// dcor_tables.h; same code as oracle/orc_zig).  A draw takes a 32-bit word A and a 16-bit field
+// H: j = H >> 6 picks layer L = j >> 1 and sign j & 1, and |u| = (2 x + 1) 2^-39 with the 38 bits
+// x = A : H[5:0].  d = 1 + |u| is built from bits (Y = H[5:0] << 26 | 1 << 25 carries the low
+// mantissa), so x = fma(d, SX, -SX) = round(|u| SX) with SX = (-1)^s X[L] in one fma; the draw is
+// accepted on the fast path when |x| < X[L+1] (the strip lies under the density there).
+__device__ __forceinline__ double zig_d(uint32_t A, uint32_t Y) {
+  const uint32_t hi = __builtin_amdgcn_alignbit(0x3ffu, A, 12u);
+  const uint32_t lo = __builtin_amdgcn_alignbit(A, Y, 12u);
+  return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+__device__ __forceinline__ uint32_t zig_y_lo(uint32_t H16) { return (H16 << 26) | 0x2000000u; }
+// z1 takes H = w2 & 0xffff, z2 takes H = w2 >> 16
+__device__ __forceinline__ uint32_t zig_y1(uint32_t w2) { return (w2 << 26) | 0x2000000u; }
+__device__ __forceinline__ uint32_t zig_y2(uint32_t w2) { return ((w2 << 10) & 0xfc000000u) | 0x2000000u; }
+__device__ __forceinline__ uint32_t zig_j1(uint32_t w2) { return (w2 >> 6) & 1023u; }
+__device__ __forceinline__ uint32_t zig_j2(uint32_t w2) { return w2 >> 22; }
+
+// The full draw from attempt 0's (A, H): fast test, then the wedge test (L >= 1) against
+// f(x) = exp(-x^2/2) compared in logs, or the base layer's tail (L = 0: Marsaglia's x = -log(U1)/r,
+// accepted when -2 log(U2) > x^2), and otherwise a new attempt from block (i, rep, ZIG, 2a + which).
+__device__ __forceinline__ double zig_slow(uint32_t i, uint32_t which, uint32_t rep, uint32_t k0,
+                                        uint32_t k1, uint32_t A, uint32_t H) {
+  for (uint32_t a = 0;; ++a) {
+    const U4 q = philox(i, rep, DCOR_SITE_ZIG, 2u * a + which, k0, k1);
+    if (a > 0) { A = q.w0; H = q.w1 & 0xffffu; }
+    const uint32_t j = H >> 6, L = j >> 1;
+    const double sx = dcor_zig_tab[j][0];
+    const double x = fma(zig_d(A, zig_y_lo(H)), sx, -sx);
+    if (fabs(x) < dcor_zig_tab[j][1]) return x;
+    if (L == 0) {
+      for (uint32_t t = 0;; ++t) {
+        const U4 b = philox(i, rep, DCOR_SITE_ZIG_TAIL, 2u * t + which, k0, k1);
+        const double xt = -dlog(u53(b.w0, b.w1)) * DCOR_ZIG_RINV;
+        const double yt = -dlog(u53(b.w2, b.w3));
+        if (yt + yt > xt * xt) return (j & 1u) ? -(DCOR_ZIG_R + xt) : (DCOR_ZIG_R + xt);
+      }
+    }
+    const double y = fma(u53(q.w2, q.w3), dcor_zig_wedge[L][1], dcor_zig_wedge[L][0]);
+    if (dlog(y) < -0.5 * (x * x)) return x;
+  }
+}
+
+// One draw: the fast path inline, the rest out of line.
+__device__ __forceinline__ double zig_draw(uint32_t i, uint32_t which, uint32_t rep, uint32_t k0,
+                                           uint32_t k1, uint32_t A, uint32_t H) {
+  const uint32_t j = H >> 6;
+  const double sx = dcor_zig_tab[j][0];
+  const double x = fma(zig_d(A, zig_y_lo(H)), sx, -sx);
+  if (fabs(x) < dcor_zig_tab[j][1]) return x;
+  return zig_slow(i, which, rep, k0, k1, A, H);
+}
+
+// mu + A z of MASS::mvrnorm (vert-cor.R:389-394) for z = (z1, z2) (same code as oracle/orc_mvn_z).
+__device__ __forceinline__ void mvn_z(double z1, double z2, double mu0, double mu1, double a00,
+                                      double a01, double a10, double a11, double* x, double* y) {
+  *x = fma(a00, z1, fma(a01, z2, mu0));
+  *y = fma(a10, z1, fma(a11, z2, mu1));
 }
 
 __device__ __forceinline__ void normal_pair(const U4& w, double* z1, double* z2) {

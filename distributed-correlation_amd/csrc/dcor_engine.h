@@ -135,6 +135,8 @@ struct CodesBufs {
 int launch_sign_fused_codes(const SignConst& c, int64_t reps, int64_t chunk, const CodesBufs& bf,
                             dcor_rep_out* out, void* stream);
 int launch_subg_fused(const SubgConst& c, int64_t reps, dcor_rep_out* out, void* stream);
+int launch_dgp(const DgpConst& g, uint32_t k0, uint32_t k1, int64_t rep_begin, int64_t reps,
+               int64_t n, double* X, double* Y, void* stream);
 
 // ---- batched grid launches (dcor_grid_launch): many cells' replicates per launch ----------
 // One work item = one replicate: the cell's constants come from a device table, so a launch

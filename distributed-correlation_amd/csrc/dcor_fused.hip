@@ -18,32 +18,32 @@ namespace dcor {
 // Sample i of a replicate from the draw-site contract of include/dcor.h.
 template <int DGP> struct Dgp;
 
-template <> struct Dgp<DCOR_DGP_GAUSSIAN> {  // MASS::mvrnorm (vert-cor.R:389-394), 2 samples/block
-  // Sample i: words (wa, wb) = (w0, w1) or (w2, w3) of DGP_A block i/2, Box-Muller from the
-  // 32-bit uniforms (wa + 1/2) 2^-32 (radius) and (wb + 1/2) 2^-32 (angle); the sign family's
-  // INT flips come from the FLIP site.  Half a Philox block per sample.
-  static constexpr bool spare_flip = false;
-  static __device__ __forceinline__ void from_words(const DgpConst& g, uint32_t wa, uint32_t wb,
-                                                    double& x, double& y) {
-    double r, s, cs;
-    normal_polar32(wa, wb, &r, &s, &cs);
-    mvn_polar(r, s, cs, g.mu0, g.mu1, g.a00, g.a01, g.a10, g.a11, &x, &y);
+// Where a DGP's sign-family INT flips come from (vert-cor.R:175).
+enum { FLIP_SITE = 0, FLIP_SPARE24 = 1, FLIP_SPARE32 = 2 };
+
+template <> struct Dgp<DCOR_DGP_GAUSSIAN> {  // MASS::mvrnorm (vert-cor.R:389-394), 1 sample/block
+  // Sample i: block (i, rep, DGP_A) = (w0, w1, w2, w3); the ziggurat normals z1 = zig(w0, w2 &
+  // 0xffff), z2 = zig(w1, w2 >> 16) (dcor_device.h), x = mu + A z; the sign family's INT flip is
+  // w3 < ceil(p 2^32).
+  static constexpr int flip_src = FLIP_SPARE32;
+  static __device__ __forceinline__ void one_w3(const DgpConst& g, uint32_t i, uint32_t rep,
+                                                uint32_t k0, uint32_t k1, double& x, double& y,
+                                                uint32_t& w3) {
+    const U4 w = draw(i, rep, DCOR_SITE_DGP_A, k0, k1);
+    const double z1 = zig_draw(i, 0u, rep, k0, k1, w.w0, w.w2 & 0xffffu);
+    const double z2 = zig_draw(i, 1u, rep, k0, k1, w.w1, w.w2 >> 16);
+    mvn_z(z1, z2, g.mu0, g.mu1, g.a00, g.a01, g.a10, g.a11, &x, &y);
+    w3 = w.w3;
   }
   static __device__ __forceinline__ void one(const DgpConst& g, uint32_t i, uint32_t rep,
                                              uint32_t k0, uint32_t k1, double& x, double& y) {
-    const U4 w = draw(i >> 1, rep, DCOR_SITE_DGP_A, k0, k1);
-    if (i & 1) from_words(g, w.w2, w.w3, x, y);
-    else from_words(g, w.w0, w.w1, x, y);
+    uint32_t w3;
+    one_w3(g, i, rep, k0, k1, x, y, w3);
   }
-  // i0 even
   static __device__ __forceinline__ void quad(const DgpConst& g, uint32_t i0, uint32_t rep,
                                               uint32_t k0, uint32_t k1, double* x, double* y) {
-    const U4 a = draw(i0 >> 1, rep, DCOR_SITE_DGP_A, k0, k1);
-    const U4 b = draw((i0 >> 1) + 1, rep, DCOR_SITE_DGP_A, k0, k1);
-    from_words(g, a.w0, a.w1, x[0], y[0]);
-    from_words(g, a.w2, a.w3, x[1], y[1]);
-    from_words(g, b.w0, b.w1, x[2], y[2]);
-    from_words(g, b.w2, b.w3, x[3], y[3]);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) one(g, i0 + q, rep, k0, k1, x[q], y[q]);
   }
   static __device__ __forceinline__ double lap(uint32_t i, uint32_t rep, uint32_t k0, uint32_t k1) {
     const U4 v = draw(i, rep, DCOR_SITE_DGP_B, k0, k1);
@@ -54,8 +54,8 @@ template <> struct Dgp<DCOR_DGP_GAUSSIAN> {  // MASS::mvrnorm (vert-cor.R:389-39
 template <> struct Dgp<DCOR_DGP_BERNOULLI> {  // gen_bernoulli (vert-cor.R:78-98), 2 samples/block
   // Sample words (wa, wb) = (w0, w1) or (w2, w3) of block i/2: u < 0.5 is the top bit of wa
   // (wa < 2^31, exact); v < thr is the low 24 bits of wa against ceil(thr 2^24) (|bias| <
-  // 2^-24); the sign family's INT flip is wb >> 8 against ceil(p 2^24) (spare_flip).
-  static constexpr bool spare_flip = true;
+  // 2^-24); the sign family's INT flip is wb >> 8 against ceil(p 2^24).
+  static constexpr int flip_src = FLIP_SPARE24;
   static __device__ __forceinline__ bool xbit(uint32_t wa) { return wa < 0x80000000u; }
   static __device__ __forceinline__ bool ybit(const DgpConst& g, uint32_t wa, bool xb) {
     return (wa & 0xFFFFFFu) < (xb ? g.T1_24 : g.T0_24);
@@ -102,7 +102,7 @@ template <> struct Dgp<DCOR_DGP_BERNOULLI> {  // gen_bernoulli (vert-cor.R:78-98
 };
 
 template <> struct Dgp<DCOR_DGP_BOUNDED_FACTOR> {  // gen_bounded_factor (ver-cor-subG.R:141-154)
-  static constexpr bool spare_flip = false;  // INT flips from the FLIP site
+  static constexpr int flip_src = FLIP_SITE;
   static __device__ __forceinline__ void one_lap(const DgpConst& g, uint32_t i, uint32_t rep,
                                                  uint32_t k0, uint32_t k1, double& x, double& y,
                                                  double* lap) {
@@ -125,7 +125,7 @@ template <> struct Dgp<DCOR_DGP_BOUNDED_FACTOR> {  // gen_bounded_factor (ver-co
 };
 
 template <> struct Dgp<DCOR_DGP_MIX_GAUSSIAN> {  // gen_mix_gaussian (ver-cor-subG.R:113-133)
-  static constexpr bool spare_flip = false;  // INT flips from the FLIP site
+  static constexpr int flip_src = FLIP_SITE;
   // One DGP_A block: Box-Muller from the top 52 bits of (w0,w1), (w2,w3); the component label
   // from the 24 bits Box-Muller leaves unused (low 12 of w1 and of w3): u24 < ceil(pi 2^24)
   // (exact for pi = .5, the R default; |bias| < 2^-24 otherwise).  Row shuffling
@@ -314,6 +314,12 @@ __device__ __forceinline__ void exact_signs(const SignConst& c, const SignStd& s
 // is positive and finite (signs = signs of clip(x) - mu), or +Inf / NaN exactly when the noise
 // terms overflow -- the same for every such value -- so the slot carries 0 and every sign, hence
 // every result, is unchanged.
+// Gaussian DGP in pass 1: the ziggurat's fast path inline; a sample with a normal that misses it
+// (1.6 % of samples) is queued in a per-wave LDS list and generated in full later by the whole
+// wave at once (zig_slow would otherwise run under divergence nearly every iteration).  The
+// queued sample's record is rewritten and its clipped values enter the sums at the drain.
+#define ZQ_CAP 512  // per-wave queue; a group iteration adds at most 256 entries per wave
+
 template <int DGP>
 __device__ __forceinline__ void sign_pass1_body(const SignConst& c, uint32_t rep,
                                                 uint32_t* __restrict__ slab,
@@ -321,46 +327,118 @@ __device__ __forceinline__ void sign_pass1_body(const SignConst& c, uint32_t rep
   __shared__ double red[16 * DCOR_WAVES];
   const int tid = threadIdx.x;
   DD sx{0.0, 0.0}, sy{0.0, 0.0};
-  // group g4 = samples 4 g4 .. 4 g4 + 3; FULL: all four exist (the hot loop has no guards)
-  auto group = [&](int64_t g4, auto full_tag) {
-    constexpr bool FULL = decltype(full_tag)::value;
-    const uint32_t i0 = (uint32_t)(4 * g4);
-    double x[4], y[4];
-    uint32_t fl[4];  // INT flip bits (vert-cor.R:175)
-    if constexpr (Dgp<DGP>::spare_flip) {
-      uint32_t u24[4];
-      Dgp<DGP>::quad_u24(c.g, i0, rep, c.k0, c.k1, x, y, u24);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) fl[q] = u24[q] < c.flipT24 ? 1u : 0u;
-    } else {
-      const U4 fw = draw((uint32_t)g4, rep, DCOR_SITE_FLIP, c.k0, c.k1);
-      Dgp<DGP>::quad(c.g, i0, rep, c.k0, c.k1, x, y);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) fl[q] = ((uint64_t)word(fw, q) < c.flipT) ? 1u : 0u;
-    }
-    uint32_t rec[4];
-    double gx = 0.0, gy = 0.0;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const double xc = rclip_fin(x[q], c.L), yc = rclip_fin(y[q], c.L);
-      if (FULL || (int64_t)(i0 + q) < c.n) { gx += xc; gy += yc; }
-      const uint32_t qx = code16(xc, c.cinv_xf, c.cnb_xf, 65535.0f);
-      const uint32_t qy = code16(yc, c.cinv_yf, c.cnb_yf, 32767.0f);
-      rec[q] = qx | (qy << 16) | (fl[q] << 31);
-    }
-    ks_acc(sx, gx);
-    ks_acc(sy, gy);
-    if (FULL) {
-      *reinterpret_cast<uint4*>(slab + i0) = make_uint4(rec[0], rec[1], rec[2], rec[3]);
-    } else {
-      for (int q = 0; q < 4; ++q) if ((int64_t)(i0 + q) < c.n) slab[i0 + q] = rec[q];
-    }
+  auto record = [&](double xc, double yc, uint32_t fl) {
+    const uint32_t qx = code16(xc, c.cinv_xf, c.cnb_xf, 65535.0f);
+    const uint32_t qy = code16(yc, c.cinv_yf, c.cnb_yf, 32767.0f);
+    return qx | (qy << 16) | (fl << 31);
   };
   // each thread runs its groups in increasing order; the partial last group (n % 4) is the last
-  // group of its thread, so the per-thread accumulation order is the same as one guarded loop
+  // group of its thread
   const int64_t nfull = c.n / 4;
-  for (int64_t g4 = tid; g4 < nfull; g4 += DCOR_BLOCK) group(g4, std::true_type());
-  if ((c.n & 3) && tid == (int)(nfull % DCOR_BLOCK)) group(nfull, std::false_type());
+  if constexpr (DGP == DCOR_DGP_GAUSSIAN) {
+    __shared__ double2 zt[2 * DCOR_ZIG_N];
+    __shared__ uint32_t zq[DCOR_WAVES][ZQ_CAP];
+    __shared__ uint32_t zqn[DCOR_WAVES];
+    const int wv = tid >> 6, lane = tid & 63;
+    for (int e = tid; e < 2 * DCOR_ZIG_N; e += DCOR_BLOCK)
+      zt[e] = make_double2(dcor_zig_tab[e][0], dcor_zig_tab[e][1]);
+    if (tid < DCOR_WAVES) zqn[tid] = 0u;
+    __syncthreads();
+    auto group = [&](int64_t g4, auto full_tag) {
+      constexpr bool FULL = decltype(full_tag)::value;
+      const uint32_t i0 = (uint32_t)(4 * g4);
+      uint32_t rec[4], pend = 0;
+      double gx = 0.0, gy = 0.0;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const U4 w = draw(i0 + q, rep, DCOR_SITE_DGP_A, c.k0, c.k1);
+        const double2 t1 = zt[zig_j1(w.w2)], t2 = zt[zig_j2(w.w2)];
+        const double z1 = fma(zig_d(w.w0, zig_y1(w.w2)), t1.x, -t1.x);
+        const double z2 = fma(zig_d(w.w1, zig_y2(w.w2)), t2.x, -t2.x);
+        const bool ok = ((int)(fabs(z1) < t1.y) & (int)(fabs(z2) < t2.y)) != 0;
+        double x, y;
+        mvn_z(z1, z2, c.g.mu0, c.g.mu1, c.g.a00, c.g.a01, c.g.a10, c.g.a11, &x, &y);
+        const double xc = rclip_fin(x, c.L), yc = rclip_fin(y, c.L);
+        const bool valid = FULL || (int64_t)(i0 + q) < c.n;
+        gx += (valid && ok) ? xc : 0.0;
+        gy += (valid && ok) ? yc : 0.0;
+        pend |= (valid && !ok) ? (1u << q) : 0u;
+        rec[q] = record(xc, yc, ((uint64_t)w.w3 < c.flipT) ? 1u : 0u);
+      }
+      ks_acc(sx, gx);
+      ks_acc(sy, gy);
+      if (FULL) {
+        *reinterpret_cast<uint4*>(slab + i0) = make_uint4(rec[0], rec[1], rec[2], rec[3]);
+      } else {
+        for (int q = 0; q < 4; ++q) if ((int64_t)(i0 + q) < c.n) slab[i0 + q] = rec[q];
+      }
+      if (pend) {
+        uint32_t pos = atomicAdd(&zqn[wv], (uint32_t)__popc(pend));
+        for (; pend; pend &= pend - 1u) zq[wv][pos++] = i0 + (uint32_t)(__ffs(pend) - 1);
+      }
+    };
+    // the whole wave, converged: each lane takes queued samples lane, lane + 64, ...
+    auto drain = [&]() {
+      const uint32_t cnt = __builtin_amdgcn_readfirstlane(zqn[wv]);
+      if (cnt == 0) return;
+      __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the placeholder records have landed
+      for (uint32_t k = (uint32_t)lane; k < cnt; k += 64) {
+        const uint32_t i = zq[wv][k];
+        double x, y;
+        uint32_t w3;
+        Dgp<DGP>::one_w3(c.g, i, rep, c.k0, c.k1, x, y, w3);
+        const double xc = rclip_fin(x, c.L), yc = rclip_fin(y, c.L);
+        ks_acc(sx, xc);
+        ks_acc(sy, yc);
+        slab[i] = record(xc, yc, ((uint64_t)w3 < c.flipT) ? 1u : 0u);
+      }
+      wave_sync();
+      if (lane == 0) zqn[wv] = 0u;
+      wave_sync();
+    };
+    for (int64_t b = 64 * wv; b < nfull; b += DCOR_BLOCK) {  // trip count uniform per wave
+      if (b + lane < nfull) group(b + lane, std::true_type());
+      if (__builtin_amdgcn_readfirstlane(zqn[wv]) > ZQ_CAP - 256) drain();
+    }
+    if ((c.n & 3) && tid == (int)(nfull % DCOR_BLOCK)) group(nfull, std::false_type());
+    drain();
+  } else {
+    // group g4 = samples 4 g4 .. 4 g4 + 3; FULL: all four exist (the hot loop has no guards)
+    auto group = [&](int64_t g4, auto full_tag) {
+      constexpr bool FULL = decltype(full_tag)::value;
+      const uint32_t i0 = (uint32_t)(4 * g4);
+      double x[4], y[4];
+      uint32_t fl[4];  // INT flip bits (vert-cor.R:175)
+      if constexpr (Dgp<DGP>::flip_src == FLIP_SPARE24) {
+        uint32_t u24[4];
+        Dgp<DGP>::quad_u24(c.g, i0, rep, c.k0, c.k1, x, y, u24);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) fl[q] = u24[q] < c.flipT24 ? 1u : 0u;
+      } else {
+        const U4 fw = draw((uint32_t)g4, rep, DCOR_SITE_FLIP, c.k0, c.k1);
+        Dgp<DGP>::quad(c.g, i0, rep, c.k0, c.k1, x, y);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) fl[q] = ((uint64_t)word(fw, q) < c.flipT) ? 1u : 0u;
+      }
+      uint32_t rec[4];
+      double gx = 0.0, gy = 0.0;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const double xc = rclip_fin(x[q], c.L), yc = rclip_fin(y[q], c.L);
+        if (FULL || (int64_t)(i0 + q) < c.n) { gx += xc; gy += yc; }
+        rec[q] = record(xc, yc, fl[q]);
+      }
+      ks_acc(sx, gx);
+      ks_acc(sy, gy);
+      if (FULL) {
+        *reinterpret_cast<uint4*>(slab + i0) = make_uint4(rec[0], rec[1], rec[2], rec[3]);
+      } else {
+        for (int q = 0; q < 4; ++q) if ((int64_t)(i0 + q) < c.n) slab[i0 + q] = rec[q];
+      }
+    };
+    for (int64_t g4 = tid; g4 < nfull; g4 += DCOR_BLOCK) group(g4, std::true_type());
+    if ((c.n & 3) && tid == (int)(nfull % DCOR_BLOCK)) group(nfull, std::false_type());
+  }
   DD d2[2] = {sx, sy};
   block_sum_dd<2>(d2, red);
   if (tid == 0) {
@@ -925,10 +1003,14 @@ __device__ __forceinline__ void sign_fused_body(const SignConst& c, uint32_t rep
   long long core = 0;
   auto signs = [&](uint32_t i, int& nx, int& ny, int& ix, int& iy, bool& bni, int& flip) {
     double x, y;
-    if constexpr (Dgp<DGP>::spare_flip) {
+    if constexpr (Dgp<DGP>::flip_src == FLIP_SPARE24) {
       uint32_t u24;
       Dgp<DGP>::one_u24(c.g, i, rep, c.k0, c.k1, x, y, u24);
       flip = u24 < c.flipT24 ? 1 : -1;
+    } else if constexpr (Dgp<DGP>::flip_src == FLIP_SPARE32) {
+      uint32_t w3;
+      Dgp<DGP>::one_w3(c.g, i, rep, c.k0, c.k1, x, y, w3);
+      flip = ((uint64_t)w3 < c.flipT) ? 1 : -1;
     } else {
       Dgp<DGP>::one(c.g, i, rep, c.k0, c.k1, x, y);
       flip = fl.get(i, rep, c.k0, c.k1, c.flipT);
@@ -1286,6 +1368,33 @@ int launch_sign_bern(SignConst c, int64_t reps, int64_t chunk, uint64_t* scratch
     if (int e = last_err()) return e;
   }
   return 0;
+}
+
+// The cell's DGP samples (Dgp<DGP>::one, the full draw contract): X, Y [reps][n].
+template <int DGP>
+__global__ __launch_bounds__(DCOR_BLOCK) void k_dgp(DgpConst g, uint32_t k0, uint32_t k1,
+                                                   int64_t rep_begin, int64_t n, double* X,
+                                                   double* Y) {
+  const int64_t i = (int64_t)blockIdx.x * DCOR_BLOCK + threadIdx.x;
+  if (i >= n) return;
+  double x, y;
+  Dgp<DGP>::one(g, (uint32_t)i, (uint32_t)(rep_begin + blockIdx.y), k0, k1, x, y);
+  X[blockIdx.y * n + i] = x;
+  Y[blockIdx.y * n + i] = y;
+}
+
+int launch_dgp(const DgpConst& g, uint32_t k0, uint32_t k1, int64_t rep_begin, int64_t reps,
+               int64_t n, double* X, double* Y, void* stream) {
+  if (reps <= 0 || n <= 0) return 0;
+  const dim3 gr((unsigned)((n + DCOR_BLOCK - 1) / DCOR_BLOCK), (unsigned)reps), b(DCOR_BLOCK);
+  const hipStream_t st = (hipStream_t)stream;
+  switch (g.dgp) {
+    case DCOR_DGP_GAUSSIAN: hipLaunchKernelGGL(k_dgp<DCOR_DGP_GAUSSIAN>, gr, b, 0, st, g, k0, k1, rep_begin, n, X, Y); break;
+    case DCOR_DGP_BERNOULLI: hipLaunchKernelGGL(k_dgp<DCOR_DGP_BERNOULLI>, gr, b, 0, st, g, k0, k1, rep_begin, n, X, Y); break;
+    case DCOR_DGP_MIX_GAUSSIAN: hipLaunchKernelGGL(k_dgp<DCOR_DGP_MIX_GAUSSIAN>, gr, b, 0, st, g, k0, k1, rep_begin, n, X, Y); break;
+    default: hipLaunchKernelGGL(k_dgp<DCOR_DGP_BOUNDED_FACTOR>, gr, b, 0, st, g, k0, k1, rep_begin, n, X, Y);
+  }
+  return last_err();
 }
 
 int launch_subg_fused(const SubgConst& c, int64_t reps, dcor_rep_out* out, void* stream) {

@@ -153,6 +153,7 @@ SIGNATURES = {
                                     _P, _P]),
     "dcor_perm_launch": (C.c_int, [C.c_uint64, C.c_int, C.c_int64, C.c_int64, C.c_int64, C.c_int64,
                                    _P, _P]),
+    "dcor_dgp_launch": (C.c_int, [C.POINTER(Cell), C.c_int64, C.c_int64, _P, _P, _P]),
     "dcor_dp_sd": (C.c_int, [_D, C.c_int64, C.c_double, C.c_double, C.c_double, C.c_double, _D, _D]),
     # R-surface helpers (R/dcor*.R): the GPU half of wrappers that draw with R's own RNG
     "dcor_int_subg_sd_uc": (C.c_int, [_D, _D, C.c_int64, C.c_double, C.c_double, C.c_double,

@@ -360,6 +360,13 @@ int dcor_mix_gaussian(const double* z0, int64_t n0, const double* z1, int64_t n1
 int dcor_draws_launch(int kind, uint64_t seed, int site, int64_t rep_begin, int64_t reps,
                       int64_t count, double* d_out, void* stream);
 
+/* The cell's DGP samples from the fused engine's draw contract (the sites below): d_X, d_Y
+ * [reps][n] for replicates rep_begin .. rep_begin + reps - 1 -- the (X, Y) every fused kernel
+ * generates for those replicates (gen_bernoulli, mvrnorm, gen_bounded_factor, gen_mix_gaussian
+ * of vert-cor.R:78-98,389-394 / ver-cor-subG.R:113-154). */
+int dcor_dgp_launch(const dcor_cell* cell, int64_t rep_begin, int64_t reps, double* d_X,
+                    double* d_Y, void* stream);
+
 /* On-device keyed random batches for the HRS NI estimator: d_out[r][t] = P_r(t), t < count,
  * where P_r is a pseudo-random permutation of [0, n) (4-round Feistel, cycle-walked, keyed by
  * Philox block (0, rep_begin + r, site, 0)) -- the role of sample.int(n, k*m) 0-based
@@ -368,16 +375,23 @@ int dcor_perm_launch(uint64_t seed, int site, int64_t rep_begin, int64_t reps, i
                      int64_t count, int32_t* d_out, void* stream);
 
 /* Draw-site contract of the fused engine (DESIGN.md "RNG"): Philox4x32-10 with
- * key = (seed lo32, seed hi32), counter = (index, rep, site, 0). */
+ * key = (seed lo32, seed hi32), counter = (index, rep, site, 0) unless noted.
+ * Gaussian DGP sample i: block (i, rep, DGP_A) = (w0, w1, w2, w3); z1 = ziggurat(w0, w2 & 0xffff),
+ * z2 = ziggurat(w1, w2 >> 16), INT flip = (w3 < ceil(p 2^32)).  A ziggurat draw that misses the
+ * fast test continues on blocks (i, rep, ZIG, 2a + which) (attempt a >= 1 draws its layer and
+ * magnitude there; every attempt's wedge uniform is words 2,3) and, in the base layer, on tail
+ * blocks (i, rep, ZIG_TAIL, 2t + which); which = 0 for z1, 1 for z2. */
 enum {
-  DCOR_SITE_DGP_A = 1,   /* 2 Gaussian samples (32-bit uniforms) / 2 Bernoulli samples / U,E1 */
+  DCOR_SITE_DGP_A = 1,   /* 1 Gaussian sample + its flip / 2 Bernoulli samples / U,E1 */
   DCOR_SITE_DGP_B = 2,   /* bounded-factor E2 (w0,w1) ; sub-G local Laplace (w2,w3) */
-  DCOR_SITE_FLIP = 3,    /* sign-family INT flips, 4 samples per block            */
+  DCOR_SITE_FLIP = 3,    /* sign-family INT flips, 4 samples per block (bounded factor, mixture) */
   DCOR_SITE_NI_LAP = 4,  /* batch j: Laplace X (w0,w1), Y (w2,w3)                  */
   DCOR_SITE_SCALAR = 5,  /* blocks 0..4: NI mu/m2 X, NI mu/m2 Y, INT mu/m2 X, INT mu/m2 Y, Z */
   DCOR_SITE_MIX_Z = 6,   /* mixquant normals, 2 per block                         */
   DCOR_SITE_MIX_L = 7,   /* mixquant unit Laplace, 2 per block                    */
-  DCOR_SITE_PERM = 8     /* HRS random-batch permutation keys (dcor_perm_launch)  */
+  DCOR_SITE_PERM = 8,    /* HRS random-batch permutation keys (dcor_perm_launch)  */
+  DCOR_SITE_ZIG = 9,     /* Gaussian DGP ziggurat retries (counter word 3 = 2 attempt + which) */
+  DCOR_SITE_ZIG_TAIL = 10 /* Gaussian DGP ziggurat tail (counter word 3 = 2 step + which) */
 };
 
 #ifdef __cplusplus

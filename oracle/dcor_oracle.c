@@ -538,13 +538,60 @@ static void orc_normal_polar(const uint32_t w[4], double* r, double* s, double* 
   orc_sincospi(u2 * 128.0, s, c);
 }
 
-/* The Gaussian DGP's pair from two 32-bit words (dcor_device.h normal_polar32): u1 = (a + 1/2)
- * 2^-32, u2 = (b + 1/2) 2^-32, both exact. */
-static void orc_normal_polar32(uint32_t a, uint32_t b, double* r, double* s, double* c) {
-  const double u1 = ((double)a + 0.5) * 0x1p-32;
-  const double u2 = ((double)b + 0.5) * 0x1p-32;
-  *r = sqrt(-2.0 * orc_log(u1));
-  orc_sincospi(u2 * 128.0, s, c);
+/* The Gaussian DGP's ziggurat normal (dcor_device.h zig_d / zig_slow / zig_draw; Marsaglia &
+ * Tsang, 512 layers, tables in dcor_tables.h).  Attempt 0 takes a 32-bit word A and a 16-bit
+ * field H from the sample's DGP_A block: j = H >> 6 (layer j >> 1, sign j & 1), |u| = (2 x + 1)
+ * 2^-39 with x = A : H[5:0], x_draw = round(|u| (-1)^s X[L]) = fma(1 + |u|, SX, -SX). */
+static double orc_zig_d(uint32_t A, uint32_t H) {
+  const uint64_t hi = 0x3ff00000ull | (A >> 12);
+  const uint64_t lo = ((uint64_t)(A & 0xfffu) << 20) | ((uint64_t)(H & 0x3fu) << 14) | (1u << 13);
+  const uint64_t bits = (hi << 32) | lo;
+  double d;
+  memcpy(&d, &bits, 8);
+  return d;
+}
+
+static void blk(uint64_t seed, uint32_t idx, uint32_t rep, uint32_t site, uint32_t w[4]);
+static void blk4(uint64_t seed, uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t w[4]) {
+  const uint32_t ctr[4] = {c0, c1, c2, c3};
+  orc_philox4x32_10(ctr, (uint32_t)seed, (uint32_t)(seed >> 32), w);
+}
+
+double orc_zig(uint64_t seed, uint32_t i, uint32_t which, uint32_t rep, uint32_t A, uint32_t H) {
+  for (uint32_t a = 0;; ++a) {
+    uint32_t q[4];
+    blk4(seed, i, rep, DCOR_SITE_ZIG, 2u * a + which, q);
+    if (a > 0) { A = q[0]; H = q[1] & 0xffffu; }
+    const uint32_t j = H >> 6, L = j >> 1;
+    const double sx = dcor_zig_tab[j][0];
+    const double x = fma(orc_zig_d(A, H), sx, -sx);
+    if (fabs(x) < dcor_zig_tab[j][1]) return x;     /* fast test: inside the strip's rectangle */
+    if (L == 0) {                                      /* base layer: Marsaglia's tail beyond r */
+      for (uint32_t t = 0;; ++t) {
+        uint32_t b[4];
+        blk4(seed, i, rep, DCOR_SITE_ZIG_TAIL, 2u * t + which, b);
+        const double xt = -orc_log(orc_u53(b[0], b[1])) * DCOR_ZIG_RINV;
+        const double yt = -orc_log(orc_u53(b[2], b[3]));
+        if (yt + yt > xt * xt) return (j & 1u) ? -(DCOR_ZIG_R + xt) : (DCOR_ZIG_R + xt);
+      }
+    }
+    /* wedge: f(X[L]) + U (f(X[L+1]) - f(X[L])) < exp(-x^2/2), compared in logs */
+    const double y = fma(orc_u53(q[2], q[3]), dcor_zig_wedge[L][1], dcor_zig_wedge[L][0]);
+    if (orc_log(y) < -0.5 * (x * x)) return x;
+  }
+}
+
+/* Sample i of the Gaussian DGP: block (i, rep, DGP_A) -> z1 = zig(w0, w2 & 0xffff),
+ * z2 = zig(w1, w2 >> 16); mu + A z (dcor_device.h mvn_z).  *w3 = the sign family's flip word. */
+static void orc_gauss_sample(uint64_t seed, uint32_t i, uint32_t rep, const double mu[2],
+                             const double a[4], double* x, double* y, uint32_t* w3) {
+  uint32_t w[4];
+  blk(seed, i, rep, DCOR_SITE_DGP_A, w);
+  const double z1 = orc_zig(seed, i, 0u, rep, w[0], w[2] & 0xffffu);
+  const double z2 = orc_zig(seed, i, 1u, rep, w[1], w[2] >> 16);
+  *x = fma(a[0], z1, fma(a[1], z2, mu[0]));
+  *y = fma(a[2], z1, fma(a[3], z2, mu[1]));
+  if (w3) *w3 = w[3];
 }
 
 void orc_normal_pair(const uint32_t w[4], double* z1, double* z2) {
@@ -608,12 +655,7 @@ static void gen_xy(const dcor_cell* c, int64_t rep, double* X, double* Y, double
   for (int64_t i = 0; i < n; ++i) {
     uint32_t w[4];
     if (c->dgp == DCOR_DGP_GAUSSIAN) {
-      /* two samples per block: words (w0, w1) for even i, (w2, w3) for odd i */
-      blk(c->seed, (uint32_t)(i >> 1), (uint32_t)rep, DCOR_SITE_DGP_A, w);
-      const int b = 2 * (int)(i & 1);
-      double r, s, cs;
-      orc_normal_polar32(w[b], w[b + 1], &r, &s, &cs);
-      orc_mvn_rsc(r, s, cs, c->mu, A, &X[i], &Y[i]);
+      orc_gauss_sample(c->seed, (uint32_t)i, (uint32_t)rep, c->mu, A, &X[i], &Y[i], NULL);
     } else if (c->dgp == DCOR_DGP_MIX_GAUSSIAN) {
       /* gen_mix_gaussian (ver-cor-subG.R:113-133): label = rbinom(1, pi_mix) from the 24
        * bits the normal pair leaves unused, u24 < ceil(pi * 2^24); component mvrnorm;
@@ -705,6 +747,10 @@ int orc_sim_rep(const void* cellp, int64_t rep, double out[6]) {
           blk(c->seed, (uint32_t)(i >> 1), (uint32_t)rep, DCOR_SITE_DGP_A, w);
           const uint32_t u24 = w[2 * (i & 1) + 1] >> 8;
           fl[i] = ((double)u24 * 0x1p-24 < p) ? 1 : 0;
+        } else if (c->dgp == DCOR_DGP_GAUSSIAN) {
+          /* the sample's own DGP_A block, word 3 */
+          blk(c->seed, (uint32_t)i, (uint32_t)rep, DCOR_SITE_DGP_A, w);
+          fl[i] = ((double)w[3] * 0x1p-32 < p) ? 1 : 0;
         } else {
           blk(c->seed, (uint32_t)(i >> 2), (uint32_t)rep, DCOR_SITE_FLIP, w);
           fl[i] = ((double)w[i & 3] * 0x1p-32 < p) ? 1 : 0;

@@ -109,6 +109,8 @@ void orc_gen_bounded_factor(const double* u, const double* e1, const double* e2,
 /* ---- counter-based RNG restatement (the engine's draw-site contract) ----- */
 void   orc_philox4x32_10(const uint32_t ctr[4], uint32_t k0, uint32_t k1, uint32_t out[4]);
 double orc_u53(uint32_t a, uint32_t b);
+/* The Gaussian DGP's ziggurat normal from attempt 0's word A and 16-bit field H (dcor.h sites). */
+double orc_zig(uint64_t seed, uint32_t i, uint32_t which, uint32_t rep, uint32_t A, uint32_t H);
 double orc_log(double x);
 void   orc_sincospi(double t64, double* s, double* c);  /* sin, cos(pi t), t64 = 64 t in [0, 128] */
 double orc_unit_laplace(double u);

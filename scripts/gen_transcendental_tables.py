@@ -12,6 +12,12 @@ sin(pi t) = S_j cos d + C_j sin d, cos(pi t) = C_j cos d - S_j sin d, with S_j, 
 sin, cos(pi j / 64) and degree-7 / degree-6 Taylor polynomials in d (truncation d^8/8! <
 3.3e-18).
 
+Ziggurat (the Gaussian DGP's normals, Marsaglia & Tsang 2000 with 512 layers): f(x) =
+exp(-x^2/2); r solves the layer recursion X[1] = r, X[i+1] = f^-1(v / X[i] + f(X[i])) with the
+top layer closing at f(0) = 1 (v = r f(r) + int_r^inf f, X[0] = v / f(r), X[512] = 0).
+dcor_zig_tab[2L + s] = {(-1)^s X[L], X[L+1]} (the signed strip width and the fast-accept bound);
+dcor_zig_wedge[L] = {f(X[L]), f(X[L+1]) - f(X[L])}.  Computed with mpmath at 50 digits.
+
 The R-stream mode's accurate log (csrc/dcor_rstream.h) uses the 7-bit table dcor_log_tab with
 log(c) as a double-double (dcor_log_tab_lo) and its own log1p tail.
 
@@ -92,6 +98,48 @@ def log8_table():
     return rows
 
 
+ZIG_N = 512
+
+
+def zig_tables():
+    import mpmath as mp
+    mp.mp.dps = 50
+    f = lambda x: mp.e ** (-x * x / 2)
+    finv = lambda y: mp.sqrt(-2 * mp.log(y))
+    tail = lambda r: mp.sqrt(mp.pi / 2) * mp.erfc(r / mp.sqrt(2))
+
+    def build(r):
+        v = r * f(r) + tail(r)
+        X = [v / f(r), r]
+        for _ in range(2, ZIG_N):
+            y = v / X[-1] + f(X[-1])
+            if y >= 1:
+                return None, v
+            X.append(finv(y))
+        return X, v
+
+    def close(r):  # > 0: r too small (the layers overshoot f(0) = 1)
+        X, v = build(r)
+        return 1 if X is None else v / X[-1] + f(X[-1]) - 1
+
+    lo, hi = mp.mpf(3), mp.mpf(5)
+    for _ in range(200):
+        mid = (lo + hi) / 2
+        if close(mid) > 0:
+            lo = mid
+        else:
+            hi = mid
+    X, v = build(hi)
+    X.append(mp.mpf(0))
+    tab = []
+    for L in range(ZIG_N):
+        xl, xn = float(X[L]), float(X[L + 1])
+        tab += [(xl, xn), (-xl, xn)]
+    wedge = [(float(f(X[L])), float(f(X[L + 1]) - f(X[L]))) for L in range(ZIG_N)]
+    r = float(X[1])
+    return r, float(v), tab, wedge
+
+
 def main():
     ln2 = Decimal(2).ln()
     ln2_hi = float.fromhex("0x1.62e42fefa3800p-1")          # 42 significant bits: k * ln2_hi exact
@@ -141,6 +189,17 @@ def main():
           "DCOR_TABLE_ATTR static const double dcor_sincospi_tab[129][2] = {"]
     for s, c in scp:
         L.append(f"  {{{hx(s)}, {hx(c)}}},")
+    zr, zv, ztab, zwedge = zig_tables()
+    L += ["};", "", f"/* ziggurat normal, {ZIG_N} layers (v = {zv!r}) */", f"#define DCOR_ZIG_N {ZIG_N}",
+          f"#define DCOR_ZIG_R {hx(zr)}", f"#define DCOR_ZIG_RINV {hx(1.0 / zr)}",
+          "/* {(-1)^s X[L], X[L+1]} at 2L + s */",
+          f"DCOR_TABLE_ATTR static const double dcor_zig_tab[{2 * ZIG_N}][2] = {{"]
+    for a, b in ztab:
+        L.append(f"  {{{hx(a)}, {hx(b)}}},")
+    L += ["};", "", "/* {f(X[L]), f(X[L+1]) - f(X[L])}, f(x) = exp(-x^2/2) */",
+          f"DCOR_TABLE_ATTR static const double dcor_zig_wedge[{ZIG_N}][2] = {{"]
+    for a, b in zwedge:
+        L.append(f"  {{{hx(a)}, {hx(b)}}},")
     L += ["};", "", "#endif /* DCOR_TABLES_H */", ""]
     open(OUT, "w").write("\n".join(L))
     print("wrote", OUT)

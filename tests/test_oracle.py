@@ -336,11 +336,11 @@ def test_perm_uniformity():
     assert stats.chisquare(pair, exp).pvalue > 1e-4
 
 
-def test_gaussian_dgp_law_two_samples_per_block():
-    """The Gaussian DGP's draw contract (two samples per DGP_A block, Box-Muller on 32-bit
-    uniforms): MASS::mvrnorm's moments (vert-cor.R:389-394), normal quantiles of the
-    standardised marginals, independence of the two samples sharing a block, and the radius
-    cut-off sqrt(-2 ln 2^-33) = 6.76 sd."""
+def test_gaussian_dgp_law_ziggurat():
+    """The Gaussian DGP's draw contract (one DGP_A block per sample, two 512-layer ziggurat
+    normals): MASS::mvrnorm's moments (vert-cor.R:389-394), normal quantiles of the standardised
+    marginals, independence of neighbouring samples, and the tail beyond the base layer's
+    r = 3.852 drawn at its normal rate."""
     import sys
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                                     "distributed-correlation_amd"))
@@ -355,9 +355,19 @@ def test_gaussian_dgp_law_two_samples_per_block():
     assert abs(zx.var() - 1) < 5 * math.sqrt(2) * se and abs(zy.var() - 1) < 5 * math.sqrt(2) * se
     assert abs(np.corrcoef(zx, zy)[0, 1] - 0.5) < 5 * 0.75 * se
     assert stats.kstest(zx, "norm").pvalue > 1e-4 and stats.kstest(zy, "norm").pvalue > 1e-4
-    # samples 2b and 2b+1 come from one Philox block: uncorrelated, in both coordinates
+    # neighbouring samples (neighbouring Philox counters) are uncorrelated, in both coordinates
     assert abs(np.corrcoef(zx[0::2], zx[1::2])[0, 1]) < 5 * math.sqrt(2) * se
     assert abs(np.corrcoef(zy[0::2], zx[1::2])[0, 1]) < 5 * math.sqrt(2) * se
-    # radius of the underlying standard pair never exceeds the 32-bit cut-off
-    r = np.hypot(zx, (zy - 0.5 * zx) / math.sqrt(0.75))
-    assert r.max() <= math.sqrt(-2 * math.log(2.0 ** -33)) + 1e-9
+    # whitened pair (zx and the Cholesky residual of zy): independent N(0, 1); tails near and past
+    # the base layer's r occur at 2 (1 - Phi(t)) per coordinate
+    z1 = zx
+    z2 = (zy - 0.5 * zx) / math.sqrt(0.75)
+    assert abs(np.corrcoef(z1, z2)[0, 1]) < 5 * se
+    assert stats.kstest(z2, "norm").pvalue > 1e-4
+    r = 3.852046150368391
+    for z in (z1, z2):
+        # |z| > 3.3: 2 (1 - Phi(3.3)) = 9.67e-4 (strips and wedges near the base); > r: the tail
+        for t in (3.3, r):
+            p = 2 * stats.norm.sf(t)
+            cnt = int(np.sum(np.abs(z) > t))
+            assert abs(cnt - n * p) < 5 * math.sqrt(n * p) + 1, (t, cnt, n * p)
