@@ -454,6 +454,9 @@ __device__ __forceinline__ void sign_pass1_body(const SignConst& c, uint32_t rep
 #ifndef DCOR_P2_WPE
 #define DCOR_P2_WPE 1
 #endif
+#ifndef DCOR_P2_DEPTH
+#define DCOR_P2_DEPTH 2  // batches of slab loads in flight ahead of the current one (m = 8)
+#endif
 template <int DGP>
 __global__ __launch_bounds__(DCOR_BLOCK, DCOR_P1_WPE) void k_sign_pass1(SignConst c,
                                                            uint32_t* __restrict__ scratch,
@@ -534,33 +537,47 @@ __device__ __forceinline__ void sign_pass2_body(const SignConst& c, uint32_t rep
     cy += ny - sgnq(qy, qNy);
     cc += f * (ix * iy - sgnq(qx, qIx) * sgnq(qy, qIy));
   };
-  auto batch_T = [&](int64_t j, int cx, int cy) {
+  // mean of m signs = count / m (exact quotient for the configs' m); a power-of-two m divides by
+  // an exact multiply.  M8: the headline geometry, m = 8 known at compile time.
+  auto batch_T = [&](int64_t j, int cx, int cy, auto m8_tag) {
+    constexpr bool M8 = decltype(m8_tag)::value;
     const U4 w = draw((uint32_t)j, rep, DCOR_SITE_NI_LAP, c.k0, c.k1);   // vert-cor.R:230-231
-    // mean of m signs = count / m (exact quotient for the configs' m); a power-of-two m
-    // divides by an exact multiply
-    const double mx = c.md_pow2 ? (double)cx * c.inv_md : (double)cx / c.md;
-    const double my = c.md_pow2 ? (double)cy * c.inv_md : (double)cy / c.md;
+    double mx, my;
+    if constexpr (M8) {
+      mx = (double)cx * 0.125;
+      my = (double)cy * 0.125;
+    } else {
+      mx = c.md_pow2 ? (double)cx * c.inv_md : (double)cx / c.md;
+      my = c.md_pow2 ? (double)cy * c.inv_md : (double)cy / c.md;
+    }
     const double xt = mx + c.bx * unit_laplace(u53(w.w0, w.w1));
     const double yt = my + c.by * unit_laplace(u53(w.w2, w.w3));
-    const double T = c.md * xt * yt;                                     // vert-cor.R:233
+    const double T = (M8 ? 8.0 : c.md) * xt * yt;                        // vert-cor.R:233
     ks_acc(sT, T);  // compensated (error ~ k 2^-106): the T mean / sd inputs
     ks_acc(sT2, T * T);
   };
   if (c.m == 8) {
-    // headline geometry: one thread = one batch = two 16-B loads; the next batch's loads
-    // are issued before the current batch is decided (two batches in flight per thread).
+    // headline geometry: one thread = one batch = two 16-B loads; the loads of the thread's next
+    // DCOR_P2_DEPTH batches are in flight while the current batch is decided.
     int64_t j = tid;
-    uint4 a0 = make_uint4(0, 0, 0, 0), a1 = a0;
-    if (j < c.k) {
-      a0 = *reinterpret_cast<const uint4*>(slab + 8 * j);
-      a1 = *reinterpret_cast<const uint4*>(slab + 8 * j + 4);
+    uint4 a0[DCOR_P2_DEPTH], a1[DCOR_P2_DEPTH];
+#pragma unroll
+    for (int d = 0; d < DCOR_P2_DEPTH; ++d) {
+      const int64_t jd = j + (int64_t)d * DCOR_BLOCK;
+      a0[d] = a1[d] = make_uint4(0, 0, 0, 0);
+      if (jd < c.k) {
+        a0[d] = *reinterpret_cast<const uint4*>(slab + 8 * jd);
+        a1[d] = *reinterpret_cast<const uint4*>(slab + 8 * jd + 4);
+      }
     }
     for (; j < c.k; j += DCOR_BLOCK) {
-      const int64_t jn = j + DCOR_BLOCK;
-      const U4 w0{a0.x, a0.y, a0.z, a0.w}, w1{a1.x, a1.y, a1.z, a1.w};
+      const int64_t jn = j + (int64_t)DCOR_P2_DEPTH * DCOR_BLOCK;
+      const U4 w0{a0[0].x, a0[0].y, a0[0].z, a0[0].w}, w1{a1[0].x, a1[0].y, a1[0].z, a1[0].w};
+#pragma unroll
+      for (int d = 0; d + 1 < DCOR_P2_DEPTH; ++d) { a0[d] = a0[d + 1]; a1[d] = a1[d + 1]; }
       if (jn < c.k) {
-        a0 = *reinterpret_cast<const uint4*>(slab + 8 * jn);
-        a1 = *reinterpret_cast<const uint4*>(slab + 8 * jn + 4);
+        a0[DCOR_P2_DEPTH - 1] = *reinterpret_cast<const uint4*>(slab + 8 * jn);
+        a1[DCOR_P2_DEPTH - 1] = *reinterpret_cast<const uint4*>(slab + 8 * jn + 4);
       }
       int cx = 0, cy = 0, cc = 0;
       uint32_t tie = 0;
@@ -573,7 +590,7 @@ __device__ __forceinline__ void sign_pass2_body(const SignConst& c, uint32_t rep
           if ((tie >> q) & 1u) fixup(8 * j + q, slab[8 * j + q], cx, cy, cc, bad_ni);
       }
       core += cc;
-      batch_T(j, cx, cy);
+      batch_T(j, cx, cy, std::true_type());
     }
   } else {
     for (int64_t j = tid; j < c.k; j += DCOR_BLOCK) {
@@ -590,7 +607,7 @@ __device__ __forceinline__ void sign_pass2_body(const SignConst& c, uint32_t rep
         }
       }
       core += cc;
-      batch_T(j, cx, cy);
+      batch_T(j, cx, cy, std::false_type());
     }
   }
   for (int64_t i = c.k * c.m + tid; i < c.n; i += DCOR_BLOCK) {  // tail: INT only
