@@ -673,6 +673,190 @@ __global__ __launch_bounds__(DICT_NT, WPE) void k_premat_subg_dict(PrematSubgCon
   }
 }
 
+// Uncoded shared panel, m = 2, k even, n < 65536: the L2-gather kernel's replicate with the
+// NI gathers served from LDS tiles instead of L2 (real-data-sims.R:115-147, 176-252).  Per
+// replicate the workgroup sweeps the panel in tiles of consecutive samples (tile_pairs INT
+// sample pairs each); filling a tile reads the packed clipped panel (k_premat_xy_pack: xyc, soc)
+// from L2, coalesced, and the INT noise from HBM, adds the INT terms of its pairs, and stores
+// the NI clips (clip(X, l1), clip(Y, l2)) to LDS.  Every thread holds the sample indices of its
+// NQ batch pairs in registers (u16) and, per tile, adds the LDS entry of each index that falls in
+// the tile to its batch sums: an index outside the tile reads a -0.0 sentinel, and -0.0 + a = a,
+// a + -0.0 = a, so each batch sum ends as fl(a + b) = fl(b + a) whatever the tiles' order.  A
+// random 16-B L2 gather per NI sample (19,432 per C5 replicate) becomes a share of a coalesced
+// tile fill plus an LDS read.  Batch pairs beyond NQ * NT per thread take further rounds of
+// tiles (NI only).  Threads own INT pairs and NI batch pairs q = tid (mod NT), ascending, as in
+// the L2 kernel; with NT = 512 and NA = 1 the sums are the L2 kernel's bit for bit, otherwise
+// they differ in the compensated low bits only.
+// Measured (C5-continuous, 8192 replicates): 1.10 ms against 1.28 ms for the L2 kernel.  The
+// HBM stream is not what binds: with every load removed the kernel still takes 0.6 ms (fp64
+// compensated sums at one or two workgroups per CU, behind the tile barriers), and each class
+// of loads removed (noise, panel, permutations, gathers) takes off 0.1-0.3 ms.
+// NT threads per workgroup; NQ batch pairs per thread per round; FU fill pairs per loop trip; GB
+// batch pairs gathered per scheduling group; NA accumulator sets; WPE waves per SIMD.
+template <int NT, int NQ, int FU, int GB, int NA, int WPE>
+__global__ __launch_bounds__(NT, WPE) void k_premat_subg_tiled(PrematSubgConst p,
+                                                              const int* __restrict__ dict_ok,
+                                                              int64_t reps, int64_t tile_pairs_,
+                                                              SubgPartial* __restrict__ part) {
+  constexpr int NW = NT / 64;
+  extern __shared__ double dsm[];
+  if (dict_ok != nullptr && *dict_ok != 0) return;  // the coded kernel owns this launch
+  const SubgConst& c = p.s;
+  const uint32_t tid = threadIdx.x;
+  double* red = dsm;
+  double2* tile = reinterpret_cast<double2*>(dsm + 20 * NW);
+  const double2* __restrict__ xy = p.xyc;  // clip(X, l1), clip(Y, l2): the NI values
+  const double2* __restrict__ so = p.soc;  // clip(S, ls), clip(O, lo): the INT values
+  // every index fits 32 bits (n < 65536): VGPR offsets from uniform bases
+  const uint32_t n = (uint32_t)c.n;
+  const uint32_t nbp = (uint32_t)(c.k >> 1);  // batch pairs (k even)
+  const uint32_t tile_pairs = (uint32_t)tile_pairs_;
+  for (int64_t it = blockIdx.x; it < reps; it += gridDim.x) {
+    const int64_t rep = it;
+    const double* __restrict__ ll = p.lap_local + rep * c.n;
+    const iv4* __restrict__ p4 = reinterpret_cast<const iv4*>(p.perm + rep * (c.k * 2));
+    const dv2* __restrict__ x2 = reinterpret_cast<const dv2*>(p.lap_ni_x + rep * c.k);
+    const dv2* __restrict__ y2 = reinterpret_cast<const dv2*>(p.lap_ni_y + rep * c.k);
+    // two independent accumulator sets (the first / second sample of an INT pair, the first /
+    // second batch of a batch pair): twice the fp64 dependency chains in flight per thread at
+    // two waves per SIMD; the sets are merged with dd_add before the wave reduction
+    DD sP[NA] = {}, sT[NA] = {}, sT2[NA] = {}, sU[NA] = {}, sU2[NA] = {};
+    auto merged = [](const DD (&a)[NA]) { return NA == 1 ? a[0] : dd_add(a[0], a[NA - 1]); };
+    auto uterm = [&](double2 v, double l, int w) {  // ver-cor-subG.R:88-90; rds:222-232
+      const double Uc = rclip((v.x + c.bs * l) * v.y, c.lr);
+      ks_acc(sU[w % NA], Uc);
+      ks_acc(sU2[w % NA], Uc * Uc);
+    };
+    // INT sample pairs (h + 2q, h + 2q + 1), as in the L2 kernel; the head sample (h = 1) joins
+    // tile 0, the odd tail sample the last tile.
+    const uint32_t h = (reinterpret_cast<uintptr_t>(ll) & 15) ? 1u : 0u;
+    const uint32_t np = (n - h) >> 1;
+    const dv2* __restrict__ l2 = reinterpret_cast<const dv2*>(ll + h);
+    const uint32_t ntiles = np > 0 ? (np + tile_pairs - 1) / tile_pairs : 1u;
+    double* rb = red + (((it - blockIdx.x) / gridDim.x) & 1) * (10 * NW);
+    auto wave_put = [&](int v, DD a) {
+      a = wave_sum_dd(a);
+      if ((tid & 63) == 0) {
+        rb[(2 * v) * NW + (tid >> 6)] = a.hi;
+        rb[(2 * v + 1) * NW + (tid >> 6)] = a.lo;
+      }
+    };
+    // rounds of NQ * NT batch pairs; the INT terms ride along the first round's fills
+    for (uint32_t qb = 0; qb == 0 || qb < nbp; qb += (uint32_t)NQ * NT) {
+      const bool first = qb == 0;
+      uint32_t sa[NQ], sb[NQ];  // (a | b << 16) of the pair's two batches
+      double ax[NQ][2], ay[NQ][2];
+#pragma unroll
+      for (int u = 0; u < NQ; ++u) {
+        const uint32_t q = qb + tid + (uint32_t)u * NT;
+        sa[u] = sb[u] = 0xFFFFFFFFu;  // 65535 is never a sample index (n < 65536)
+        if (q < nbp) {
+          const iv4 pr = __builtin_nontemporal_load(p4 + q);
+          sa[u] = (uint32_t)pr.x | ((uint32_t)pr.y << 16);
+          sb[u] = (uint32_t)pr.z | ((uint32_t)pr.w << 16);
+        }
+        ax[u][0] = ax[u][1] = ay[u][0] = ay[u][1] = -0.0;
+      }
+      for (uint32_t tp = 0; tp < ntiles; ++tp) {
+        const uint32_t pa = tp * tile_pairs;
+        const uint32_t pb = pa + tile_pairs < np ? pa + tile_pairs : np;
+        const uint32_t lo = tp == 0 ? 0u : h + 2 * pa;
+        const uint32_t hi = tp == ntiles - 1 ? n : h + 2 * pb;
+        const uint32_t tn = hi - lo;
+        __syncthreads();  // the previous tile's readers are done
+        // fill: this thread's INT pairs q = tid (mod NT) in [pa, pb), FU per loop trip
+        uint32_t q = pa + ((tid + NT - pa % NT) % NT);
+        for (; q + (FU - 1) * NT < pb; q += FU * NT) {
+          double2 a0[FU], a1[FU], s0[FU], s1[FU];
+          dv2 lv[FU];
+#pragma unroll
+          for (int u = 0; u < FU; ++u) {
+            const uint32_t i = h + 2 * (q + u * NT);
+            a0[u] = xy[i]; a1[u] = xy[i + 1];
+            if (first) {
+              s0[u] = so[i]; s1[u] = so[i + 1];
+              lv[u] = __builtin_nontemporal_load(l2 + (q + u * NT));
+            }
+          }
+#pragma unroll
+          for (int u = 0; u < FU; ++u) {
+            const uint32_t i = h + 2 * (q + u * NT);
+            tile[i - lo] = a0[u];
+            tile[i + 1 - lo] = a1[u];
+            if (first) {
+              uterm(s0[u], lv[u].x, 0);
+              uterm(s1[u], lv[u].y, 1);
+            }
+          }
+        }
+        for (; q < pb; q += NT) {
+          const uint32_t i = h + 2 * q;
+          tile[i - lo] = xy[i];
+          tile[i + 1 - lo] = xy[i + 1];
+          if (first) {
+            const dv2 l = __builtin_nontemporal_load(l2 + q);
+            uterm(so[i], l.x, 0);
+            uterm(so[i + 1], l.y, 1);
+          }
+        }
+        if (tp == 0 && h && tid == 0) tile[0] = xy[0];
+        if (tp == ntiles - 1 && h + 2 * np < n && tid == NT - 1) tile[n - 1 - lo] = xy[n - 1];
+        if (tid == 0) tile[tn] = make_double2(-0.0, -0.0);  // the out-of-tile sentinel
+        __syncthreads();
+        // gather: every index of this thread's batch pairs against the tile
+#pragma unroll
+        for (int u = 0; u < NQ; ++u) {
+          const uint32_t i0 = sa[u] & 0xFFFFu, i1 = sa[u] >> 16, i2 = sb[u] & 0xFFFFu, i3 = sb[u] >> 16;
+          const double2 t0 = tile[min(i0 - lo, tn)], t1 = tile[min(i1 - lo, tn)];
+          const double2 t2 = tile[min(i2 - lo, tn)], t3 = tile[min(i3 - lo, tn)];
+          ax[u][0] = (ax[u][0] + t0.x) + t1.x;
+          ay[u][0] = (ay[u][0] + t0.y) + t1.y;
+          ax[u][1] = (ax[u][1] + t2.x) + t3.x;
+          ay[u][1] = (ay[u][1] + t2.y) + t3.y;
+          // GB pairs' LDS reads in flight at a time: the scheduler would otherwise hoist all 4 NQ
+          // reads (16 VGPRs each) above the adds
+          if ((u + 1) % GB == 0) __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+      if (first) {
+        if (tid == 0 && h) uterm(so[0], ll[0], 0);
+        if (tid == NT - 1 && h + 2 * np < n) uterm(so[n - 1], ll[n - 1], 1);
+        wave_put(3, merged(sU));
+        wave_put(4, merged(sU2));
+      }
+      // NI terms of this round's batch pairs, ascending q (real-data-sims.R:131-137)
+#pragma unroll
+      for (int u = 0; u < NQ; ++u) {
+        const uint32_t q = qb + tid + (uint32_t)u * NT;
+        if (q < nbp) {
+          const dv2 lx = __builtin_nontemporal_load(x2 + q), ly = __builtin_nontemporal_load(y2 + q);
+#pragma unroll
+          for (int b = 0; b < 2; ++b) {
+            const double xt = ax[u][b] * 0.5 + c.bx * lx[b];
+            const double yt = ay[u][b] * 0.5 + c.by * ly[b];
+            ks_acc(sP[b % NA], xt * yt);
+            const double T = c.md * xt * yt;
+            ks_acc(sT[b % NA], T);
+            ks_acc(sT2[b % NA], T * T);
+          }
+        }
+      }
+    }
+    wave_put(0, merged(sP));
+    wave_put(1, merged(sT));
+    wave_put(2, merged(sT2));
+    __syncthreads();
+    if (tid < 5) {
+      DD a{rb[(2 * tid) * NW], rb[(2 * tid + 1) * NW]};
+#pragma unroll
+      for (int w = 1; w < NW; ++w)
+        a = dd_add(a, DD{rb[(2 * tid) * NW + w], rb[(2 * tid + 1) * NW + w]});
+      part[it].s[2 * tid] = a.hi;
+      part[it].s[2 * tid + 1] = a.lo;
+    }
+  }
+}
+
 // ======================================================== accumulation ===
 // Deterministic per-method summary of `count` records (one workgroup).
 // Stage 1: block b folds records [b*per, min((b+1)*per, count)) of both methods into a
@@ -1466,6 +1650,36 @@ static DictKernel l2_kernel() {
   return ks[v];
 }
 
+// Tiled uncoded-panel kernel variants (threads, batch pairs per thread per round, fill unroll,
+// gather group, accumulator sets, waves per SIMD) and the LDS each workgroup may give its tile.
+// Default: two 512-thread workgroups per CU, four 80-KB tiles and two rounds at C5's n (C5-
+// continuous: 1.10 ms per 8192 replicates vs 1.28 ms for the L2-gather kernel).  Measured and
+// kept for A/B (DCOR_TILED_VARIANT=1..2): one 1024-thread workgroup per CU, two 156-KB tiles,
+// 1.21 ms; one 512-thread workgroup per CU, 1.32-1.38 ms.  DCOR_TILED=0 runs the L2-gather kernel.
+struct TiledKernel {
+  void (*k)(PrematSubgConst, const int*, int64_t, int64_t, SubgPartial*);
+  int nt;
+  size_t lds_budget;
+};
+static TiledKernel tiled_kernel() {
+  static const TiledKernel ks[3] = {{k_premat_subg_tiled<512, 5, 1, 1, 1, 4>, 512, 80 * 1024},
+                                    {k_premat_subg_tiled<1024, 5, 1, 1, 1, 4>, 1024, 160 * 1024},
+                                    {k_premat_subg_tiled<512, 10, 2, 10, 2, 2>, 512, 160 * 1024}};
+  static const int v = [] {
+    const char* e = std::getenv("DCOR_TILED_VARIANT");
+    const int x = e ? std::atoi(e) : 0;
+    return (x >= 0 && x < 3) ? x : 0;
+  }();
+  return ks[v];
+}
+static bool tiled_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("DCOR_TILED");
+    return !(e && std::strcmp(e, "0") == 0);
+  }();
+  return on;
+}
+
 // Workgroup slots of the coded-panel kernel (CUs x resident workgroups at this LDS size).
 static int premat_dict_slots(int64_t n, int* slots) {
   const size_t lds = premat_dict_lds_bytes(n);
@@ -1508,11 +1722,37 @@ int launch_premat_subg(const PrematSubgConst& c0, int64_t reps, void* part, dcor
   }
   if (c.xyc != nullptr) {
     // shared panel, random batches, no dictionary (or the device probe may find none): the
-    // clipped panel packed once, then the persistent kernel gathering it from L2
+    // clipped panel packed once, then for m = 2 with every row 16-B aligned and u16 sample
+    // indices the tiled kernel, otherwise the persistent kernel gathering it from L2.
+    const bool tiled = c.dict_built != 2 && tiled_enabled() && c.s.m == 2 && (c.s.k & 1) == 0 &&
+                       c.s.k >= 2 && c.s.n < 65536 &&
+                       ((reinterpret_cast<uintptr_t>(c.perm) | reinterpret_cast<uintptr_t>(c.lap_ni_x) |
+                         reinterpret_cast<uintptr_t>(c.lap_ni_y)) & 15) == 0;
     hipLaunchKernelGGL(k_premat_xy_pack, dim3((unsigned)((c.s.n + DCOR_BLOCK - 1) / DCOR_BLOCK)),
                        dim3(DCOR_BLOCK), 0, (hipStream_t)stream, c, (double2*)c.xyc,
                        (double2*)c.soc);
-    if (c.dict_built != 2) {
+    if (tiled) {
+      const TiledKernel tk = tiled_kernel();
+      const int64_t np = c.s.n >> 1;  // INT pairs (at most; h = 1 rows have (n - 1) / 2)
+      const size_t red_b = (size_t)(20 * (tk.nt / 64)) * sizeof(double);
+      const int64_t tp_max = (int64_t)((tk.lds_budget - red_b) / 16 - 3) / 2;
+      const int64_t ntiles = np > 0 ? (np + tp_max - 1) / tp_max : 1;
+      const int64_t tile_pairs = np > 0 ? (np + ntiles - 1) / ntiles : 1;
+      const size_t lds = red_b + (size_t)(2 * tile_pairs + 3) * 16;
+      if (hipFuncSetAttribute((const void*)tk.k, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024) != hipSuccess)
+        return last_err();
+      int dev = 0, cus = 0, per_cu = 0;
+      if (hipGetDevice(&dev) != hipSuccess) return last_err();
+      if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        return last_err();
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, tk.k, tk.nt, lds) != hipSuccess)
+        return last_err();
+      const int64_t slots = (int64_t)cus * (per_cu < 1 ? 1 : per_cu);
+      const int64_t grid = reps < slots ? reps : slots;
+      hipLaunchKernelGGL(tk.k, dim3((unsigned)grid), dim3((unsigned)tk.nt), lds, (hipStream_t)stream, c,
+                         (const int*)c.dict_ok, reps, tile_pairs, (SubgPartial*)part);
+    } else if (c.dict_built != 2) {
       const DictKernel kl = l2_kernel();
       const size_t lds = (size_t)(20 * DICT_NW) * sizeof(double);
       int dev = 0, cus = 0, per_cu = 0;

@@ -286,3 +286,48 @@ def test_hrs_fused_large_uncoded_panel_materialises():
     fu = hrs.hrs_replicates(*args, rep_begin=2, mode="fused")
     pm = hrs.hrs_replicates(*args, rep_begin=2)
     np.testing.assert_array_equal(fu.view(np.int64), pm.view(np.int64))
+
+
+_TILED_CASES = ((1001, 2.0, 5, 3), (19433, 2.0, 5, 17), (30001, 2.0, 3, 0), (19433, 0.5, 2, 0))
+
+
+def _premat_continuous_runs():
+    from dcor import hrs
+    out = {}
+    for n, eps, reps, rb in _TILED_CASES:
+        z = _continuous(n, seed=n)
+        out[f"{n}_{eps}"] = hrs.hrs_replicates(z["age_z"], z["bmi_z"], z["lambda_age_z"], z["lambda_bmi_z"], eps,
+                                               reps, seed_ni=31, seed_int=32, rep_begin=rb)
+    return out
+
+
+def test_premat_tiled_kernel_matches_l2_kernel():
+    """Continuous panels, m = 2 (and one m > 2 case): the tiled LDS kernel (default) agrees with
+    the L2-gather kernel (DCOR_TILED=0) within the estimator tolerance, and every tiled variant
+    returns the default's bits.  n = 1001 is one tile, 19,433 four (variant 0) or two; 30,001
+    takes two rounds of batch pairs in every variant, 19,433 in variant 0; odd n puts every other replicate's noise row off a
+    16-B boundary (the head-sample path).  The estimators against the oracle on this path:
+    test_gpu_more.py::test_premat_subg_hrs_shared_panel."""
+    import os
+    import subprocess
+    import sys
+    import tempfile
+    got = _premat_continuous_runs()
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    paths = [root, os.path.join(root, "distributed-correlation_amd"), os.path.join(root, "tests")]
+    code = ("import sys, numpy as np; sys.path[:0] = %r; import test_gpu_hrs as t; "
+            "np.savez(sys.argv[1], **t._premat_continuous_runs())") % (paths,)
+    for env_over in ({"DCOR_TILED": "0"}, *({"DCOR_TILED_VARIANT": str(v)} for v in range(1, 3))):
+        with tempfile.TemporaryDirectory() as d:
+            env = dict(os.environ, **env_over)
+            subprocess.run([sys.executable, "-c", code, os.path.join(d, "o.npz")], check=True, env=env,
+                           timeout=120)
+            ref = np.load(os.path.join(d, "o.npz"))
+            for key, v in got.items():
+                assert np.isfinite(v).all()
+                if "DCOR_TILED" in env_over and not key.endswith("_0.5"):
+                    for r in range(len(v)):
+                        assert_close(v[r], ref[key][r], what=f"{key} rep {r} tiled vs L2")
+                else:
+                    np.testing.assert_array_equal(v.view(np.int64), ref[key].view(np.int64),
+                                                  err_msg=f"{key} vs {env_over}")
