@@ -685,15 +685,16 @@ __global__ __launch_bounds__(DICT_NT, WPE) void k_premat_subg_dict(PrematSubgCon
 // random 16-B L2 gather per NI sample (19,432 per C5 replicate) becomes a share of a coalesced
 // tile fill plus an LDS read.  Batch pairs beyond NQ * NT per thread take further rounds of
 // tiles (NI only).  Threads own INT pairs and NI batch pairs q = tid (mod NT), ascending, as in
-// the L2 kernel; with NT = 512 and NA = 1 the sums are the L2 kernel's bit for bit, otherwise
-// they differ in the compensated low bits only.
-// Measured (C5-continuous, 8192 replicates): 1.10 ms against 1.28 ms for the L2 kernel.  The
+// the L2 kernel; with NT = 512, NA = 1 and per-term sums (PG false) the sums are the L2 kernel's
+// bit for bit.  PG adds the two terms of an INT pair (of a batch pair) plainly and compensates the
+// pair sums: half the TwoSum chains, sums that differ in the low bits only.
+// Measured (C5-continuous, 8192 replicates): 1.08 ms against 1.28 ms for the L2 kernel.  The
 // HBM stream is not what binds: with every load removed the kernel still takes 0.6 ms (fp64
 // compensated sums at one or two workgroups per CU, behind the tile barriers), and each class
 // of loads removed (noise, panel, permutations, gathers) takes off 0.1-0.3 ms.
 // NT threads per workgroup; NQ batch pairs per thread per round; FU fill pairs per loop trip; GB
 // batch pairs gathered per scheduling group; NA accumulator sets; WPE waves per SIMD.
-template <int NT, int NQ, int FU, int GB, int NA, int WPE>
+template <int NT, int NQ, int FU, int GB, int NA, int WPE, bool PG = false>
 __global__ __launch_bounds__(NT, WPE) void k_premat_subg_tiled(PrematSubgConst p,
                                                               const int* __restrict__ dict_ok,
                                                               int64_t reps, int64_t tile_pairs_,
@@ -726,6 +727,13 @@ __global__ __launch_bounds__(NT, WPE) void k_premat_subg_tiled(PrematSubgConst p
       const double Uc = rclip((v.x + c.bs * l) * v.y, c.lr);
       ks_acc(sU[w % NA], Uc);
       ks_acc(sU2[w % NA], Uc * Uc);
+    };
+    // PG: an INT pair's two terms added plainly, the pair sum compensated
+    auto uterm2 = [&](double2 v0, double l0, double2 v1, double l1) {
+      const double U0 = rclip((v0.x + c.bs * l0) * v0.y, c.lr);
+      const double U1 = rclip((v1.x + c.bs * l1) * v1.y, c.lr);
+      ks_acc(sU[0], U0 + U1);
+      ks_acc(sU2[0], U0 * U0 + U1 * U1);
     };
     // INT sample pairs (h + 2q, h + 2q + 1), as in the L2 kernel; the head sample (h = 1) joins
     // tile 0, the odd tail sample the last tile.
@@ -784,8 +792,12 @@ __global__ __launch_bounds__(NT, WPE) void k_premat_subg_tiled(PrematSubgConst p
             tile[i - lo] = a0[u];
             tile[i + 1 - lo] = a1[u];
             if (first) {
-              uterm(s0[u], lv[u].x, 0);
-              uterm(s1[u], lv[u].y, 1);
+              if (PG) {
+                uterm2(s0[u], lv[u].x, s1[u], lv[u].y);
+              } else {
+                uterm(s0[u], lv[u].x, 0);
+                uterm(s1[u], lv[u].y, 1);
+              }
             }
           }
         }
@@ -795,8 +807,12 @@ __global__ __launch_bounds__(NT, WPE) void k_premat_subg_tiled(PrematSubgConst p
           tile[i + 1 - lo] = xy[i + 1];
           if (first) {
             const dv2 l = __builtin_nontemporal_load(l2 + q);
-            uterm(so[i], l.x, 0);
-            uterm(so[i + 1], l.y, 1);
+            if (PG) {
+              uterm2(so[i], l.x, so[i + 1], l.y);
+            } else {
+              uterm(so[i], l.x, 0);
+              uterm(so[i + 1], l.y, 1);
+            }
           }
         }
         if (tp == 0 && h && tid == 0) tile[0] = xy[0];
@@ -830,14 +846,23 @@ __global__ __launch_bounds__(NT, WPE) void k_premat_subg_tiled(PrematSubgConst p
         const uint32_t q = qb + tid + (uint32_t)u * NT;
         if (q < nbp) {
           const dv2 lx = __builtin_nontemporal_load(x2 + q), ly = __builtin_nontemporal_load(y2 + q);
+          if (PG) {  // the pair's two batch terms added plainly, the pair sums compensated
+            const double xt0 = ax[u][0] * 0.5 + c.bx * lx[0], yt0 = ay[u][0] * 0.5 + c.by * ly[0];
+            const double xt1 = ax[u][1] * 0.5 + c.bx * lx[1], yt1 = ay[u][1] * 0.5 + c.by * ly[1];
+            const double T0 = c.md * xt0 * yt0, T1 = c.md * xt1 * yt1;
+            ks_acc(sP[0], xt0 * yt0 + xt1 * yt1);
+            ks_acc(sT[0], T0 + T1);
+            ks_acc(sT2[0], T0 * T0 + T1 * T1);
+          } else {
 #pragma unroll
-          for (int b = 0; b < 2; ++b) {
-            const double xt = ax[u][b] * 0.5 + c.bx * lx[b];
-            const double yt = ay[u][b] * 0.5 + c.by * ly[b];
-            ks_acc(sP[b % NA], xt * yt);
-            const double T = c.md * xt * yt;
-            ks_acc(sT[b % NA], T);
-            ks_acc(sT2[b % NA], T * T);
+            for (int b = 0; b < 2; ++b) {
+              const double xt = ax[u][b] * 0.5 + c.bx * lx[b];
+              const double yt = ay[u][b] * 0.5 + c.by * ly[b];
+              ks_acc(sP[b % NA], xt * yt);
+              const double T = c.md * xt * yt;
+              ks_acc(sT[b % NA], T);
+              ks_acc(sT2[b % NA], T * T);
+            }
           }
         }
       }
@@ -1651,20 +1676,21 @@ static DictKernel l2_kernel() {
 }
 
 // Tiled uncoded-panel kernel variants (threads, batch pairs per thread per round, fill unroll,
-// gather group, accumulator sets, waves per SIMD) and the LDS each workgroup may give its tile.
-// Default: two 512-thread workgroups per CU, four 80-KB tiles and two rounds at C5's n (C5-
-// continuous: 1.10 ms per 8192 replicates vs 1.28 ms for the L2-gather kernel).  Measured and
-// kept for A/B (DCOR_TILED_VARIANT=1..2): one 1024-thread workgroup per CU, two 156-KB tiles,
-// 1.21 ms; one 512-thread workgroup per CU, 1.32-1.38 ms.  DCOR_TILED=0 runs the L2-gather kernel.
+// gather group, accumulator sets, waves per SIMD, pair-grouped sums) and the LDS each workgroup
+// may give its tile.  Default: two 512-thread workgroups per CU, four 80-KB tiles and two rounds
+// at C5's n, pair-grouped sums (C5-continuous: 1.08 ms per 8192 replicates against 1.28 ms for
+// the L2-gather kernel; 1.15 ms with per-term sums).  For A/B (DCOR_TILED_VARIANT): 1, one
+// 1024-thread workgroup per CU with two 156-KB tiles (1.21 ms per-term); 2, the default with
+// per-term sums, which returns the L2-gather kernel's bits.  DCOR_TILED=0 runs the L2 kernel.
 struct TiledKernel {
   void (*k)(PrematSubgConst, const int*, int64_t, int64_t, SubgPartial*);
   int nt;
   size_t lds_budget;
 };
 static TiledKernel tiled_kernel() {
-  static const TiledKernel ks[3] = {{k_premat_subg_tiled<512, 5, 1, 1, 1, 4>, 512, 80 * 1024},
-                                    {k_premat_subg_tiled<1024, 5, 1, 1, 1, 4>, 1024, 160 * 1024},
-                                    {k_premat_subg_tiled<512, 10, 2, 10, 2, 2>, 512, 160 * 1024}};
+  static const TiledKernel ks[3] = {{k_premat_subg_tiled<512, 5, 1, 1, 1, 4, true>, 512, 80 * 1024},
+                                    {k_premat_subg_tiled<1024, 5, 1, 1, 1, 4, true>, 1024, 160 * 1024},
+                                    {k_premat_subg_tiled<512, 5, 1, 1, 1, 4, false>, 512, 80 * 1024}};
   static const int v = [] {
     const char* e = std::getenv("DCOR_TILED_VARIANT");
     const int x = e ? std::atoi(e) : 0;
