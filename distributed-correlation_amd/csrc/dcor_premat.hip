@@ -1303,10 +1303,18 @@ __global__ __launch_bounds__(DICT_NT, WPE) void k_hrs_fused(PrematSubgConst p, H
   for (int64_t it = blockIdx.x; it < reps; it += gridDim.x) {
     const uint32_t rep = hk.rep_begin + (uint32_t)it;
     DD sP{0, 0}, sT{0, 0}, sT2{0, 0}, sU{0, 0}, sU2{0, 0};
-    auto uterm = [&](uint32_t cd, double l) {  // real-data-sims.R:222-232
-      const double Uc = rclip((dS[cd & 255u] + c.bs * l) * dO[cd >> 8], c.lr);
+    auto uval = [&](uint32_t cd, double l) {  // real-data-sims.R:222-232
+      return rclip((dS[cd & 255u] + c.bs * l) * dO[cd >> 8], c.lr);
+    };
+    auto uterm = [&](double Uc) {
       ks_acc(sU, Uc);
       ks_acc(sU2, Uc * Uc);
+    };
+    // a pair of INT terms (of NI batches) is added plainly and the pair sum compensated: half
+    // the TwoSum chains of per-term sums
+    auto uterm2 = [&](double U0, double U1) {
+      ks_acc(sU, U0 + U1);
+      ks_acc(sU2, U0 * U0 + U1 * U1);
     };
     // Phase A: the panel codes at the permuted batch slots, gs[t] = code[P(t)], t < k m, into
     // this workgroup's scratch row (L2-resident, reused by every replicate of the workgroup).
@@ -1330,12 +1338,12 @@ __global__ __launch_bounds__(DICT_NT, WPE) void k_hrs_fused(PrematSubgConst p, H
       const int64_t nb = c.n >> 1;
       for (int64_t b = tid; b < nb; b += DICT_NT) {
         const U4 w = draw((uint32_t)b, rep, HRS_SITE_LOCAL, hk.in0, hk.in1);
-        uterm(cod[2 * b], unit_laplace(u53(w.w0, w.w1)));
-        uterm(cod[2 * b + 1], unit_laplace(u53(w.w2, w.w3)));
+        uterm2(uval(cod[2 * b], unit_laplace(u53(w.w0, w.w1))),
+               uval(cod[2 * b + 1], unit_laplace(u53(w.w2, w.w3))));
       }
       if ((c.n & 1) && tid == DICT_NT - 1) {
         const U4 w = draw((uint32_t)nb, rep, HRS_SITE_LOCAL, hk.in0, hk.in1);
-        uterm(cod[c.n - 1], unit_laplace(u53(w.w0, w.w1)));
+        uterm(uval(cod[c.n - 1], unit_laplace(u53(w.w0, w.w1))));
       }
     }
     double* rb = red + (((it - blockIdx.x) / gridDim.x) & 1) * (10 * DICT_NW);
@@ -1355,19 +1363,33 @@ __global__ __launch_bounds__(DICT_NT, WPE) void k_hrs_fused(PrematSubgConst p, H
       ks_acc(sT, T);
       ks_acc(sT2, T * T);
     };
+    auto nterm2 = [&](double xt0, double yt0, double xt1, double yt1) {
+      const double T0 = c.md * xt0 * yt0, T1 = c.md * xt1 * yt1;
+      ks_acc(sP, xt0 * yt0 + xt1 * yt1);
+      ks_acc(sT, T0 + T1);
+      ks_acc(sT2, T0 * T0 + T1 * T1);
+    };
     if (c.m == 2) {  // batches 2q, 2q+1 share one Philox block of X noise and one of Y noise
       const uint32_t* __restrict__ g2 = reinterpret_cast<const uint32_t*>(gs);  // batch j's codes
-      auto pair = [&](uint32_t ab, double lxj, double lyj) {
-        const uint32_t a = ab & 0xFFFFu, b = ab >> 16;
-        nterm((dX[a & 255u] + dX[b & 255u]) * 0.5 + c.bx * lxj,
-              (dY[a >> 8] + dY[b >> 8]) * 0.5 + c.by * lyj);
+      auto xt_of = [&](uint32_t ab, double lxj) {
+        return (dX[(ab & 0xFFFFu) & 255u] + dX[(ab >> 16) & 255u]) * 0.5 + c.bx * lxj;
+      };
+      auto yt_of = [&](uint32_t ab, double lyj) {
+        return (dY[(ab & 0xFFFFu) >> 8] + dY[(ab >> 16) >> 8]) * 0.5 + c.by * lyj;
       };
       for (int64_t q = tid; 2 * q < c.k; q += DICT_NT) {
         const U4 wx = draw((uint32_t)q, rep, HRS_SITE_NI_X, hk.ni0, hk.ni1);
         const U4 wy = draw((uint32_t)q, rep, HRS_SITE_NI_Y, hk.ni0, hk.ni1);
-        pair(g2[2 * q], unit_laplace(u53(wx.w0, wx.w1)), unit_laplace(u53(wy.w0, wy.w1)));
-        if (2 * q + 1 < c.k)
-          pair(g2[2 * q + 1], unit_laplace(u53(wx.w2, wx.w3)), unit_laplace(u53(wy.w2, wy.w3)));
+        const uint32_t ab0 = g2[2 * q];
+        const double xt0 = xt_of(ab0, unit_laplace(u53(wx.w0, wx.w1)));
+        const double yt0 = yt_of(ab0, unit_laplace(u53(wy.w0, wy.w1)));
+        if (2 * q + 1 < c.k) {
+          const uint32_t ab1 = g2[2 * q + 1];
+          nterm2(xt0, yt0, xt_of(ab1, unit_laplace(u53(wx.w2, wx.w3))),
+                 yt_of(ab1, unit_laplace(u53(wy.w2, wy.w3))));
+        } else {
+          nterm(xt0, yt0);
+        }
       }
     } else {
       for (int64_t j = tid; j < c.k; j += DICT_NT) {
@@ -1422,10 +1444,16 @@ __global__ __launch_bounds__(DICT_NT, WPE) void k_hrs_fused_l2(PrematSubgConst p
   for (int64_t it = blockIdx.x; it < reps; it += gridDim.x) {
     const uint32_t rep = hk.rep_begin + (uint32_t)it;
     DD sP{0, 0}, sT{0, 0}, sT2{0, 0}, sU{0, 0}, sU2{0, 0};
-    auto uterm = [&](double2 v, double l) {  // real-data-sims.R:222-232
-      const double Uc = rclip((v.x + c.bs * l) * v.y, c.lr);
+    auto uval = [&](double2 v, double l) {  // real-data-sims.R:222-232
+      return rclip((v.x + c.bs * l) * v.y, c.lr);
+    };
+    auto uterm = [&](double Uc) {
       ks_acc(sU, Uc);
       ks_acc(sU2, Uc * Uc);
+    };
+    auto uterm2 = [&](double U0, double U1) {  // as k_hrs_fused: pair sums compensated
+      ks_acc(sU, U0 + U1);
+      ks_acc(sU2, U0 * U0 + U1 * U1);
     };
     // Phase A: gs[t] = P(t), t < k m (sample.int(n, k*m) - 1, real-data-sims.R:131); the
     // previous item's readers are past the barrier that ends its reduction.
@@ -1447,12 +1475,11 @@ __global__ __launch_bounds__(DICT_NT, WPE) void k_hrs_fused_l2(PrematSubgConst p
       for (int64_t b = tid; b < nb; b += DICT_NT) {
         const U4 w = draw((uint32_t)b, rep, HRS_SITE_LOCAL, hk.in0, hk.in1);
         const double2 v0 = so[2 * b], v1 = so[2 * b + 1];
-        uterm(v0, unit_laplace(u53(w.w0, w.w1)));
-        uterm(v1, unit_laplace(u53(w.w2, w.w3)));
+        uterm2(uval(v0, unit_laplace(u53(w.w0, w.w1))), uval(v1, unit_laplace(u53(w.w2, w.w3))));
       }
       if ((c.n & 1) && tid == DICT_NT - 1) {
         const U4 w = draw((uint32_t)nb, rep, HRS_SITE_LOCAL, hk.in0, hk.in1);
-        uterm(so[c.n - 1], unit_laplace(u53(w.w0, w.w1)));
+        uterm(uval(so[c.n - 1], unit_laplace(u53(w.w0, w.w1))));
       }
     }
     double* rb = red + (((it - blockIdx.x) / gridDim.x) & 1) * (10 * DICT_NW);
@@ -1472,20 +1499,29 @@ __global__ __launch_bounds__(DICT_NT, WPE) void k_hrs_fused_l2(PrematSubgConst p
       ks_acc(sT, T);
       ks_acc(sT2, T * T);
     };
+    auto nterm2 = [&](double xt0, double yt0, double xt1, double yt1) {
+      const double T0 = c.md * xt0 * yt0, T1 = c.md * xt1 * yt1;
+      ks_acc(sP, xt0 * yt0 + xt1 * yt1);
+      ks_acc(sT, T0 + T1);
+      ks_acc(sT2, T0 * T0 + T1 * T1);
+    };
     if (c.m == 2) {
       const uint32_t* __restrict__ g2 = reinterpret_cast<const uint32_t*>(gs);
-      auto pair = [&](uint32_t ab, double lxj, double lyj) {
-        const double2 a = xy[ab & 0xFFFFu], b = xy[ab >> 16];
-        nterm((a.x + b.x) * 0.5 + c.bx * lxj, (a.y + b.y) * 0.5 + c.by * lyj);
-      };
       for (int64_t q = tid; 2 * q < c.k; q += DICT_NT) {
         const uint32_t ab0 = g2[2 * q];
         const uint32_t ab1 = 2 * q + 1 < c.k ? g2[2 * q + 1] : 0u;
         const U4 wx = draw((uint32_t)q, rep, HRS_SITE_NI_X, hk.ni0, hk.ni1);
         const U4 wy = draw((uint32_t)q, rep, HRS_SITE_NI_Y, hk.ni0, hk.ni1);
-        pair(ab0, unit_laplace(u53(wx.w0, wx.w1)), unit_laplace(u53(wy.w0, wy.w1)));
-        if (2 * q + 1 < c.k)
-          pair(ab1, unit_laplace(u53(wx.w2, wx.w3)), unit_laplace(u53(wy.w2, wy.w3)));
+        const double2 a0 = xy[ab0 & 0xFFFFu], b0 = xy[ab0 >> 16];
+        const double xt0 = (a0.x + b0.x) * 0.5 + c.bx * unit_laplace(u53(wx.w0, wx.w1));
+        const double yt0 = (a0.y + b0.y) * 0.5 + c.by * unit_laplace(u53(wy.w0, wy.w1));
+        if (2 * q + 1 < c.k) {
+          const double2 a1 = xy[ab1 & 0xFFFFu], b1 = xy[ab1 >> 16];
+          nterm2(xt0, yt0, (a1.x + b1.x) * 0.5 + c.bx * unit_laplace(u53(wx.w2, wx.w3)),
+                 (a1.y + b1.y) * 0.5 + c.by * unit_laplace(u53(wy.w2, wy.w3)));
+        } else {
+          nterm(xt0, yt0);
+        }
       }
     } else {
       for (int64_t j = tid; j < c.k; j += DICT_NT) {
