@@ -541,7 +541,7 @@ __global__ __launch_bounds__(DICT_NT, WPE) void k_premat_subg_dict(PrematSubgCon
     const double* __restrict__ ll = p.lap_local + rep * c.n;
     const int32_t* __restrict__ pm = p.perm + rep * (c.k * c.m);
     DD sP{0, 0}, sT{0, 0}, sT2{0, 0}, sU{0, 0}, sU2{0, 0};
-    auto uterm = [&](int64_t i, double l) {  // ver-cor-subG.R:88-90; real-data-sims.R:222-232
+    auto uval = [&](int64_t i, double l) {  // ver-cor-subG.R:88-90; real-data-sims.R:222-232
       double sv, ov;
       if constexpr (L2) {
         const double2 v = sop[i];
@@ -550,9 +550,19 @@ __global__ __launch_bounds__(DICT_NT, WPE) void k_premat_subg_dict(PrematSubgCon
         const uint32_t cd = cod[i];
         sv = dS[cd & 255u]; ov = dO[cd >> 8];
       }
-      const double Uc = rclip((sv + c.bs * l) * ov, c.lr);
+      return rclip((sv + c.bs * l) * ov, c.lr);
+    };
+    auto uterm = [&](int64_t i, double l) {
+      const double Uc = uval(i, l);
       ks_acc(sU, Uc);
       ks_acc(sU2, Uc * Uc);
+    };
+    // an INT sample pair's two terms (a batch pair's) added plainly, the pair sum compensated:
+    // half the TwoSum chains of per-term sums
+    auto uterm2 = [&](int64_t i, double l0, double l1) {
+      const double U0 = uval(i, l0), U1 = uval(i + 1, l1);
+      ks_acc(sU, U0 + U1);
+      ks_acc(sU2, U0 * U0 + U1 * U1);
     };
     // INT stream: sample pairs (h + 2q, h + 2q + 1); h = 1 when the replicate's noise row
     // starts off a 16-B boundary (odd n).  Slice 0 takes the head sample, slice S-1 the tail.
@@ -567,17 +577,11 @@ __global__ __launch_bounds__(DICT_NT, WPE) void k_premat_subg_dict(PrematSubgCon
 #pragma unroll
         for (int u = 0; u < DUNR; ++u) v[u] = __builtin_nontemporal_load(l2 + q + u * DICT_NT);
 #pragma unroll
-        for (int u = 0; u < DUNR; ++u) {
-          const int64_t i = h + 2 * (q + u * DICT_NT);
-          uterm(i, v[u].x);
-          uterm(i + 1, v[u].y);
-        }
+        for (int u = 0; u < DUNR; ++u) uterm2(h + 2 * (q + u * DICT_NT), v[u].x, v[u].y);
       }
       for (; q < q1; q += DICT_NT) {
         const dv2 v = __builtin_nontemporal_load(l2 + q);
-        const int64_t i = h + 2 * q;
-        uterm(i, v.x);
-        uterm(i + 1, v.y);
+        uterm2(h + 2 * q, v.x, v.y);
       }
       if (tid == 0 && t == 0 && h) uterm(0, ll[0]);
       if (tid == DICT_NT - 1 && t == S - 1 && h + 2 * np < c.n) uterm(c.n - 1, ll[c.n - 1]);
@@ -605,6 +609,16 @@ __global__ __launch_bounds__(DICT_NT, WPE) void k_premat_subg_dict(PrematSubgCon
         ks_acc(sT, T);
         ks_acc(sT2, T * T);
       };
+      // batches j, j + 1 (indices iv4, noise x2 / y2): the pair's terms added plainly
+      auto pair2 = [&](iv4 pr, dv2 lx2, dv2 ly2) {
+        const double2 a0 = ni_xy(pr.x), b0 = ni_xy(pr.y), a1 = ni_xy(pr.z), b1 = ni_xy(pr.w);
+        const double xt0 = (a0.x + b0.x) * 0.5 + c.bx * lx2.x, yt0 = (a0.y + b0.y) * 0.5 + c.by * ly2.x;
+        const double xt1 = (a1.x + b1.x) * 0.5 + c.bx * lx2.y, yt1 = (a1.y + b1.y) * 0.5 + c.by * ly2.y;
+        const double T0 = c.md * xt0 * yt0, T1 = c.md * xt1 * yt1;
+        ks_acc(sP, xt0 * yt0 + xt1 * yt1);
+        ks_acc(sT, T0 + T1);
+        ks_acc(sT2, T0 * T0 + T1 * T1);
+      };
       const bool al = ((reinterpret_cast<uintptr_t>(pm) | reinterpret_cast<uintptr_t>(lx) |
                         reinterpret_cast<uintptr_t>(ly)) & 15) == 0;
       if (al) {  // two batches per lane: int4 of indices, double2 of each noise row
@@ -624,16 +638,12 @@ __global__ __launch_bounds__(DICT_NT, WPE) void k_premat_subg_dict(PrematSubgCon
             ay[u] = __builtin_nontemporal_load(y2 + q + u * DICT_NT);
           }
 #pragma unroll
-          for (int u = 0; u < DUNR / 2; ++u) {
-            pair(pr[u].x, pr[u].y, ax[u].x, ay[u].x);
-            pair(pr[u].z, pr[u].w, ax[u].y, ay[u].y);
-          }
+          for (int u = 0; u < DUNR / 2; ++u) pair2(pr[u], ax[u], ay[u]);
         }
         for (; q < q1; q += DICT_NT) {
           const iv4 pr = __builtin_nontemporal_load(p4 + q);
           const dv2 ax = __builtin_nontemporal_load(x2 + q), ay = __builtin_nontemporal_load(y2 + q);
-          pair(pr.x, pr.y, ax.x, ay.x);
-          pair(pr.z, pr.w, ax.y, ay.y);
+          pair2(pr, ax, ay);
         }
         if (tid == DICT_NT - 1 && t == S - 1 && (c.k & 1))
           pair(pm[2 * (c.k - 1)], pm[2 * (c.k - 1) + 1], lx[c.k - 1], ly[c.k - 1]);
@@ -685,9 +695,8 @@ __global__ __launch_bounds__(DICT_NT, WPE) void k_premat_subg_dict(PrematSubgCon
 // random 16-B L2 gather per NI sample (19,432 per C5 replicate) becomes a share of a coalesced
 // tile fill plus an LDS read.  Batch pairs beyond NQ * NT per thread take further rounds of
 // tiles (NI only).  Threads own INT pairs and NI batch pairs q = tid (mod NT), ascending, as in
-// the L2 kernel; with NT = 512, NA = 1 and per-term sums (PG false) the sums are the L2 kernel's
-// bit for bit.  PG adds the two terms of an INT pair (of a batch pair) plainly and compensates the
-// pair sums: half the TwoSum chains, sums that differ in the low bits only.
+// the L2 kernel; PG adds the two terms of an INT pair (of a batch pair) plainly and compensates
+// the pair sums, as the L2 kernel does, so with NT = 512 and NA = 1 the sums are its bit for bit.
 // Measured (C5-continuous, 8192 replicates): 1.08 ms against 1.28 ms for the L2 kernel.  The
 // HBM stream is not what binds: with every load removed the kernel still takes 0.6 ms (fp64
 // compensated sums at one or two workgroups per CU, behind the tile barriers), and each class
@@ -1714,23 +1723,22 @@ static DictKernel l2_kernel() {
 // Tiled uncoded-panel kernel variants (threads, batch pairs per thread per round, fill unroll,
 // gather group, accumulator sets, waves per SIMD, pair-grouped sums) and the LDS each workgroup
 // may give its tile.  Default: two 512-thread workgroups per CU, four 80-KB tiles and two rounds
-// at C5's n, pair-grouped sums (C5-continuous: 1.08 ms per 8192 replicates against 1.28 ms for
-// the L2-gather kernel; 1.15 ms with per-term sums).  For A/B (DCOR_TILED_VARIANT): 1, one
-// 1024-thread workgroup per CU with two 156-KB tiles (1.21 ms per-term); 2, the default with
-// per-term sums, which returns the L2-gather kernel's bits.  DCOR_TILED=0 runs the L2 kernel.
+// at C5's n (C5-continuous: 1.08 ms per 8192 replicates against 1.28 ms for the L2-gather
+// kernel; 1.15 ms with per-term sums); its sums are the L2-gather kernel's bit for bit.  For A/B
+// (DCOR_TILED_VARIANT=1): one 1024-thread workgroup per CU with two 156-KB tiles (1.11 ms).
+// DCOR_TILED=0 runs the L2-gather kernel.
 struct TiledKernel {
   void (*k)(PrematSubgConst, const int*, int64_t, int64_t, SubgPartial*);
   int nt;
   size_t lds_budget;
 };
 static TiledKernel tiled_kernel() {
-  static const TiledKernel ks[3] = {{k_premat_subg_tiled<512, 5, 1, 1, 1, 4, true>, 512, 80 * 1024},
-                                    {k_premat_subg_tiled<1024, 5, 1, 1, 1, 4, true>, 1024, 160 * 1024},
-                                    {k_premat_subg_tiled<512, 5, 1, 1, 1, 4, false>, 512, 80 * 1024}};
+  static const TiledKernel ks[2] = {{k_premat_subg_tiled<512, 5, 1, 1, 1, 4, true>, 512, 80 * 1024},
+                                    {k_premat_subg_tiled<1024, 5, 1, 1, 1, 4, true>, 1024, 160 * 1024}};
   static const int v = [] {
     const char* e = std::getenv("DCOR_TILED_VARIANT");
     const int x = e ? std::atoi(e) : 0;
-    return (x >= 0 && x < 3) ? x : 0;
+    return (x >= 0 && x < 2) ? x : 0;
   }();
   return ks[v];
 }

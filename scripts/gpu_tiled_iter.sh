@@ -11,5 +11,5 @@ run() {  # name, env...
   env "$@" timeout -k 10 300 python -u bench_configs.py --only C5c > $O/$N.jsonl 2> $O/$N.err || return $?
   python3 -c "import json; d=json.loads(open('$O/$N.jsonl').read().splitlines()[-1]); print('$N', round(d['seconds']*1e6), 'us', round(d['hbm_frac'], 3))"
 }
-for V in 0 1 2; do run v$V DCOR_TILED_VARIANT=$V || exit $?; done
+for V in 0 1; do run v$V DCOR_TILED_VARIANT=$V || exit $?; done
 run l2 DCOR_TILED=0 || exit $?
