@@ -215,9 +215,10 @@ __device__ __forceinline__ void mvn_polar(double r, double s, double c, double m
 
 // ------------------------------------------------------------- R helpers
 __device__ __forceinline__ double rclip(double x, double L) {  // pmax(pmin(x, L), -L)
-  if (x != x) return x;
-  const double t = (x < L) ? x : L;
-  return (t > -L) ? t : -L;
+  // v_min_f64 + v_max_f64 (which return the non-NaN operand), then R's NaN passed through:
+  // the same value for every x as the compare-and-select form, in 5 VALU instead of 9
+  const double t = fmax(fmin(x, L), -L);
+  return (x != x) ? x : t;
 }
 // Same clip for inputs known not to be NaN (generated samples): one v_min + one v_max.
 __device__ __forceinline__ double rclip_fin(double x, double L) { return fmax(fmin(x, L), -L); }
