@@ -134,7 +134,7 @@ def _hrs_panel(kind, n, g):
                                         ("coded", 19433, 0.5), ("coded", 1001, 2.0),
                                         ("coded", 1002, 2.0), ("coded", 1003, 2.0),
                                         ("d256", 5000, 2.0), ("d257", 5000, 2.0),
-                                        ("continuous", 3000, 0.5)])
+                                        ("continuous", 3000, 0.5), ("continuous", 4999, 2.0)])
 def test_premat_subg_hrs_shared_panel(dc, orc, kind, n, eps):
     """HRS mode: one shared (X, Y) panel (stride 0), per-replicate perms and noise; the
     dictionary-coded kernel (few distinct values) and the L2-gather fallback."""
