@@ -134,17 +134,27 @@ def _hrs_panel(kind, n, g):
                                         ("coded", 19433, 0.5), ("coded", 1001, 2.0),
                                         ("coded", 1002, 2.0), ("coded", 1003, 2.0),
                                         ("d256", 5000, 2.0), ("d257", 5000, 2.0),
-                                        ("continuous", 3000, 0.5), ("continuous", 4999, 2.0)])
+                                        ("continuous", 3000, 0.5), ("continuous", 4999, 2.0),
+                                        ("continuous-dup", 19433, 2.0), ("continuous-dup", 1001, 2.0)])
 def test_premat_subg_hrs_shared_panel(dc, orc, kind, n, eps):
     """HRS mode: one shared (X, Y) panel (stride 0), per-replicate perms and noise; the
-    dictionary-coded kernel (few distinct values) and the L2-gather fallback."""
+    dictionary-coded kernel (few distinct values) and the uncoded kernels (tiled for m = 2,
+    L2-gather otherwise).  'continuous-dup': replicates 1 and 3 draw their batches WITH
+    replacement (the ABI takes any index rows, not only sample.int's): a repeated sample index
+    must be read twice, whatever the kernel."""
     import torch
     from dcor import _lib
     R = 5
     g = np.random.default_rng(7)
+    dup = kind.endswith("-dup")
+    kind = kind.replace("-dup", "")
     age, bmi = _hrs_panel(kind, n, g)
     k, m = dc.api.batch_geometry(n, eps, eps, "subG", hrs=True)
     perms = np.stack([g.permutation(n)[: k * m] for _ in range(R)]).astype(np.int32)
+    if dup:
+        perms[1] = g.integers(0, n, k * m)
+        perms[3] = perms[0]
+        perms[3][5] = perms[3][9]
     lx, ly = unit_laplace(g, (R, k)), unit_laplace(g, (R, k))
     ll, lc = unit_laplace(g, (R, n)), unit_laplace(g, R)
     mz, ml = g.standard_normal((R, 2000)), unit_laplace(g, (R, 2000))
