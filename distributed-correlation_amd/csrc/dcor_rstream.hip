@@ -4,8 +4,9 @@
 // R's generator is one sequential Mersenne-Twister stream per set.seed() (vert-cor.R:364;
 // ver-cor-subG.R:169), consumed in the call order of SURVEY.md Appendix A.  The engine keeps
 // that contract and puts the parallelism where R's stream allows it:
-//   k_rs_stream       one wave per grid cell: MT19937 blocks of 624 words (the recurrence
-//                     is wave-parallel: every dependency is >= 227 words back), tempered
+//   k_rs_stream       one 256-thread workgroup per grid cell: MT19937 blocks of 624 words
+//                     (the recurrence is parallel: every dependency is >= 227 words back,
+//                     so each of a block's three phases is one step of 256 threads), tempered
 //                     words streamed to HBM, and the data-dependent consumption --
 //                     exp_rand inside mixquant, sample.int's rejection in gen_mix_gaussian --
 //                     walked in order, so every replicate's offset in the stream is known.
@@ -184,12 +185,14 @@ __device__ __forceinline__ double rs_rld(double v, int s) {
 // One MT19937 block in three phases, each issuing all of its LDS reads before any write:
 // kk < 227 reads mt[kk+397] (old); 227 <= kk < 454 reads mt[kk-227] (new, phase 1);
 // kk >= 454 reads mt[kk-227] (new, phase 2) and, for kk = 623, mt[0] (new).  One wave.
+// NT threads of the workgroup share the phase (NT = 64: one wave).
+template <int NT = 64>
 __device__ __forceinline__ void rs_mt_phase(uint32_t* mt, int lane, int k0, int k1) {
-  constexpr int S = 4;
+  constexpr int S = (RS_N - RS_M + NT - 1) / NT;
   uint32_t a[S], b[S], src[S];
 #pragma unroll
   for (int i = 0; i < S; ++i) {
-    const int kk = k0 + lane + 64 * i;
+    const int kk = k0 + lane + NT * i;
     if (kk < k1) {
       a[i] = mt[kk];
       b[i] = mt[kk == RS_N - 1 ? 0 : kk + 1];
@@ -199,7 +202,7 @@ __device__ __forceinline__ void rs_mt_phase(uint32_t* mt, int lane, int k0, int 
   __syncthreads();
 #pragma unroll
   for (int i = 0; i < S; ++i) {
-    const int kk = k0 + lane + 64 * i;
+    const int kk = k0 + lane + NT * i;
     if (kk < k1) {
       const uint32_t y = (a[i] & 0x80000000u) | (b[i] & 0x7fffffffu);
       mt[kk] = src[i] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
@@ -207,10 +210,11 @@ __device__ __forceinline__ void rs_mt_phase(uint32_t* mt, int lane, int k0, int 
   }
   __syncthreads();
 }
+template <int NT = 64>
 __device__ __forceinline__ void rs_mt_block(uint32_t* mt, int lane) {
-  rs_mt_phase(mt, lane, 0, RS_N - RS_M);
-  rs_mt_phase(mt, lane, RS_N - RS_M, 2 * (RS_N - RS_M));
-  rs_mt_phase(mt, lane, 2 * (RS_N - RS_M), RS_N);
+  rs_mt_phase<NT>(mt, lane, 0, RS_N - RS_M);
+  rs_mt_phase<NT>(mt, lane, RS_N - RS_M, 2 * (RS_N - RS_M));
+  rs_mt_phase<NT>(mt, lane, 2 * (RS_N - RS_M), RS_N);
 }
 
 // set.seed(seed): RNG_Init's scrambling and 625 words (word 0, the position, is 624)
@@ -224,11 +228,17 @@ __device__ __forceinline__ void rs_seed_mt(uint32_t* mt, int32_t seed, int lane)
   __syncthreads();
 }
 
-// One wave per cell.  mt[] holds the raw state of the newest block; ring[] the tempered words
+// One workgroup per cell.  Its four waves generate each MT block together; every wave runs the
+// walk below on the same words (the walk is uniform control flow plus wave-wide window
+// classification), so they all call next_block() at the same points, and only wave 0 stores
+// the walk's results.  Four waves measured 1.25x (R1) to 1.35x (RG) the one-wave kernel.
+// mt[] holds the raw state of the newest block; ring[] the tempered words
 // of the last two blocks (slot = absolute word index mod 1248), so exp_rand draws can look
 // up to 17 words ahead while the walk stays at most one block behind generation.
 // Positions are chunk-relative: P words consumed, Q words produced (and written to HBM).
-__global__ __launch_bounds__(64) void k_rs_stream(RsCell* cells, int32_t rc) {
+#define RS_STREAM_NT 256
+__global__ __launch_bounds__(RS_STREAM_NT) void k_rs_stream(RsCell* cells, int32_t rc) {
+  constexpr int NT = RS_STREAM_NT;
   __shared__ uint32_t mt[RS_N];
   __shared__ uint32_t ring[2 * RS_N];
   // every field in registers: the kernel's stores could alias the descriptor, and a reload
@@ -245,9 +255,10 @@ __global__ __launch_bounds__(64) void k_rs_stream(RsCell* cells, int32_t rc) {
   RS_G int64_t* const rep_off = (RS_G int64_t*)cg.rep_off;
   RS_G int64_t* const exp_end = (RS_G int64_t*)cg.exp_end;
   RS_G double* const gexpv = (RS_G double*)cg.expv;
-  const int lane = threadIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const bool w0 = tid < 64;  // the wave that stores the walk's results
   RsState* st = cg.st;
-  for (int t = lane; t < RS_N; t += 64) mt[t] = st->mt[t];
+  for (int t = tid; t < RS_N; t += NT) mt[t] = st->mt[t];
   // uniform by construction: readfirstlane keeps the walk's counters in scalar registers
   const int mti0 = __builtin_amdgcn_readfirstlane(st->mti);
   int par = __builtin_amdgcn_readfirstlane(st->pad[0]) & 1;  // ring half of mt[]'s block
@@ -256,7 +267,7 @@ __global__ __launch_bounds__(64) void k_rs_stream(RsCell* cells, int32_t rc) {
   RS_G uint32_t* const out = (RS_G uint32_t*)cg.words;
   int64_t P = 0, Q = 0;
   if (mti0 < RS_N) {                      // the rest of the current block comes first
-    for (int t = lane; t < RS_N; t += 64) {
+    for (int t = tid; t < RS_N; t += NT) {
       const uint32_t w = rs_temper(mt[t]);
       ring[par * RS_N + t] = w;
       if (t >= mti0) out[t - mti0] = w;
@@ -267,9 +278,9 @@ __global__ __launch_bounds__(64) void k_rs_stream(RsCell* cells, int32_t rc) {
   // ring slot of the consumption point P (absolute word index mod 1248)
   int pslot = (par0 * RS_N + mti0) % (2 * RS_N);
   auto next_block = [&]() {
-    rs_mt_block(mt, lane);
+    rs_mt_block<NT>(mt, tid);
     par ^= 1;
-    for (int t = lane; t < RS_N; t += 64) {
+    for (int t = tid; t < RS_N; t += NT) {
       const uint32_t w = rs_temper(mt[t]);
       ring[par * RS_N + t] = w;
       out[Q + t] = w;
@@ -283,7 +294,7 @@ __global__ __launch_bounds__(64) void k_rs_stream(RsCell* cells, int32_t rc) {
   // 4: fixed words after it; 1: exp_rand; 2: mixquant's rbinom
   int phase = 0;
   int64_t left = c_pre_a, j = 0, sdn = 0;
-  if (lane == 0) rep_off[0] = 0;
+  if (tid == 0) rep_off[0] = 0;
   while (r < rc) {
     // the walk is uniform; say so, or the structurizer keeps it in vector registers under
     // exec masks
@@ -322,7 +333,7 @@ __global__ __launch_bounds__(64) void k_rs_stream(RsCell* cells, int32_t rc) {
         pslot = rs_wrap(pslot + W);
       }
       if (sdn == 0) {
-        if (lane == 0) shuf_end[r] = P;
+        if (tid == 0) shuf_end[r] = P;
         phase = 4;
         left = c_pre - c_pre_a;
       }
@@ -341,7 +352,7 @@ __global__ __launch_bounds__(64) void k_rs_stream(RsCell* cells, int32_t rc) {
           phase = 1; j = 0;
         } else {
           ++r;
-          if (r < rc && lane == 0) rep_off[r] = P;
+          if (r < rc && tid == 0) rep_off[r] = P;
           phase = 0; left = c_pre_a;
         }
       }
@@ -395,7 +406,7 @@ __global__ __launch_bounds__(64) void k_rs_stream(RsCell* cells, int32_t rc) {
     }
     const int last = 63 - __builtin_clzll(starts);
     const int s = rs_u(last + rs_rl(len, last));
-    if ((starts >> lane) & 1ull) {
+    if (w0 && ((starts >> lane) & 1ull)) {
       double e;
       if (len == 1) {
         e = a + eu;
@@ -414,12 +425,12 @@ __global__ __launch_bounds__(64) void k_rs_stream(RsCell* cells, int32_t rc) {
     P += s;
     pslot = rs_wrap(pslot + s);
     if (j == c_nsim) {
-      if (lane == 0) exp_end[r] = P;
+      if (tid == 0) exp_end[r] = P;
       phase = 2; left = c_nsim;
     }
   }
   if (ovf) {                               // word buffer exhausted (sample.int's rejection
-    if (lane == 0) st->pad[1] = 1;        // sampling ran far past its bound): flag, stop
+    if (tid == 0) st->pad[1] = 1;         // sampling ran far past its bound): flag, stop
     return;
   }
   // .Random.seed at the consumption point P: in the newest block, just past it, or (after an
@@ -428,14 +439,14 @@ __global__ __launch_bounds__(64) void k_rs_stream(RsCell* cells, int32_t rc) {
   const int64_t blk = o / RS_N, newest = (Q + mti0) / RS_N - 1;
   const int off = (int)(o % RS_N);
   if (blk > newest) {                     // P == Q at a block boundary
-    for (int t = lane; t < RS_N; t += 64) st->mt[t] = mt[t];
-    if (lane == 0) { st->mti = RS_N; st->pad[0] = par; }
+    for (int t = tid; t < RS_N; t += NT) st->mt[t] = mt[t];
+    if (tid == 0) { st->mti = RS_N; st->pad[0] = par; }
   } else if (blk == newest) {
-    for (int t = lane; t < RS_N; t += 64) st->mt[t] = mt[t];
-    if (lane == 0) { st->mti = off; st->pad[0] = par; }
+    for (int t = tid; t < RS_N; t += NT) st->mt[t] = mt[t];
+    if (tid == 0) { st->mti = off; st->pad[0] = par; }
   } else {
-    for (int t = lane; t < RS_N; t += 64) st->mt[t] = rs_untemper(ring[(par ^ 1) * RS_N + t]);
-    if (lane == 0) { st->mti = off; st->pad[0] = par ^ 1; }
+    for (int t = tid; t < RS_N; t += NT) st->mt[t] = rs_untemper(ring[(par ^ 1) * RS_N + t]);
+    if (tid == 0) { st->mti = off; st->pad[0] = par ^ 1; }
   }
 }
 
@@ -822,7 +833,7 @@ int launch_rs_hrs_ni(const int32_t* d_seeds, int64_t runs, int64_t n, int64_t km
 }
 
 int launch_rs_stream(RsCell* d_cells, int ncells, int32_t rc, void* stream) {
-  hipLaunchKernelGGL(k_rs_stream, dim3(ncells), dim3(64), 0, (hipStream_t)stream, d_cells, rc);
+  hipLaunchKernelGGL(k_rs_stream, dim3(ncells), dim3(RS_STREAM_NT), 0, (hipStream_t)stream, d_cells, rc);
   return (int)hipGetLastError();
 }
 
