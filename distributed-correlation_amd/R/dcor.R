@@ -68,7 +68,10 @@
   out <- data.frame(repl = seq_len(B), ni_hat = ni_hat, int_hat = int_hat,
                     ni_se2 = (ni_hat - rho)^2, int_se2 = (int_hat - rho)^2,
                     ni_low = ni_low, ni_up = ni_up, int_low = int_low, int_up = int_up,
-                    ni_cover = .r_cover(rho, ni_low, ni_up), int_cover = .r_cover(rho, int_low, int_up),
+                    # integer 0/1/NA: vert-cor.R:381-382 starts the columns as NA_integer_ and
+                    # assigns the logical cover into them (:405, :416)
+                    ni_cover = as.integer(.r_cover(rho, ni_low, ni_up)),
+                    int_cover = as.integer(.r_cover(rho, int_low, int_up)),
                     ni_ci_len = ni_up - ni_low, int_ci_len = int_up - int_low)
   summarise <- function(est, se2, cover, lo, up)   # vert-cor.R:422-430
     c(mse = mean(se2), bias = mean(est) - rho, var = var(est), coverage = mean(cover),
@@ -170,7 +173,10 @@ run_sim_one <- function(n, rho, eps1, eps2,
 ## ================================================================= grid ====
 ## Every cell of `design` (data.frame with n, rho, eps1, eps2; one row per cell) for B
 ## replicates in one .Call: replaces the expand.grid + mclapply blocks of vert-cor.R:486-554
-## and ver-cor-subG.R:245-296.  Cell i is seeded 1e6 + i as there.  family "sign" / "subG";
+## and ver-cor-subG.R:245-296, and the merge + summary blocks after them: `detail_all` (with
+## detail = TRUE) and `summ_all` are the tables of vert-cor.R:556-597 / ver-cor-subG.R:301-333
+## (columns, order, cover type and data.table's group order), so the figure code after them runs
+## unchanged.  Cell i is seeded 1e6 + i as there.  family "sign" / "subG";
 ## dgp "gaussian" / "bernoulli" / "bounded_factor" / "mix_gaussian" (gen_mix_gaussian's
 ## arguments in `mix`).  rng "philox" shards replicates over `devices` (0-based HIP ids; all
 ## visible GPUs by default); "R" replays R's own streams cell by cell.
@@ -195,5 +201,8 @@ dcor_grid <- function(design, B = 250, alpha = 0.05, mu = c(0, 0), sigma = c(1, 
               dimnames = list(NULL, c("mse", "bias", "var", "coverage", "ci_length")))
   summ <- data.frame(design[rep(seq_len(nc), each = 2), , drop = FALSE],
                      method = rep(c("NI", "INT"), nc), s, row.names = NULL)
-  list(summary = summ, detail = if (detail) r[[2]] else NULL)
+  as_dt <- function(x) if (!is.null(x) && requireNamespace("data.table", quietly = TRUE))
+    data.table::setDT(x) else x
+  list(summary = summ, detail = if (detail) r[[2]] else NULL,
+       detail_all = as_dt(r[[3]]), summ_all = as_dt(r[[4]]))
 }

@@ -1210,6 +1210,16 @@ int dcor_perm_launch(uint64_t seed, int site, int64_t rep_begin, int64_t reps, i
 }
 
 int dcor_shutdown(void) {
+  const int owner = g_owner_pid.load();
+  if (owner != 0 && owner != (int)getpid()) {
+    // A forked child: the inherited contexts' streams, events and allocations belong to the
+    // parent's HIP runtime.  Forget them without a single HIP call (their host memory is the
+    // child's copy; nothing is freed twice) and report the fork.
+    std::lock_guard<std::mutex> lk(g_ctx_mu);
+    g_ctxs.clear();
+    g_ctx_gen.fetch_add(1);
+    return fork_guard();
+  }
   std::vector<Ctx*> all;
   {
     std::lock_guard<std::mutex> lk(g_ctx_mu);

@@ -141,16 +141,18 @@ def r_cover(rho: float, lo, up) -> np.ndarray:
 
 
 def detail_frame(rec: np.ndarray, rho: float) -> dict:
-    """run_sim_one's `detail` (vert-cor.R:367-417) from the six per-replicate numbers."""
+    """run_sim_one's `detail` (vert-cor.R:367-417; ver-cor-subG.R:170-206) from the six
+    per-replicate numbers, columns in ver-cor-subG.R's order (tables.DETAIL_ORDER[:13])."""
     rec = np.asarray(rec, dtype=np.float64).reshape(-1, 6)
     d = {"repl": np.arange(1, rec.shape[0] + 1)}
     for i, name in enumerate(DETAIL_COLS):
         d[name] = rec[:, i]
     for m in ("ni", "int"):
-        lo, up, hat = d[f"{m}_low"], d[f"{m}_up"], d[f"{m}_hat"]
-        d[f"{m}_se2"] = (hat - rho) ** 2
-        d[f"{m}_cover"] = r_cover(rho, lo, up)
-        d[f"{m}_ci_len"] = up - lo
+        d[f"{m}_se2"] = (d[f"{m}_hat"] - rho) ** 2
+    for m in ("ni", "int"):
+        d[f"{m}_cover"] = r_cover(rho, d[f"{m}_low"], d[f"{m}_up"])
+    for m in ("ni", "int"):
+        d[f"{m}_ci_len"] = d[f"{m}_up"] - d[f"{m}_low"]
     return d
 
 

@@ -13,11 +13,18 @@ typedef struct SEXPREC* SEXP;
 typedef enum { FALSE = 0, TRUE } Rboolean;
 
 #define NILSXP 0
+#define SYMSXP 1
+#define CHARSXP 9
 #define LGLSXP 10
 #define INTSXP 13
 #define REALSXP 14
+#define STRSXP 16
 #define VECSXP 19
 #define RAWSXP 24
+
+#define NA_INTEGER (-2147483647 - 1)
+#define NA_LOGICAL NA_INTEGER
+#define ISNAN(x) __builtin_isnan(x)
 
 void* R_alloc(size_t n, int size);
 void Rf_error(const char* fmt, ...) __attribute__((noreturn));

@@ -1,6 +1,7 @@
 /* rstub.c -- test stub of R's C API (TEST INFRASTRUCTURE, see R.h): SEXP records, R_alloc,
  * Rf_error via longjmp, routine registration, and a ctypes-facing call wrapper so Python can
  * run the package's .Call routines exactly as R would hand them their arguments. */
+#define _POSIX_C_SOURCE 200809L  /* strdup */
 #include <setjmp.h>
 #include <stdarg.h>
 #include <stdio.h>
@@ -11,14 +12,17 @@
 #include "R_ext/Rdynload.h"
 #include "Rinternals.h"
 
+#define MAX_ATTR 8
 struct SEXPREC {
   int type;
   R_xlen_t len;
   int nrow, ncol;   /* allocMatrix dims (0: plain vector) */
-  void* data;
+  void* data;       /* elements; SYMSXP / CHARSXP: the NUL-terminated name / string */
+  int nattr;        /* attributes: (symbol, value) pairs, as setAttrib stores them */
+  SEXP attr_name[MAX_ATTR], attr_val[MAX_ATTR];
 };
 
-static struct SEXPREC nil = {NILSXP, 0, 0, 0, NULL};
+static struct SEXPREC nil = {NILSXP, 0, 0, 0, NULL, 0, {0}, {0}};
 SEXP R_NilValue = &nil;
 
 /* R_alloc memory lives until the end of the current .Call (freed by rs_call) */
@@ -49,7 +53,7 @@ static size_t elt_size(int type) {
     case REALSXP: return sizeof(double);
     case INTSXP: case LGLSXP: return sizeof(int);
     case RAWSXP: return 1;
-    case VECSXP: return sizeof(SEXP);
+    case VECSXP: case STRSXP: return sizeof(SEXP);
     default: return 1;
   }
 }
@@ -59,9 +63,60 @@ SEXP Rf_allocVector(int type, R_xlen_t n) {
   s->type = type;
   s->len = n;
   s->data = calloc((size_t)(n ? n : 1), elt_size(type));
-  if (type == VECSXP)
+  if (type == VECSXP || type == STRSXP)
     for (R_xlen_t i = 0; i < n; ++i) ((SEXP*)s->data)[i] = R_NilValue;
   return s;
+}
+
+/* symbols are interned (R compares attribute names by pointer) */
+static SEXP g_syms[64];
+static int g_nsyms = 0;
+SEXP Rf_install(const char* name) {
+  for (int i = 0; i < g_nsyms; ++i)
+    if (strcmp((const char*)g_syms[i]->data, name) == 0) return g_syms[i];
+  SEXP s = (SEXP)calloc(1, sizeof(struct SEXPREC));
+  s->type = SYMSXP;
+  s->data = strdup(name);
+  s->len = (R_xlen_t)strlen(name);
+  if (g_nsyms < 64) g_syms[g_nsyms++] = s;
+  return s;
+}
+SEXP R_NamesSymbol, R_ClassSymbol, R_RowNamesSymbol;
+__attribute__((constructor)) static void init_symbols(void) {
+  R_NamesSymbol = Rf_install("names");
+  R_ClassSymbol = Rf_install("class");
+  R_RowNamesSymbol = Rf_install("row.names");
+}
+
+SEXP Rf_mkChar(const char* str) {
+  SEXP s = (SEXP)calloc(1, sizeof(struct SEXPREC));
+  s->type = CHARSXP;
+  s->data = strdup(str);
+  s->len = (R_xlen_t)strlen(str);
+  return s;
+}
+SEXP Rf_mkString(const char* str) {
+  SEXP s = Rf_allocVector(STRSXP, 1);
+  ((SEXP*)s->data)[0] = Rf_mkChar(str);
+  return s;
+}
+void SET_STRING_ELT(SEXP x, R_xlen_t i, SEXP v) {
+  if (x->type != STRSXP || v->type != CHARSXP) Rf_error("SET_STRING_ELT: wrong types");
+  ((SEXP*)x->data)[i] = v;
+}
+SEXP STRING_ELT(SEXP x, R_xlen_t i) { return ((SEXP*)x->data)[i]; }
+SEXP Rf_setAttrib(SEXP x, SEXP name, SEXP value) {
+  for (int i = 0; i < x->nattr; ++i)
+    if (x->attr_name[i] == name) { x->attr_val[i] = value; return value; }
+  if (x->nattr == MAX_ATTR) Rf_error("setAttrib: too many attributes");
+  x->attr_name[x->nattr] = name;
+  x->attr_val[x->nattr++] = value;
+  return value;
+}
+SEXP Rf_getAttrib(SEXP x, SEXP name) {
+  for (int i = 0; i < x->nattr; ++i)
+    if (x->attr_name[i] == name) return x->attr_val[i];
+  return R_NilValue;
 }
 
 SEXP Rf_allocMatrix(int type, int nrow, int ncol) {
@@ -85,6 +140,7 @@ int* INTEGER(SEXP x) { need(x, INTSXP, "INTEGER"); return (int*)x->data; }
 int* LOGICAL(SEXP x) { need(x, LGLSXP, "LOGICAL"); return (int*)x->data; }
 Rbyte* RAW(SEXP x) { need(x, RAWSXP, "RAW"); return (Rbyte*)x->data; }
 R_xlen_t XLENGTH(SEXP x) { return x->len; }
+int TYPEOF(SEXP x) { return x->type; }
 int LENGTH(SEXP x) { return (int)x->len; }
 int Rf_isNull(SEXP x) { return x->type == NILSXP; }
 
@@ -141,6 +197,8 @@ int rs_nrow(SEXP s) { return s->nrow; }
 void* rs_data(SEXP s) { return s->data; }
 SEXP rs_elt(SEXP s, R_xlen_t i) { return VECTOR_ELT(s, i); }
 const char* rs_error(void) { return g_err; }
+const char* rs_char(SEXP s) { return s->type == CHARSXP ? (const char*)s->data : NULL; }
+SEXP rs_attr(SEXP s, const char* name) { return Rf_getAttrib(s, Rf_install(name)); }
 
 /* Number of arguments a registered routine takes (-1: not registered). */
 int rs_nargs(const char* name) {

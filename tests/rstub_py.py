@@ -8,7 +8,8 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB = os.path.join(ROOT, "tests", "rstub", "build", "libdcor_r_stub.so")
-NILSXP, LGLSXP, INTSXP, REALSXP, VECSXP, RAWSXP = 0, 10, 13, 14, 19, 24
+NILSXP, LGLSXP, INTSXP, REALSXP, STRSXP, VECSXP, RAWSXP = 0, 10, 13, 14, 16, 19, 24
+NA_INTEGER = -2 ** 31
 
 
 class RError(RuntimeError):
@@ -24,7 +25,8 @@ class RStub:
                                 ("rs_int", P, [P, C.c_ssize_t, C.c_int]), ("rs_type", C.c_int, [P]),
                                 ("rs_length", C.c_ssize_t, [P]), ("rs_nrow", C.c_int, [P]),
                                 ("rs_data", P, [P]), ("rs_elt", P, [P, C.c_ssize_t]),
-                                ("rs_error", C.c_char_p, []), ("rs_nargs", C.c_int, [C.c_char_p]),
+                                ("rs_error", C.c_char_p, []), ("rs_char", C.c_char_p, [P]),
+                                ("rs_attr", P, [P, C.c_char_p]), ("rs_nargs", C.c_int, [C.c_char_p]),
                                 ("rs_call", C.c_int, [C.c_char_p, C.c_int, P, P])):
             f = getattr(self.lib, name)
             f.restype, f.argtypes = res, args
@@ -60,10 +62,13 @@ class RStub:
         return out.value
 
     def value(self, s):
-        """numpy array (REAL/INTEGER/LOGICAL/RAW; matrices as [nrow, ncol]) or list (VECSXP)."""
+        """numpy array (REAL/INTEGER/LOGICAL/RAW; matrices as [nrow, ncol]), list (VECSXP) or
+        list of str (STRSXP)."""
         t, n = self.lib.rs_type(s), self.lib.rs_length(s)
         if t == VECSXP:
             return [self.value(self.lib.rs_elt(s, i)) for i in range(n)]
+        if t == STRSXP:
+            return [self.lib.rs_char(self.lib.rs_elt(s, i)).decode() for i in range(n)]
         if t == NILSXP:
             return None
         ct = {REALSXP: C.c_double, INTSXP: C.c_int, LGLSXP: C.c_int, RAWSXP: C.c_uint8}[t]
@@ -72,3 +77,18 @@ class RStub:
         a = np.ctypeslib.as_array(C.cast(self.lib.rs_data(s), C.POINTER(ct)), shape=(n,)).copy()
         nr = self.lib.rs_nrow(s)
         return a.reshape(nr, n // nr, order="F") if nr else a
+
+    def attr(self, s, name):
+        """Attribute `name` of a SEXP (as setAttrib stored it), as value() reads it; None if unset."""
+        return self.value(self.lib.rs_attr(s, name.encode()))
+
+    def type(self, s):
+        return self.lib.rs_type(s)
+
+    def elt(self, s, i):
+        return self.lib.rs_elt(s, i)
+
+    def frame(self, s):
+        """A data.frame-shaped VECSXP -> (dict column -> numpy array / list, class attribute)."""
+        names = self.attr(s, "names")
+        return {k: self.value(self.lib.rs_elt(s, i)) for i, k in enumerate(names)}, self.attr(s, "class")

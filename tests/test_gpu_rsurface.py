@@ -154,7 +154,7 @@ def test_grid_routine_equals_python_grid(rs):
         rs.logical([True] * nc), rs.integer([0] * nc), rs.real(col(lambda c: c.seed)), rs.real(B),
         rs.logical(True), rs.real([0, 0, 1, 1, 3, 3, 2, 0.5, 0.5]), rs.logical(False),
         rs.real([1000] * nc), rs.integer([0])))
-    summ, det = out
+    summ, det = out[:2]
     ref = run_grid(cells, B, detail=True, devices=[0])
     assert np.array_equal(_bits(det.reshape(nc * B, 6)), _bits(np.concatenate([r["records"] for r in ref])))
     for i, r in enumerate(ref):
@@ -162,3 +162,85 @@ def test_grid_routine_equals_python_grid(rs):
             s = summ[(2 * i + m) * 5:(2 * i + m + 1) * 5]
             want = [r["summary"][meth][k] for k in ("mse", "bias", "var", "coverage", "ci_length")]
             assert np.array_equal(_bits(s), _bits(want))
+
+
+def _grid_call(rs, cells, B, detail=True):
+    nc = len(cells)
+    col = lambda f: [f(c) for c in cells]  # noqa: E731
+    fam = {"sign": 0, "subG": 1}
+    dg = {"gaussian": 0, "bernoulli": 1, "bounded_factor": 2, "mix_gaussian": 3}
+    return rs.call(
+        "dcor_R_grid_run", rs.integer(col(lambda c: fam[c.family])), rs.integer(col(lambda c: dg[c.dgp])),
+        rs.real(col(lambda c: c.n)), rs.real(col(lambda c: c.rho)), rs.real(col(lambda c: c.eps1)),
+        rs.real(col(lambda c: c.eps2)), rs.real([0.05] * nc), rs.real(col(lambda c: c.mu[0])),
+        rs.real(col(lambda c: c.mu[1])), rs.real(col(lambda c: c.sigma[0])), rs.real(col(lambda c: c.sigma[1])),
+        rs.logical([True] * nc), rs.integer([0] * nc), rs.real(col(lambda c: c.seed)), rs.real(B),
+        rs.logical(detail), rs.real([0, 0, 1, 1, 3, 3, 2, 0.5, 0.5]), rs.logical(False),
+        rs.real([1000] * nc), rs.integer([0]))
+
+
+@pytest.mark.parametrize("family", ["sign", "subG"])
+def test_grid_routine_tables_equal_python_tables(rs, family):
+    """f2 on the R side: dcor_R_grid_run's detail_all and summ_all (vert-cor.R:556-597;
+    ver-cor-subG.R:301-333) equal dcor.tables.grid_detail / grid_summary byte for byte -- the
+    family's column order, integer (sign) or logical (sub-G) cover with NA, the setting columns,
+    data.table's first-appearance group order with a repeated setting pooled, NI rows then INT."""
+    from dcor import tables
+    from dcor.sim import expand_grid, run_grid
+    from rstub_py import INTSXP, LGLSXP, NA_INTEGER
+    kw = (dict(family="sign", dgp="gaussian", mu=(0.5, 0.5), sigma=(2.0, 2.0)) if family == "sign"
+          else dict(family="subG", dgp="bounded_factor"))
+    cells = expand_grid([1200, 2500], [0.0, 0.5], [(1.0, 1.0), (0.2, 0.2)], **kw)  # (.2, .2) at 1200: k = 6
+    cells.append(cells[1])            # a repeated setting: data.table pools its rows into one group
+    B = 23
+    out = _grid_call(rs, cells, B)
+    det_s, cls = rs.frame(rs.elt(out, 2))
+    summ_s, cls2 = rs.frame(rs.elt(out, 3))
+    assert cls == ["data.frame"] and cls2 == ["data.frame"]
+    assert list(rs.attr(rs.elt(out, 2), "row.names")) == [NA_INTEGER, -B * len(cells)]
+    res = run_grid(cells, B, detail=True, devices=[0])
+    det_p = tables.grid_detail(cells, res)
+    assert list(det_s) == list(det_p) == list(tables.detail_order(family))
+    cover_type = INTSXP if family == "sign" else LGLSXP
+    for j, name in enumerate(det_s):
+        got, want = det_s[name], det_p[name]
+        if name.endswith("_cover"):
+            assert rs.type(rs.elt(rs.elt(out, 2), j)) == cover_type
+            want_i = np.where(np.isnan(want), NA_INTEGER, want).astype(np.int64)
+            assert np.array_equal(got.astype(np.int64), want_i), name
+        elif name == "repl":
+            assert rs.type(rs.elt(rs.elt(out, 2), j)) == INTSXP
+            assert np.array_equal(got, want), name
+        else:
+            assert np.array_equal(_bits(got), _bits(want)), name
+    summ_p = tables.grid_summary(cells, res)
+    assert len(summ_p) == 2 * (len(cells) - 1)
+    assert list(summ_s) == list(tables.SUMMARY_ORDER)
+    assert summ_s["method"] == [r["method"] for r in summ_p]
+    for name in tables.SUMMARY_ORDER[:-1]:
+        assert np.array_equal(_bits(summ_s[name]), _bits([r[name] for r in summ_p])), name
+    # k = 6 batches at n = 1200, eps = (.2, .2): finite; the NI summary of the pooled group counts 2B rows
+    assert np.all(np.isfinite(summ_s["mse"]))
+
+
+def test_grid_routine_without_detail_has_summ_all_only(rs):
+    from dcor.sim import expand_grid
+    cells = expand_grid([1000], [0.3], [(1.0, 1.0)], family="sign", dgp="gaussian")
+    out = _grid_call(rs, cells, 5, detail=False)
+    assert rs.value(rs.elt(out, 2)) is None
+    summ, _ = rs.frame(rs.elt(out, 3))
+    assert summ["method"] == ["NI", "INT"] and len(summ["mse"]) == 2
+
+
+def test_grid_routine_refuses_ragged_cells(rs):
+    from rstub_py import RError
+    from dcor.sim import expand_grid
+    cells = expand_grid([1000, 2000], [0.3], [(1.0, 1.0)], family="sign", dgp="gaussian")
+    args = [rs.integer([0, 0]), rs.integer([0, 0]), rs.real([1000, 2000]), rs.real([0.3]),  # rho: 1 value
+            rs.real([1, 1]), rs.real([1, 1]), rs.real([0.05] * 2), rs.real([0, 0]), rs.real([0, 0]),
+            rs.real([1, 1]), rs.real([1, 1]), rs.logical([True] * 2), rs.integer([0, 0]),
+            rs.real([1e6 + 1, 1e6 + 2]), rs.real(5), rs.logical(False), rs.real([0, 0, 1, 1, 3, 3, 2, 0.5, 0.5]),
+            rs.logical(False), rs.real([1000] * 2), rs.integer([0])]
+    assert len(cells) == 2
+    with pytest.raises(RError, match="per-cell"):
+        rs.call("dcor_R_grid_run", *args)

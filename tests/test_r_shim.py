@@ -102,3 +102,89 @@ def test_error_path_is_rf_error(rs):
         rs.call("dcor_R_mixquant", z, z, rs.real(1.0), rs.real(0.975))
     with pytest.raises(ValueError):
         rs.call("dcor_R_mixquant", z, z)          # wrong arity: not callable
+
+
+def test_shim_checks_lengths_before_reading(rs):
+    """The routines refuse vectors shorter than the C side would read (R's error path, before any
+    device work), so a direct .Call cannot read past an R vector."""
+    z = lambda n: rs.real(np.zeros(n))  # noqa: E731
+    cases = [
+        ("dcor_R_gen_bernoulli", (z(5), z(4), rs.real(0.5)), "same length"),
+        ("dcor_R_gen_bounded_factor", (z(5), z(5), z(3)), "same length"),
+        ("dcor_R_mix_gaussian", (z(4), rs.real(2), z(2), rs.real(1), rs.integer([0, 1, 2]), rs.real(0.5),
+                                 z(1), z(2), z(2), z(2)), "length 2"),
+        ("dcor_R_mixquant", (z(10), z(9), rs.real(1.0), rs.real(0.975)), "length 10"),
+        ("dcor_R_priv_standardize", (z(10), rs.real(1.0), rs.real(6.0), z(1)), "length 2"),
+        # n = 100, eps = (1, 1): m = 8, k = 12 Laplace draws per side
+        ("dcor_R_ci_NI_signbatch", (z(100), z(100), rs.real(1.0), rs.real(1.0), rs.real(0.05),
+                                    rs.logical(True), z(4), z(11), z(12)), "lap_x"),
+        ("dcor_R_ci_NI_signbatch", (z(100), z(99), rs.real(1.0), rs.real(1.0), rs.real(0.05),
+                                    rs.logical(True), z(4), z(12), z(12)), "same length"),
+        ("dcor_R_ci_INT_signflip", (z(100), z(100), rs.real(1.0), rs.real(1.0), rs.real(0.05), rs.integer(1),
+                                    rs.logical(True), z(4), rs.integer(np.zeros(99)), rs.real(0.1), z(5), z(5)),
+         "flips"),
+        ("dcor_R_ci_INT_subG", (z(50), z(50), rs.real(1.0), rs.real(1.0), rs.real(1.0), rs.real(1.0),
+                                rs.real(0.05), rs.logical(False), rs.real(np.nan), rs.real(np.nan),
+                                rs.real(np.nan), rs.real(np.nan), z(49), rs.real(0.1), z(5), z(5)), "lap_local"),
+        # HRS NI: n = 9, eps = (2, 2): m = 2, k = 4; perm must hold k m = 8 indices
+        ("dcor_R_correlation_NI_subG", (z(9), z(9), rs.real(2.0), rs.real(2.0), rs.real(1.0), rs.real(1.0),
+                                        rs.real(0.05), rs.logical(True), rs.real(2.0), rs.real(2.0),
+                                        rs.integer(np.arange(7)), z(4), z(4)), "perm"),
+    ]
+    for name, args, msg in cases:
+        with pytest.raises(RError, match=msg):
+            rs.call(name, *args)
+
+
+FORK_SCRIPT = r"""
+import ctypes as C, os, sys
+root = sys.argv[1]
+eng = C.CDLL(os.path.join(root, "distributed-correlation_amd", "dcor", "libdcor.so"), mode=C.RTLD_GLOBAL)
+sys.path.insert(0, os.path.join(root, "tests"))
+import rstub_py
+rs = rstub_py.RStub.__new__(rstub_py.RStub)   # without `import dcor` (torch): the engine is loaded above
+rs.lib = C.CDLL(rstub_py.LIB)
+P = C.c_void_p
+for name, res, args in (("rs_real", P, [P, C.c_ssize_t]), ("rs_error", C.c_char_p, []),
+                        ("rs_call", C.c_int, [C.c_char_p, C.c_int, P, P])):
+    f = getattr(rs.lib, name); f.restype, f.argtypes = res, args
+z = rs.real([0.0] * 5)
+def call():
+    try:
+        rs.call("dcor_R_mixquant", z, z, rs.real([1.0]), rs.real([0.975]))
+        return "ok"
+    except rstub_py.RError as e:
+        return str(e)
+parent = call()                # the parent runs run_sim_one first (vert-cor.R:449)
+pid = os.fork()                # then mclapply forks its workers (vert-cor.R:534)
+if pid == 0:
+    msg = call()
+    st = eng.dcor_shutdown()   # a forked child's shutdown touches no HIP state either
+    os.write(1, ("CHILD:" + msg + "|SHUTDOWN:" + str(st) + "\n").encode())
+    os._exit(0)
+os.waitpid(pid, 0)
+print("PARENT:" + parent)
+"""
+
+
+def test_forked_child_fails_loudly(tmp_path):
+    """The reference's own flow (vert-cor.R:449 runs run_sim_one in the parent; :534-553 then runs
+    it in mclapply children) on the drop-in surface: the engine never touches HIP in a child forked
+    after the parent used it.  The child's .Call raises R's error with a message naming the fork
+    and the remedy (dcor_grid from the parent) -- what mclapply then reports in its try-error --
+    and dcor_shutdown in the child returns DCOR_EFORK without HIP calls.  Host-only (the parent's
+    first call takes the ENODEV path here)."""
+    import subprocess
+    import sys
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("fork rehearsal runs on a host without a GPU")
+    p = tmp_path / "fork_flow.py"
+    p.write_text(FORK_SCRIPT)
+    out = subprocess.run([sys.executable, str(p), ROOT], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr
+    lines = dict(l.split(":", 1) for l in out.stdout.split("\n") if ":" in l and l.split(":")[0] in ("CHILD", "PARENT"))
+    assert "status 5" in lines["PARENT"]                       # DCOR_ENODEV: no GPU here
+    child, shut = lines["CHILD"].split("|SHUTDOWN:")
+    assert "forked" in child and "dcor_grid" in child and "status 6" in child, child   # DCOR_EFORK
+    assert shut == "6"
