@@ -75,7 +75,11 @@ double r_max(double a, double b) { return (std::isnan(a) || std::isnan(b)) ? NAN
 struct DevBuf {  // RAII device allocation for the host-pointer entry points
   void* p = nullptr;
   ~DevBuf() { if (p) (void)hipFree(p); }
-  hipError_t alloc(size_t bytes) { return hipMalloc(&p, bytes ? bytes : 8); }
+  hipError_t alloc(size_t bytes) {
+    const hipError_t e = hipMalloc(&p, bytes ? bytes : 8);
+    if (e == hipSuccess) count_alloc();
+    return e;
+  }
   template <class T> T* as() const { return static_cast<T*>(p); }
 };
 
@@ -330,10 +334,12 @@ void ctx_free(Ctx* c) {
     (void)hipEventDestroy(c->pipe.fork);
     (void)hipEventDestroy(c->pipe.join);
   }
-  if (c->staging_free) { (void)hipEventSynchronize(c->staging_free); (void)hipEventDestroy(c->staging_free); }
-  if (c->staging) (void)hipHostFree(c->staging);
+  for (Pinned* b : {&c->stage[0], &c->stage[1], &c->hrec}) {
+    if (b->done) { (void)hipEventSynchronize(b->done); (void)hipEventDestroy(b->done); }
+    if (b->p) (void)hipHostFree(b->p);
+  }
   if (c->work) { (void)hipStreamSynchronize(c->work); (void)hipStreamDestroy(c->work); }
-  for (Arena* a : {&c->codes, &c->rs, &c->grid, &c->out})
+  for (Arena* a : {&c->codes, &c->rs, &c->grid, &c->gpart, &c->out})
     if (a->p) (void)hipFree(a->p);
   delete c;
 }
@@ -381,6 +387,9 @@ int pipe_get(Pipe** out) {
   return DCOR_OK;
 }
 
+std::atomic<int64_t> g_alloc_count{0};
+void count_alloc() { g_alloc_count.fetch_add(1); }
+
 int arena_grow(Arena& a, size_t bytes, void** out) {
   if (a.bytes < bytes) {
     // the old block may still be read by work queued earlier: wait for the device
@@ -390,9 +399,29 @@ int arena_grow(Arena& a, size_t bytes, void** out) {
       a.p = nullptr;
       return fail(DCOR_ENOMEM, "scratch arena: cannot allocate %zu bytes", bytes);
     }
+    count_alloc();
     a.bytes = bytes;
   }
   *out = a.p;
+  return DCOR_OK;
+}
+
+int pinned_grow(Pinned& b, size_t bytes, void** out) {
+  if (!b.done) HIPCHK(hipEventCreateWithFlags(&b.done, hipEventDisableTiming));
+  HIPCHK(hipEventSynchronize(b.done));   // a never-recorded event is complete
+  if (b.bytes < bytes) {
+    if (b.p) HIPCHK(hipHostFree(b.p));
+    b.p = nullptr;
+    b.bytes = 0;
+    if (hipHostMalloc(&b.p, bytes, hipHostMallocDefault) != hipSuccess) {
+      (void)hipGetLastError();
+      b.p = nullptr;
+      return fail(DCOR_ENOMEM, "pinned staging: cannot allocate %zu bytes", bytes);
+    }
+    count_alloc();
+    b.bytes = bytes;
+  }
+  *out = b.p;
   return DCOR_OK;
 }
 
@@ -771,6 +800,7 @@ static int hrs_fused_materialised(const dcor_premat_subg* d, const dcor_panel* p
     (void)hipGetLastError();
     return fail(DCOR_ENOMEM, "hrs_fused: cannot allocate %zu noise bytes", per * (size_t)cr);
   }
+  count_alloc();
   int32_t* perm = (int32_t*)buf;
   double* lx = (double*)(buf + al((size_t)cr * k * m * 4));
   double* ly = lx + (al((size_t)cr * k * 8) / 8);
@@ -820,6 +850,7 @@ int dcor_panel_create(const double* d_X, const double* d_Y, int64_t n, void* str
     delete pn;
     return fail(DCOR_ENOMEM, "panel_create: cannot allocate the coded panel");
   }
+  count_alloc();
   int rc = 0;
   if (n <= DCOR_DICT_NMAX && premat_dict_lds_bytes(n) <= 150 * 1024)
     rc = launch_panel_dict(d_X, d_Y, n, pn->codes(), pn->dict(), pn->ok(), stream);
@@ -901,6 +932,7 @@ int dcor_hrs_fused_launch(const dcor_premat_subg* d, const dcor_panel* panel, ui
     (void)hipGetLastError();
     return fail(DCOR_ENOMEM, "hrs_fused: cannot allocate %zu scratch bytes", bytes);
   }
+  count_alloc();
   if (!coded) {
     p.xyc = (const double2*)((char*)part + part_b);
     p.soc = p.xyc + d->n;
@@ -943,6 +975,7 @@ static int premat_subg_run(const dcor_premat_subg* d, const dcor_panel* panel, d
     (void)hipGetLastError();
     return fail(DCOR_ENOMEM, "premat sub-G: cannot allocate %zu scratch bytes", bytes);
   }
+  count_alloc();
   if (pack) {
     p.xyc = (const double2*)((char*)part + part_b);
     p.soc = p.xyc + p.s.n;
@@ -1209,9 +1242,20 @@ int dcor_perm_launch(uint64_t seed, int site, int64_t rep_begin, int64_t reps, i
   return DCOR_OK;
 }
 
+int64_t dcor_alloc_count(void) { return g_alloc_count.load(); }
+
+int64_t dcor_device_bytes(void) {
+  std::lock_guard<std::mutex> lk(g_ctx_mu);
+  int64_t b = 0;
+  for (const Ctx* c : g_ctxs)
+    for (const Arena* a : {&c->codes, &c->rs, &c->grid, &c->gpart, &c->out}) b += (int64_t)a->bytes;
+  return b;
+}
+
 int dcor_shutdown(void) {
   const int owner = g_owner_pid.load();
   if (owner != 0 && owner != (int)getpid()) {
+    grid_workers_stop(true);
     // A forked child: the inherited contexts' streams, events and allocations belong to the
     // parent's HIP runtime.  Forget them without a single HIP call (their host memory is the
     // child's copy; nothing is freed twice) and report the fork.
@@ -1220,6 +1264,7 @@ int dcor_shutdown(void) {
     g_ctx_gen.fetch_add(1);
     return fork_guard();
   }
+  grid_workers_stop(false);   // idle workers first: their contexts are freed below
   std::vector<Ctx*> all;
   {
     std::lock_guard<std::mutex> lk(g_ctx_mu);

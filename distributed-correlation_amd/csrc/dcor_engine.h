@@ -149,11 +149,26 @@ struct GridItem {
                       // planes: u64 words)
   uint64_t out;       // index of its output record
 };
+// A run of consecutive replicates of one cell inside one chunk launch; the launch's work items
+// are expanded from these on the device (launch_grid_expand), so the host plans O(cells + chunks)
+// records instead of one per replicate.
+struct GridPiece {
+  uint32_t cell;        // index into the launch's constant table
+  uint32_t rep0;        // replicate of the first item
+  uint64_t item0;       // first item index (within the chunk launch)
+  uint64_t count;       // items
+  uint64_t out0;        // output record of the first item
+  uint64_t scr0;        // scratch element of the first item
+  uint64_t scr_stride;  // scratch elements per item
+};
+int launch_grid_expand(const GridPiece* pieces, int64_t npieces, GridItem* items, void* stream);
 enum GridKind { GK_SIGN_CODES = 0, GK_SIGN_REGEN = 1, GK_SIGN_BERN_W = 2, GK_SIGN_BERN = 3, GK_SUBG = 4 };
 // per-item scratch of the kinds that use it
 #define GRID_BERN_W_NMAX 16384
 // doubles per replicate handed from the one-pass sign kernel's pass 1 to pass 2
 #define SIGN_SUMS 8
+// bytes of a SignPartial (pass 2 -> epilogue; dcor_fused.hip)
+#define SIGN_PARTIAL_BYTES 48
 // Pass 1 + pass 2 over `nitems` items (scratch: the items' code slabs; sums: SIGN_SUMS doubles per
 // item; part: per-item SignPartial), then the wave epilogue writing out[item.out].
 int launch_grid_sign_codes(int dgp, const SignConst* cells, const GridItem* items, int64_t nitems,
@@ -166,13 +181,27 @@ int launch_grid_sign_bern(bool wave, const SignConst* cells, const GridItem* ite
                           void* stream);
 int launch_grid_subg(int dgp, const SubgConst* cells, const GridItem* items, int64_t nitems,
                      dcor_rep_out* out, void* stream);
-// Accumulators of ncells cell segments of `rec` (segment i: seg_off[i], seg_cnt[i] records, rho[i])
-// into acc[2 i], acc[2 i + 1]; byte-identical to launch_accumulate on each segment.  part: scratch
-// of 512 * 2 accumulators per cell (cells with more than 2048 records).
-int launch_accumulate_seg(const dcor_rep_out* rec, int ncells, const int64_t* seg_off,
-                          const int64_t* seg_cnt, const double* rho, int max_nb, dcor_accum* part,
-                          dcor_accum* acc, void* stream);
-int accumulate_blocks(int64_t count);   // launch_accumulate's partition of `count` records
+// Accumulators of grid cells, computed in passes over bounded record buffers.  Cell c's records
+// are partitioned as launch_accumulate partitions them (accumulate_blocks(count) blocks of
+// accumulate_per(count)); a pass holds whole blocks.  Entry: blocks [blo, bhi) of one cell whose
+// records start (at block blo) at rec[base]; poff: the cell's first partial in `part` (cells with
+// more than one block).  The block partials and their merge are byte-identical to
+// launch_accumulate on the cell's records alone.
+struct AccEntry {
+  int64_t base, blo, bhi, count, poff;
+  double rho;
+  int32_t cell, pad;
+};
+struct AccCell {   // a multi-block cell for the final merge
+  int64_t count, poff;
+  int32_t cell, pad;
+};
+int accumulate_blocks(int64_t count);
+int64_t accumulate_per(int64_t count);
+int launch_accumulate_pass(const dcor_rep_out* rec, const AccEntry* ent, int nent, int max_span,
+                           dcor_accum* part, dcor_accum* acc, void* stream);
+int launch_accumulate_merge_cells(const AccCell* cells, int ncells, const dcor_accum* part,
+                                  dcor_accum* acc, void* stream);
 int launch_premat_sign(const PrematSignConst& c, int64_t reps, dcor_rep_out* out, void* stream);
 // part: reps * 80 B scratch (stream -> epilogue partial sums).
 // epi_stream / ev: if non-null the epilogue runs on epi_stream after an event recorded on

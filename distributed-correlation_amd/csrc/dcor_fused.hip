@@ -480,6 +480,7 @@ struct SignPartial {
   long long core;        // sum of (2S-1) sign(X) sign(Y) (vert-cor.R:178-183)
   long long flags;       // bit 0: NI saw NaN, bit 1: INT saw NaN
 };
+static_assert(sizeof(SignPartial) == SIGN_PARTIAL_BYTES, "dcor_engine.h SIGN_PARTIAL_BYTES");
 
 // Pass 2: signs from the codes (exact regeneration on a code tie), batch counts, NI
 // Laplace, T sums and the INT flip sum.  Lean: the mixquant/CI epilogue is its own kernel.
@@ -1225,8 +1226,23 @@ __global__ __launch_bounds__(DCOR_BLOCK) void k_grid_subg(const SubgConst* __res
   subg_fused_body<DGP>(cells[it.cell], it.rep, out + it.out);
 }
 
+// Work items of one chunk launch from its pieces: workgroup p writes piece p's items.
+__global__ __launch_bounds__(DCOR_BLOCK) void k_grid_expand(const GridPiece* __restrict__ pieces,
+                                                            GridItem* __restrict__ items) {
+  const GridPiece pc = pieces[blockIdx.x];
+  for (uint64_t t = threadIdx.x; t < pc.count; t += DCOR_BLOCK)
+    items[pc.item0 + t] = GridItem{pc.cell, pc.rep0 + (uint32_t)t, pc.scr0 + t * pc.scr_stride, pc.out0 + t};
+}
+
 // ============================================================ launchers ===
 static inline int last_err() { return (int)hipGetLastError(); }
+
+int launch_grid_expand(const GridPiece* pieces, int64_t npieces, GridItem* items, void* stream) {
+  if (npieces <= 0) return 0;
+  hipLaunchKernelGGL(k_grid_expand, dim3((unsigned)npieces), dim3(DCOR_BLOCK), 0, (hipStream_t)stream,
+                     pieces, items);
+  return last_err();
+}
 
 static inline unsigned wave_groups(int64_t n) { return (unsigned)((n + DCOR_WAVES - 1) / DCOR_WAVES); }
 

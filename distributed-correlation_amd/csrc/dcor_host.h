@@ -30,23 +30,32 @@ double r_max(double a, double b);
 
 struct Arena { void* p = nullptr; size_t bytes = 0; };
 struct Pipe { hipStream_t s = nullptr; hipEvent_t fork = nullptr, join = nullptr; };
+// Pinned host memory with the event that marks the end of the last copy that read or wrote it.
+struct Pinned { void* p = nullptr; size_t bytes = 0; hipEvent_t done = nullptr; };
 // The library's state for one (host thread, device): scratch arenas, the auxiliary stream of the
-// two-stream chunk pipeline, and a pinned staging buffer (the grid's tables) with the event that
-// marks the end of its last upload.
+// two-stream chunk pipeline, and pinned staging buffers (the grid's tables, two slots used in
+// turn so one upload can be in flight while the next is written; the records of a pass).
 struct Ctx {
   int dev = -1;
   Arena codes, rs, grid;
+  Arena gpart;                    // the grid's accumulate block partials (multi-block cells)
   Arena out;                      // the synchronous grid entries' replicate records + accumulators
   hipStream_t work = nullptr;     // ... and their stream
   Pipe pipe;
-  void* staging = nullptr;
-  size_t staging_bytes = 0;
-  hipEvent_t staging_free = nullptr;
+  Pinned stage[2];
+  int stage_next = 0;
+  Pinned hrec;                    // a pass's records on their way to the caller's detail array
 };
 int ctx_get(Ctx** out);          // the calling thread's context on the current device
 void ctx_release_thread();       // free every context of the calling thread
 int pipe_get(Pipe** out);
+// Device arena of at least `bytes` (grows, never shrinks; counted by dcor_alloc_count()).
 int arena_grow(Arena& a, size_t bytes, void** out);
+// Pinned host buffer of at least `bytes`, after its previous copy finished (counted likewise).
+int pinned_grow(Pinned& b, size_t bytes, void** out);
+void count_alloc();
+// Stop the grid's persistent device workers (dcor_shutdown); `forked`: forget them unjoined.
+void grid_workers_stop(bool forked);              // one more device or pinned allocation (dcor_alloc_count)
 
 // All constants of one fused cell and the kernel family that runs it.
 struct CellPlan {

@@ -928,13 +928,12 @@ __device__ __forceinline__ void acc_write(dcor_accum* dst, int64_t n, const DD* 
   *dst = a;
 }
 
-__global__ __launch_bounds__(DCOR_BLOCK) void k_accumulate(const dcor_rep_out* rec, int64_t count,
-                                                           int64_t per, double rho,
-                                                           dcor_accum* part) {
-  __shared__ double red[16 * DCOR_WAVES];
-  __shared__ long long redi[DCOR_WAVES];
-  const int64_t b0 = (int64_t)blockIdx.x * per;
-  const int64_t b1 = (b0 + per < count) ? b0 + per : count;
+// One accumulate block: records [b0, b1) of one cell (both methods) into dst[0], dst[1].  Every
+// accumulate kernel runs this body, so a block's partial is the same bits whichever kernel, launch
+// or pass computed it.
+__device__ __forceinline__ void acc_block_body(const dcor_rep_out* rec, int64_t b0, int64_t b1,
+                                               double rho, dcor_accum* dst, double* red,
+                                               long long* redi) {
   for (int meth = 0; meth < 2; ++meth) {
     DD s[6] = {{0, 0}, {0, 0}, {0, 0}, {0, 0}, {0, 0}, {0, 0}};
     long long cnt[4] = {0, 0, 0, 0};  // cover, cover_na, na_est, na_ci
@@ -946,18 +945,17 @@ __global__ __launch_bounds__(DCOR_BLOCK) void k_accumulate(const dcor_rep_out* r
     long long tot[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) tot[q] = block_sum_i(cnt[q], redi);
-    if (threadIdx.x == 0) acc_write(part + 2 * blockIdx.x + meth, b1 > b0 ? b1 - b0 : 0, s, tot);
+    if (threadIdx.x == 0) acc_write(dst + meth, b1 > b0 ? b1 - b0 : 0, s, tot);
   }
 }
 
-__global__ __launch_bounds__(DCOR_BLOCK) void k_accumulate_merge(const dcor_accum* part, int nb,
-                                                                 int64_t count, dcor_accum* acc) {
-  __shared__ double red[16 * DCOR_WAVES];
-  __shared__ long long redi[DCOR_WAVES];
+// Merge nb block partials (part[2 b + meth]) in block order into acc[0], acc[1].
+__device__ __forceinline__ void acc_merge_body(const dcor_accum* part, int64_t nb, int64_t count,
+                                               dcor_accum* acc, double* red, long long* redi) {
   for (int meth = 0; meth < 2; ++meth) {
     DD s[6] = {{0, 0}, {0, 0}, {0, 0}, {0, 0}, {0, 0}, {0, 0}};
     long long cnt[4] = {0, 0, 0, 0};
-    for (int b = threadIdx.x; b < nb; b += DCOR_BLOCK) {
+    for (int64_t b = threadIdx.x; b < nb; b += DCOR_BLOCK) {
       const dcor_accum& a = part[2 * b + meth];
       s[0] = dd_add(s[0], DD{a.est[0], a.est[1]});
       s[1] = dd_add(s[1], DD{a.est2[0], a.est2[1]});
@@ -975,74 +973,63 @@ __global__ __launch_bounds__(DCOR_BLOCK) void k_accumulate_merge(const dcor_accu
   }
 }
 
-// Segmented form for the batched grid: block (b, i) runs block b of cell segment i's partition
-// (accumulate_blocks), exactly the work k_accumulate's block b does on that segment alone; a
-// one-block segment writes its accumulators directly, the others through `part` and the merge.
-__global__ __launch_bounds__(DCOR_BLOCK) void k_accumulate_seg(const dcor_rep_out* rec,
-                                                               const int64_t* __restrict__ seg_off,
-                                                               const int64_t* __restrict__ seg_cnt,
-                                                               const double* __restrict__ rho,
-                                                               int max_nb, dcor_accum* part,
-                                                               dcor_accum* acc) {
-  __shared__ double red[16 * DCOR_WAVES];
-  __shared__ long long redi[DCOR_WAVES];
-  const int cell = blockIdx.y;
-  const int64_t count = seg_cnt[cell];
+// launch_accumulate's partition of `count` records: ~2048 per block, at most 512 blocks.
+__host__ __device__ __forceinline__ int64_t acc_nblocks(int64_t count) {
   int64_t nb = (count + 2047) / 2048;
   if (nb < 1) nb = 1;
   if (nb > 512) nb = 512;
-  if ((int64_t)blockIdx.x >= nb) return;
-  const int64_t per = (count + nb - 1) / nb > 0 ? (count + nb - 1) / nb : 1;
-  const int64_t b0 = (int64_t)blockIdx.x * per;
-  const int64_t b1 = (b0 + per < count) ? b0 + per : count;
-  const dcor_rep_out* r0 = rec + seg_off[cell];
-  dcor_accum* dst = nb == 1 ? acc + 2 * cell : part + ((size_t)cell * max_nb + blockIdx.x) * 2;
-  for (int meth = 0; meth < 2; ++meth) {
-    DD s[6] = {{0, 0}, {0, 0}, {0, 0}, {0, 0}, {0, 0}, {0, 0}};
-    long long cnt[4] = {0, 0, 0, 0};
-    for (int64_t b = b0 + threadIdx.x; b < b1; b += DCOR_BLOCK) {
-      const double* r = &r0[b].ni_hat + 3 * meth;
-      acc_record(r[0], r[1], r[2], rho[cell], s, cnt);
-    }
-    block_sum_dd<6>(s, red);
-    long long tot[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) tot[q] = block_sum_i(cnt[q], redi);
-    if (threadIdx.x == 0) acc_write(dst + meth, b1 > b0 ? b1 - b0 : 0, s, tot);
-  }
+  return nb;
+}
+__host__ __device__ __forceinline__ int64_t acc_per(int64_t count, int64_t nb) {
+  return (count + nb - 1) / nb > 0 ? (count + nb - 1) / nb : 1;
 }
 
-__global__ __launch_bounds__(DCOR_BLOCK) void k_accumulate_seg_merge(const int64_t* __restrict__ seg_cnt,
-                                                                     int max_nb,
-                                                                     const dcor_accum* part,
-                                                                     dcor_accum* acc) {
+__global__ __launch_bounds__(DCOR_BLOCK) void k_accumulate(const dcor_rep_out* rec, int64_t count,
+                                                           int64_t per, double rho,
+                                                           dcor_accum* part) {
   __shared__ double red[16 * DCOR_WAVES];
   __shared__ long long redi[DCOR_WAVES];
-  const int cell = blockIdx.x;
-  const int64_t count = seg_cnt[cell];
-  int64_t nb = (count + 2047) / 2048;
-  if (nb > 512) nb = 512;
-  if (nb <= 1) return;
-  const dcor_accum* p = part + (size_t)cell * max_nb * 2;
-  for (int meth = 0; meth < 2; ++meth) {
-    DD s[6] = {{0, 0}, {0, 0}, {0, 0}, {0, 0}, {0, 0}, {0, 0}};
-    long long cnt[4] = {0, 0, 0, 0};
-    for (int b = threadIdx.x; b < nb; b += DCOR_BLOCK) {
-      const dcor_accum& a = p[2 * b + meth];
-      s[0] = dd_add(s[0], DD{a.est[0], a.est[1]});
-      s[1] = dd_add(s[1], DD{a.est2[0], a.est2[1]});
-      s[2] = dd_add(s[2], DD{a.se2[0], a.se2[1]});
-      s[3] = dd_add(s[3], DD{a.len[0], a.len[1]});
-      s[4] = dd_add(s[4], DD{a.lo[0], a.lo[1]});
-      s[5] = dd_add(s[5], DD{a.hi[0], a.hi[1]});
-      cnt[0] += a.n_cover; cnt[1] += a.n_cover_na; cnt[2] += a.n_na_est; cnt[3] += a.n_na_ci;
-    }
-    block_sum_dd<6>(s, red);
-    long long tot[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) tot[q] = block_sum_i(cnt[q], redi);
-    if (threadIdx.x == 0) acc_write(acc + 2 * cell + meth, count, s, tot);
-  }
+  const int64_t b0 = (int64_t)blockIdx.x * per;
+  const int64_t b1 = (b0 + per < count) ? b0 + per : count;
+  acc_block_body(rec, b0, b1, rho, part + 2 * blockIdx.x, red, redi);
+}
+
+__global__ __launch_bounds__(DCOR_BLOCK) void k_accumulate_merge(const dcor_accum* part, int nb,
+                                                                 int64_t count, dcor_accum* acc) {
+  __shared__ double red[16 * DCOR_WAVES];
+  __shared__ long long redi[DCOR_WAVES];
+  acc_merge_body(part, nb, count, acc, red, redi);
+}
+
+// Pass form for the batched grid: entry j of a pass names blocks [blo, bhi) of one cell's
+// partition (acc_nblocks of the cell's count), whose records sit in this pass's buffer at
+// rec + base (record r of the cell -- cell-relative -- at rec[base + r - blo per]).  Block (t, j)
+// runs block blo + t exactly as k_accumulate would on the cell alone; a one-block cell writes its
+// accumulators directly, the others their partial at part[2 (poff + b)].
+__global__ __launch_bounds__(DCOR_BLOCK) void k_accumulate_pass(const dcor_rep_out* rec,
+                                                                const AccEntry* __restrict__ ent,
+                                                                dcor_accum* part, dcor_accum* acc) {
+  __shared__ double red[16 * DCOR_WAVES];
+  __shared__ long long redi[DCOR_WAVES];
+  const AccEntry e = ent[blockIdx.y];
+  const int64_t b = e.blo + (int64_t)blockIdx.x;
+  if (b >= e.bhi) return;
+  const int64_t nb = acc_nblocks(e.count), per = acc_per(e.count, nb);
+  const int64_t r0 = b * per;
+  const int64_t r1 = (r0 + per < e.count) ? r0 + per : e.count;
+  dcor_accum* dst = nb == 1 ? acc + 2 * (int64_t)e.cell : part + 2 * (e.poff + b);
+  // the same records, thread assignment and order as k_accumulate's block b on the cell alone
+  acc_block_body(rec + e.base + (r0 - e.blo * per), 0, r1 - r0, e.rho, dst, red, redi);
+}
+
+// Merge of every multi-block cell's partials after the last pass (cells[] lists them).
+__global__ __launch_bounds__(DCOR_BLOCK) void k_accumulate_merge_cells(const AccCell* __restrict__ cells,
+                                                                       const dcor_accum* part,
+                                                                       dcor_accum* acc) {
+  __shared__ double red[16 * DCOR_WAVES];
+  __shared__ long long redi[DCOR_WAVES];
+  const AccCell c = cells[blockIdx.x];
+  acc_merge_body(part + 2 * c.poff, acc_nblocks(c.count), c.count, acc + 2 * (int64_t)c.cell, red, redi);
 }
 
 // ================================================== single-call helpers ===
@@ -1864,33 +1851,29 @@ int launch_premat_subg(const PrematSubgConst& c0, int64_t reps, void* part, dcor
                        (hipStream_t)stream, c, reps, (const SubgPartial*)part, out);
   return last_err();
 }
-int accumulate_blocks(int64_t count) {
-  int64_t nb = (count + 2047) / 2048;
-  if (nb < 1) nb = 1;
-  if (nb > 512) nb = 512;
-  return (int)nb;
+int accumulate_blocks(int64_t count) { return (int)acc_nblocks(count); }
+int64_t accumulate_per(int64_t count) { return acc_per(count, acc_nblocks(count)); }
+
+int launch_accumulate_pass(const dcor_rep_out* rec, const AccEntry* ent, int nent, int max_span,
+                           dcor_accum* part, dcor_accum* acc, void* stream) {
+  if (nent <= 0) return 0;
+  hipLaunchKernelGGL(k_accumulate_pass, dim3((unsigned)max_span, (unsigned)nent), dim3(DCOR_BLOCK), 0,
+                     (hipStream_t)stream, rec, ent, part, acc);
+  return last_err();
 }
 
-int launch_accumulate_seg(const dcor_rep_out* rec, int ncells, const int64_t* seg_off,
-                          const int64_t* seg_cnt, const double* rho, int max_nb, dcor_accum* part,
-                          dcor_accum* acc, void* stream) {
+int launch_accumulate_merge_cells(const AccCell* cells, int ncells, const dcor_accum* part,
+                                  dcor_accum* acc, void* stream) {
   if (ncells <= 0) return 0;
-  const hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(k_accumulate_seg, dim3((unsigned)max_nb, (unsigned)ncells), dim3(DCOR_BLOCK), 0,
-                     st, rec, seg_off, seg_cnt, rho, max_nb, part, acc);
-  if (max_nb > 1)
-    hipLaunchKernelGGL(k_accumulate_seg_merge, dim3((unsigned)ncells), dim3(DCOR_BLOCK), 0, st, seg_cnt,
-                       max_nb, part, acc);
+  hipLaunchKernelGGL(k_accumulate_merge_cells, dim3((unsigned)ncells), dim3(DCOR_BLOCK), 0,
+                     (hipStream_t)stream, cells, part, acc);
   return last_err();
 }
 
 int launch_accumulate(const dcor_rep_out* d_out, int64_t count, double rho, dcor_accum* acc,
                       void* stream) {
   // ~2048 records per block, at most 512 blocks; 1 block writes acc directly.
-  int64_t nb = (count + 2047) / 2048;
-  if (nb < 1) nb = 1;
-  if (nb > 512) nb = 512;
-  const int64_t per = (count + nb - 1) / nb > 0 ? (count + nb - 1) / nb : 1;
+  const int64_t nb = acc_nblocks(count), per = acc_per(count, nb);
   if (nb == 1) {
     hipLaunchKernelGGL(k_accumulate, dim3(1), dim3(DCOR_BLOCK), 0, (hipStream_t)stream, d_out,
                        count, per, rho, acc);

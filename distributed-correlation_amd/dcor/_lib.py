@@ -106,6 +106,8 @@ SIGNATURES = {
     "dcor_last_error": (C.c_int, [C.c_char_p, C.c_size_t]),
     "dcor_device_count": (C.c_int, []),
     "dcor_shutdown": (C.c_int, []),
+    "dcor_alloc_count": (C.c_int64, []),
+    "dcor_device_bytes": (C.c_int64, []),
     "dcor_lambda_n": (C.c_double, [C.c_double, C.c_double]),
     "dcor_lambda_int_n": (None, [C.c_double, C.c_double, C.c_double, C.c_double, _D]),
     "dcor_lambda_receiver_from_noise": (C.c_double, [C.c_double] * 4),

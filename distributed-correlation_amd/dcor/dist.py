@@ -55,29 +55,40 @@ def merge_ranked(per_rank: List[List[_lib.Accum]]) -> List[_lib.Accum]:
     return [merge([per_rank[r][i] for r in range(len(per_rank))]) for i in range(n)]
 
 
-def run_grid_distributed(cells, B: int, group=None, stream=None):
-    """Every rank runs its replicate shard of every cell; returns the merged
-    (NI, INT) accumulators per cell, identical on all ranks."""
+def run_grid_distributed(cells, B: int, group=None, stream=None, return_records: bool = False):
+    """Every rank runs its replicate shard [g B / G, (g+1) B / G) of EVERY cell in one batched
+    launch sequence (dcor_grid_launch: all cells' replicates share the launches, so a rank's few
+    replicates per cell still fill its GPU), then the per-cell accumulators are all-gathered --
+    straight from device memory under RCCL -- copied to the host once and merged in rank order.
+    Returns [(NI, INT)] per cell, identical on all ranks; with return_records also this rank's
+    (b0, records [ncells, nb, 6]) (byte-identical to the same replicates of a world-1 run)."""
     import torch
     import torch.distributed as dist
 
-    from .sim import accum_from_bytes, accumulate, simulate
+    from .sim import grid_launch
 
     rank, world = dist.get_rank(group), dist.get_world_size(group)
     b0, nb = shard(B, rank, world)
-    local = []
+    nc = len(cells)
     s = torch.cuda.current_stream() if stream is None else stream
-    with torch.cuda.stream(s):   # torch's D2H copies run on the current stream
-        buf = torch.empty((max(nb, 1), 6), dtype=torch.float64, device="cuda")
-        for cell in cells:
-            if nb > 0:
-                simulate(cell, nb, b0, out=buf, stream=s)
-                acc = accumulate(buf[:nb], cell.rho, stream=s)
-                local.extend(accum_from_bytes(acc.cpu().numpy().tobytes()))
-            else:
-                local.extend([_lib.Accum(), _lib.Accum()])
-    merged = merge_ranked(gather_accums(local, group))
-    return [(merged[2 * i], merged[2 * i + 1]) for i in range(len(cells))]
+    with torch.cuda.stream(s):   # torch's copies and the collective's device work run on `s`
+        if nb > 0:
+            out, acc = grid_launch(cells, b0, nb, stream=s)
+        else:
+            out = None
+            acc = torch.zeros(2 * nc * ACC_BYTES, dtype=torch.uint8, device="cuda")
+        t = acc if dist.get_backend(group) == "nccl" else acc.cpu()
+        outs = [torch.empty_like(t) for _ in range(world)]
+        dist.all_gather(outs, t, group=group)
+        raw = torch.cat(outs).cpu().numpy().tobytes()          # the one D2H copy
+        rec = out.cpu().numpy().reshape(nc, nb, 6) if (return_records and out is not None) else None
+    per_rank = [[_lib.Accum.from_buffer_copy(raw[(r * 2 * nc + i) * ACC_BYTES:(r * 2 * nc + i + 1) * ACC_BYTES])
+                 for i in range(2 * nc)] for r in range(world)]
+    merged = merge_ranked(per_rank)
+    pairs = [(merged[2 * i], merged[2 * i + 1]) for i in range(nc)]
+    if return_records:
+        return pairs, (b0, rec if rec is not None else np.zeros((nc, 0, 6)))
+    return pairs
 
 
 # ------------------------------------------------------ R-stream mode (by cell)

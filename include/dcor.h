@@ -99,10 +99,18 @@ int dcor_last_error(char* buf, size_t len);
 /* Number of visible HIP devices (0 on a host without GPU; never fails). */
 int dcor_device_count(void);
 /* Release the library-owned scratch: per (host thread, device) the one-pass sign kernel's
- * chunk x n x 4 B slab of per-sample codes, the grid tables and the auxiliary stream.  Each host
- * thread has its own, so threads never share scratch; launches of ONE thread on different
- * streams of one device must be ordered by the caller.  Call when no work is in flight. */
+ * chunk x n x 4 B slab of per-sample codes, the grid tables and the auxiliary stream, and stop
+ * dcor_grid_run_multi's persistent device workers.  Each host thread has its own, so threads never
+ * share scratch; launches of ONE thread on different streams of one device must be ordered by the
+ * caller.  Call when no work is in flight.  In a process forked after its parent used the engine
+ * it makes no HIP call and returns DCOR_EFORK. */
 int dcor_shutdown(void);
+/* Device and pinned-host allocations the library has made so far (its scratch arenas, staging
+ * buffers, panels and the host-pointer entries' transfer buffers): a repeated call of the same
+ * shape on warm contexts adds none. */
+int64_t dcor_alloc_count(void);
+/* Device bytes held by the library's scratch arenas over every live context. */
+int64_t dcor_device_bytes(void);
 
 /* ---- calibration scalars (host closed forms) ----------------------------- */
 /* lambda_n, ver-cor-subG.R:1 (= real-data-sims.R:109). */
@@ -152,8 +160,12 @@ int dcor_grid_launch(const dcor_cell* cells, int ncells, const int64_t* rep_begi
                      void* stream);
 /* The grid over several GPUs of one node, synchronous, host buffers: every cell's B replicates are
  * split into contiguous ranges, shard g = [g B / G, (g+1) B / G) on device_ids[g] from its own host
- * thread (a device may appear more than once); accumulators are merged in device-list order, so
- * the summary is deterministic for a given list, and per-replicate records do not depend on it.
+ * thread (a device may appear more than once; with more than one shard the threads are persistent
+ * workers, one per (device, listing), whose scratch survives across calls until dcor_shutdown);
+ * accumulators are merged in device-list order, so the summary is deterministic for a given list,
+ * and per-replicate records do not depend on it.  Device memory is bounded whatever B is: the
+ * replicates run through a record buffer of DCOR_GRID_REC_MB (default 256) MiB in passes of whole
+ * accumulate blocks, so the accumulators equal dcor_accumulate_launch over each cell's records.
  * device_ids = NULL / ndev = 0: every visible device.  Replaces mclapply over cells
  * (vert-cor.R:534-553; ver-cor-subG.R:294-295). */
 int dcor_grid_run_multi(const dcor_cell* cells, int ncells, int64_t B, const int* device_ids,

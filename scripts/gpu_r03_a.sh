@@ -1,12 +1,14 @@
-# Round 3, first GPU call: the new C4 + R-table tests, the grid tests, then a kernel-trace profile
-# of the reference grids (VG, SG) on the round-2 grid engine (the A side of the grid rework).
+# Round 3: the grid engine rework (device-expanded items, bounded passes, persistent workers,
+# batched RCCL path) and the new C4 / R-table tests, then the reference grids (VG, SG) timed and
+# kernel-traced.
 set -o pipefail
 export TMPDIR=/tmp
 O=gpurun_out
 mkdir -p $O
-timeout -k 10 600 python -u -m pytest tests/test_gpu_c4.py tests/test_gpu_rsurface.py tests/test_gpu_grid.py \
+timeout -k 10 700 python -u -m pytest tests/test_gpu_grid.py tests/test_gpu_dist.py tests/test_gpu_c4.py \
+  tests/test_gpu_rsurface.py tests/test_tables.py tests/test_gpu_launch_shape.py \
   -x -v --timeout 300 --timeout-method thread > $O/r03a_pytest.log 2>&1
-rc=$?; echo "pytest rc=$rc"; tail -6 $O/r03a_pytest.log
+rc=$?; echo "pytest rc=$rc"; tail -8 $O/r03a_pytest.log
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 timeout -k 10 300 python -u bench_configs.py --only VG,SG > $O/r03a_cfg.jsonl 2> $O/r03a_cfg.err || exit $?
 cat $O/r03a_cfg.jsonl

@@ -70,7 +70,8 @@ def _worker(rank, world, port, q):
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from dcor.dist import run_grid_distributed
-    q.put((rank, _flat(run_grid_distributed(_cells(), B))))
+    pairs, (b0, rec) = run_grid_distributed(_cells(), B, return_records=True)
+    q.put((rank, (_flat(pairs), b0, rec.tobytes(), rec.shape)))
     dist.destroy_process_group()
 
 
@@ -81,13 +82,23 @@ def test_run_grid_distributed_two_ranks_on_gpu():
     procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    res = dict(q.get(timeout=100) for _ in range(world))
+    got = dict(q.get(timeout=100) for _ in range(world))
     for p in procs:
         p.join(timeout=30)
         assert p.exitcode == 0
+    res = {r: v[0] for r, v in got.items()}
     assert res[0] == res[1]
     assert res[0] == _expected(world)
     _assert_equals_world1(res[0])
+    # the batched shards' replicates, concatenated in rank order, are the world-1 run's bit for bit
+    import numpy as np
+    from dcor.sim import simulate
+    parts = [np.frombuffer(got[r][2], dtype=np.float64).reshape(got[r][3]) for r in range(world)]
+    assert [got[r][1] for r in range(world)] == [0, B // 2]
+    for i, cell in enumerate(_cells()):
+        want = simulate(cell, B, 0).cpu().numpy()
+        have = np.concatenate([p[i] for p in parts])
+        assert np.array_equal(have.view(np.uint64), want.view(np.uint64)), cell
 
 
 def _world1():

@@ -152,3 +152,45 @@ def test_two_host_threads_on_one_device(dc):
         t.join()
     for g, r in zip(got, ref):
         assert np.array_equal(_bits(g), _bits(r))
+
+
+def test_grid_run_multi_persistent_workers_allocate_once(dc):
+    """dcor_grid_run_multi keeps one persistent worker per (device, listing): a second call with the
+    same device list and grid makes no new device or pinned allocation (dcor_alloc_count), for the
+    calling-thread path (one device) and the worker path (device 0 listed twice)."""
+    from dcor import _lib
+    from dcor.sim import run_grid
+    cells = _mixed_cells()
+    for devices in ([0], [0, 0]):
+        first = run_grid(cells, 101, detail=True, devices=devices)
+        n0 = _lib.lib.dcor_alloc_count()
+        again = run_grid(cells, 101, detail=True, devices=devices)
+        assert _lib.lib.dcor_alloc_count() == n0, devices
+        for a, b in zip(first, again):
+            assert np.array_equal(_bits(a["records"]), _bits(b["records"]))
+            assert [bytes(x) for x in a["accum"]] == [bytes(x) for x in b["accum"]]
+
+
+def test_grid_memory_bounded_in_B(dc, monkeypatch):
+    """Device memory does not grow with B: with a 1 MiB record buffer the replicates
+    run in many passes of whole accumulate blocks; the accumulators are still byte-identical to
+    one dcor_accumulate_launch over each cell's records, the detail records to the per-cell
+    launches, and a 4x larger B holds the same device bytes."""
+    from dcor import _lib
+    from dcor.sim import CellSpec, run_grid
+    monkeypatch.setenv("DCOR_GRID_REC_MB", "1")            # 21,845 records per pass
+    monkeypatch.setenv("DCOR_GRID_CHUNK_ITEMS", "4096")    # and many chunks per pass
+    cells = [CellSpec(n=1000, rho=0.3, eps1=1.0, eps2=1.0, family="subG", dgp="bounded_factor", seed=1_000_031),
+             CellSpec(n=1200, rho=0.5, eps1=1.0, eps2=1.0, mu=(0.5, 0.5), sigma=(2.0, 2.0), seed=1_000_032),
+             CellSpec(n=900, rho=0.65, eps1=0.5, eps2=0.5, dgp="bernoulli", seed=1_000_033)]
+    B = 30_011      # 15 accumulate blocks per cell, passes split cells
+    res = run_grid(cells, B, detail=True, devices=[0])
+    ref, ref_acc = _per_cell(cells, [0] * 3, [B] * 3)
+    assert np.array_equal(_bits(np.concatenate([r["records"] for r in res])), _bits(ref))
+    assert [bytes(a) for r in res for a in r["accum"]] == ref_acc
+    run_grid(cells, 20_000, devices=[0])
+    held = _lib.lib.dcor_device_bytes()
+    res4 = run_grid(cells, 4 * 20_000, devices=[0])          # no detail: accumulators only
+    # only the block partials may grow (<= 512 per cell, 2 x 160 B each), never the record buffer
+    assert _lib.lib.dcor_device_bytes() - held <= 3 * 512 * 2 * 160
+    assert all(r["accum"][0].n == 80_000 for r in res4)
