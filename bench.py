@@ -95,8 +95,31 @@ def cpu_baseline(cell, seconds: float = 12.0):
                                  "detectCores() - 1 workers, capped at this box's CPU share"}
 
 
+def src_sha16(root: str = ROOT) -> str:
+    """sha256 (first 16 hex) of the engine's sources -- csrc/*.hip, *.h, *.cpp and include/dcor.h --
+    as they are on disk: stamped into every committed profile summary by scripts/summarize_prof.py,
+    so the bench line can tell whether the profile it quotes was taken on this code."""
+    import hashlib
+    h = hashlib.sha256()
+    cs = os.path.join(root, "distributed-correlation_amd", "csrc")
+    files = sorted(f for f in os.listdir(cs) if f.endswith((".hip", ".h", ".cpp")))
+    for f in [os.path.join(cs, f) for f in files] + [os.path.join(root, "include", "dcor.h")]:
+        h.update(os.path.basename(f).encode())
+        h.update(open(f, "rb").read())
+    return h.hexdigest()[:16]
+
+
+def profile_stamp(path):
+    """(git head, fresh) of a committed profile summary: fresh = its source hash equals this tree's."""
+    try:
+        d = json.load(open(path))
+        return d.get("git_head"), d.get("src_sha16") == src_sha16()
+    except (OSError, ValueError, TypeError):
+        return None, False
+
+
 def _profile(name):
-    for tag in ("r02", "r01"):
+    for tag in ("r03", "r02", "r01"):
         p = os.path.join(ROOT, "profiles", f"{tag}_{name}_summary.json")
         if os.path.exists(p):
             return p
@@ -239,7 +262,12 @@ def main():
                                             "SIMD-cycles), time-weighted over the sign kernels "
                                             "profiled serially; the VALU-bound kernels' roofline",
                          "issue_source": isrc,
+                         "issue_source_head": profile_stamp(os.path.join(ROOT, isrc))[0] if isrc else None,
+                         "issue_source_fresh": profile_stamp(os.path.join(ROOT, isrc))[1] if isrc else False,
                          "traffic": pmc_traffic(),
+                         "traffic_source": os.path.relpath(_profile("headline"), ROOT) if _profile("headline") else None,
+                         "traffic_source_head": profile_stamp(_profile("headline"))[0] if _profile("headline") else None,
+                         "traffic_source_fresh": profile_stamp(_profile("headline"))[1] if _profile("headline") else False,
                          "traffic_unit": "HBM B per simulate() call (rocprofv3 PMC, FETCH_SIZE x2 + WRITE_SIZE)",
                          "kernel": "k_sign_pass1 + k_sign_pass2 + k_sign_epilogue_w (one simulate() call)",
                          "kernel_ms_avg": kern_ms,

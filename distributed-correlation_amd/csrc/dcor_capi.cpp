@@ -334,7 +334,7 @@ void ctx_free(Ctx* c) {
     (void)hipEventDestroy(c->pipe.fork);
     (void)hipEventDestroy(c->pipe.join);
   }
-  for (Pinned* b : {&c->stage[0], &c->stage[1], &c->hrec}) {
+  for (Pinned* b : {&c->stage[0], &c->stage[1], &c->hrec, &c->hacc}) {
     if (b->done) { (void)hipEventSynchronize(b->done); (void)hipEventDestroy(b->done); }
     if (b->p) (void)hipHostFree(b->p);
   }
@@ -483,7 +483,7 @@ int prepare_cell(const dcor_cell& c, CellPlan& p) {
     else if (force_regen || !c.normalise)
       p.kind = GK_SIGN_REGEN;
     else
-      p.kind = GK_SIGN_CODES;
+      p.kind = c.n <= SIGN_W_NMAX ? GK_SIGN_CODES_W : GK_SIGN_CODES;
     p.vpl32 = k.mix.nsim > 1024 ? 1 : 0;
   } else if (c.family == DCOR_FAMILY_SUBG) {
     SubgConst& k = p.subg;
@@ -633,7 +633,7 @@ int dcor_sim_launch(const dcor_cell* cell, int64_t rep_begin, int64_t rep_count,
       if (int st = arena_get(plane_bytes + (size_t)chunk * 64, &scratch)) return st;
       rc = launch_sign_bern(k, rep_count, chunk, (uint64_t*)scratch,
                             (SignPartial*)((char*)scratch + plane_bytes), d_out, stream);
-    } else if (cp.kind != GK_SIGN_CODES || rep_count == 0) {
+    } else if ((cp.kind != GK_SIGN_CODES && cp.kind != GK_SIGN_CODES_W) || rep_count == 0) {
       rc = launch_sign_fused(k, rep_count, d_out, stream);
     } else {
       // two slabs (two-stream chunk pipeline), each within a budget of >= 1 GiB and

@@ -162,7 +162,11 @@ struct GridPiece {
   uint64_t scr_stride;  // scratch elements per item
 };
 int launch_grid_expand(const GridPiece* pieces, int64_t npieces, GridItem* items, void* stream);
-enum GridKind { GK_SIGN_CODES = 0, GK_SIGN_REGEN = 1, GK_SIGN_BERN_W = 2, GK_SIGN_BERN = 3, GK_SUBG = 4 };
+enum GridKind { GK_SIGN_CODES = 0, GK_SIGN_REGEN = 1, GK_SIGN_BERN_W = 2, GK_SIGN_BERN = 3, GK_SUBG = 4,
+                GK_SIGN_CODES_W = 5 };
+// one-pass sign cells up to this n run the wave-per-replicate kernels (GK_SIGN_CODES_W), in the
+// grid and in dcor_sim_launch alike, so a replicate's bits do not depend on the entry point
+#define SIGN_W_NMAX 16384
 // per-item scratch of the kinds that use it
 #define GRID_BERN_W_NMAX 16384
 // doubles per replicate handed from the one-pass sign kernel's pass 1 to pass 2
@@ -174,6 +178,9 @@ enum GridKind { GK_SIGN_CODES = 0, GK_SIGN_REGEN = 1, GK_SIGN_BERN_W = 2, GK_SIG
 int launch_grid_sign_codes(int dgp, const SignConst* cells, const GridItem* items, int64_t nitems,
                            uint32_t* scratch, double* sums, SignPartial* part, int vpl32,
                            dcor_rep_out* out, void* stream);
+// Small cells: wave pass 1 + wave pass 2 / epilogue (sums: SIGN_SUMS doubles per item, no partials).
+int launch_grid_sign_codes_w(int dgp, const SignConst* cells, const GridItem* items, int64_t nitems,
+                             uint32_t* scratch, double* sums, int vpl32, dcor_rep_out* out, void* stream);
 int launch_grid_sign_regen(int dgp, const SignConst* cells, const GridItem* items, int64_t nitems,
                            dcor_rep_out* out, void* stream);
 int launch_grid_sign_bern(bool wave, const SignConst* cells, const GridItem* items, int64_t nitems,

@@ -320,12 +320,16 @@ __device__ __forceinline__ void exact_signs(const SignConst& c, const SignStd& s
 // queued sample's record is rewritten and its clipped values enter the sums at the drain.
 #define ZQ_CAP 512  // per-wave queue; a group iteration adds at most 256 entries per wave
 
-template <int DGP>
-__device__ __forceinline__ void sign_pass1_body(const SignConst& c, uint32_t rep,
+// WAVE = false: one 256-thread workgroup per replicate; WAVE = true: one wave per replicate (the
+// caller's workgroup has loaded the ziggurat table `zt` into LDS once for all its replicates).
+// zq / zqn: the calling wave's slow-normal queue and its counter (LDS).
+template <int DGP, bool WAVE>
+__device__ __forceinline__ void sign_pass1_core(const SignConst& c, uint32_t rep,
                                                 uint32_t* __restrict__ slab,
-                                                double* __restrict__ sums_out) {
-  __shared__ double red[16 * DCOR_WAVES];
-  const int tid = threadIdx.x;
+                                                double* __restrict__ sums_out, const double2* zt,
+                                                uint32_t* zq, uint32_t* zqn) {
+  constexpr int NT = WAVE ? 64 : DCOR_BLOCK;
+  const int tid = WAVE ? (int)(threadIdx.x & 63) : (int)threadIdx.x;
   DD sx{0.0, 0.0}, sy{0.0, 0.0};
   auto record = [&](double xc, double yc, uint32_t fl) {
     const uint32_t qx = code16(xc, c.cinv_xf, c.cnb_xf, 65535.0f);
@@ -336,14 +340,7 @@ __device__ __forceinline__ void sign_pass1_body(const SignConst& c, uint32_t rep
   // group of its thread
   const int64_t nfull = c.n / 4;
   if constexpr (DGP == DCOR_DGP_GAUSSIAN) {
-    __shared__ double2 zt[2 * DCOR_ZIG_N];
-    __shared__ uint32_t zq[DCOR_WAVES][ZQ_CAP];
-    __shared__ uint32_t zqn[DCOR_WAVES];
-    const int wv = tid >> 6, lane = tid & 63;
-    for (int e = tid; e < 2 * DCOR_ZIG_N; e += DCOR_BLOCK)
-      zt[e] = make_double2(dcor_zig_tab[e][0], dcor_zig_tab[e][1]);
-    if (tid < DCOR_WAVES) zqn[tid] = 0u;
-    __syncthreads();
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     auto group = [&](int64_t g4, auto full_tag) {
       constexpr bool FULL = decltype(full_tag)::value;
       const uint32_t i0 = (uint32_t)(4 * g4);
@@ -373,17 +370,17 @@ __device__ __forceinline__ void sign_pass1_body(const SignConst& c, uint32_t rep
         for (int q = 0; q < 4; ++q) if ((int64_t)(i0 + q) < c.n) slab[i0 + q] = rec[q];
       }
       if (pend) {
-        uint32_t pos = atomicAdd(&zqn[wv], (uint32_t)__popc(pend));
-        for (; pend; pend &= pend - 1u) zq[wv][pos++] = i0 + (uint32_t)(__ffs(pend) - 1);
+        uint32_t pos = atomicAdd(zqn, (uint32_t)__popc(pend));
+        for (; pend; pend &= pend - 1u) zq[pos++] = i0 + (uint32_t)(__ffs(pend) - 1);
       }
     };
     // the whole wave, converged: each lane takes queued samples lane, lane + 64, ...
     auto drain = [&]() {
-      const uint32_t cnt = __builtin_amdgcn_readfirstlane(zqn[wv]);
+      const uint32_t cnt = __builtin_amdgcn_readfirstlane(*zqn);
       if (cnt == 0) return;
       __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the placeholder records have landed
       for (uint32_t k = (uint32_t)lane; k < cnt; k += 64) {
-        const uint32_t i = zq[wv][k];
+        const uint32_t i = zq[k];
         double x, y;
         uint32_t w3;
         Dgp<DGP>::one_w3(c.g, i, rep, c.k0, c.k1, x, y, w3);
@@ -393,14 +390,14 @@ __device__ __forceinline__ void sign_pass1_body(const SignConst& c, uint32_t rep
         slab[i] = record(xc, yc, ((uint64_t)w3 < c.flipT) ? 1u : 0u);
       }
       wave_sync();
-      if (lane == 0) zqn[wv] = 0u;
+      if (lane == 0) *zqn = 0u;
       wave_sync();
     };
-    for (int64_t b = 64 * wv; b < nfull; b += DCOR_BLOCK) {  // trip count uniform per wave
+    for (int64_t b = WAVE ? 0 : 64 * wv; b < nfull; b += NT) {  // trip count uniform per wave
       if (b + lane < nfull) group(b + lane, std::true_type());
-      if (__builtin_amdgcn_readfirstlane(zqn[wv]) > ZQ_CAP - 256) drain();
+      if (__builtin_amdgcn_readfirstlane(*zqn) > ZQ_CAP - 256) drain();
     }
-    if ((c.n & 3) && tid == (int)(nfull % DCOR_BLOCK)) group(nfull, std::false_type());
+    if ((c.n & 3) && tid == (int)(nfull % NT)) group(nfull, std::false_type());
     drain();
   } else {
     // group g4 = samples 4 g4 .. 4 g4 + 3; FULL: all four exist (the hot loop has no guards)
@@ -436,14 +433,39 @@ __device__ __forceinline__ void sign_pass1_body(const SignConst& c, uint32_t rep
         for (int q = 0; q < 4; ++q) if ((int64_t)(i0 + q) < c.n) slab[i0 + q] = rec[q];
       }
     };
-    for (int64_t g4 = tid; g4 < nfull; g4 += DCOR_BLOCK) group(g4, std::true_type());
-    if ((c.n & 3) && tid == (int)(nfull % DCOR_BLOCK)) group(nfull, std::false_type());
+    for (int64_t g4 = tid; g4 < nfull; g4 += NT) group(g4, std::true_type());
+    if ((c.n & 3) && tid == (int)(nfull % NT)) group(nfull, std::false_type());
   }
   DD d2[2] = {sx, sy};
-  block_sum_dd<2>(d2, red);
+  if constexpr (WAVE) {
+    d2[0] = wave_sum_dd(d2[0]);
+    d2[1] = wave_sum_dd(d2[1]);
+  } else {
+    __shared__ double red[16 * DCOR_WAVES];
+    block_sum_dd<2>(d2, red);
+  }
   if (tid == 0) {
     sums_out[0] = d2[0].hi; sums_out[1] = d2[0].lo; sums_out[2] = 0.0;
     sums_out[3] = d2[1].hi; sums_out[4] = d2[1].lo; sums_out[5] = 0.0;
+  }
+}
+
+template <int DGP>
+__device__ __forceinline__ void sign_pass1_body(const SignConst& c, uint32_t rep,
+                                                uint32_t* __restrict__ slab,
+                                                double* __restrict__ sums_out) {
+  if constexpr (DGP == DCOR_DGP_GAUSSIAN) {
+    __shared__ double2 zt[2 * DCOR_ZIG_N];
+    __shared__ uint32_t zq[DCOR_WAVES][ZQ_CAP];
+    __shared__ uint32_t zqn[DCOR_WAVES];
+    const int tid = threadIdx.x, wv = tid >> 6;
+    for (int e = tid; e < 2 * DCOR_ZIG_N; e += DCOR_BLOCK)
+      zt[e] = make_double2(dcor_zig_tab[e][0], dcor_zig_tab[e][1]);
+    if (tid < DCOR_WAVES) zqn[tid] = 0u;
+    __syncthreads();
+    sign_pass1_core<DGP, false>(c, rep, slab, sums_out, zt, zq[wv], &zqn[wv]);
+  } else {
+    sign_pass1_core<DGP, false>(c, rep, slab, sums_out, nullptr, nullptr, nullptr);
   }
 }
 
@@ -484,17 +506,49 @@ static_assert(sizeof(SignPartial) == SIGN_PARTIAL_BYTES, "dcor_engine.h SIGN_PAR
 
 // Pass 2: signs from the codes (exact regeneration on a code tie), batch counts, NI
 // Laplace, T sums and the INT flip sum.  Lean: the mixquant/CI epilogue is its own kernel.
-template <int DGP>
-__device__ __forceinline__ void sign_pass2_body(const SignConst& c, uint32_t rep,
-                                                const uint32_t* __restrict__ slab,
-                                                const double* __restrict__ sums_in,
-                                                SignPartial* __restrict__ part_out) {
-  __shared__ double red[16 * DCOR_WAVES];
-  __shared__ long long redi[DCOR_WAVES];
-  __shared__ double lap[10];
-  const int tid = threadIdx.x;
-  scalar_laplace(rep, c.k0, c.k1, lap);
-  __syncthreads();
+// The reduced per-replicate results of pass 2 (every lane / thread holds them).
+struct P2Result {
+  DD sT, sT2;
+  long long core;
+  bool bad_ni, bad_int;
+  double lapz;   // SITE_SCALAR block 4's first draw: the INT estimate's Z (vert-cor.R:188)
+};
+
+// The 10 SITE_SCALAR draws of one replicate in every lane of a wave (lanes 0-4 draw, shuffles).
+__device__ __forceinline__ void scalar_laplace_wave(uint32_t rep, uint32_t k0, uint32_t k1,
+                                                    double (&lap)[10]) {
+  const int lane = threadIdx.x & 63;
+  double a = 0.0, b = 0.0;
+  if (lane < 5) {
+    const U4 w = draw((uint32_t)lane, rep, DCOR_SITE_SCALAR, k0, k1);
+    a = unit_laplace(u53(w.w0, w.w1));
+    b = unit_laplace(u53(w.w2, w.w3));
+  }
+#pragma unroll
+  for (int q = 0; q < 5; ++q) {
+    lap[2 * q] = __shfl(a, q, 64);
+    lap[2 * q + 1] = __shfl(b, q, 64);
+  }
+}
+
+// WAVE = false: one 256-thread workgroup per replicate (barriers, LDS reductions); WAVE = true:
+// one wave per replicate (wave reductions only) -- the same arithmetic per batch and sample.
+template <int DGP, bool WAVE>
+__device__ __forceinline__ P2Result sign_pass2_core(const SignConst& c, uint32_t rep,
+                                                    const uint32_t* __restrict__ slab,
+                                                    const double* __restrict__ sums_in) {
+  constexpr int NT = WAVE ? 64 : DCOR_BLOCK;   // threads sharing the replicate
+  const int tid = WAVE ? (int)(threadIdx.x & 63) : (int)threadIdx.x;
+  double lap[10];
+  if constexpr (WAVE) {
+    scalar_laplace_wave(rep, c.k0, c.k1, lap);
+  } else {
+    __shared__ double lap_s[10];
+    scalar_laplace(rep, c.k0, c.k1, lap_s);
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 10; ++q) lap[q] = lap_s[q];
+  }
   SignStd s;
   {
     double l8[8];
@@ -564,15 +618,15 @@ __device__ __forceinline__ void sign_pass2_body(const SignConst& c, uint32_t rep
     uint4 a0[DCOR_P2_DEPTH], a1[DCOR_P2_DEPTH];
 #pragma unroll
     for (int d = 0; d < DCOR_P2_DEPTH; ++d) {
-      const int64_t jd = j + (int64_t)d * DCOR_BLOCK;
+      const int64_t jd = j + (int64_t)d * NT;
       a0[d] = a1[d] = make_uint4(0, 0, 0, 0);
       if (jd < c.k) {
         a0[d] = *reinterpret_cast<const uint4*>(slab + 8 * jd);
         a1[d] = *reinterpret_cast<const uint4*>(slab + 8 * jd + 4);
       }
     }
-    for (; j < c.k; j += DCOR_BLOCK) {
-      const int64_t jn = j + (int64_t)DCOR_P2_DEPTH * DCOR_BLOCK;
+    for (; j < c.k; j += NT) {
+      const int64_t jn = j + (int64_t)DCOR_P2_DEPTH * NT;
       const U4 w0{a0[0].x, a0[0].y, a0[0].z, a0[0].w}, w1{a1[0].x, a1[0].y, a1[0].z, a1[0].w};
 #pragma unroll
       for (int d = 0; d + 1 < DCOR_P2_DEPTH; ++d) { a0[d] = a0[d + 1]; a1[d] = a1[d + 1]; }
@@ -594,7 +648,7 @@ __device__ __forceinline__ void sign_pass2_body(const SignConst& c, uint32_t rep
       batch_T(j, cx, cy, std::true_type());
     }
   } else {
-    for (int64_t j = tid; j < c.k; j += DCOR_BLOCK) {
+    for (int64_t j = tid; j < c.k; j += NT) {
       int cx = 0, cy = 0, cc = 0;
       const int64_t i0 = j * c.m;
       bool any = false;
@@ -611,25 +665,52 @@ __device__ __forceinline__ void sign_pass2_body(const SignConst& c, uint32_t rep
       batch_T(j, cx, cy, std::false_type());
     }
   }
-  for (int64_t i = c.k * c.m + tid; i < c.n; i += DCOR_BLOCK) {  // tail: INT only
+  for (int64_t i = c.k * c.m + tid; i < c.n; i += NT) {  // tail: INT only
     int dx = 0, dy = 0, cc = 0;
     bool ignore = false;  // NI never reads the tail
     const uint32_t w = slab[i];
     if (fast(w, dx, dy, cc) || force_exact) fixup(i, w, dx, dy, cc, ignore);
     core += cc;
   }
-  DD d2[2] = {sT, sT2};
-  block_sum_dd<2>(d2, red);
-  core = block_sum_i(core, redi);
-  const long long nbad = block_sum_i((bad_ni ? 1LL : 0LL) + (bad_int ? (1LL << 20) : 0LL), redi);
-  if (tid == 0) {
+  P2Result r;
+  r.lapz = lap[8];
+  if constexpr (WAVE) {
+    r.sT = wave_sum_dd(sT);
+    r.sT2 = wave_sum_dd(sT2);
+    r.core = wave_sum_i(core);
+    r.bad_ni = __ballot(bad_ni) != 0;
+    r.bad_int = __ballot(bad_int) != 0;
+  } else {
+    __shared__ double red[16 * DCOR_WAVES];
+    __shared__ long long redi[DCOR_WAVES];
+    DD d2[2] = {sT, sT2};
+    block_sum_dd<2>(d2, red);
+    r.sT = d2[0];
+    r.sT2 = d2[1];
+    r.core = block_sum_i(core, redi);
+    const long long nbad = block_sum_i((bad_ni ? 1LL : 0LL) + (bad_int ? (1LL << 20) : 0LL), redi);
+    r.bad_ni = (nbad & 0xFFFFF) != 0;
+    r.bad_int = (nbad >> 20) != 0;
+  }
+  return r;
+}
+
+template <int DGP>
+__device__ __forceinline__ void sign_pass2_body(const SignConst& c, uint32_t rep,
+                                                const uint32_t* __restrict__ slab,
+                                                const double* __restrict__ sums_in,
+                                                SignPartial* __restrict__ part_out) {
+  const P2Result r = sign_pass2_core<DGP, false>(c, rep, slab, sums_in);
+  if (threadIdx.x == 0) {
     SignPartial p;
-    p.sT[0] = d2[0].hi; p.sT[1] = d2[0].lo; p.sT2[0] = d2[1].hi; p.sT2[1] = d2[1].lo;
-    p.core = core;
-    p.flags = ((nbad & 0xFFFFF) ? 1 : 0) | ((nbad >> 20) ? 2 : 0);
+    p.sT[0] = r.sT.hi; p.sT[1] = r.sT.lo; p.sT2[0] = r.sT2.hi; p.sT2[1] = r.sT2.lo;
+    p.core = r.core;
+    p.flags = (r.bad_ni ? 1 : 0) | (r.bad_int ? 2 : 0);
     *part_out = p;
   }
 }
+
+
 
 template <int DGP>
 __global__ __launch_bounds__(DCOR_BLOCK, DCOR_P2_WPE) void k_sign_pass2(SignConst c,
@@ -641,19 +722,16 @@ __global__ __launch_bounds__(DCOR_BLOCK, DCOR_P2_WPE) void k_sign_pass2(SignCons
                        sums + SIGN_SUMS * (size_t)blockIdx.x, part + blockIdx.x);
 }
 
-// Wave-per-replicate epilogue (four replicates per workgroup, no workgroup barriers):
-// NI estimate/CI, INT estimate, mixquant, INT CI (vert-cor.R:233-254, 186-194, 281-313).
+// The INT side and the record of one replicate from its pass-2 result, one wave: NI estimate/CI,
+// INT estimate, mixquant, INT CI (vert-cor.R:233-254, 186-194, 281-313).
 template <int VPL>
-__device__ __forceinline__ void sign_epilogue_wave(const SignConst& c, uint32_t rep,
-                                                   const SignPartial& p, dcor_rep_out* dst,
-                                                   WaveSel* ws) {
+__device__ __forceinline__ void sign_finish_wave(const SignConst& c, uint32_t rep, const P2Result& p,
+                                                 dcor_rep_out* dst, WaveSel* ws) {
   const int lane = threadIdx.x & 63;
-  const U4 wz = draw(4u, rep, DCOR_SITE_SCALAR, c.k0, c.k1);  // SCALAR block 4: Z (vert-cor.R:188)
-  const double lapz = unit_laplace(u53(wz.w0, wz.w1));
   double o[6];
-  ni_sign_result(c, DD{p.sT[0], p.sT[1]}, DD{p.sT2[0], p.sT2[1]}, (p.flags & 1) != 0, o);
+  ni_sign_result(c, p.sT, p.sT2, p.bad_ni, o);
   double rho, eta, se, cstar;
-  int_sign_point(c, p.core, lapz, rho, eta, se, cstar);
+  int_sign_point(c, p.core, p.lapz, rho, eta, se, cstar);
   double w;
   if (c.mode_normal)
     w = wave_mixquant_fused<VPL>(c.mix, cstar, rep, c.k0, c.k1, ws) * se;
@@ -662,8 +740,99 @@ __device__ __forceinline__ void sign_epilogue_wave(const SignConst& c, uint32_t 
   o[3] = rho;
   o[4] = sin(M_PI / 2.0 * rmax(eta - w, -1.0));
   o[5] = sin(M_PI / 2.0 * rmin(eta + w, 1.0));
-  if (p.flags & 2) o[3] = o[4] = o[5] = dnan();
+  if (p.bad_int) o[3] = o[4] = o[5] = dnan();
   if (lane == 0) *dst = dcor_rep_out{o[0], o[1], o[2], o[3], o[4], o[5]};
+}
+
+// Wave-per-replicate epilogue (four replicates per workgroup, no workgroup barriers) from the
+// SignPartial a workgroup-per-replicate pass 2 left.
+template <int VPL>
+__device__ __forceinline__ void sign_epilogue_wave(const SignConst& c, uint32_t rep,
+                                                   const SignPartial& sp, dcor_rep_out* dst,
+                                                   WaveSel* ws) {
+  const U4 wz = draw(4u, rep, DCOR_SITE_SCALAR, c.k0, c.k1);  // SCALAR block 4: Z (vert-cor.R:188)
+  P2Result p;
+  p.lapz = unit_laplace(u53(wz.w0, wz.w1));
+  p.sT = DD{sp.sT[0], sp.sT[1]};
+  p.sT2 = DD{sp.sT2[0], sp.sT2[1]};
+  p.core = sp.core;
+  p.bad_ni = (sp.flags & 1) != 0;
+  p.bad_int = (sp.flags & 2) != 0;
+  sign_finish_wave<VPL>(c, rep, p, dst, ws);
+}
+
+// ---- small cells (n <= SIGN_W_NMAX): one wave per replicate for both passes ------------------
+#ifndef DCOR_P2E_WPE
+#define DCOR_P2E_WPE 3  // waves per SIMD the pass 2 + epilogue wave kernel is compiled for
+#endif
+// At the reference grids' n (1000-12000) a 256-thread workgroup per replicate spends much of
+// its time in per-replicate fixed work -- the ziggurat table load, the scalar draws, the
+// barriers of its reductions.  Here pass 1 runs in persistent workgroups that load the table
+// once and give each wave one replicate at a time, and pass 2 and the epilogue are one wave
+// per replicate with wave reductions only.  Same per-sample and per-batch arithmetic as the
+// workgroup kernels; the sums are folded in a different (wave) order.
+template <int DGP>
+__device__ __forceinline__ void pass1_w_setup(double2* zt, uint32_t* zqn) {
+  if constexpr (DGP == DCOR_DGP_GAUSSIAN) {
+    for (int e = threadIdx.x; e < 2 * DCOR_ZIG_N; e += DCOR_BLOCK)
+      zt[e] = make_double2(dcor_zig_tab[e][0], dcor_zig_tab[e][1]);
+    if (threadIdx.x < DCOR_WAVES) zqn[threadIdx.x] = 0u;
+  }
+  __syncthreads();
+}
+
+template <int DGP>
+__global__ __launch_bounds__(DCOR_BLOCK) void k_sign_pass1_w(SignConst c, int64_t nreps,
+                                                             uint32_t* __restrict__ scratch,
+                                                             double* __restrict__ sums) {
+  __shared__ double2 zt[DGP == DCOR_DGP_GAUSSIAN ? 2 * DCOR_ZIG_N : 1];
+  __shared__ uint32_t zq[DCOR_WAVES][DGP == DCOR_DGP_GAUSSIAN ? ZQ_CAP : 1];
+  __shared__ uint32_t zqn[DCOR_WAVES];
+  pass1_w_setup<DGP>(zt, zqn);
+  const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  for (int64_t r = (int64_t)blockIdx.x * DCOR_WAVES + wv; r < nreps; r += (int64_t)gridDim.x * DCOR_WAVES)
+    sign_pass1_core<DGP, true>(c, (uint32_t)(c.rep_begin + r), scratch + (size_t)r * (size_t)c.n,
+                               sums + SIGN_SUMS * (size_t)r, zt, zq[wv], &zqn[wv]);
+}
+
+// Pass 2 alone, one wave per replicate, writing the SignPartial the wave epilogue reads.
+template <int DGP>
+__device__ __forceinline__ void sign_pass2_wave_part(const SignConst& c, uint32_t rep, const uint32_t* slab,
+                                                     const double* sums_in, SignPartial* part_out) {
+  const P2Result r = sign_pass2_core<DGP, true>(c, rep, slab, sums_in);
+  if ((threadIdx.x & 63) == 0) {
+    SignPartial p;
+    p.sT[0] = r.sT.hi; p.sT[1] = r.sT.lo; p.sT2[0] = r.sT2.hi; p.sT2[1] = r.sT2.lo;
+    p.core = r.core;
+    p.flags = (r.bad_ni ? 1 : 0) | (r.bad_int ? 2 : 0);
+    *part_out = p;
+  }
+}
+
+template <int DGP>
+__global__ __launch_bounds__(DCOR_BLOCK) void k_sign_pass2_w(SignConst c, int64_t nreps,
+                                                             const uint32_t* __restrict__ scratch,
+                                                             const double* __restrict__ sums,
+                                                             SignPartial* __restrict__ part) {
+  const int64_t r = (int64_t)blockIdx.x * DCOR_WAVES + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  if (r >= nreps) return;
+  sign_pass2_wave_part<DGP>(c, (uint32_t)(c.rep_begin + r), scratch + (size_t)r * (size_t)c.n,
+                            sums + SIGN_SUMS * (size_t)r, part + r);
+}
+
+template <int DGP, int VPL>
+__global__ __launch_bounds__(DCOR_BLOCK, DCOR_P2E_WPE) void k_sign_p2e_w(SignConst c, int64_t nreps,
+                                                           const uint32_t* __restrict__ scratch,
+                                                           const double* __restrict__ sums,
+                                                           dcor_rep_out* out) {
+  __shared__ WaveSel wsel[DCOR_WAVES];
+  const int wv = threadIdx.x >> 6;
+  const int64_t r = (int64_t)blockIdx.x * DCOR_WAVES + __builtin_amdgcn_readfirstlane(wv);
+  if (r >= nreps) return;  // whole waves only
+  const uint32_t rep = (uint32_t)(c.rep_begin + r);
+  const P2Result p = sign_pass2_core<DGP, true>(c, rep, scratch + (size_t)r * (size_t)c.n,
+                                                sums + SIGN_SUMS * (size_t)r);
+  sign_finish_wave<VPL>(c, rep, p, out + r, &wsel[wv]);
 }
 
 template <int VPL>
@@ -1191,6 +1360,55 @@ __global__ __launch_bounds__(DCOR_BLOCK) void k_grid_sign_epilogue(const SignCon
   sign_epilogue_wave<VPL>(cells[it.cell], it.rep, part[r], out + it.out, &wsel[threadIdx.x >> 6]);
 }
 
+// Small cells (n <= SIGN_W_NMAX): wave-per-replicate pass 1 (persistent workgroups) and pass 2 +
+// epilogue over the work items.
+template <int DGP>
+__global__ __launch_bounds__(DCOR_BLOCK) void k_grid_sign_pass1_w(const SignConst* __restrict__ cells,
+                                                                  const GridItem* __restrict__ items,
+                                                                  int64_t nitems,
+                                                                  uint32_t* __restrict__ scratch,
+                                                                  double* __restrict__ sums) {
+  __shared__ double2 zt[DGP == DCOR_DGP_GAUSSIAN ? 2 * DCOR_ZIG_N : 1];
+  __shared__ uint32_t zq[DCOR_WAVES][DGP == DCOR_DGP_GAUSSIAN ? ZQ_CAP : 1];
+  __shared__ uint32_t zqn[DCOR_WAVES];
+  pass1_w_setup<DGP>(zt, zqn);
+  const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  for (int64_t r = (int64_t)blockIdx.x * DCOR_WAVES + wv; r < nitems; r += (int64_t)gridDim.x * DCOR_WAVES) {
+    const GridItem it = items[r];
+    sign_pass1_core<DGP, true>(cells[it.cell], it.rep, scratch + it.scratch, sums + SIGN_SUMS * (size_t)r,
+                               zt, zq[wv], &zqn[wv]);
+  }
+}
+
+template <int DGP>
+__global__ __launch_bounds__(DCOR_BLOCK) void k_grid_sign_pass2_w(const SignConst* __restrict__ cells,
+                                                                  const GridItem* __restrict__ items,
+                                                                  int64_t nitems,
+                                                                  const uint32_t* __restrict__ scratch,
+                                                                  const double* __restrict__ sums,
+                                                                  SignPartial* __restrict__ part) {
+  const int64_t r = wave_item();
+  if (r >= nitems) return;
+  const GridItem it = items[r];
+  sign_pass2_wave_part<DGP>(cells[it.cell], it.rep, scratch + it.scratch, sums + SIGN_SUMS * (size_t)r, part + r);
+}
+
+template <int DGP, int VPL>
+__global__ __launch_bounds__(DCOR_BLOCK, DCOR_P2E_WPE) void k_grid_sign_p2e_w(const SignConst* __restrict__ cells,
+                                                                const GridItem* __restrict__ items,
+                                                                int64_t nitems,
+                                                                const uint32_t* __restrict__ scratch,
+                                                                const double* __restrict__ sums,
+                                                                dcor_rep_out* out) {
+  __shared__ WaveSel wsel[DCOR_WAVES];
+  const int64_t r = wave_item();
+  if (r >= nitems) return;  // whole waves only
+  const GridItem it = items[r];
+  const SignConst& c = cells[it.cell];
+  const P2Result p = sign_pass2_core<DGP, true>(c, it.rep, scratch + it.scratch, sums + SIGN_SUMS * (size_t)r);
+  sign_finish_wave<VPL>(c, it.rep, p, out + it.out, &wsel[threadIdx.x >> 6]);
+}
+
 template <int DGP>
 __global__ __launch_bounds__(DCOR_BLOCK) void k_grid_sign_regen(const SignConst* __restrict__ cells,
                                                                 const GridItem* __restrict__ items,
@@ -1280,6 +1498,53 @@ int launch_grid_sign_codes(int dgp, const SignConst* cells, const GridItem* item
   return last_err();
 }
 
+// persistent pass-1 workgroups: at most 8 per CU of the largest part (256 CUs)
+static inline unsigned persistent_groups(int64_t nitems) {
+  const unsigned g = wave_groups(nitems);
+  return g < 2048u ? g : 2048u;
+}
+
+static bool p2e_fused() {
+  static const bool v = [] {
+    const char* e = std::getenv("DCOR_SIGN_P2E");
+    return e && std::strcmp(e, "1") == 0;
+  }();
+  return v;
+}
+
+template <int DGP>
+static void grid_codes_w_t(const SignConst* cells, const GridItem* items, int64_t nitems, uint32_t* scratch,
+                           double* sums, int vpl32, dcor_rep_out* out, hipStream_t st) {
+  hipLaunchKernelGGL(k_grid_sign_pass1_w<DGP>, dim3(persistent_groups(nitems)), dim3(DCOR_BLOCK), 0, st, cells,
+                     items, nitems, scratch, sums);
+  if (!p2e_fused()) {
+    SignPartial* part = reinterpret_cast<SignPartial*>(sums + SIGN_SUMS * nitems);
+    hipLaunchKernelGGL(k_grid_sign_pass2_w<DGP>, dim3(wave_groups(nitems)), dim3(DCOR_BLOCK), 0, st, cells,
+                       items, nitems, scratch, sums, part);
+    launch_grid_epilogue(cells, items, nitems, part, vpl32, out, st);
+    return;
+  }
+  if (vpl32)
+    hipLaunchKernelGGL((k_grid_sign_p2e_w<DGP, 32>), dim3(wave_groups(nitems)), dim3(DCOR_BLOCK), 0, st, cells,
+                       items, nitems, scratch, sums, out);
+  else
+    hipLaunchKernelGGL((k_grid_sign_p2e_w<DGP, 16>), dim3(wave_groups(nitems)), dim3(DCOR_BLOCK), 0, st, cells,
+                       items, nitems, scratch, sums, out);
+}
+
+int launch_grid_sign_codes_w(int dgp, const SignConst* cells, const GridItem* items, int64_t nitems,
+                             uint32_t* scratch, double* sums, int vpl32, dcor_rep_out* out, void* stream) {
+  if (nitems <= 0) return 0;
+  const hipStream_t st = (hipStream_t)stream;
+  switch (dgp) {
+    case DCOR_DGP_GAUSSIAN: grid_codes_w_t<DCOR_DGP_GAUSSIAN>(cells, items, nitems, scratch, sums, vpl32, out, st); break;
+    case DCOR_DGP_BERNOULLI: grid_codes_w_t<DCOR_DGP_BERNOULLI>(cells, items, nitems, scratch, sums, vpl32, out, st); break;
+    case DCOR_DGP_MIX_GAUSSIAN: grid_codes_w_t<DCOR_DGP_MIX_GAUSSIAN>(cells, items, nitems, scratch, sums, vpl32, out, st); break;
+    default: grid_codes_w_t<DCOR_DGP_BOUNDED_FACTOR>(cells, items, nitems, scratch, sums, vpl32, out, st);
+  }
+  return last_err();
+}
+
 int launch_grid_sign_regen(int dgp, const SignConst* cells, const GridItem* items, int64_t nitems,
                            dcor_rep_out* out, void* stream) {
   if (nitems <= 0) return 0;
@@ -1358,6 +1623,23 @@ static int launch_codes_t(SignConst c, int64_t reps, int64_t chunk, const CodesB
     const int64_t nr = (reps - r < chunk) ? reps - r : chunk;
     const int b = two ? (int)(t & 1) : 0;
     c.rep_begin = rep0 + r;
+    if (c.n <= SIGN_W_NMAX) {   // small cells: the wave-per-replicate kernels (as the grid runs them)
+      hipLaunchKernelGGL(k_sign_pass1_w<DGP>, dim3(persistent_groups(nr)), dim3(DCOR_BLOCK), 0, st[b], c, nr,
+                         bf.slab[b], bf.sums[b]);
+      if (!p2e_fused()) {
+        SignPartial* part = reinterpret_cast<SignPartial*>(bf.sums[b] + SIGN_SUMS * chunk);
+        hipLaunchKernelGGL(k_sign_pass2_w<DGP>, dim3(wave_groups(nr)), dim3(DCOR_BLOCK), 0, st[b], c, nr,
+                           bf.slab[b], bf.sums[b], part);
+        launch_sign_epilogue(c, nr, part, out + r, st[b]);
+      } else if (c.mix.nsim > 1024)
+        hipLaunchKernelGGL((k_sign_p2e_w<DGP, 32>), dim3(wave_groups(nr)), dim3(DCOR_BLOCK), 0, st[b], c, nr,
+                           bf.slab[b], bf.sums[b], out + r);
+      else
+        hipLaunchKernelGGL((k_sign_p2e_w<DGP, 16>), dim3(wave_groups(nr)), dim3(DCOR_BLOCK), 0, st[b], c, nr,
+                           bf.slab[b], bf.sums[b], out + r);
+      if (int e = last_err()) return e;
+      continue;
+    }
     SignPartial* part = reinterpret_cast<SignPartial*>(bf.sums[b] + SIGN_SUMS * chunk);
     hipLaunchKernelGGL(k_sign_pass1<DGP>, dim3((unsigned)nr), dim3(DCOR_BLOCK), 0, st[b], c,
                        bf.slab[b], bf.sums[b]);

@@ -47,9 +47,11 @@ size_t env_size(const char* name, size_t dflt, int shift) {
   return v > 0 ? (size_t)v << shift : dflt;
 }
 
+bool codes_kind(int kind) { return kind == GK_SIGN_CODES || kind == GK_SIGN_CODES_W; }
+
 uint64_t item_scratch(int kind, int64_t n) {
   // code slabs start on 256-B boundaries (the kernels move records 16 B at a time)
-  if (kind == GK_SIGN_CODES) return ((uint64_t)n + 63) & ~(uint64_t)63;   // u32 records
+  if (codes_kind(kind)) return ((uint64_t)n + 63) & ~(uint64_t)63;   // u32 records
   if (kind == GK_SIGN_BERN) return (uint64_t)3 * 4 * ((n + 255) / 256);  // u64 plane words
   return 0;
 }
@@ -70,7 +72,8 @@ struct Group {
   std::vector<GridPiece> pieces;
   std::vector<size_t> chunk_p;             // first piece of each chunk (+ end sentinel)
   std::vector<uint64_t> chunk_items;       // items per chunk
-  size_t tab_off = 0, piece_off = 0;       // byte offsets in the uploaded table block
+  std::vector<uint64_t> chunk_base;        // first item of each chunk in the exec's item table
+  size_t tab_off = 0;                      // byte offset of the constants in the uploaded block
 };
 
 // The kernels of a set of ranges on `st0` (plus the context's auxiliary stream for the one-pass
@@ -97,6 +100,30 @@ int exec_ranges(const dcor_cell* cells, const std::vector<CellPlan>& cp, const s
   // chunk state per group while pieces are laid out
   struct Fill { uint64_t items = 0, used = 0; };
   std::map<std::tuple<int, int, int>, Fill> fill;
+  // per-group chunk limits: the scratch budget and the item cap, and for the one-pass sign
+  // kernels at least DCOR_GRID_MIN_CHUNKS (default 4) equal chunks once there are 2048 items, so
+  // pass 2 (latency-bound) of one chunk runs beside pass 1 (VALU-bound) of the next on the two
+  // streams -- at the reference grids' n (1000-12000) pass 2 costs as much as pass 1
+  struct Lim { uint64_t items = 0, scratch = 0, cap_items = 0, cap_scr = 0; };
+  std::map<std::tuple<int, int, int>, Lim> lim;
+  const uint64_t min_chunks = env_size("DCOR_GRID_MIN_CHUNKS", 4, 0);
+  for (const Range& r : ranges) {
+    const CellPlan& p = cp[(size_t)r.cell];
+    if (r.count == 0 || p.nan_dgp) continue;
+    Lim& l = lim[std::make_tuple(p.kind, p.dgp, p.vpl32)];
+    l.items += (uint64_t)r.count;
+    l.scratch += (uint64_t)r.count * item_scratch(p.kind, cells[r.cell].n) * (p.kind == GK_SIGN_BERN ? 2 : 1);
+  }
+  for (auto& kv : lim) {
+    Lim& l = kv.second;
+    l.cap_items = item_cap;
+    l.cap_scr = budget_el;
+    if (codes_kind(std::get<0>(kv.first)) && l.items >= 2048 && min_chunks > 1) {
+      uint64_t nch = std::max<uint64_t>(min_chunks, (l.scratch + budget_el - 1) / budget_el);
+      nch = std::max<uint64_t>(nch, (l.items + item_cap - 1) / item_cap);
+      l.cap_items = std::min<uint64_t>(item_cap, (l.items + nch - 1) / nch);
+    }
+  }
   for (int q : order) {
     const Range& r = ranges[(size_t)q];
     const CellPlan& p = cp[(size_t)r.cell];
@@ -124,11 +151,12 @@ int exec_ranges(const dcor_cell* cells, const std::vector<CellPlan>& cp, const s
     const int64_t n = cells[r.cell].n;
     const uint64_t need = item_scratch(p.kind, n);
     const uint64_t unit = (p.kind == GK_SIGN_BERN) ? 2 : 1;
+    const Lim& lm = lim[key];
     int64_t done = 0;
     while (done < r.count) {
       uint64_t fit = (uint64_t)(r.count - done);
-      fit = std::min<uint64_t>(fit, item_cap - f.items);
-      if (need) fit = std::min<uint64_t>(fit, (budget_el / unit - f.used) / need);
+      fit = std::min<uint64_t>(fit, lm.cap_items - f.items);
+      if (need) fit = std::min<uint64_t>(fit, (lm.cap_scr / unit - f.used) / need);
       if (fit == 0) {   // chunk full: close it (a fresh chunk always takes >= 1024 items)
         if (f.items == 0) return fail(DCOR_EINVAL, "grid: a replicate of cell %d exceeds the scratch budget", r.cell);
         g.chunk_items.push_back(f.items);
@@ -143,7 +171,9 @@ int exec_ranges(const dcor_cell* cells, const std::vector<CellPlan>& cp, const s
       done += (int64_t)fit;
     }
   }
-  size_t max_items = 1, max_scr_b = 0, max_sums_b = 0, ncodes_chunks = 0;
+  size_t max_scr_b = 0, max_sums_b = 0, ncodes_chunks = 0;
+  uint64_t tot_items = 0;   // every chunk's items, one table expanded by one launch
+  std::vector<GridPiece> all_pieces;
   for (auto& kv : groups) {
     Group& g = kv.second;
     const Fill& f = fill[kv.first];
@@ -153,35 +183,42 @@ int exec_ranges(const dcor_cell* cells, const std::vector<CellPlan>& cp, const s
     }
     for (size_t c = 0; c + 1 < g.chunk_p.size(); ++c) {
       const uint64_t ni = g.chunk_items[c];
-      max_items = std::max<size_t>(max_items, ni);
+      g.chunk_base.push_back(tot_items);
+      for (size_t q = g.chunk_p[c]; q < g.chunk_p[c + 1]; ++q) {
+        GridPiece pc = g.pieces[q];
+        pc.item0 += tot_items;
+        all_pieces.push_back(pc);
+      }
+      tot_items += ni;
       uint64_t used = 0;
       for (size_t q = g.chunk_p[c]; q < g.chunk_p[c + 1]; ++q) used += g.pieces[q].count * g.pieces[q].scr_stride;
       max_scr_b = std::max<size_t>(max_scr_b, used * (g.kind == GK_SIGN_BERN ? 8 : 4));
       if (g.kind == GK_SIGN_CODES)
         max_sums_b = std::max<size_t>(max_sums_b, ni * (SIGN_SUMS * sizeof(double) + SIGN_PARTIAL_BYTES));
+      else if (g.kind == GK_SIGN_CODES_W)   // the partials too (the unfused wave pass 2)
+        max_sums_b = std::max<size_t>(max_sums_b, ni * (SIGN_SUMS * sizeof(double) + SIGN_PARTIAL_BYTES));
       else if (g.kind == GK_SIGN_BERN || g.kind == GK_SIGN_BERN_W)
         max_sums_b = std::max<size_t>(max_sums_b, ni * SIGN_PARTIAL_BYTES);
     }
-    if (g.kind == GK_SIGN_CODES) ncodes_chunks += g.chunk_p.size() - 1;
+    if (codes_kind(g.kind)) ncodes_chunks += g.chunk_p.size() - 1;
   }
-  // ---- the table block: per group its constants and pieces; then the caller's extra tables
+  // ---- the table block: per group its constants; every piece; then the caller's extra tables
   size_t tb = 0;
   for (auto& kv : groups) {
     Group& g = kv.second;
     g.tab_off = tb;
     tb += al256(g.kind == GK_SUBG ? g.subg.size() * sizeof(SubgConst) : g.sign.size() * sizeof(SignConst));
-    g.piece_off = tb;
-    tb += al256(g.pieces.size() * sizeof(GridPiece));
   }
+  const size_t piece_off = tb;
+  tb += al256(all_pieces.size() * sizeof(GridPiece));
   const size_t extra_off = tb;
   tb += al256(extra_b);
   tb = std::max<size_t>(tb, 256);
   const bool two = ncodes_chunks > 1 && !(std::getenv("DCOR_SIGN_PIPELINE") &&
                                          std::strcmp(std::getenv("DCOR_SIGN_PIPELINE"), "0") == 0);
   const int nslot = two ? 2 : 1;
-  const size_t items_one = al256(max_items * sizeof(GridItem));
   const size_t sums_one = al256(std::max<size_t>(max_sums_b, 8));
-  const size_t items_off = al256(tb), sums_off = items_off + (size_t)nslot * items_one;
+  const size_t items_off = al256(tb), sums_off = items_off + al256(std::max<uint64_t>(tot_items, 1) * sizeof(GridItem));
   const size_t total = sums_off + (size_t)nslot * sums_one;
   void* garena = nullptr;
   if (int st = arena_grow(ctx->grid, total, &garena)) return st;
@@ -200,14 +237,17 @@ int exec_ranges(const dcor_cell* cells, const std::vector<CellPlan>& cp, const s
     const Group& g = kv.second;
     if (g.kind == GK_SUBG) std::memcpy(hs + g.tab_off, g.subg.data(), g.subg.size() * sizeof(SubgConst));
     else std::memcpy(hs + g.tab_off, g.sign.data(), g.sign.size() * sizeof(SignConst));
-    std::memcpy(hs + g.piece_off, g.pieces.data(), g.pieces.size() * sizeof(GridPiece));
   }
+  std::memcpy(hs + piece_off, all_pieces.data(), all_pieces.size() * sizeof(GridPiece));
   if (extra_b) std::memcpy(hs + extra_off, extra, extra_b);
   char* dg = (char*)garena;
   HIPCHK(hipMemcpyAsync(dg, hs, tb, hipMemcpyHostToDevice, st0));
   HIPCHK(hipEventRecord(stg.done, st0));
   if (extra_dev) *extra_dev = dg + extra_off;
-  // ---- launches: per chunk, expand the items, then the family's kernels
+  // ---- launches: one expansion of every chunk's items, then per chunk the family's kernels
+  GridItem* items_all = (GridItem*)(dg + items_off);
+  if (int rc = launch_grid_expand((const GridPiece*)(dg + piece_off), (int64_t)all_pieces.size(), items_all, st0))
+    return hip_fail((hipError_t)rc, "grid item expansion");
   Pipe* pp = nullptr;
   hipStream_t sts[2] = {st0, st0};
   if (two) {
@@ -221,15 +261,16 @@ int exec_ranges(const dcor_cell* cells, const std::vector<CellPlan>& cp, const s
     const Group& g = kv.second;
     const SignConst* dsign = (const SignConst*)(dg + g.tab_off);
     const SubgConst* dsubg = (const SubgConst*)(dg + g.tab_off);
-    const GridPiece* dpieces = (const GridPiece*)(dg + g.piece_off);
     for (size_t c = 0; c + 1 < g.chunk_p.size(); ++c) {
       const int64_t nit = (int64_t)g.chunk_items[c];
-      const int b = (two && g.kind == GK_SIGN_CODES) ? (int)(tcodes++ & 1) : 0;
-      GridItem* items = (GridItem*)(dg + items_off + (size_t)b * items_one);
+      const int b = (two && codes_kind(g.kind)) ? (int)(tcodes++ & 1) : 0;
+      const GridItem* items = items_all + g.chunk_base[c];
       char* sums = dg + sums_off + (size_t)b * sums_one;
-      int rc = launch_grid_expand(dpieces + g.chunk_p[c], (int64_t)(g.chunk_p[c + 1] - g.chunk_p[c]), items, sts[b]);
-      if (rc) return hip_fail((hipError_t)rc, "grid item expansion");
-      if (g.kind == GK_SIGN_CODES) {
+      int rc = 0;
+      if (g.kind == GK_SIGN_CODES_W) {
+        rc = launch_grid_sign_codes_w(g.dgp, dsign, items, nit, (uint32_t*)((char*)scr + (size_t)b * slab_one),
+                                      (double*)sums, g.vpl32, d_out, sts[b]);
+      } else if (g.kind == GK_SIGN_CODES) {
         rc = launch_grid_sign_codes(g.dgp, dsign, items, nit, (uint32_t*)((char*)scr + (size_t)b * slab_one),
                                     (double*)sums, (SignPartial*)(sums + SIGN_SUMS * sizeof(double) * (size_t)nit),
                                     g.vpl32, d_out, sts[b]);
@@ -433,8 +474,14 @@ int run_shard(const dcor_cell* cells, int ncells, int64_t B, dcor_rep_out* h_det
     if (int rc = launch_accumulate_merge_cells((const AccCell*)dm, (int)multi.size(), (const dcor_accum*)part, d_acc, st))
       return hip_fail((hipError_t)rc, "grid accumulate merge");
   }
-  if (nb > 0) {
-    HIPCHK(hipMemcpyAsync(s.acc.data(), d_acc, s.acc.size() * sizeof(dcor_accum), hipMemcpyDeviceToHost, st));
+  if (nb > 0) {   // through pinned memory: a pageable D2H copy would stage and block
+    void* ha = nullptr;
+    const size_t ab = s.acc.size() * sizeof(dcor_accum);
+    if (int e = pinned_grow(ctx->hacc, ab, &ha)) return e;
+    HIPCHK(hipMemcpyAsync(ha, d_acc, ab, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipEventRecord(ctx->hacc.done, st));
+    HIPCHK(hipStreamSynchronize(st));
+    std::memcpy(s.acc.data(), ha, ab);
   }
   HIPCHK(hipStreamSynchronize(st));
   return DCOR_OK;

@@ -47,7 +47,17 @@ def short(name):
     return name.split("(")[0].replace("void ", "").strip()
 
 
-out = {"kernels": {}}
+sys.path.insert(0, root)
+from bench import src_sha16  # noqa: E402
+import subprocess  # noqa: E402
+try:
+    head = subprocess.run(["git", "-C", root, "rev-parse", "--short=12", "HEAD"], capture_output=True,
+                          text=True, check=True).stdout.strip()
+except (OSError, subprocess.CalledProcessError):
+    head = None
+# the tree this summary describes: the committed head it was profiled at and the hash of the engine
+# sources (bench.py compares the hash with its own tree's: roofline.*_source_fresh)
+out = {"kernels": {}, "git_head": os.environ.get("PROF_HEAD", head), "src_sha16": src_sha16(root)}
 stats = os.path.join(src, "prof_trace", "run_kernel_stats.csv")
 if os.path.exists(stats):
     shutil.copy(stats, os.path.join(dst, f"{tag}_kernel_stats.csv"))
@@ -120,6 +130,7 @@ if os.path.exists(trace):
 
 json.dump(out, open(os.path.join(dst, f"{tag}_summary.json"), "w"), indent=1, sort_keys=True)
 lines = [f"# rocprofv3 summary `{tag}`", "",
+         f"Profiled at git head `{out['git_head']}` (engine sources sha256 `{out['src_sha16']}`).", "",
          "| kernel | calls | avg µs | % time | VGPR | HBM read B (corr.) | HBM write B | VALU active / wave-cycles | VALU instr / CU-cycle | VALU time / SIMD-cycles | VALUBusy | clock GHz |",
          "|---|---|---|---|---|---|---|---|---|---|---|---|"]
 for kname, k in sorted(out["kernels"].items(), key=lambda kv: -kv[1].get("pct_time", 0)):
