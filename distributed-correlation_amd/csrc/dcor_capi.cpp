@@ -491,7 +491,8 @@ int prepare_cell(const dcor_cell& c, CellPlan& p) {
                            NAN, NAN, c.nsim, k, nullptr, nullptr)) return st;
     k.g = g;
     k.k0 = (uint32_t)c.seed; k.k1 = (uint32_t)(c.seed >> 32);
-    p.kind = GK_SUBG;
+    p.kind = c.n <= SUBG_W_NMAX ? GK_SUBG_W : GK_SUBG;
+    p.vpl32 = k.mix.nsim > 1024 ? 1 : 0;
   } else {
     return fail(DCOR_EINVAL, "unknown family %d", c.family);
   }
@@ -613,7 +614,7 @@ int dcor_sim_launch(const dcor_cell* cell, int64_t rep_begin, int64_t rep_count,
     return DCOR_OK;
   }
   int rc;
-  if (cp.kind == GK_SUBG) {
+  if (cp.kind == GK_SUBG || cp.kind == GK_SUBG_W) {
     SubgConst k = cp.subg;
     k.rep_begin = rep_begin;
     rc = launch_subg_fused(k, rep_count, d_out, stream);

@@ -644,13 +644,34 @@ __device__ __forceinline__ double wave_select(const double (&v)[VPL], int pos, W
       const int bits = 64 - __clzll((long long)d);
       bm.sh = bits > 8 ? bits - 8 : 0;
     }
+    // every active key's bin, once per round, packed 4 per register (the round's three uses read
+    // these: computing bm() at each use kept both mappings' temporaries live, ~180 VGPRs); the
+    // mapping is wave-uniform, so one branch picks it for all keys
+    uint32_t pk[(VPL + 3) / 4];
+#pragma unroll
+    for (int q = 0; q < (VPL + 3) / 4; ++q) pk[q] = 0u;
+    if (bm.by_value) {
+#pragma unroll
+      for (int s = 0; s < VPL; ++s) {
+        const double t = (0.5 * v[s] - 0.5 * lo) * bm.scale;
+        const uint32_t b = t < 255.0 ? (uint32_t)(int)t : 255u;
+        pk[s >> 2] |= (((act >> s) & 1u) ? b : 0u) << (8 * (s & 3));
+      }
+    } else {
+#pragma unroll
+      for (int s = 0; s < VPL; ++s) {
+        const uint32_t b = (uint32_t)((sel_key(v[s]) - bm.klo) >> bm.sh);
+        pk[s >> 2] |= (((act >> s) & 1u) ? (b & 255u) : 0u) << (8 * (s & 3));
+      }
+    }
+    auto bin = [&](int s) -> int { return (int)((pk[s >> 2] >> (8 * (s & 3))) & 255u); };
 #pragma unroll
     for (int q = 0; q < 4; ++q) ws->hist[4 * lane + q] = 0u;
     if (lane == 0) ws->ncand = 0;
     wave_sync();
 #pragma unroll
     for (int s = 0; s < VPL; ++s)
-      if ((act >> s) & 1u) atomicAdd(&ws->hist[bm(v[s])], 1u);
+      if ((act >> s) & 1u) atomicAdd(&ws->hist[bin(s)], 1u);
     wave_sync();
     uint32_t hb[4], s4 = 0;
 #pragma unroll
@@ -679,7 +700,7 @@ __device__ __forceinline__ double wave_select(const double (&v)[VPL], int pos, W
     if (cnt <= 64) {  // rank the bin's keys directly
 #pragma unroll
       for (int s = 0; s < VPL; ++s)
-        if (((act >> s) & 1u) && bm(v[s]) == B) ws->cand[atomicAdd(&ws->ncand, 1)] = v[s];
+        if (((act >> s) & 1u) && bin(s) == B) ws->cand[atomicAdd(&ws->ncand, 1)] = v[s];
       wave_sync();
       if ((uint32_t)lane < cnt) {
         const double x = ws->cand[lane];
@@ -697,7 +718,142 @@ __device__ __forceinline__ double wave_select(const double (&v)[VPL], int pos, W
     }
     uint32_t keep = 0;  // the crowded bin becomes the active set
 #pragma unroll
-    for (int s = 0; s < VPL; ++s) keep |= (bm(v[s]) == B ? 1u : 0u) << s;
+    for (int s = 0; s < VPL; ++s) keep |= (bin(s) == B ? 1u : 0u) << s;
+    act &= keep;
+    k = (int)kk;
+  }
+  return dnan();
+}
+
+
+// The same order statistic over keys kept in LDS (keys[lane + 64 s], s < VPL; NaN = absent):
+// only the per-round bins (8 bits a key, packed) and the active mask live in registers, so an
+// epilogue that generates its keys and selects runs at 4-5 waves per SIMD instead of the 2 the
+// register-resident select allows (its 16 keys and their per-round temporaries take ~170 VGPRs).
+struct WaveSelL {
+  uint32_t hist[256];
+  double cand[64];
+  int ncand;
+  int pad;
+  double res;
+};
+
+template <int VPL>
+__device__ __forceinline__ double wave_select_lds(const double* kv, int pos, WaveSelL* ws) {
+  static_assert(VPL <= 32, "active keys are a 32-bit mask per lane");
+  const int lane = threadIdx.x & 63;
+  const double INF = __longlong_as_double(0x7FF0000000000000LL);
+  auto key = [&](int s) -> double { return kv[lane + 64 * s]; };
+  uint32_t act = 0;
+#pragma unroll
+  for (int s = 0; s < VPL; ++s) { const double x = key(s); act |= (x == x ? 1u : 0u) << s; }
+  const int nact = wave_sum_int(__popc(act));
+  int k = pos;
+  if (k < 0 || k >= nact) return dnan();
+  {  // peel -inf / +inf keys (binning needs a finite range)
+    uint32_t mlo = 0, mhi = 0;
+#pragma unroll
+    for (int s = 0; s < VPL; ++s) {
+      const double x = key(s);
+      mlo |= (x == -INF ? 1u : 0u) << s;
+      mhi |= (x == INF ? 1u : 0u) << s;
+    }
+    const int nlo = wave_sum_int(__popc(mlo)), nhi = wave_sum_int(__popc(mhi));
+    if (k < nlo) return -INF;
+    if (k >= nact - nhi) return INF;
+    act &= ~(mlo | mhi);
+    k -= nlo;
+  }
+  for (int iter = 0; iter < 80; ++iter) {
+    double lo = INF, hi = -INF;
+#pragma unroll
+    for (int s = 0; s < VPL; ++s)
+      if ((act >> s) & 1u) { const double x = key(s); lo = fmin(lo, x); hi = fmax(hi, x); }
+    lo = wave_min(lo);
+    hi = wave_max(hi);
+    if (!(hi > lo)) return lo;  // every active key equal
+    const double h = 0.5 * hi - 0.5 * lo;
+    const double scale = 128.0 / h;
+    const bool by_value = (h > 0.0) && (scale < INF);
+    const unsigned long long klo = sel_key(lo);
+    int sh;
+    {
+      const unsigned long long d = sel_key(hi) - klo;
+      const int bits = 64 - __clzll((long long)d);
+      sh = bits > 8 ? bits - 8 : 0;
+    }
+    uint32_t pk[(VPL + 3) / 4];
+#pragma unroll
+    for (int q = 0; q < (VPL + 3) / 4; ++q) pk[q] = 0u;
+    if (by_value) {   // the BinMap of wave_select, one uniform branch per round
+#pragma unroll
+      for (int s = 0; s < VPL; ++s) {
+        const double t = (0.5 * key(s) - 0.5 * lo) * scale;
+        const uint32_t b = t < 255.0 ? (uint32_t)(int)t : 255u;
+        pk[s >> 2] |= (((act >> s) & 1u) ? b : 0u) << (8 * (s & 3));
+      }
+    } else {
+#pragma unroll
+      for (int s = 0; s < VPL; ++s) {
+        const uint32_t b = (uint32_t)((sel_key(key(s)) - klo) >> sh);
+        pk[s >> 2] |= (((act >> s) & 1u) ? (b & 255u) : 0u) << (8 * (s & 3));
+      }
+    }
+    auto bin = [&](int s) -> int { return (int)((pk[s >> 2] >> (8 * (s & 3))) & 255u); };
+#pragma unroll
+    for (int q = 0; q < 4; ++q) ws->hist[4 * lane + q] = 0u;
+    if (lane == 0) ws->ncand = 0;
+    wave_sync();
+#pragma unroll
+    for (int s = 0; s < VPL; ++s)
+      if ((act >> s) & 1u) atomicAdd(&ws->hist[bin(s)], 1u);
+    wave_sync();
+    uint32_t hb[4], s4 = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) { hb[q] = ws->hist[4 * lane + q]; s4 += hb[q]; }
+    uint32_t inc = s4;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t t = __shfl_up(inc, o, 64);
+      if (lane >= o) inc += t;
+    }
+    const uint32_t ex = inc - s4;
+    int B = -1;
+    uint32_t cnt = 0, kk = 0;
+    if ((uint32_t)k >= ex && (uint32_t)k < inc) {
+      uint32_t base = ex;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        if (B < 0 && (uint32_t)k < base + hb[q]) { B = 4 * lane + q; cnt = hb[q]; kk = (uint32_t)k - base; }
+        base += hb[q];
+      }
+    }
+    const int owner = __ffsll((long long)__ballot(B >= 0)) - 1;
+    B = __shfl(B, owner, 64);
+    cnt = __shfl(cnt, owner, 64);
+    kk = __shfl(kk, owner, 64);
+    if (cnt <= 64) {  // rank the bin's keys directly
+#pragma unroll
+      for (int s = 0; s < VPL; ++s)
+        if (((act >> s) & 1u) && bin(s) == B) ws->cand[atomicAdd(&ws->ncand, 1)] = key(s);
+      wave_sync();
+      if ((uint32_t)lane < cnt) {
+        const double x = ws->cand[lane];
+        uint32_t r = 0;
+        for (uint32_t j = 0; j < cnt; ++j) {
+          const double y = ws->cand[j];
+          r += (y < x) || (y == x && j < (uint32_t)lane);
+        }
+        if (r == kk) ws->res = x;
+      }
+      wave_sync();
+      const double res = ws->res;
+      wave_sync();
+      return res;
+    }
+    uint32_t keep = 0;  // the crowded bin becomes the active set
+#pragma unroll
+    for (int s = 0; s < VPL; ++s) keep |= (bin(s) == B ? 1u : 0u) << s;
     act &= keep;
     k = (int)kk;
   }

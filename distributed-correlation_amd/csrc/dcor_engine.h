@@ -163,7 +163,9 @@ struct GridPiece {
 };
 int launch_grid_expand(const GridPiece* pieces, int64_t npieces, GridItem* items, void* stream);
 enum GridKind { GK_SIGN_CODES = 0, GK_SIGN_REGEN = 1, GK_SIGN_BERN_W = 2, GK_SIGN_BERN = 3, GK_SUBG = 4,
-                GK_SIGN_CODES_W = 5 };
+                GK_SIGN_CODES_W = 5, GK_SUBG_W = 6 };
+// sub-G cells up to this n run one wave per replicate (GK_SUBG_W), in the grid and dcor_sim_launch
+#define SUBG_W_NMAX 16384
 // one-pass sign cells up to this n run the wave-per-replicate kernels (GK_SIGN_CODES_W), in the
 // grid and in dcor_sim_launch alike, so a replicate's bits do not depend on the entry point
 #define SIGN_W_NMAX 16384
@@ -186,6 +188,8 @@ int launch_grid_sign_regen(int dgp, const SignConst* cells, const GridItem* item
 int launch_grid_sign_bern(bool wave, const SignConst* cells, const GridItem* items, int64_t nitems,
                           uint64_t* scratch, SignPartial* part, int vpl32, dcor_rep_out* out,
                           void* stream);
+int launch_grid_subg_w(int dgp, const SubgConst* cells, const GridItem* items, int64_t nitems, int vpl32,
+                       dcor_rep_out* out, void* stream);
 int launch_grid_subg(int dgp, const SubgConst* cells, const GridItem* items, int64_t nitems,
                      dcor_rep_out* out, void* stream);
 // Accumulators of grid cells, computed in passes over bounded record buffers.  Cell c's records

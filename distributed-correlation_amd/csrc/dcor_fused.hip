@@ -221,26 +221,34 @@ __device__ __forceinline__ void scalar_laplace(uint32_t rep, uint32_t k0, uint32
 }
 
 // Wave-level mixquant from Philox (one replicate per wave): the same elements as
-// mixquant_fused, VPL keys per lane.
+// mixquant_fused, VPL keys per lane, written to the wave's LDS and selected there.
+template <int VPL>
+struct WaveMix {
+  double keys[64 * VPL];
+  WaveSelL sel;
+};
+
 template <int VPL>
 __device__ __forceinline__ double wave_mixquant_fused(const MixConst& mx, double c, uint32_t rep,
-                                                      uint32_t k0, uint32_t k1, WaveSel* ws) {
+                                                      uint32_t k0, uint32_t k1, WaveMix<VPL>* ws) {
   const int lane = threadIdx.x & 63;
-  double val[VPL];
 #pragma unroll
   for (int s = 0; s < VPL / 2; ++s) {
     const int b = lane + 64 * s;  // Philox block b -> elements 2b, 2b+1
-    val[2 * s] = val[2 * s + 1] = dnan();
+    double v0 = dnan(), v1 = dnan();
     if (2 * b < mx.nsim) {
       const U4 wz = draw((uint32_t)b, rep, DCOR_SITE_MIX_Z, k0, k1);
       const U4 wl = draw((uint32_t)b, rep, DCOR_SITE_MIX_L, k0, k1);
       double z0, z1;
       normal_pair(wz, &z0, &z1);
-      val[2 * s] = z0 + c * unit_laplace(u53(wl.w0, wl.w1));
-      if (2 * b + 1 < mx.nsim) val[2 * s + 1] = z1 + c * unit_laplace(u53(wl.w2, wl.w3));
+      v0 = z0 + c * unit_laplace(u53(wl.w0, wl.w1));
+      if (2 * b + 1 < mx.nsim) v1 = z1 + c * unit_laplace(u53(wl.w2, wl.w3));
     }
+    ws->keys[lane + 64 * (2 * s)] = v0;
+    ws->keys[lane + 64 * (2 * s + 1)] = v1;
   }
-  return wave_select<VPL>(val, mx.pos, ws);
+  wave_sync();
+  return wave_select_lds<VPL>(ws->keys, mx.pos, &ws->sel);
 }
 
 // INT epilogue + CI write shared by the sign kernels (vert-cor.R:281-313).
@@ -726,7 +734,7 @@ __global__ __launch_bounds__(DCOR_BLOCK, DCOR_P2_WPE) void k_sign_pass2(SignCons
 // INT estimate, mixquant, INT CI (vert-cor.R:233-254, 186-194, 281-313).
 template <int VPL>
 __device__ __forceinline__ void sign_finish_wave(const SignConst& c, uint32_t rep, const P2Result& p,
-                                                 dcor_rep_out* dst, WaveSel* ws) {
+                                                 dcor_rep_out* dst, WaveMix<VPL>* ws) {
   const int lane = threadIdx.x & 63;
   double o[6];
   ni_sign_result(c, p.sT, p.sT2, p.bad_ni, o);
@@ -749,7 +757,7 @@ __device__ __forceinline__ void sign_finish_wave(const SignConst& c, uint32_t re
 template <int VPL>
 __device__ __forceinline__ void sign_epilogue_wave(const SignConst& c, uint32_t rep,
                                                    const SignPartial& sp, dcor_rep_out* dst,
-                                                   WaveSel* ws) {
+                                                   WaveMix<VPL>* ws) {
   const U4 wz = draw(4u, rep, DCOR_SITE_SCALAR, c.k0, c.k1);  // SCALAR block 4: Z (vert-cor.R:188)
   P2Result p;
   p.lapz = unit_laplace(u53(wz.w0, wz.w1));
@@ -763,7 +771,7 @@ __device__ __forceinline__ void sign_epilogue_wave(const SignConst& c, uint32_t 
 
 // ---- small cells (n <= SIGN_W_NMAX): one wave per replicate for both passes ------------------
 #ifndef DCOR_P2E_WPE
-#define DCOR_P2E_WPE 3  // waves per SIMD the pass 2 + epilogue wave kernel is compiled for
+#define DCOR_P2E_WPE 4  // waves per SIMD the pass 2 + epilogue wave kernel is compiled for
 #endif
 // At the reference grids' n (1000-12000) a 256-thread workgroup per replicate spends much of
 // its time in per-replicate fixed work -- the ziggurat table load, the scalar draws, the
@@ -825,7 +833,7 @@ __global__ __launch_bounds__(DCOR_BLOCK, DCOR_P2E_WPE) void k_sign_p2e_w(SignCon
                                                            const uint32_t* __restrict__ scratch,
                                                            const double* __restrict__ sums,
                                                            dcor_rep_out* out) {
-  __shared__ WaveSel wsel[DCOR_WAVES];
+  __shared__ WaveMix<VPL> wsel[DCOR_WAVES];
   const int wv = threadIdx.x >> 6;
   const int64_t r = (int64_t)blockIdx.x * DCOR_WAVES + __builtin_amdgcn_readfirstlane(wv);
   if (r >= nreps) return;  // whole waves only
@@ -839,7 +847,7 @@ template <int VPL>
 __global__ __launch_bounds__(DCOR_BLOCK) void k_sign_epilogue_w(SignConst c, int64_t nreps,
                                                                 const SignPartial* __restrict__ part,
                                                                 dcor_rep_out* out) {
-  __shared__ WaveSel wsel[DCOR_WAVES];
+  __shared__ WaveMix<VPL> wsel[DCOR_WAVES];
   const int wv = threadIdx.x >> 6;
   const int64_t r = (int64_t)blockIdx.x * DCOR_WAVES + wv;
   if (r >= nreps) return;  // whole waves only
@@ -1254,14 +1262,16 @@ __global__ __launch_bounds__(DCOR_BLOCK) void k_sign_fused(SignConst c, dcor_rep
 // ===================================================== fused sub-G family ===
 // correlation_NI_subG + ci_INT_subG (ver-cor-subG.R:25-108): single pass (the clip
 // thresholds are data-independent).  Each thread owns whole contiguous batches.
-template <int DGP>
-__device__ __forceinline__ void subg_fused_body(const SubgConst& c, uint32_t rep, dcor_rep_out* dst) {
-  __shared__ double red[16 * DCOR_WAVES];
-  __shared__ double lapz;
-  __shared__ SelScratch sel;
-  const int tid = threadIdx.x;
-  if (tid == 0) {
-    const U4 w = draw(4u, rep, DCOR_SITE_SCALAR, c.k0, c.k1);
+// WAVE = false: one 256-thread workgroup per replicate; WAVE = true: one wave per replicate (cells
+// with n <= SUBG_W_NMAX, the reference grid's sizes), wave reductions and the wave mixquant.
+template <int DGP, bool WAVE, int VPL = 16>
+__device__ __forceinline__ void subg_fused_core(const SubgConst& c, uint32_t rep, dcor_rep_out* dst,
+                                                SelScratch* sel, WaveMix<VPL>* ws) {
+  constexpr int NT = WAVE ? 64 : DCOR_BLOCK;
+  const int tid = WAVE ? (int)(threadIdx.x & 63) : (int)threadIdx.x;
+  double lapz;
+  {
+    const U4 w = draw(4u, rep, DCOR_SITE_SCALAR, c.k0, c.k1);   // uniform: every thread draws it
     lapz = unit_laplace(u53(w.w0, w.w1));
   }
   DD sP{0, 0}, sT{0, 0}, sT2{0, 0}, sU{0, 0}, sU2{0, 0};
@@ -1271,7 +1281,7 @@ __device__ __forceinline__ void subg_fused_body(const SubgConst& c, uint32_t rep
     ks_acc(sU, Uc);  // compensated sums (error ~ n 2^-106): the mean / sd of Uc
     ks_acc(sU2, Uc * Uc);
   };
-  for (int64_t j = tid; j < c.k; j += DCOR_BLOCK) {
+  for (int64_t j = tid; j < c.k; j += NT) {
     double sx = 0.0, sy = 0.0;
     const int64_t i0 = j * c.m;
     for (int r = 0; r < c.m; ++r) {
@@ -1291,13 +1301,19 @@ __device__ __forceinline__ void subg_fused_body(const SubgConst& c, uint32_t rep
     ks_acc(sT, T);
     ks_acc(sT2, T * T);
   }
-  for (int64_t i = c.k * c.m + tid; i < c.n; i += DCOR_BLOCK) {
+  for (int64_t i = c.k * c.m + tid; i < c.n; i += NT) {
     double x, y, l;
     sample_lap<DGP>(c.g, (uint32_t)i, rep, c.k0, c.k1, x, y, l);
     int_term(x, y, l);
   }
   DD d5[5] = {sP, sT, sT2, sU, sU2};
-  block_sum_dd<5>(d5, red);
+  if constexpr (WAVE) {
+#pragma unroll
+    for (int q = 0; q < 5; ++q) d5[q] = wave_sum_dd(d5[q]);
+  } else {
+    __shared__ double red[16 * DCOR_WAVES];
+    block_sum_dd<5>(d5, red);
+  }
   double o[6];
   ni_subg_result(c, d5[0], d5[1], d5[2], o);
   const DD mU = dd_div_d(d5[3], c.nd);
@@ -1305,12 +1321,29 @@ __device__ __forceinline__ void subg_fused_body(const SubgConst& c, uint32_t rep
   const double sd = sqrt(dd_var(d5[3], d5[4], c.nd));
   const double se_norm = sqrt(sd * sd + c.sn2x2);                      // :99
   const double cstar = 2.0 / (c.sqrt_n * sd * c.eps_r);                // :100
-  const double q = mixquant_fused(c.mix, cstar, rep, c.k0, c.k1, &sel);
+  double q;
+  if constexpr (WAVE) q = wave_mixquant_fused<VPL>(c.mix, cstar, rep, c.k0, c.k1, ws);
+  else q = mixquant_fused(c.mix, cstar, rep, c.k0, c.k1, sel);
   const double width = q * se_norm / c.sqrt_n;                         // :101
   o[3] = rho;
   o[4] = rmax(rho - width, -1.0);
   o[5] = rmin(rho + width, 1.0);
   if (tid == 0) *dst = dcor_rep_out{o[0], o[1], o[2], o[3], o[4], o[5]};
+}
+
+template <int DGP>
+__device__ __forceinline__ void subg_fused_body(const SubgConst& c, uint32_t rep, dcor_rep_out* dst) {
+  __shared__ SelScratch sel;
+  subg_fused_core<DGP, false, 16>(c, rep, dst, &sel, nullptr);
+}
+
+template <int DGP, int VPL>
+__global__ __launch_bounds__(DCOR_BLOCK) void k_subg_fused_w(SubgConst c, int64_t nreps, dcor_rep_out* out) {
+  __shared__ WaveMix<VPL> wsel[DCOR_WAVES];
+  const int wv = threadIdx.x >> 6;
+  const int64_t r = (int64_t)blockIdx.x * DCOR_WAVES + __builtin_amdgcn_readfirstlane(wv);
+  if (r >= nreps) return;  // whole waves only
+  subg_fused_core<DGP, true, VPL>(c, (uint32_t)(c.rep_begin + r), out + r, nullptr, &wsel[wv]);
 }
 
 template <int DGP>
@@ -1353,7 +1386,7 @@ __global__ __launch_bounds__(DCOR_BLOCK) void k_grid_sign_epilogue(const SignCon
                                                                    int64_t nitems,
                                                                    const SignPartial* __restrict__ part,
                                                                    dcor_rep_out* out) {
-  __shared__ WaveSel wsel[DCOR_WAVES];
+  __shared__ WaveMix<VPL> wsel[DCOR_WAVES];
   const int64_t r = wave_item();
   if (r >= nitems) return;  // whole waves only
   const GridItem it = items[r];
@@ -1400,7 +1433,7 @@ __global__ __launch_bounds__(DCOR_BLOCK, DCOR_P2E_WPE) void k_grid_sign_p2e_w(co
                                                                 const uint32_t* __restrict__ scratch,
                                                                 const double* __restrict__ sums,
                                                                 dcor_rep_out* out) {
-  __shared__ WaveSel wsel[DCOR_WAVES];
+  __shared__ WaveMix<VPL> wsel[DCOR_WAVES];
   const int64_t r = wave_item();
   if (r >= nitems) return;  // whole waves only
   const GridItem it = items[r];
@@ -1450,6 +1483,17 @@ __global__ __launch_bounds__(DCOR_BLOCK) void k_grid_expand(const GridPiece* __r
   const GridPiece pc = pieces[blockIdx.x];
   for (uint64_t t = threadIdx.x; t < pc.count; t += DCOR_BLOCK)
     items[pc.item0 + t] = GridItem{pc.cell, pc.rep0 + (uint32_t)t, pc.scr0 + t * pc.scr_stride, pc.out0 + t};
+}
+
+template <int DGP, int VPL>
+__global__ __launch_bounds__(DCOR_BLOCK) void k_grid_subg_w(const SubgConst* __restrict__ cells,
+                                                            const GridItem* __restrict__ items,
+                                                            int64_t nitems, dcor_rep_out* out) {
+  __shared__ WaveMix<VPL> wsel[DCOR_WAVES];
+  const int64_t r = wave_item();
+  if (r >= nitems) return;  // whole waves only
+  const GridItem it = items[r];
+  subg_fused_core<DGP, true, VPL>(cells[it.cell], it.rep, out + it.out, nullptr, &wsel[threadIdx.x >> 6]);
 }
 
 // ============================================================ launchers ===
@@ -1571,6 +1615,30 @@ int launch_grid_sign_bern(bool wave, const SignConst* cells, const GridItem* ite
     hipLaunchKernelGGL(k_grid_sign_bern, dim3((unsigned)nitems), dim3(DCOR_BLOCK), 0, st, cells, items,
                        scratch, part);
   launch_grid_epilogue(cells, items, nitems, part, vpl32, out, st);
+  return last_err();
+}
+
+template <int DGP>
+static void grid_subg_w_t(const SubgConst* cells, const GridItem* items, int64_t nitems, int vpl32,
+                          dcor_rep_out* out, hipStream_t st) {
+  if (vpl32)
+    hipLaunchKernelGGL((k_grid_subg_w<DGP, 32>), dim3(wave_groups(nitems)), dim3(DCOR_BLOCK), 0, st, cells, items,
+                       nitems, out);
+  else
+    hipLaunchKernelGGL((k_grid_subg_w<DGP, 16>), dim3(wave_groups(nitems)), dim3(DCOR_BLOCK), 0, st, cells, items,
+                       nitems, out);
+}
+
+int launch_grid_subg_w(int dgp, const SubgConst* cells, const GridItem* items, int64_t nitems, int vpl32,
+                       dcor_rep_out* out, void* stream) {
+  if (nitems <= 0) return 0;
+  const hipStream_t st = (hipStream_t)stream;
+  switch (dgp) {
+    case DCOR_DGP_GAUSSIAN: grid_subg_w_t<DCOR_DGP_GAUSSIAN>(cells, items, nitems, vpl32, out, st); break;
+    case DCOR_DGP_BERNOULLI: grid_subg_w_t<DCOR_DGP_BERNOULLI>(cells, items, nitems, vpl32, out, st); break;
+    case DCOR_DGP_MIX_GAUSSIAN: grid_subg_w_t<DCOR_DGP_MIX_GAUSSIAN>(cells, items, nitems, vpl32, out, st); break;
+    default: grid_subg_w_t<DCOR_DGP_BOUNDED_FACTOR>(cells, items, nitems, vpl32, out, st);
+  }
   return last_err();
 }
 
@@ -1712,8 +1780,26 @@ int launch_dgp(const DgpConst& g, uint32_t k0, uint32_t k1, int64_t rep_begin, i
   return last_err();
 }
 
+template <int DGP>
+static void subg_w_t(const SubgConst& c, int64_t reps, dcor_rep_out* out, hipStream_t st) {
+  if (c.mix.nsim > 1024)
+    hipLaunchKernelGGL((k_subg_fused_w<DGP, 32>), dim3(wave_groups(reps)), dim3(DCOR_BLOCK), 0, st, c, reps, out);
+  else
+    hipLaunchKernelGGL((k_subg_fused_w<DGP, 16>), dim3(wave_groups(reps)), dim3(DCOR_BLOCK), 0, st, c, reps, out);
+}
+
 int launch_subg_fused(const SubgConst& c, int64_t reps, dcor_rep_out* out, void* stream) {
   if (reps <= 0) return 0;
+  if (c.n <= SUBG_W_NMAX) {   // small cells: one wave per replicate (as the grid runs them)
+    const hipStream_t st = (hipStream_t)stream;
+    switch (c.g.dgp) {
+      case DCOR_DGP_GAUSSIAN: subg_w_t<DCOR_DGP_GAUSSIAN>(c, reps, out, st); break;
+      case DCOR_DGP_BERNOULLI: subg_w_t<DCOR_DGP_BERNOULLI>(c, reps, out, st); break;
+      case DCOR_DGP_MIX_GAUSSIAN: subg_w_t<DCOR_DGP_MIX_GAUSSIAN>(c, reps, out, st); break;
+      default: subg_w_t<DCOR_DGP_BOUNDED_FACTOR>(c, reps, out, st);
+    }
+    return last_err();
+  }
   const dim3 g((unsigned)reps), b(DCOR_BLOCK);
   switch (c.g.dgp) {
     case DCOR_DGP_GAUSSIAN:

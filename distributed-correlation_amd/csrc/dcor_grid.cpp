@@ -48,6 +48,7 @@ size_t env_size(const char* name, size_t dflt, int shift) {
 }
 
 bool codes_kind(int kind) { return kind == GK_SIGN_CODES || kind == GK_SIGN_CODES_W; }
+bool subg_kind(int kind) { return kind == GK_SUBG || kind == GK_SUBG_W; }
 
 uint64_t item_scratch(int kind, int64_t n) {
   // code slabs start on 256-B boundaries (the kernels move records 16 B at a time)
@@ -142,8 +143,8 @@ int exec_ranges(const dcor_cell* cells, const std::vector<CellPlan>& cp, const s
     auto it = g.slot.find(r.cell);
     uint32_t ci;
     if (it == g.slot.end()) {
-      ci = (uint32_t)(p.kind == GK_SUBG ? g.subg.size() : g.sign.size());
-      if (p.kind == GK_SUBG) g.subg.push_back(p.subg); else g.sign.push_back(p.sign);
+      ci = (uint32_t)(subg_kind(p.kind) ? g.subg.size() : g.sign.size());
+      if (subg_kind(p.kind)) g.subg.push_back(p.subg); else g.sign.push_back(p.sign);
       g.slot[r.cell] = ci;
     } else {
       ci = it->second;
@@ -207,7 +208,7 @@ int exec_ranges(const dcor_cell* cells, const std::vector<CellPlan>& cp, const s
   for (auto& kv : groups) {
     Group& g = kv.second;
     g.tab_off = tb;
-    tb += al256(g.kind == GK_SUBG ? g.subg.size() * sizeof(SubgConst) : g.sign.size() * sizeof(SignConst));
+    tb += al256(subg_kind(g.kind) ? g.subg.size() * sizeof(SubgConst) : g.sign.size() * sizeof(SignConst));
   }
   const size_t piece_off = tb;
   tb += al256(all_pieces.size() * sizeof(GridPiece));
@@ -235,7 +236,7 @@ int exec_ranges(const dcor_cell* cells, const std::vector<CellPlan>& cp, const s
   char* hs = (char*)hsv;
   for (auto& kv : groups) {
     const Group& g = kv.second;
-    if (g.kind == GK_SUBG) std::memcpy(hs + g.tab_off, g.subg.data(), g.subg.size() * sizeof(SubgConst));
+    if (subg_kind(g.kind)) std::memcpy(hs + g.tab_off, g.subg.data(), g.subg.size() * sizeof(SubgConst));
     else std::memcpy(hs + g.tab_off, g.sign.data(), g.sign.size() * sizeof(SignConst));
   }
   std::memcpy(hs + piece_off, all_pieces.data(), all_pieces.size() * sizeof(GridPiece));
@@ -279,6 +280,8 @@ int exec_ranges(const dcor_cell* cells, const std::vector<CellPlan>& cp, const s
       } else if (g.kind == GK_SIGN_BERN_W || g.kind == GK_SIGN_BERN) {
         rc = launch_grid_sign_bern(g.kind == GK_SIGN_BERN_W, dsign, items, nit, (uint64_t*)scr,
                                    (SignPartial*)sums, g.vpl32, d_out, st0);
+      } else if (g.kind == GK_SUBG_W) {
+        rc = launch_grid_subg_w(g.dgp, dsubg, items, nit, g.vpl32, d_out, st0);
       } else {
         rc = launch_grid_subg(g.dgp, dsubg, items, nit, d_out, st0);
       }
