@@ -83,8 +83,42 @@ def run_grid_gpu(cells, B, chunk=1 << 15):
     return acc
 
 
+# config line -> (committed rocprofv3 summary, kernel-name filter of the line's own launches)
+PROFILE_OF = {"VG": ("r03_vg", "k_grid_"), "SG": ("r03_sg", "k_grid_"), "C2": ("r03_c2", "k_grid_"),
+              "C3": ("r03_c3", "k_grid_"), "C5": ("r03_c5", "k_premat_subg_dict"),
+              "C5-continuous": ("r03_c5c", "k_premat_subg_tiled"), "C5-fused": ("r03_c5f", "k_hrs_fused"),
+              "S": ("r03_s", "k_subg_fused")}
+
+
+def measured(name):
+    """The line's hardware counters from its committed profile (scripts/summarize_prof.py):
+    issue_frac = VALUBusy time-weighted over the line's kernels, the HBM bytes they moved per
+    call (FETCH_SIZE x2 + WRITE_SIZE), and whether the profile was taken on this tree's sources."""
+    from bench import profile_stamp
+    if name not in PROFILE_OF:
+        return {}
+    tag, filt = PROFILE_OF[name]
+    path = os.path.join(ROOT, "profiles", f"{tag}_summary.json")
+    try:
+        ks = json.load(open(path))["kernels"]
+    except (OSError, ValueError, KeyError):
+        return {}
+    num = den = 0.0
+    per = {}
+    for kname, v in ks.items():
+        if filt in kname and "valu_busy" in v and v.get("avg_ns"):
+            w = v["avg_ns"] * v.get("calls", 1)
+            num += v["valu_busy"] * w
+            den += w
+            per[kname.split("::")[-1]] = round(v["valu_busy"], 3)
+    head, fresh = profile_stamp(path)
+    return {"issue_frac": (num / den) if den else None, "issue_frac_per_kernel": per or None,
+            "issue_source": os.path.relpath(path, ROOT), "issue_source_head": head, "issue_source_fresh": fresh}
+
+
 def line(name, **kw):
     kw["config"] = name
+    kw.update(measured(name))
     print(json.dumps(kw), flush=True)
 
 
