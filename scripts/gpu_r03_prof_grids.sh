@@ -1,0 +1,6 @@
+# Round 3: rocprofv3 kernel stats + PMC passes of the grid config lines (VG, SG, C2, C3).
+set -o pipefail
+for c in VG SG C2 C3; do
+  t=$(echo $c | tr 'A-Z' 'a-z')
+  TAG=r03_$t bash scripts/gpu_prof_cfg.sh python3 bench_configs.py --only $c --c3-reps 512 || exit $?
+done
