@@ -1668,6 +1668,12 @@ int dcor_rstream_draws(const dcor_cell* cell, int64_t reps, const dcor_rs_draws*
   return st ? DCOR_EHIP : DCOR_OK;
 }
 
+int dcor_rstream_mt_jump(int32_t seed, int64_t J, uint32_t* h_out) {
+  if (!h_out || J < 0) return fail(DCOR_EINVAL, "bad mt_jump arguments");
+  if (mt_charpoly_degree() != 19937) return fail(DCOR_EINVAL, "MT19937 characteristic polynomial not found");
+  return mt_jump_window(seed, J, h_out);
+}
+
 int dcor_rstream_words(int32_t seed, int64_t count, uint32_t* h_out) {
   if (!h_out || count < 1 || count > ((int64_t)1 << 30)) return fail(DCOR_EINVAL, "bad rstream_words arguments");
   if (int st = need_device()) return st;

@@ -58,6 +58,13 @@ void count_alloc();
 // Stop the grid's persistent device workers (dcor_shutdown); `forked`: forget them unjoined.
 void grid_workers_stop(bool forked);              // one more device or pinned allocation (dcor_alloc_count)
 
+// MT19937 jump-ahead (dcor_mtjump.cpp): the degree of the characteristic polynomial found by
+// Berlekamp-Massey (19937); the cached table of nseg polynomials x^((s + 1) L - 624) mod phi,
+// words 64-bit words each; the host-side jumped window (test reference).
+int mt_charpoly_degree();
+int mt_segment_polys(int64_t L, int nseg, const uint64_t** table, int* words);
+int mt_jump_window(int32_t seed, int64_t J, uint32_t out[624]);
+
 // All constants of one fused cell and the kernel family that runs it.
 struct CellPlan {
   int kind;        // GridKind

@@ -125,6 +125,7 @@ SIGNATURES = {
                                         C.POINTER(RepOut)]),
     "dcor_rstream_draws": (C.c_int, [C.POINTER(Cell), C.c_int64, C.POINTER(RsDraws)]),
     "dcor_rstream_words": (C.c_int, [C.c_int32, C.c_int64, C.POINTER(C.c_uint32)]),
+    "dcor_rstream_mt_jump": (C.c_int, [C.c_int32, C.c_int64, C.POINTER(C.c_uint32)]),
     "dcor_rstream_hrs_draws": (C.c_int, [C.c_int64, C.c_int64, C.c_int64, C.c_int64, C.c_int64,
                                          C.POINTER(C.c_int32), C.POINTER(C.c_int32), _P, _P, _P, _P,
                                          _P, _P, _P, _P]),

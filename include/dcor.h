@@ -197,6 +197,12 @@ int dcor_rstream_draws(const dcor_cell* cell, int64_t reps, const dcor_rs_draws*
 /* The first `count` tempered Mersenne-Twister words after set.seed(seed), from the GPU
  * generator (unif_rand() = fixup(word * 2^-32)). */
 int dcor_rstream_words(int32_t seed, int64_t count, uint32_t* h_out);
+/* Jump-ahead of R's Mersenne-Twister stream (host computation, no device): the 624 raw state words
+ * J words past the first generated block of set.seed(seed) -- raw words 624 + J .. 624 + J + 623 of
+ * the stream (raw word 624 + k = the k-th word MT generates; tempering makes the k-th unif_rand).
+ * By x^J mod phi (phi: MT19937's characteristic polynomial, Berlekamp-Massey); the device does
+ * the same per segment when one long stream is generated by many workgroups. */
+int dcor_rstream_mt_jump(int32_t seed, int64_t J, uint32_t* h_out);
 /* The HRS runs' noise on R's streams (real-data-sims.R:355-404), in the explicit-input layout
  * of dcor_premat_subg (hrs = 1), DEVICE outputs, synchronous on `stream`:
  *  run r, NI: set.seed(h_ni_seeds[r]); sample.int(n, k*m) -> d_perm[r][k*m] (0-based), then
