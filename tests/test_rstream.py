@@ -185,3 +185,31 @@ def test_mt_words_match_numpy_mt19937(orc):
                     "state": {"key": np.array(st.mt[:], dtype=np.uint32), "pos": 624}}
         np.testing.assert_array_equal(bg.random_raw(200_000).astype(np.uint32),
                                       orc.rs_stream(seed, "word", 200_000))
+
+
+def _mt_raw_numpy(st_mt, count):
+    """Raw (untempered) MT19937 words: R[0..623] = the state block, then the recurrence
+    w[t] = w[t-227] ^ twist(upper(w[t-624]) | lower(w[t-623])), 227 words at a time."""
+    R = np.zeros(count, dtype=np.uint32)
+    R[:624] = np.array(st_mt[:], dtype=np.uint32)
+    t = 624
+    while t < count:
+        e = min(t + 227, count)
+        y = (R[t - 624:e - 624] & np.uint32(0x80000000)) | (R[t - 623:e - 623] & np.uint32(0x7FFFFFFF))
+        R[t:e] = R[t - 227:e - 227] ^ (y >> np.uint32(1)) ^ np.where(y & np.uint32(1), np.uint32(0x9908B0DF),
+                                                                      np.uint32(0))
+        t = e
+    return R
+
+
+@pytest.mark.parametrize("seed,J", [(1_000_073, 0), (1_000_073, 1), (7, 20000), (2 ** 31 - 1, 61234)])
+def test_mt_jump_ahead_matches_sequential(orc, seed, J):
+    """dcor_rstream_mt_jump (host: Berlekamp-Massey characteristic polynomial, x^J mod phi, GF(2)
+    combination of raw words) lands on the window the recurrence reaches J words later."""
+    import ctypes as C
+    from dcor import _lib
+    st = orc.rs_state(seed)
+    R = _mt_raw_numpy(st.mt, 624 + J + 624)
+    out = (C.c_uint32 * 624)()
+    assert _lib.lib.dcor_rstream_mt_jump(seed, J, out) == 0, _lib.last_error()
+    np.testing.assert_array_equal(np.frombuffer(out, dtype=np.uint32), R[624 + J:624 + J + 624])
