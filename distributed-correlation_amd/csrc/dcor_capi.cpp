@@ -339,7 +339,7 @@ void ctx_free(Ctx* c) {
     if (b->p) (void)hipHostFree(b->p);
   }
   if (c->work) { (void)hipStreamSynchronize(c->work); (void)hipStreamDestroy(c->work); }
-  for (Arena* a : {&c->codes, &c->rs, &c->grid, &c->gpart, &c->out})
+  for (Arena* a : {&c->codes, &c->rs, &c->grid, &c->gpart, &c->out, &c->rsj})
     if (a->p) (void)hipFree(a->p);
   delete c;
 }
@@ -435,6 +435,25 @@ int rs_arena_get(size_t bytes, void** out) {
   Ctx* c = nullptr;
   if (int st = ctx_get(&c)) return st;
   return arena_grow(c->rs, bytes, out);
+}
+
+// The first n jump polynomials of the R-stream jump path on this device (host table:
+// mt_segment_polys, computed once per process; uploaded when the device copy is short).
+int rsj_polys(int n, const uint64_t** out) {
+  Ctx* c = nullptr;
+  if (int st = ctx_get(&c)) return st;
+  if (c->rsj_npoly < n) {
+    const uint64_t* table = nullptr;
+    int words = 0;
+    if (int st = mt_segment_polys(RSJ_L, n, &table, &words)) return st;
+    if (words != RSJ_PW) return fail(DCOR_EINVAL, "jump polynomial width %d", words);
+    void* d = nullptr;
+    if (int st = arena_grow(c->rsj, (size_t)n * RSJ_PW * 8, &d)) return st;
+    HIPCHK(hipMemcpy(d, table, (size_t)n * RSJ_PW * 8, hipMemcpyHostToDevice));
+    c->rsj_npoly = n;
+  }
+  *out = (const uint64_t*)c->rsj.p;
+  return DCOR_OK;
 }
 
 // Monotone code map of clip(v): base + [0, 2R) -> [0, levels).  Only affects speed (how many
@@ -1249,7 +1268,7 @@ int64_t dcor_device_bytes(void) {
   std::lock_guard<std::mutex> lk(g_ctx_mu);
   int64_t b = 0;
   for (const Ctx* c : g_ctxs)
-    for (const Arena* a : {&c->codes, &c->rs, &c->grid, &c->gpart, &c->out}) b += (int64_t)a->bytes;
+    for (const Arena* a : {&c->codes, &c->rs, &c->grid, &c->gpart, &c->out, &c->rsj}) b += (int64_t)a->bytes;
   return b;
 }
 
@@ -1371,6 +1390,8 @@ void rs_mvrnorm_factor(const double sigma[2], double rho, double A[4]) {
 struct RsPlan {
   RsCell c;
   int64_t rep_max;       // words per replicate, upper bound (exp_rand takes <= 17 words)
+  int64_t jrep;          // words per replicate the jump path budgets (exp_rand: 2 words per draw
+                         // and a margin; the mean is 1.69, sd 1.09)
   size_t per_rep;        // device bytes per replicate in flight
 };
 
@@ -1462,6 +1483,11 @@ int rs_plan(const dcor_cell& cell, RsPlan& p) {
   if (c.has_mix) pre += 2 * c.nsim;
   c.pre = pre;
   p.rep_max = pre + shuffle_words + (c.has_mix ? 18 * c.nsim : 0);
+  c.jpost = c.has_mix ? c.nsim : 0;
+  p.jrep = pre + (c.has_mix ? c.nsim + 2 * c.nsim + 64 + 8 * (int64_t)std::ceil(std::sqrt((double)c.nsim)) : 0);
+  if (std::getenv("DCOR_RSJ_TIGHT"))   // test hook: a budget every mixquant chunk overruns
+    p.jrep = pre + (c.has_mix ? c.nsim + c.nsim : 0);
+  p.rep_max = std::max(p.rep_max, p.jrep);
   const int64_t fw = (n + 31) / 32;
   p.per_rep = (size_t)p.rep_max * 4 + (size_t)c.nsim * 8 * 3 + (size_t)n * 16 + 64 +
               (size_t)c.k * 16 + (size_t)fw * 4 + (subg ? (size_t)n * 8 : 0) + 8 + 16 +
@@ -1535,6 +1561,30 @@ struct View {  // a typed window into the R-stream arena
   template <class T> T* as() const { return static_cast<T*>(p); }
 };
 
+// The jump path's tables for a chunk of rc replicates of cell p (launch_rsj): budget jN words,
+// T levels 2^k <= nsim, G levels 2^k <= rc.
+int rs_bits(int64_t v) { int b = 0; while (v) { ++b; v >>= 1; } return b; }
+void rsj_dims(RsPlan& p, int64_t rc) {
+  RsCell& c = p.c;
+  c.jN = rc * p.jrep + 256;
+  c.jlt = c.has_mix ? rs_bits(c.nsim) : 0;
+  c.jlg = c.has_mix ? rs_bits(rc) : 0;
+}
+size_t rsj_cell_bytes(const RsPlan& p) {
+  const RsCell& c = p.c;
+  return al256((size_t)RSJ_L * 4) + al256((size_t)(c.jlt + c.jlg) * (size_t)(c.jN + 1) * 4) + 256;
+}
+// DCOR_RS_JUMP: 0 never, 1 whenever the batch allows it, unset: batches of at most 64 cells
+// (below that k_rs_stream leaves CUs idle; above it its one-CU-per-cell walk is the cheaper).
+// Cells with gen_mix_gaussian's sample.int rejection walk stay on k_rs_stream.
+bool rsj_use(const std::vector<RsPlan>& plan, int i0, int nb) {
+  for (int i = 0; i < nb; ++i)
+    if (plan[(size_t)(i0 + i)].c.shuffle) return false;
+  const char* e = std::getenv("DCOR_RS_JUMP");
+  if (e && *e) return std::atoi(e) != 0;
+  return nb <= 64;
+}
+
 size_t rs_budget() {
   const char* e = std::getenv("DCOR_RS_BUDGET_MB");
   const long mb = e ? std::atol(e) : 4096;
@@ -1569,21 +1619,43 @@ int dcor_rstream_grid_run(const dcor_cell* cells, int ncells, int64_t B, dcor_ac
     rc = std::max<int64_t>(1, std::min<int64_t>({rc, B, (int64_t)(0x7fffffff / nb)}));
     if (const char* e = std::getenv("DCOR_RS_MAX_CHUNK"))   // test hook: force short chunks
       rc = std::max<int64_t>(1, std::min<int64_t>(rc, std::atol(e)));
-    size_t bytes = 0;
-    for (int i = 0; i < nb; ++i) bytes += rs_cell_bytes(plan[(size_t)(i0 + i)], (int32_t)rc);
-    // one library-owned arena (kept across calls): cell buffers | states | descriptors |
-    // replicate records | accumulators
-    const size_t off_st = bytes, off_cells = off_st + al256(sizeof(RsState) * (size_t)nb);
-    const size_t off_out = off_cells + al256(sizeof(RsCell) * (size_t)nb);
+    bool jump = rsj_use(plan, i0, nb);
+    size_t bytes = 0, jbytes = 0;
+    for (;;) {
+      bytes = jbytes = 0;
+      bool fits32 = true;
+      for (int i = 0; i < nb; ++i) {
+        RsPlan& p = plan[(size_t)(i0 + i)];
+        bytes += rs_cell_bytes(p, (int32_t)rc);
+        if (jump) {
+          rsj_dims(p, rc);
+          jbytes += rsj_cell_bytes(p);
+          fits32 = fits32 && p.c.jN < 0x7ffffff0ll;
+        }
+      }
+      if ((fits32 && bytes + jbytes <= budget) || rc == 1) {
+        if (!fits32) jump = false;
+        break;
+      }
+      rc = (rc + 1) / 2;
+    }
+    if (!jump) jbytes = 0;
+    // one library-owned arena (kept across calls): cell buffers | jump tables | states |
+    // descriptors (and the fallback's) | replicate records | accumulators
+    const size_t off_st = bytes + jbytes, off_cells = off_st + al256(sizeof(RsState) * (size_t)nb);
+    const size_t off_sub = off_cells + al256(sizeof(RsCell) * (size_t)nb);
+    const size_t off_out = off_sub + al256(sizeof(RsCell) * (size_t)nb);
     const size_t off_acc = off_out + al256(sizeof(dcor_rep_out) * (size_t)B * (size_t)nb);
     void* arena = nullptr;
     if (int st = rs_arena_get(off_acc + al256(sizeof(dcor_accum) * 2 * (size_t)nb), &arena))
       return st;
     const View buf{arena}, dst{(char*)arena + off_st}, dcells{(char*)arena + off_cells},
-        dout{(char*)arena + off_out}, acc{(char*)arena + off_acc};
+        dsub{(char*)arena + off_sub}, dout{(char*)arena + off_out}, acc{(char*)arena + off_acc};
     std::vector<RsState> hst((size_t)nb);
     std::vector<RsCell> hc((size_t)nb);
     char* base = buf.as<char>();
+    int64_t max_pos = 0, max_exp = 0, need = 0;
+    int max_lt = 0, max_lg = 0;
     for (int i = 0; i < nb; ++i) {
       rs_seed((int32_t)cells[i0 + i].seed, hst[(size_t)i]);
       RsPlan& p = plan[(size_t)(i0 + i)];
@@ -1591,14 +1663,53 @@ int dcor_rstream_grid_run(const dcor_cell* cells, int ncells, int64_t B, dcor_ac
       p.c.st = dst.as<RsState>() + i;
       hc[(size_t)i] = p.c;
     }
+    const uint64_t* d_polys = nullptr;
+    int nseg = 1;
+    if (jump) {
+      for (int i = 0; i < nb; ++i) {
+        RsCell& c = hc[(size_t)i];
+        c.raw = (uint32_t*)base;
+        base += al256((size_t)RSJ_L * 4);
+        c.lift = (int32_t*)base;
+        base += al256((size_t)(c.jlt + c.jlg) * (size_t)(c.jN + 1) * 4);
+        max_pos = std::max(max_pos, c.jN + 1);
+        max_exp = std::max(max_exp, c.has_mix ? rc * c.nsim : 0);
+        max_lt = std::max(max_lt, (int)c.jlt);
+        max_lg = std::max(max_lg, (int)c.jlg);
+        need = std::max(need, 624 + c.jN + 64 + 623);
+      }
+      int32_t* flags = (int32_t*)base;   // one flag per cell, read back in one copy
+      base += al256((size_t)nb * 4);
+      for (int i = 0; i < nb; ++i) hc[(size_t)i].jflag = flags + i;
+      nseg = (int)((need + RSJ_L - 1) / RSJ_L);
+      if (nseg > 1)
+        if (int st = rsj_polys(nseg - 1, &d_polys)) return st;
+    }
     HIPCHK(hipMemcpy(dst.p, hst.data(), sizeof(RsState) * (size_t)nb, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(dcells.p, hc.data(), sizeof(RsCell) * (size_t)nb, hipMemcpyHostToDevice));
     size_t mix_lds = 0;
     for (int i = 0; i < nb; ++i)
       if (hc[(size_t)i].shuffle) mix_lds = std::max(mix_lds, rs_mix_lds_bytes(hc[(size_t)i].n));
+    std::vector<int32_t> hflag((size_t)nb);
     for (int64_t done = 0; done < B; done += rc) {
       const int32_t rcc = (int32_t)std::min<int64_t>(rc, B - done);
-      int e = launch_rs_stream(dcells.as<RsCell>(), nb, rcc, nullptr);
+      int e = 0;
+      if (jump) {
+        e = launch_rsj(dcells.as<RsCell>(), nb, rcc, d_polys, nseg, max_pos, max_lt, max_lg, max_exp, nullptr);
+        if (e) return hip_fail((hipError_t)e, "rstream jump launch");
+        // a cell whose chunk ran past its word budget (never seen: the budget is ~10 sd above the
+        // mean) kept its state; k_rs_stream walks it instead
+        HIPCHK(hipMemcpy(hflag.data(), hc[0].jflag, 4 * (size_t)nb, hipMemcpyDeviceToHost));
+        std::vector<RsCell> sub;
+        for (int i = 0; i < nb; ++i)
+          if (hflag[(size_t)i]) sub.push_back(hc[(size_t)i]);
+        if (!sub.empty()) {
+          HIPCHK(hipMemcpy(dsub.p, sub.data(), sizeof(RsCell) * sub.size(), hipMemcpyHostToDevice));
+          e = launch_rs_stream(dsub.as<RsCell>(), (int)sub.size(), rcc, nullptr);
+        }
+      } else {
+        e = launch_rs_stream(dcells.as<RsCell>(), nb, rcc, nullptr);
+      }
       if (e) return hip_fail((hipError_t)e, "rstream stream launch");
       if (mix_lds) {   // gen_mix_gaussian: sample.int's rejection is unbounded; check the flag
         HIPCHK(hipMemcpy(hst.data(), dst.p, sizeof(RsState) * (size_t)nb, hipMemcpyDeviceToHost));

@@ -293,7 +293,26 @@ struct RsCell {
   int32_t* shuf;               // [rc][n] the shuffled row order (0-based)
   int64_t words_cap;           // capacity of `words`; the walker stops (RsState.pad[1] = 1)
                                // rather than overrun it
+  // The jump path (launch_rsj): the chunk's stream generated segment-parallel from MT19937
+  // jump-ahead windows, the walk replaced by pointer doubling over consumption positions
+  // 0 .. jN (jN: the chunk's word budget; position jN stands for "past the budget").
+  uint32_t* raw;               // [RSJ_L] raw words of the chunk's first segment (state block first)
+  int32_t* lift;               // [jlt + jlg][jN + 1]: T_k(P) = the position 2^k exp_rand draws
+                               // on from P; G_k(P) = 2^k replicates on from replicate start P
+  int32_t* jflag;              // set when the chunk ran past jN (the host re-runs it by k_rs_stream)
+  int64_t jN, jpost;           // word budget; fixed words after the exp_rand segment (rbinom)
+  int32_t jlt, jlg;            // levels of T and of G
 };
+// Raw words per jump segment (a multiple of 624, >= 624 + 19937 + 624 so segment 0 holds the
+// base window every jump combines), and 64-bit words per jump polynomial.
+#define RSJ_L (624 * 48)
+#define RSJ_PW 312
+// Runs the jump path over d_cells[0..ncells): generation (segment 0 sequential, the rest from
+// the nseg - 1 jump polynomials d_polys), the walk by pointer doubling, the exp_rand values and
+// the .Random.seed after the chunk.  max_pos: the largest jN + 1; max_lt / max_lg: the largest
+// jlt / jlg; max_exp: the largest rc * nsim.
+int launch_rsj(RsCell* d_cells, int ncells, int32_t rc, const uint64_t* d_polys, int nseg,
+               int64_t max_pos, int max_lt, int max_lg, int64_t max_exp, void* stream);
 // RsCell.family for the HRS INT runs: rLap(n), rLap(1), mixquant (real-data-sims.R:375-402)
 #define RS_FAMILY_HRS_INT 2
 int launch_rs_stream(RsCell* d_cells, int ncells, int32_t rc, void* stream);

@@ -46,6 +46,8 @@ struct Ctx {
   int stage_next = 0;
   Pinned hrec;                    // a pass's records on their way to the caller's detail array
   Pinned hacc;                    // a shard's accumulators on their way to the host
+  Arena rsj;                      // the R-stream jump polynomials (rsj_npoly of them)
+  int rsj_npoly = 0;
 };
 int ctx_get(Ctx** out);          // the calling thread's context on the current device
 void ctx_release_thread();       // free every context of the calling thread

@@ -148,6 +148,27 @@ __device__ __forceinline__ double rs_lap(uint32_t w) {
    0.9999999924734159, 0.9999999995283275, 0.9999999999728814, 0.9999999999985598,         \
    0.9999999999999289, 0.9999999999999968, 0.9999999999999999, 1.0000000000000000}
 
+// exp_rand (sexp.c) from the draw's first word w: a (the doubling loop's multiple of ln 2) and u,
+// and the number of words the draw consumes -- 1 when u <= q[0], else 2 + i for the index i of
+// the first q[i] >= u (the do-loop's draws); the value is a + u, or a + q[0] * min of the words
+// after the first.
+__device__ __forceinline__ int rs_exp_head(uint32_t w, double& a, double& eu) {
+  constexpr double q[16] = RS_Q_TABLE;
+  a = 0.;
+  eu = rs_unif(w);
+  for (;;) {
+    eu += eu;
+    if (eu > 1.) break;
+    a += q[0];
+  }
+  eu -= 1.;
+  if (eu <= q[0]) return 1;
+  int ie = 1;
+#pragma unroll
+  for (int t = 1; t < 15; ++t) ie += (eu > q[t]) ? 1 : 0;
+  return 2 + ie;
+}
+
 __device__ __forceinline__ uint32_t rs_temper(uint32_t y) {
   y ^= (y >> 11);
   y ^= (y << 7) & 0x9d2c5680u;
@@ -366,21 +387,7 @@ __global__ __launch_bounds__(RS_STREAM_NT) void k_rs_stream(RsCell* cells, int32
     const int64_t pos = P + lane;
     double a = 0., eu = 0.;
     int len = 1;
-    if (pos < Q) {
-      eu = rs_unif(ring[rs_wrap(pslot + lane)]);
-      for (;;) {
-        eu += eu;
-        if (eu > 1.) break;
-        a += q[0];
-      }
-      eu -= 1.;
-      if (!(eu <= q[0])) {
-        int ie = 1;
-#pragma unroll
-        for (int t = 1; t < 15; ++t) ie += (eu > q[t]) ? 1 : 0;
-        len = 2 + ie;
-      }
-    }
+    if (pos < Q) len = rs_exp_head(ring[rs_wrap(pslot + lane)], a, eu);
     // Chain of draw starts from lane 0 by pointer doubling: lane l holds the set M of chain
     // positions reachable from l and the first position J past it; six rounds of
     // M |= M[J], J = J[J] cover the window.
@@ -448,6 +455,233 @@ __global__ __launch_bounds__(RS_STREAM_NT) void k_rs_stream(RsCell* cells, int32
     for (int t = tid; t < RS_N; t += NT) st->mt[t] = rs_untemper(ring[(par ^ 1) * RS_N + t]);
     if (tid == 0) { st->mti = off; st->pad[0] = par ^ 1; }
   }
+}
+
+// ------------------------------------------------------------ jump path ---
+// k_rs_stream is one workgroup per cell: a single cell (R1: one grid point, B = 1000) runs on
+// one CU, generation and walk alike.  The jump path spreads one cell's chunk over the chip:
+//   k_rsj_gen0   segment 0 (RSJ_L raw words) sequentially from the state block;
+//   k_rsj_jump   segment s >= 1: its first block is sum_{i : g_i = 1} w[624 + i + p] for the jump
+//                polynomial g = x^(s RSJ_L - 624) mod phi (dcor_mtjump.cpp) over segment 0's
+//                words, then the recurrence; all segments of all cells at once;
+//   k_rsj_len    T_0(P) = P + the words an exp_rand draw starting at P consumes;
+//   k_rsj_lift   T_{k+1} = T_k o T_k (and G likewise): pointer doubling;
+//   k_rsj_g0     G_0(P) = T^nsim(P + pre) + post: the start of the replicate after one at P;
+//   k_rsj_chain  P_r = G^r(0) for every r <= rc (binary digits of r), exp_end = T^nsim(P_r + pre);
+//   k_rsj_expv   the d-th exp_rand value of replicate r at T^d(P_r + pre);
+//   k_rsj_state  .Random.seed at P_rc.
+// Positions are clamped at jN, so a chunk whose replicates need more words than the budget
+// ends at jN: k_rsj_chain flags it and k_rsj_state leaves the state alone (the host re-runs the
+// chunk by k_rs_stream).  Replicates without mixquant (the Laplace CI) have a fixed length: P_r =
+// r * pre, no tables.
+#define RSJ_NT 256
+#define RSJ_DEG 19937
+#define RSJ_BASEW (RSJ_DEG - 1 + 3 * RSJ_NT)   // base words read (lanes past 623 read, unused)
+
+__device__ __forceinline__ int64_t rsj_need(int64_t jN, int mti) {  // raw words the chunk may read
+  return (mti + jN + 64 + RS_N - 1) / RS_N * RS_N;
+}
+
+// x advanced by m steps of T (levels T_k at lift + k * S); x, every table entry <= N
+__device__ __forceinline__ int32_t rsj_adv(const int32_t* __restrict__ lift, int64_t S, int32_t x, int64_t m) {
+  for (int k = 0; m; ++k, m >>= 1)
+    if (m & 1) x = lift[(int64_t)k * S + x];
+  return x;
+}
+
+__global__ __launch_bounds__(RSJ_NT) void k_rsj_gen0(const RsCell* cells) {
+  __shared__ uint32_t mt[RS_N];
+  const RsCell& c = cells[blockIdx.x];
+  const int tid = threadIdx.x;
+  const int mti = c.st->mti;
+  for (int t = tid; t < RS_N; t += RSJ_NT) mt[t] = c.st->mt[t];
+  __syncthreads();
+  const int64_t need = rsj_need(c.jN, mti);
+  const int64_t end = need < RSJ_L ? need : RSJ_L;
+  RS_G uint32_t* const raw = (RS_G uint32_t*)c.raw;
+  RS_G uint32_t* const W = (RS_G uint32_t*)c.words;
+  for (int64_t b0 = 0; b0 < end; b0 += RS_N) {
+    if (b0) rs_mt_block<RSJ_NT>(mt, tid);
+    for (int t = tid; t < RS_N; t += RSJ_NT) {
+      const uint32_t v = mt[t];
+      raw[b0 + t] = v;
+      if (b0 + t >= mti) W[b0 + t - mti] = rs_temper(v);
+    }
+  }
+}
+
+__global__ __launch_bounds__(RSJ_NT) void k_rsj_jump(const RsCell* cells, const uint64_t* __restrict__ polys) {
+  extern __shared__ uint32_t rsj_base[];   // raw[624 .. 624 + RSJ_BASEW)
+  __shared__ uint32_t mt[RS_N];
+  const RsCell& c = cells[blockIdx.y];
+  const int s = blockIdx.x + 1, tid = threadIdx.x;
+  const int mti = c.st->mti;
+  const int64_t need = rsj_need(c.jN, mti), s0 = (int64_t)s * RSJ_L;
+  if (s0 >= need) return;
+  const uint32_t* raw = c.raw;
+  for (int i = tid; i < RSJ_BASEW; i += RSJ_NT) rsj_base[i] = raw[RS_N + i];
+  __syncthreads();
+  // window[p] = XOR over the set bits i of g of w[624 + i + p]; the bit loop is uniform
+  const uint64_t* g = polys + (size_t)(s - 1) * RSJ_PW;
+  uint32_t a0 = 0, a1 = 0, a2 = 0;
+  for (int w = 0; w < RSJ_PW; ++w) {
+    uint64_t bits = g[w];
+    while (bits) {
+      const uint32_t* q = rsj_base + 64 * w + __builtin_ctzll(bits) + tid;
+      bits &= bits - 1;
+      a0 ^= q[0];
+      a1 ^= q[RSJ_NT];
+      a2 ^= q[2 * RSJ_NT];
+    }
+  }
+  mt[tid] = a0;
+  mt[tid + RSJ_NT] = a1;
+  if (tid + 2 * RSJ_NT < RS_N) mt[tid + 2 * RSJ_NT] = a2;
+  __syncthreads();
+  RS_G uint32_t* const W = (RS_G uint32_t*)c.words;
+  const int64_t end = (s0 + RSJ_L < need) ? s0 + RSJ_L : need;
+  for (int64_t b0 = s0; b0 < end; b0 += RS_N) {
+    if (b0 != s0) rs_mt_block<RSJ_NT>(mt, tid);
+    for (int t = tid; t < RS_N; t += RSJ_NT) W[b0 + t - mti] = rs_temper(mt[t]);
+  }
+}
+
+__global__ __launch_bounds__(256) void k_rsj_len(const RsCell* cells) {
+  const RsCell& c = cells[blockIdx.y];
+  if (!c.has_mix) return;
+  const int64_t N = c.jN;
+  const uint32_t* W = c.words;
+  RS_G int32_t* const T0 = (RS_G int32_t*)c.lift;
+  for (int64_t P = (int64_t)blockIdx.x * 256 + threadIdx.x; P <= N; P += (int64_t)gridDim.x * 256) {
+    int64_t v = N;
+    if (P < N) {
+      double a, eu;
+      v = P + rs_exp_head(W[P], a, eu);
+      v = v < N ? v : N;
+    }
+    T0[P] = (int32_t)v;
+  }
+}
+
+// level lvl of T (g = 0) or G (g = 1) from level lvl - 1
+__global__ __launch_bounds__(256) void k_rsj_lift(const RsCell* cells, int lvl, int g) {
+  const RsCell& c = cells[blockIdx.y];
+  if (!c.has_mix || lvl >= (g ? c.jlg : c.jlt)) return;
+  const int64_t S = c.jN + 1;
+  const int32_t* src = c.lift + (int64_t)((g ? c.jlt : 0) + lvl - 1) * S;
+  RS_G int32_t* const dst = (RS_G int32_t*)(c.lift + (int64_t)((g ? c.jlt : 0) + lvl) * S);
+  for (int64_t P = (int64_t)blockIdx.x * 256 + threadIdx.x; P < S; P += (int64_t)gridDim.x * 256)
+    dst[P] = src[src[P]];
+}
+
+__global__ __launch_bounds__(256) void k_rsj_g0(const RsCell* cells) {
+  const RsCell& c = cells[blockIdx.y];
+  if (!c.has_mix) return;
+  const int64_t N = c.jN, S = N + 1, pre = c.pre, post = c.jpost, nsim = c.nsim;
+  const int32_t* lift = c.lift;
+  RS_G int32_t* const G0 = (RS_G int32_t*)(c.lift + (int64_t)c.jlt * S);
+  for (int64_t P = (int64_t)blockIdx.x * 256 + threadIdx.x; P < S; P += (int64_t)gridDim.x * 256) {
+    int64_t v = N;
+    if (P + pre < N) {
+      v = (int64_t)rsj_adv(lift, S, (int32_t)(P + pre), nsim) + post;
+      v = v < N ? v : N;
+    }
+    G0[P] = (int32_t)v;
+  }
+}
+
+__device__ __forceinline__ int64_t rsj_rep_start(const RsCell& c, int64_t r) {
+  if (!c.has_mix) return r * c.pre;
+  const int64_t S = c.jN + 1;
+  return rsj_adv(c.lift + (int64_t)c.jlt * S, S, 0, r);
+}
+
+__global__ __launch_bounds__(256) void k_rsj_chain(const RsCell* cells, int32_t rc) {
+  const RsCell c = cells[blockIdx.y];   // by value: the stores below cannot alias it
+  const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (r > rc) return;
+  const int64_t P = rsj_rep_start(c, r);
+  if (r == rc) {
+    *c.jflag = (P >= c.jN) ? 1 : 0;
+    return;
+  }
+  c.rep_off[r] = P;
+  if (c.has_mix) {
+    const int64_t x = P + c.pre;
+    c.exp_end[r] = rsj_adv(c.lift, c.jN + 1, (int32_t)(x < c.jN ? x : c.jN), c.nsim);
+  }
+}
+
+__global__ __launch_bounds__(256) void k_rsj_expv(const RsCell* cells, int32_t rc) {
+  constexpr double q0 = RS_Q0;
+  const RsCell c = cells[blockIdx.y];   // by value: the stores below cannot alias it
+  if (!c.has_mix) return;
+  const int64_t nsim = c.nsim, N = c.jN, S = N + 1, total = (int64_t)rc * nsim;
+  const uint32_t* W = c.words;
+  RS_G double* const ev = (RS_G double*)c.expv;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const int64_t r = i / nsim, d = i - r * nsim;
+    const int64_t x0 = c.rep_off[r] + c.pre;
+    const int32_t x = rsj_adv(c.lift, S, (int32_t)(x0 < N ? x0 : N), d);
+    double e = 0.0;
+    if (x < N) {
+      double a, eu;
+      const int len = rs_exp_head(W[x], a, eu);
+      if (len == 1) {
+        e = a + eu;
+      } else {
+        uint32_t wmin = 0xffffffffu;
+        for (int t = 1; t < len; ++t) wmin = (W[x + t] < wmin) ? W[x + t] : wmin;
+        e = a + rs_unif(wmin) * q0;
+      }
+    }
+    ev[i] = e;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_rsj_state(const RsCell* cells, int32_t rc) {
+  const RsCell& c = cells[blockIdx.x];
+  if (*c.jflag) return;
+  RsState* st = c.st;
+  const int mti = st->mti;
+  const int64_t o = mti + rsj_rep_start(c, rc);
+  int64_t blk = o / RS_N;
+  int off = (int)(o % RS_N);
+  if (off == 0) { --blk; off = RS_N; }   // R's own form: the block consumed, position 624
+  __syncthreads();                       // every thread has read st->mti
+  for (int t = threadIdx.x; t < RS_N; t += 256)
+    st->mt[t] = (blk == 0) ? c.raw[t] : rs_untemper(c.words[blk * RS_N + t - mti]);
+  if (threadIdx.x == 0) { st->mti = off; st->pad[0] = 0; st->pad[1] = 0; }
+}
+
+int launch_rsj(RsCell* d_cells, int ncells, int32_t rc, const uint64_t* d_polys, int nseg,
+               int64_t max_pos, int max_lt, int max_lg, int64_t max_exp, void* stream) {
+  const hipStream_t s = (hipStream_t)stream;
+  const unsigned nc = (unsigned)ncells;
+  auto blocks = [](int64_t work) {
+    const int64_t b = (work + 255) / 256;
+    return (unsigned)(b < 4096 ? (b > 0 ? b : 1) : 4096);
+  };
+  hipLaunchKernelGGL(k_rsj_gen0, dim3(nc), dim3(RSJ_NT), 0, s, d_cells);
+  if (nseg > 1) {
+    const size_t lds = (size_t)RSJ_BASEW * 4;
+    // per call: the attribute is per device, and one process may drive several GPUs
+    const hipError_t e = hipFuncSetAttribute((const void*)k_rsj_jump,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return (int)e;
+    hipLaunchKernelGGL(k_rsj_jump, dim3((unsigned)(nseg - 1), nc), dim3(RSJ_NT), lds, s, d_cells, d_polys);
+  }
+  const dim3 gp(blocks(max_pos), nc);
+  if (max_lt > 0) {
+    hipLaunchKernelGGL(k_rsj_len, gp, dim3(256), 0, s, d_cells);
+    for (int l = 1; l < max_lt; ++l) hipLaunchKernelGGL(k_rsj_lift, gp, dim3(256), 0, s, d_cells, l, 0);
+    hipLaunchKernelGGL(k_rsj_g0, gp, dim3(256), 0, s, d_cells);
+    for (int l = 1; l < max_lg; ++l) hipLaunchKernelGGL(k_rsj_lift, gp, dim3(256), 0, s, d_cells, l, 1);
+  }
+  hipLaunchKernelGGL(k_rsj_chain, dim3(blocks((int64_t)rc + 1), nc), dim3(256), 0, s, d_cells, rc);
+  if (max_exp > 0) hipLaunchKernelGGL(k_rsj_expv, dim3(blocks(max_exp), nc), dim3(256), 0, s, d_cells, rc);
+  hipLaunchKernelGGL(k_rsj_state, dim3(nc), dim3(256), 0, s, d_cells, rc);
+  return (int)hipGetLastError();
 }
 
 // -------------------------------------------------------- k_rs_materialise ---

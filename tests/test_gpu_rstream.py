@@ -169,3 +169,53 @@ def test_rstream_extreme_eps_flips_take_no_words(dc, orc):
     spec = _spec(dc, eps1=40.0, eps2=1.0, n=500)
     res = dc.rstream.run_grid([spec], 3)[0]
     assert_close(res["records"], orc.rs_sim(spec.to_c(), 3))
+
+
+JUMP_CELLS = ["sign-gauss", "sign-gauss-neg", "sign-bern", "sign-nonorm-laplace", "subG-bounded",
+              "subG-gauss"]
+
+
+def _with_env(env, fn):
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        return fn()
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+def _jump_specs(dc):
+    return [_spec(dc, **CELLS[k]) for k in JUMP_CELLS] + [
+        _spec(dc, family="subG", dgp="bounded_factor", rho=0.4, n=40, nsim=3, mu=(0, 0),
+              sigma=(1, 1), eps1=2.0, eps2=2.0, seed=77)]
+
+
+@pytest.mark.parametrize("env", [{}, {"DCOR_RS_MAX_CHUNK": "7"}, {"DCOR_RSJ_TIGHT": "1"}],
+                         ids=["one-chunk", "chunks-of-7", "budget-overrun-fallback"])
+def test_jump_path_equals_sequential_walk(dc, orc, env):
+    """The jump path (segment-parallel generation from MT19937 jump-ahead windows, the walk by
+    pointer doubling) returns k_rs_stream's records byte for byte -- across chunks (the
+    .Random.seed it leaves) and when a chunk overruns its word budget (k_rs_stream re-walks
+    it from the unchanged state)."""
+    specs = _jump_specs(dc)
+    B = 40
+    walk = _with_env({"DCOR_RS_JUMP": "0"}, lambda: dc.rstream.run_grid(specs, B))
+    jump = _with_env(dict(env, DCOR_RS_JUMP="1"), lambda: dc.rstream.run_grid(specs, B))
+    for spec, a, b in zip(specs, walk, jump):
+        np.testing.assert_array_equal(a["records"], b["records"], err_msg=str(spec))
+        assert bytes(a["accum"][0]) == bytes(b["accum"][0]) and bytes(a["accum"][1]) == bytes(b["accum"][1])
+    for spec, b in zip(specs[:2], jump[:2]):
+        assert_close(b["records"][:12], orc.rs_sim(spec.to_c(), 12), what=str(spec))
+
+
+def test_jump_path_long_single_cell_against_oracle(dc, orc):
+    """One cell, 300 replicates (~3e6 words: ~100 jump segments): every replicate against the CPU
+    restatement, which walks R's stream word by word."""
+    spec = _spec(dc)
+    B = 300
+    got = _with_env({"DCOR_RS_JUMP": "1"}, lambda: dc.rstream.run_grid([spec], B))[0]
+    assert_close(got["records"], orc.rs_sim(spec.to_c(), B))
