@@ -437,9 +437,10 @@ int rs_arena_get(size_t bytes, void** out) {
   return arena_grow(c->rs, bytes, out);
 }
 
-// The first n jump polynomials of the R-stream jump path on this device (host table:
-// mt_segment_polys, computed once per process; uploaded when the device copy is short).
-int rsj_polys(int n, const uint64_t** out) {
+// The first n jump polynomials of the R-stream jump path on this device, as launch_rsj takes
+// them: per polynomial the list of its set bits (host table: mt_segment_polys, computed once per
+// process; uploaded when the device copy is short).
+int rsj_polys(int n, const uint32_t** poff, const uint32_t** pidx) {
   Ctx* c = nullptr;
   if (int st = ctx_get(&c)) return st;
   if (c->rsj_npoly < n) {
@@ -447,12 +448,26 @@ int rsj_polys(int n, const uint64_t** out) {
     int words = 0;
     if (int st = mt_segment_polys(RSJ_L, n, &table, &words)) return st;
     if (words != RSJ_PW) return fail(DCOR_EINVAL, "jump polynomial width %d", words);
+    const size_t head = (size_t)(n + 1 + 3) / 4 * 4;
+    std::vector<uint32_t> buf(head, 0u);
+    std::vector<uint16_t> idx;
+    for (int s = 0; s < n; ++s) {
+      buf[(size_t)s] = (uint32_t)(buf.size() - head);
+      idx.clear();
+      for (int w = 0; w < RSJ_PW; ++w)
+        for (uint64_t b = table[(size_t)s * RSJ_PW + w]; b; b &= b - 1)
+          idx.push_back((uint16_t)(64 * w + __builtin_ctzll(b)));
+      while (idx.size() % 8) idx.push_back((uint16_t)RSJ_PAD);
+      for (size_t i = 0; i < idx.size(); i += 2) buf.push_back((uint32_t)idx[i] | ((uint32_t)idx[i + 1] << 16));
+    }
+    buf[(size_t)n] = (uint32_t)(buf.size() - head);
     void* d = nullptr;
-    if (int st = arena_grow(c->rsj, (size_t)n * RSJ_PW * 8, &d)) return st;
-    HIPCHK(hipMemcpy(d, table, (size_t)n * RSJ_PW * 8, hipMemcpyHostToDevice));
+    if (int st = arena_grow(c->rsj, buf.size() * 4, &d)) return st;
+    HIPCHK(hipMemcpy(d, buf.data(), buf.size() * 4, hipMemcpyHostToDevice));
     c->rsj_npoly = n;
   }
-  *out = (const uint64_t*)c->rsj.p;
+  *poff = (const uint32_t*)c->rsj.p;
+  *pidx = *poff + (size_t)(c->rsj_npoly + 1 + 3) / 4 * 4;
   return DCOR_OK;
 }
 
@@ -1572,7 +1587,8 @@ void rsj_dims(RsPlan& p, int64_t rc) {
 }
 size_t rsj_cell_bytes(const RsPlan& p) {
   const RsCell& c = p.c;
-  return al256((size_t)RSJ_L * 4) + al256((size_t)(c.jlt + c.jlg) * (size_t)(c.jN + 1) * 4) + 256;
+  return al256((size_t)RSJ_L * 4) + al256((size_t)RSJ_TBYTES(c.jlt, c.jN + 1)) +
+         al256((size_t)c.jlg * (size_t)(c.jN + 1) * 4) + 256;
 }
 // DCOR_RS_JUMP: 0 never, 1 whenever the batch allows it, unset: batches of at most 64 cells
 // (below that k_rs_stream leaves CUs idle; above it its one-CU-per-cell walk is the cheaper).
@@ -1663,15 +1679,17 @@ int dcor_rstream_grid_run(const dcor_cell* cells, int ncells, int64_t B, dcor_ac
       p.c.st = dst.as<RsState>() + i;
       hc[(size_t)i] = p.c;
     }
-    const uint64_t* d_polys = nullptr;
+    const uint32_t *d_poff = nullptr, *d_pidx = nullptr;
     int nseg = 1;
     if (jump) {
       for (int i = 0; i < nb; ++i) {
         RsCell& c = hc[(size_t)i];
         c.raw = (uint32_t*)base;
         base += al256((size_t)RSJ_L * 4);
-        c.lift = (int32_t*)base;
-        base += al256((size_t)(c.jlt + c.jlg) * (size_t)(c.jN + 1) * 4);
+        c.tlift = (uint8_t*)base;
+        base += al256((size_t)RSJ_TBYTES(c.jlt, c.jN + 1));
+        c.glift = (int32_t*)base;
+        base += al256((size_t)c.jlg * (size_t)(c.jN + 1) * 4);
         max_pos = std::max(max_pos, c.jN + 1);
         max_exp = std::max(max_exp, c.has_mix ? rc * c.nsim : 0);
         max_lt = std::max(max_lt, (int)c.jlt);
@@ -1683,7 +1701,7 @@ int dcor_rstream_grid_run(const dcor_cell* cells, int ncells, int64_t B, dcor_ac
       for (int i = 0; i < nb; ++i) hc[(size_t)i].jflag = flags + i;
       nseg = (int)((need + RSJ_L - 1) / RSJ_L);
       if (nseg > 1)
-        if (int st = rsj_polys(nseg - 1, &d_polys)) return st;
+        if (int st = rsj_polys(nseg - 1, &d_poff, &d_pidx)) return st;
     }
     HIPCHK(hipMemcpy(dst.p, hst.data(), sizeof(RsState) * (size_t)nb, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(dcells.p, hc.data(), sizeof(RsCell) * (size_t)nb, hipMemcpyHostToDevice));
@@ -1695,7 +1713,7 @@ int dcor_rstream_grid_run(const dcor_cell* cells, int ncells, int64_t B, dcor_ac
       const int32_t rcc = (int32_t)std::min<int64_t>(rc, B - done);
       int e = 0;
       if (jump) {
-        e = launch_rsj(dcells.as<RsCell>(), nb, rcc, d_polys, nseg, max_pos, max_lt, max_lg, max_exp, nullptr);
+        e = launch_rsj(dcells.as<RsCell>(), nb, rcc, d_poff, d_pidx, nseg, max_pos, max_lt, max_lg, max_exp, nullptr);
         if (e) return hip_fail((hipError_t)e, "rstream jump launch");
         // a cell whose chunk ran past its word budget (never seen: the budget is ~10 sd above the
         // mean) kept its state; k_rs_stream walks it instead

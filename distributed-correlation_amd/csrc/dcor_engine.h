@@ -96,7 +96,7 @@ struct PrematSubgConst {
   const double2* xyc; const double2* soc;
   // Shared panel, random batches, n <= DCOR_DICT_NMAX: dictionary-coded panel built on device
   // per launch (k_panel_dict).  dict_ok is set by the device: 1 -> the coded kernel runs,
-  // 0 (more than 256 distinct values in a column, or a NaN) -> the L2-gather kernel runs.
+  // 0 (more than 256 distinct values in a column, a NaN or an infinity) -> the L2-gather kernel runs.
   uint16_t* dict_codes; double* dict_vals; int* dict_ok;
   // Coded-panel kernel only: each replicate's sums are split over `slices` work items (0 or 1:
   // one), whose partials part[rep * slices + t] the epilogue merges in slice order.
@@ -297,8 +297,9 @@ struct RsCell {
   // jump-ahead windows, the walk replaced by pointer doubling over consumption positions
   // 0 .. jN (jN: the chunk's word budget; position jN stands for "past the budget").
   uint32_t* raw;               // [RSJ_L] raw words of the chunk's first segment (state block first)
-  int32_t* lift;               // [jlt + jlg][jN + 1]: T_k(P) = the position 2^k exp_rand draws
-                               // on from P; G_k(P) = 2^k replicates on from replicate start P
+  uint8_t* tlift;              // T_k(P) - P, the words 2^k exp_rand draws from P take (levels
+                               // k < RSJ_T16 uint16, then uint32; level k at RSJ_TBYTES(k, jN + 1))
+  int32_t* glift;              // [jlg][jN + 1]: G_k(P) = the start 2^k replicates on from P
   int32_t* jflag;              // set when the chunk ran past jN (the host re-runs it by k_rs_stream)
   int64_t jN, jpost;           // word budget; fixed words after the exp_rand segment (rbinom)
   int32_t jlt, jlg;            // levels of T and of G
@@ -307,11 +308,18 @@ struct RsCell {
 // base window every jump combines), and 64-bit words per jump polynomial.
 #define RSJ_L (624 * 48)
 #define RSJ_PW 312
+// T levels below RSJ_T16 fit 16 bits (a draw takes <= 17 words: 17 * 2^11 < 65536)
+#define RSJ_T16 12
+#define RSJ_TBYTES(k, S) \
+  ((k) <= RSJ_T16 ? 2 * (int64_t)(S) * (k) : 2 * (int64_t)(S) * RSJ_T16 + 4 * (int64_t)(S) * ((k) - RSJ_T16))
 // Runs the jump path over d_cells[0..ncells): generation (segment 0 sequential, the rest from
-// the nseg - 1 jump polynomials d_polys), the walk by pointer doubling, the exp_rand values and
-// the .Random.seed after the chunk.  max_pos: the largest jN + 1; max_lt / max_lg: the largest
-// jlt / jlg; max_exp: the largest rc * nsim.
-int launch_rsj(RsCell* d_cells, int ncells, int32_t rc, const uint64_t* d_polys, int nseg,
+// the nseg - 1 jump polynomials), the walk by pointer doubling, the exp_rand values and the
+// .Random.seed after the chunk.  The polynomials as set-bit lists: polynomial s at
+// d_pidx[d_poff[s] .. d_poff[s + 1]), two 16-bit bit indices per word, each list padded to a
+// multiple of 8 indices with RSJ_PAD.  max_pos: the largest jN + 1; max_lt /
+// max_lg: the largest jlt / jlg; max_exp: the largest rc * nsim.
+#define RSJ_PAD (19936 + 624)
+int launch_rsj(RsCell* d_cells, int ncells, int32_t rc, const uint32_t* d_poff, const uint32_t* d_pidx, int nseg,
                int64_t max_pos, int max_lt, int max_lg, int64_t max_exp, void* stream);
 // RsCell.family for the HRS INT runs: rLap(n), rLap(1), mixquant (real-data-sims.R:375-402)
 #define RS_FAMILY_HRS_INT 2

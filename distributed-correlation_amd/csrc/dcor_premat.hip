@@ -363,7 +363,8 @@ __global__ __launch_bounds__(DCOR_BLOCK) void k_premat_subg_epilogue(PrematSubgC
 // and every INT panel read then hits LDS, and only the per-replicate noise / permutation
 // streams touch HBM.  The values are the panel's own doubles, so results are unchanged.
 // k_panel_dict builds the dictionaries with an LDS hash table (one workgroup); if a column
-// has more than 256 distinct values (or a NaN), it clears *ok and the L2-gather kernel runs.
+// has more than 256 distinct values (or a NaN or an infinity), it clears *ok and the L2-gather
+// kernel runs: the coded kernels rely on a finite dictionary.
 #define DICT_SLOTS 1024
 #define DICT_MAX 256
 #define DICT_THREADS 1024
@@ -397,7 +398,7 @@ __global__ __launch_bounds__(DICT_THREADS) void k_panel_dict(const double* __res
       if (i0 + u * DICT_THREADS >= n) break;
       if (*(volatile int*)&bad) break;
       const double v = cpt == 0 ? xv[u] : yv[u];
-      if (v != v) { bad = 1; break; }
+      if (!(fabs(v) <= 1.7976931348623157e308)) { bad = 1; break; }   // NaN or +-Inf
       const unsigned long long key = (unsigned long long)__double_as_longlong(v);
       uint32_t h = dict_hash(key);
       // Plain reads find a present key without an atomic (most samples repeat a value); the
@@ -550,7 +551,10 @@ __global__ __launch_bounds__(DICT_NT, WPE) void k_premat_subg_dict(PrematSubgCon
         const uint32_t cd = cod[i];
         sv = dS[cd & 255u]; ov = dO[cd >> 8];
       }
-      return rclip((sv + c.bs * l) * ov, c.lr);
+      // coded panel: every dictionary value is finite (k_panel_dict), so is the noise, so the
+      // product is never NaN and R's NaN-preserving clip reduces to min + max
+      if constexpr (L2) return rclip((sv + c.bs * l) * ov, c.lr);
+      else return rclip_fin((sv + c.bs * l) * ov, c.lr);
     };
     auto uterm = [&](int64_t i, double l) {
       const double Uc = uval(i, l);
@@ -1300,7 +1304,8 @@ __global__ __launch_bounds__(DICT_NT, WPE) void k_hrs_fused(PrematSubgConst p, H
     const uint32_t rep = hk.rep_begin + (uint32_t)it;
     DD sP{0, 0}, sT{0, 0}, sT2{0, 0}, sU{0, 0}, sU2{0, 0};
     auto uval = [&](uint32_t cd, double l) {  // real-data-sims.R:222-232
-      return rclip((dS[cd & 255u] + c.bs * l) * dO[cd >> 8], c.lr);
+      // finite dictionary (k_panel_dict) and noise: the product is never NaN
+      return rclip_fin((dS[cd & 255u] + c.bs * l) * dO[cd >> 8], c.lr);
     };
     auto uterm = [&](double Uc) {
       ks_acc(sU, Uc);

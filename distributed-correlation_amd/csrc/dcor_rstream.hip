@@ -465,7 +465,8 @@ __global__ __launch_bounds__(RS_STREAM_NT) void k_rs_stream(RsCell* cells, int32
 //                polynomial g = x^(s RSJ_L - 624) mod phi (dcor_mtjump.cpp) over segment 0's
 //                words, then the recurrence; all segments of all cells at once;
 //   k_rsj_len    T_0(P) = P + the words an exp_rand draw starting at P consumes;
-//   k_rsj_lift   T_{k+1} = T_k o T_k (and G likewise): pointer doubling;
+//   k_rsj_tlift  T_{k+1} = T_k o T_k (16-bit offsets while they fit), k_rsj_glift likewise for G:
+//                pointer doubling;
 //   k_rsj_g0     G_0(P) = T^nsim(P + pre) + post: the start of the replicate after one at P;
 //   k_rsj_chain  P_r = G^r(0) for every r <= rc (binary digits of r), exp_end = T^nsim(P_r + pre);
 //   k_rsj_expv   the d-th exp_rand value of replicate r at T^d(P_r + pre);
@@ -475,17 +476,24 @@ __global__ __launch_bounds__(RS_STREAM_NT) void k_rs_stream(RsCell* cells, int32
 // chunk by k_rs_stream).  Replicates without mixquant (the Laplace CI) have a fixed length: P_r =
 // r * pre, no tables.
 #define RSJ_NT 256
+#define RSJ_JNT 640                         // k_rsj_jump: one lane per window word, 10 waves
 #define RSJ_DEG 19937
-#define RSJ_BASEW (RSJ_DEG - 1 + 3 * RSJ_NT)   // base words read (lanes past 623 read, unused)
+#define RSJ_BASEW (RSJ_DEG - 1 + RS_N)      // base words one window combines
+static_assert(RSJ_PAD == RSJ_BASEW, "the list pad points at the zero words after the base");
 
 __device__ __forceinline__ int64_t rsj_need(int64_t jN, int mti) {  // raw words the chunk may read
   return (mti + jN + 64 + RS_N - 1) / RS_N * RS_N;
 }
 
-// x advanced by m steps of T (levels T_k at lift + k * S); x, every table entry <= N
-__device__ __forceinline__ int32_t rsj_adv(const int32_t* __restrict__ lift, int64_t S, int32_t x, int64_t m) {
+// T_k(x) - x (levels at t: RSJ_TBYTES)
+__device__ __forceinline__ int64_t rsj_tget(const uint8_t* t, int64_t S, int k, int64_t x) {
+  const uint8_t* lv = t + RSJ_TBYTES(k, S);
+  return (k < RSJ_T16) ? (int64_t)((const uint16_t*)lv)[x] : (int64_t)((const uint32_t*)lv)[x];
+}
+// x advanced by m exp_rand draws (x and every table entry <= N: T maps N to N)
+__device__ __forceinline__ int64_t rsj_adv_t(const uint8_t* t, int64_t S, int64_t x, int64_t m) {
   for (int k = 0; m; ++k, m >>= 1)
-    if (m & 1) x = lift[(int64_t)k * S + x];
+    if (m & 1) x += rsj_tget(t, S, k, x);
   return x;
 }
 
@@ -510,8 +518,12 @@ __global__ __launch_bounds__(RSJ_NT) void k_rsj_gen0(const RsCell* cells) {
   }
 }
 
-__global__ __launch_bounds__(RSJ_NT) void k_rsj_jump(const RsCell* cells, const uint64_t* __restrict__ polys) {
-  extern __shared__ uint32_t rsj_base[];   // raw[624 .. 624 + RSJ_BASEW)
+// One workgroup per (segment, cell); lane p < 624 combines window word p over the set-bit list
+// of the segment's jump polynomial (host-built, padded to a multiple of 8 with RSJ_PAD, which
+// points every lane at a zero word): eight LDS reads in flight per lane, the list in scalar loads.
+__global__ __launch_bounds__(RSJ_JNT) void k_rsj_jump(const RsCell* cells, const uint32_t* __restrict__ poff,
+                                                      const uint32_t* __restrict__ pidx) {
+  extern __shared__ uint32_t rsj_base[];   // raw[624 .. 624 + RSJ_BASEW), then 624 zeros
   __shared__ uint32_t mt[RS_N];
   const RsCell& c = cells[blockIdx.y];
   const int s = blockIdx.x + 1, tid = threadIdx.x;
@@ -519,30 +531,32 @@ __global__ __launch_bounds__(RSJ_NT) void k_rsj_jump(const RsCell* cells, const 
   const int64_t need = rsj_need(c.jN, mti), s0 = (int64_t)s * RSJ_L;
   if (s0 >= need) return;
   const uint32_t* raw = c.raw;
-  for (int i = tid; i < RSJ_BASEW; i += RSJ_NT) rsj_base[i] = raw[RS_N + i];
+  for (int i = tid; i < RSJ_BASEW + RS_N; i += RSJ_JNT) rsj_base[i] = (i < RSJ_BASEW) ? raw[RS_N + i] : 0u;
   __syncthreads();
-  // window[p] = XOR over the set bits i of g of w[624 + i + p]; the bit loop is uniform
-  const uint64_t* g = polys + (size_t)(s - 1) * RSJ_PW;
-  uint32_t a0 = 0, a1 = 0, a2 = 0;
-  for (int w = 0; w < RSJ_PW; ++w) {
-    uint64_t bits = g[w];
-    while (bits) {
-      const uint32_t* q = rsj_base + 64 * w + __builtin_ctzll(bits) + tid;
-      bits &= bits - 1;
-      a0 ^= q[0];
-      a1 ^= q[RSJ_NT];
-      a2 ^= q[2 * RSJ_NT];
-    }
+  const int p = tid < RS_N ? tid : RS_N - 1;
+  const uint32_t* q = rsj_base + p;
+  uint32_t acc = 0;
+  // pidx: two 16-bit bit indices per word; poff in words
+  // (scalar and LDS loads share one wait counter: the next four words are loaded before this
+  // step's reads, so waiting for the reads never waits on a fresh scalar load)
+  const uint32_t j1 = poff[s];
+  uint32_t j = poff[s - 1];
+  uint4 nx = make_uint4(0, 0, 0, 0);
+  if (j < j1) nx = *(const uint4*)(pidx + j);
+  for (; j < j1; j += 4) {
+    const uint4 pr = nx;
+    if (j + 4 < j1) nx = *(const uint4*)(pidx + j + 4);
+    const uint32_t v0 = q[pr.x & 0xffffu], v1 = q[pr.x >> 16], v2 = q[pr.y & 0xffffu], v3 = q[pr.y >> 16];
+    const uint32_t v4 = q[pr.z & 0xffffu], v5 = q[pr.z >> 16], v6 = q[pr.w & 0xffffu], v7 = q[pr.w >> 16];
+    acc ^= ((v0 ^ v1) ^ (v2 ^ v3)) ^ ((v4 ^ v5) ^ (v6 ^ v7));
   }
-  mt[tid] = a0;
-  mt[tid + RSJ_NT] = a1;
-  if (tid + 2 * RSJ_NT < RS_N) mt[tid + 2 * RSJ_NT] = a2;
+  if (tid < RS_N) mt[tid] = acc;
   __syncthreads();
   RS_G uint32_t* const W = (RS_G uint32_t*)c.words;
   const int64_t end = (s0 + RSJ_L < need) ? s0 + RSJ_L : need;
   for (int64_t b0 = s0; b0 < end; b0 += RS_N) {
-    if (b0 != s0) rs_mt_block<RSJ_NT>(mt, tid);
-    for (int t = tid; t < RS_N; t += RSJ_NT) W[b0 + t - mti] = rs_temper(mt[t]);
+    if (b0 != s0) rs_mt_block<RSJ_JNT>(mt, tid);
+    for (int t = tid; t < RS_N; t += RSJ_JNT) W[b0 + t - mti] = rs_temper(mt[t]);
   }
 }
 
@@ -551,25 +565,40 @@ __global__ __launch_bounds__(256) void k_rsj_len(const RsCell* cells) {
   if (!c.has_mix) return;
   const int64_t N = c.jN;
   const uint32_t* W = c.words;
-  RS_G int32_t* const T0 = (RS_G int32_t*)c.lift;
+  RS_G uint16_t* const T0 = (RS_G uint16_t*)c.tlift;
   for (int64_t P = (int64_t)blockIdx.x * 256 + threadIdx.x; P <= N; P += (int64_t)gridDim.x * 256) {
-    int64_t v = N;
+    int64_t v = 0;
     if (P < N) {
       double a, eu;
-      v = P + rs_exp_head(W[P], a, eu);
-      v = v < N ? v : N;
+      v = rs_exp_head(W[P], a, eu);
+      v = (P + v < N) ? v : N - P;
     }
-    T0[P] = (int32_t)v;
+    T0[P] = (uint16_t)v;
   }
 }
 
-// level lvl of T (g = 0) or G (g = 1) from level lvl - 1
-__global__ __launch_bounds__(256) void k_rsj_lift(const RsCell* cells, int lvl, int g) {
+// T level k from level k - 1: T_k(P) - P = d(P) + d(P + d(P)), d = T_{k-1} - id
+__global__ __launch_bounds__(256) void k_rsj_tlift(const RsCell* cells, int k) {
   const RsCell& c = cells[blockIdx.y];
-  if (!c.has_mix || lvl >= (g ? c.jlg : c.jlt)) return;
+  if (!c.has_mix || k >= c.jlt) return;
   const int64_t S = c.jN + 1;
-  const int32_t* src = c.lift + (int64_t)((g ? c.jlt : 0) + lvl - 1) * S;
-  RS_G int32_t* const dst = (RS_G int32_t*)(c.lift + (int64_t)((g ? c.jlt : 0) + lvl) * S);
+  const uint8_t* t = c.tlift;
+  uint8_t* const dst = c.tlift + RSJ_TBYTES(k, S);
+  for (int64_t P = (int64_t)blockIdx.x * 256 + threadIdx.x; P < S; P += (int64_t)gridDim.x * 256) {
+    const int64_t d = rsj_tget(t, S, k - 1, P);
+    const int64_t v = d + rsj_tget(t, S, k - 1, P + d);
+    if (k < RSJ_T16) ((RS_G uint16_t*)dst)[P] = (uint16_t)v;
+    else ((RS_G uint32_t*)dst)[P] = (uint32_t)v;
+  }
+}
+
+// G level k from level k - 1
+__global__ __launch_bounds__(256) void k_rsj_glift(const RsCell* cells, int k) {
+  const RsCell& c = cells[blockIdx.y];
+  if (!c.has_mix || k >= c.jlg) return;
+  const int64_t S = c.jN + 1;
+  const int32_t* src = c.glift + (int64_t)(k - 1) * S;
+  RS_G int32_t* const dst = (RS_G int32_t*)(c.glift + (int64_t)k * S);
   for (int64_t P = (int64_t)blockIdx.x * 256 + threadIdx.x; P < S; P += (int64_t)gridDim.x * 256)
     dst[P] = src[src[P]];
 }
@@ -578,12 +607,12 @@ __global__ __launch_bounds__(256) void k_rsj_g0(const RsCell* cells) {
   const RsCell& c = cells[blockIdx.y];
   if (!c.has_mix) return;
   const int64_t N = c.jN, S = N + 1, pre = c.pre, post = c.jpost, nsim = c.nsim;
-  const int32_t* lift = c.lift;
-  RS_G int32_t* const G0 = (RS_G int32_t*)(c.lift + (int64_t)c.jlt * S);
+  const uint8_t* t = c.tlift;
+  RS_G int32_t* const G0 = (RS_G int32_t*)c.glift;
   for (int64_t P = (int64_t)blockIdx.x * 256 + threadIdx.x; P < S; P += (int64_t)gridDim.x * 256) {
     int64_t v = N;
     if (P + pre < N) {
-      v = (int64_t)rsj_adv(lift, S, (int32_t)(P + pre), nsim) + post;
+      v = rsj_adv_t(t, S, P + pre, nsim) + post;
       v = v < N ? v : N;
     }
     G0[P] = (int32_t)v;
@@ -593,7 +622,10 @@ __global__ __launch_bounds__(256) void k_rsj_g0(const RsCell* cells) {
 __device__ __forceinline__ int64_t rsj_rep_start(const RsCell& c, int64_t r) {
   if (!c.has_mix) return r * c.pre;
   const int64_t S = c.jN + 1;
-  return rsj_adv(c.lift + (int64_t)c.jlt * S, S, 0, r);
+  int64_t x = 0;
+  for (int k = 0; r; ++k, r >>= 1)
+    if (r & 1) x = c.glift[(int64_t)k * S + x];
+  return x;
 }
 
 __global__ __launch_bounds__(256) void k_rsj_chain(const RsCell* cells, int32_t rc) {
@@ -608,7 +640,7 @@ __global__ __launch_bounds__(256) void k_rsj_chain(const RsCell* cells, int32_t 
   c.rep_off[r] = P;
   if (c.has_mix) {
     const int64_t x = P + c.pre;
-    c.exp_end[r] = rsj_adv(c.lift, c.jN + 1, (int32_t)(x < c.jN ? x : c.jN), c.nsim);
+    c.exp_end[r] = rsj_adv_t(c.tlift, c.jN + 1, x < c.jN ? x : c.jN, c.nsim);
   }
 }
 
@@ -622,7 +654,7 @@ __global__ __launch_bounds__(256) void k_rsj_expv(const RsCell* cells, int32_t r
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
     const int64_t r = i / nsim, d = i - r * nsim;
     const int64_t x0 = c.rep_off[r] + c.pre;
-    const int32_t x = rsj_adv(c.lift, S, (int32_t)(x0 < N ? x0 : N), d);
+    const int64_t x = rsj_adv_t(c.tlift, S, x0 < N ? x0 : N, d);
     double e = 0.0;
     if (x < N) {
       double a, eu;
@@ -654,7 +686,7 @@ __global__ __launch_bounds__(256) void k_rsj_state(const RsCell* cells, int32_t 
   if (threadIdx.x == 0) { st->mti = off; st->pad[0] = 0; st->pad[1] = 0; }
 }
 
-int launch_rsj(RsCell* d_cells, int ncells, int32_t rc, const uint64_t* d_polys, int nseg,
+int launch_rsj(RsCell* d_cells, int ncells, int32_t rc, const uint32_t* d_poff, const uint32_t* d_pidx, int nseg,
                int64_t max_pos, int max_lt, int max_lg, int64_t max_exp, void* stream) {
   const hipStream_t s = (hipStream_t)stream;
   const unsigned nc = (unsigned)ncells;
@@ -664,19 +696,19 @@ int launch_rsj(RsCell* d_cells, int ncells, int32_t rc, const uint64_t* d_polys,
   };
   hipLaunchKernelGGL(k_rsj_gen0, dim3(nc), dim3(RSJ_NT), 0, s, d_cells);
   if (nseg > 1) {
-    const size_t lds = (size_t)RSJ_BASEW * 4;
+    const size_t lds = (size_t)(RSJ_BASEW + RS_N) * 4;
     // per call: the attribute is per device, and one process may drive several GPUs
     const hipError_t e = hipFuncSetAttribute((const void*)k_rsj_jump,
                                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return (int)e;
-    hipLaunchKernelGGL(k_rsj_jump, dim3((unsigned)(nseg - 1), nc), dim3(RSJ_NT), lds, s, d_cells, d_polys);
+    hipLaunchKernelGGL(k_rsj_jump, dim3((unsigned)(nseg - 1), nc), dim3(RSJ_JNT), lds, s, d_cells, d_poff, d_pidx);
   }
   const dim3 gp(blocks(max_pos), nc);
   if (max_lt > 0) {
     hipLaunchKernelGGL(k_rsj_len, gp, dim3(256), 0, s, d_cells);
-    for (int l = 1; l < max_lt; ++l) hipLaunchKernelGGL(k_rsj_lift, gp, dim3(256), 0, s, d_cells, l, 0);
+    for (int l = 1; l < max_lt; ++l) hipLaunchKernelGGL(k_rsj_tlift, gp, dim3(256), 0, s, d_cells, l);
     hipLaunchKernelGGL(k_rsj_g0, gp, dim3(256), 0, s, d_cells);
-    for (int l = 1; l < max_lg; ++l) hipLaunchKernelGGL(k_rsj_lift, gp, dim3(256), 0, s, d_cells, l, 1);
+    for (int l = 1; l < max_lg; ++l) hipLaunchKernelGGL(k_rsj_glift, gp, dim3(256), 0, s, d_cells, l);
   }
   hipLaunchKernelGGL(k_rsj_chain, dim3(blocks((int64_t)rc + 1), nc), dim3(256), 0, s, d_cells, rc);
   if (max_exp > 0) hipLaunchKernelGGL(k_rsj_expv, dim3(blocks(max_exp), nc), dim3(256), 0, s, d_cells, rc);

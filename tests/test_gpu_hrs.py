@@ -23,11 +23,24 @@ def panel():
 
 @pytest.mark.parametrize("eps", [2.0, 0.5])
 def test_hrs_replicates_match_oracle(panel, eps):
+    _check_against_oracle(panel, eps, R=5, rb=3)
+
+
+def test_hrs_infinite_panel_value_takes_the_l2_kernel(panel):
+    """The coded kernels clip without R's NaN branch because their dictionary is finite: a panel
+    with an infinity is not coded (k_panel_dict), and the L2 kernel's results match the oracle."""
+    z = dict(panel)
+    z["age_z"] = z["age_z"].copy()
+    z["bmi_z"] = z["bmi_z"].copy()
+    z["age_z"][3] = np.inf
+    z["bmi_z"][7] = -np.inf
+    _check_against_oracle(z, 2.0, R=2, rb=0)
+
+
+def _check_against_oracle(z, eps, R, rb):
     from dcor import hrs
     from oracle import oracle as orc
-    z = panel
     n = len(z["age_z"])
-    R, rb = 5, 3
     res, noise, geo = hrs.hrs_replicates(z["age_z"], z["bmi_z"], z["lambda_age_z"], z["lambda_bmi_z"], eps,
                                          R, seed_ni=1010, seed_int=1020, rep_begin=rb, chunk=2,
                                          keep_noise=True)
