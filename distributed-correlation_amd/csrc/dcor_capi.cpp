@@ -508,7 +508,7 @@ int prepare_cell(const dcor_cell& c, CellPlan& p) {
     } else {
       cx = cy = 0.0; rx = ry = 2.0;
     }
-    code_map(cx, rx, 65536.0, &k.cbase_x, &k.cinv_x);
+    code_map(cx, rx, 32768.0, &k.cbase_x, &k.cinv_x);
     code_map(cy, ry, 32768.0, &k.cbase_y, &k.cinv_y);
     k.cinv_xf = (float)k.cinv_x; k.cnb_xf = (float)(-k.cbase_x * k.cinv_x);
     k.cinv_yf = (float)k.cinv_y; k.cnb_yf = (float)(-k.cbase_y * k.cinv_y);

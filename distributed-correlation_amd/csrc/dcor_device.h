@@ -24,11 +24,11 @@ namespace dcor {
 // ------------------------------------------------------------------ Philox
 struct U4 { uint32_t w0, w1, w2, w3; };
 
-// a ^ b ^ k in one gfx950 v_bitop3_b32 (truth table 0x96); k is wave-uniform (SGPR).
+// a ^ b ^ k in one gfx950 v_bitop3_b32 (truth table 0x96).  The builtin, not inline asm: the
+// compiler does not form bitop3 from a ^ b ^ k by itself, and after an asm statement it pads with
+// a hazard s_nop (7.5 per pass-1 sample).
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t k) {
-  uint32_t r;
-  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "s"(k));
-  return r;
+  return __builtin_amdgcn_bitop3_b32(a, b, k, 0x96);
 }
 
 __device__ __forceinline__ U4 philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
@@ -63,7 +63,10 @@ __device__ __forceinline__ double u53(uint32_t a, uint32_t b) {
 // Division-free log for positive normal x (same code as oracle/orc_log): x = 2^k z with
 // z in [0.6875, 1.375), r = fma(z, 1/c, -1) against a 256-entry table, log x = k ln2 +
 // log c + log1p(r) with a degree-6 polynomial (|r| < 2^-9).  ~12 fp64 ops; <= 2 ulp.
-__device__ __forceinline__ double dlog(double x) {
+// `tab` is dcor_log8_tab or a copy of it in LDS: a kernel that streams HBM reads its table from LDS,
+// because s_waitcnt vmcnt waits in issue order -- a table gather from global memory would wait for
+// every stream load issued before it, which defeats the stream's prefetch.
+__device__ __forceinline__ double dlog_t(double x, const double2* tab) {
   // The offset's low word is 0, so the reduction lives in the high word (32-bit ops only).
   const uint64_t ix = (uint64_t)__double_as_longlong(x);
   const uint32_t hi = (uint32_t)(ix >> 32), tmp = hi - 0x3fe60000u;
@@ -71,7 +74,8 @@ __device__ __forceinline__ double dlog(double x) {
   const int k = (int)tmp >> 20;
   const double z = __longlong_as_double(
       (long long)(((uint64_t)(hi - (tmp & 0xfff00000u)) << 32) | (uint32_t)ix));
-  const double invc = dcor_log8_tab[i][0], logc = dcor_log8_tab[i][1];
+  const double2 e = tab[i];
+  const double invc = e.x, logc = e.y;
   const double r = fma(z, invc, -1.0), kd = (double)k, r2 = r * r;
   double p = fma(r, DCOR_LOG1P_C6, DCOR_LOG1P_C5);
   p = fma(r, p, DCOR_LOG1P_C4);
@@ -79,6 +83,13 @@ __device__ __forceinline__ double dlog(double x) {
   p = fma(r, p, DCOR_LOG1P_C2);
   const double w = fma(kd, DCOR_LN2_HI, logc), lo = fma(kd, DCOR_LN2_LO, r2 * p);
   return w + (r + lo);
+}
+__device__ __forceinline__ double dlog(double x) {
+  return dlog_t(x, reinterpret_cast<const double2*>(dcor_log8_tab));
+}
+// dcor_log8_tab into LDS (256 double2, 4 KB) by the calling workgroup; the caller synchronises.
+__device__ __forceinline__ void log_tab_to_lds(double2* lt, int nthreads) {
+  for (int e = threadIdx.x; e < 256; e += nthreads) lt[e] = make_double2(dcor_log8_tab[e][0], dcor_log8_tab[e][1]);
 }
 
 // sin(pi t), cos(pi t) for t in [0, 2], given t64 = 64 t (same code as oracle/orc_sincospi):
@@ -95,10 +106,13 @@ __device__ __forceinline__ void dsincospi64(double t64, double* sp, double* cp) 
   *cp = fma(C, cm1, fma(-S, sd, C));
 }
 
-__device__ __forceinline__ double unit_laplace(double u) {
+__device__ __forceinline__ double unit_laplace_t(double u, const double2* tab) {
   const double up = u - 0.5;
-  const double g = dlog(1.0 - 2.0 * fabs(up));
+  const double g = dlog_t(1.0 - 2.0 * fabs(up), tab);
   return (up > 0) ? -g : g;
+}
+__device__ __forceinline__ double unit_laplace(double u) {
+  return unit_laplace_t(u, reinterpret_cast<const double2*>(dcor_log8_tab));
 }
 
 // Correctly rounded sqrt for positive normal x >= 2^-767 (LLVM's own f64 sqrt lowering

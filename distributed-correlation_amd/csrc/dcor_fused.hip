@@ -274,8 +274,8 @@ __device__ __forceinline__ void sign_finish(const SignConst& c, uint32_t rep, DD
 
 // ======================================== fused sign family, one pass (hot) ===
 // Pass 1 generates each sample once: the DP-mean sums of clip(x), clip(y) (vert-cor.R:
-// 328-340) and a 4-byte record per sample in a per-workgroup slab -- a monotone 16-bit
-// code of clip(x), a 15-bit code of clip(y) and the INT flip bit.  q(v) = clamp(floor(
+// 328-340) and a 4-byte record per sample in a per-workgroup slab -- monotone 15-bit codes
+// of clip(x) (bits 0-14) and clip(y) (bits 16-30) and the INT flip bit (31); bit 15 is 0.  q(v) = clamp(floor(
 // (v - base) * inv)) is monotone non-decreasing, so q(xc) != q(mu) proves sign(xc - mu);
 // pass 2 decides every sign from codes and regenerates only samples whose code ties a
 // threshold's code.  Results equal the two-pass algorithm's exactly.  Each thread
@@ -296,6 +296,17 @@ __device__ __forceinline__ int sgnd(uint32_t q, uint32_t qm) {
   int r;
   asm("v_med3_i32 %0, %1, -1, 1" : "=v"(r) : "v"(d));
   return r;
+}
+
+// Packed 16-bit halves of a record word (both codes are 15-bit): one v_pk_sub_u16 gives
+// (qx - tx, qy - ty) with the sign bits at 15 and 31, one v_pk_lshrrev_b16 moves them to 0 and 16.
+typedef unsigned short dcor_u16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t pk_sub16(uint32_t a, uint32_t b) {
+  return __builtin_bit_cast(uint32_t, __builtin_bit_cast(dcor_u16x2, a) - __builtin_bit_cast(dcor_u16x2, b));
+}
+__device__ __forceinline__ uint32_t pk_sign_bits(uint32_t a) {
+  const dcor_u16x2 v = __builtin_bit_cast(dcor_u16x2, a);
+  return __builtin_bit_cast(uint32_t, (dcor_u16x2)(v >> (dcor_u16x2){15, 15}));
 }
 
 template <int DGP>
@@ -340,7 +351,7 @@ __device__ __forceinline__ void sign_pass1_core(const SignConst& c, uint32_t rep
   const int tid = WAVE ? (int)(threadIdx.x & 63) : (int)threadIdx.x;
   DD sx{0.0, 0.0}, sy{0.0, 0.0};
   auto record = [&](double xc, double yc, uint32_t fl) {
-    const uint32_t qx = code16(xc, c.cinv_xf, c.cnb_xf, 65535.0f);
+    const uint32_t qx = code16(xc, c.cinv_xf, c.cnb_xf, 32767.0f);
     const uint32_t qy = code16(yc, c.cinv_yf, c.cnb_yf, 32767.0f);
     return qx | (qy << 16) | (fl << 31);
   };
@@ -484,9 +495,6 @@ __device__ __forceinline__ void sign_pass1_body(const SignConst& c, uint32_t rep
 #ifndef DCOR_P2_WPE
 #define DCOR_P2_WPE 1
 #endif
-#ifndef DCOR_P2_DEPTH
-#define DCOR_P2_DEPTH 2  // batches of slab loads in flight ahead of the current one (m = 8)
-#endif
 template <int DGP>
 __global__ __launch_bounds__(DCOR_BLOCK, DCOR_P1_WPE) void k_sign_pass1(SignConst c,
                                                            uint32_t* __restrict__ scratch,
@@ -544,7 +552,8 @@ __device__ __forceinline__ void scalar_laplace_wave(uint32_t rep, uint32_t k0, u
 template <int DGP, bool WAVE>
 __device__ __forceinline__ P2Result sign_pass2_core(const SignConst& c, uint32_t rep,
                                                     const uint32_t* __restrict__ slab,
-                                                    const double* __restrict__ sums_in) {
+                                                    const double* __restrict__ sums_in,
+                                                    const double2* lt) {
   constexpr int NT = WAVE ? 64 : DCOR_BLOCK;   // threads sharing the replicate
   const int tid = WAVE ? (int)(threadIdx.x & 63) : (int)threadIdx.x;
   double lap[10];
@@ -570,8 +579,8 @@ __device__ __forceinline__ P2Result sign_pass2_core(const SignConst& c, uint32_t
   // sign(d/sd) == sign(d) needs sd < 2^900 (no underflow of the quotient); else exact path.
   const bool force_exact = !(s.sdNx < 0x1p900 && s.sdNy < 0x1p900 && s.sdIx < 0x1p900 &&
                              s.sdIy < 0x1p900);
-  const uint32_t qNx = code16(s.muNx, c.cinv_xf, c.cnb_xf, 65535.0f);
-  const uint32_t qIx = code16(s.muIx, c.cinv_xf, c.cnb_xf, 65535.0f);
+  const uint32_t qNx = code16(s.muNx, c.cinv_xf, c.cnb_xf, 32767.0f);
+  const uint32_t qIx = code16(s.muIx, c.cinv_xf, c.cnb_xf, 32767.0f);
   const uint32_t qNy = code16(s.muNy, c.cinv_yf, c.cnb_yf, 32767.0f);
   const uint32_t qIy = code16(s.muIy, c.cinv_yf, c.cnb_yf, 32767.0f);
   bool bad_ni = thr_nan, bad_int = thr_nan;
@@ -613,47 +622,94 @@ __device__ __forceinline__ P2Result sign_pass2_core(const SignConst& c, uint32_t
       mx = c.md_pow2 ? (double)cx * c.inv_md : (double)cx / c.md;
       my = c.md_pow2 ? (double)cy * c.inv_md : (double)cy / c.md;
     }
-    const double xt = mx + c.bx * unit_laplace(u53(w.w0, w.w1));
-    const double yt = my + c.by * unit_laplace(u53(w.w2, w.w3));
+    const double xt = mx + c.bx * unit_laplace_t(u53(w.w0, w.w1), lt);
+    const double yt = my + c.by * unit_laplace_t(u53(w.w2, w.w3), lt);
     const double T = (M8 ? 8.0 : c.md) * xt * yt;                        // vert-cor.R:233
     ks_acc(sT, T);  // compensated (error ~ k 2^-106): the T mean / sd inputs
     ks_acc(sT2, T * T);
   };
+  // the same, kept only when `valid` (a batch computed past the last one is dropped exactly)
+  auto batch_T_if = [&](int64_t j, int cx, int cy, bool valid) {
+    const double h1 = sT.hi, l1 = sT.lo, h2 = sT2.hi, l2 = sT2.lo;  // scalars: no aggregate select
+    batch_T(j, cx, cy, std::true_type());
+    sT.hi = valid ? sT.hi : h1;
+    sT.lo = valid ? sT.lo : l1;
+    sT2.hi = valid ? sT2.hi : h2;
+    sT2.lo = valid ? sT2.lo : l2;
+  };
   if (c.m == 8) {
-    // headline geometry: one thread = one batch = two 16-B loads; the loads of the thread's next
-    // DCOR_P2_DEPTH batches are in flight while the current batch is decided.
-    int64_t j = tid;
-    uint4 a0[DCOR_P2_DEPTH], a1[DCOR_P2_DEPTH];
+    // headline geometry: one thread = one batch = two 16-B loads.
+    // Signs by packed 16-bit subtraction of the threshold pairs T = (tx, ty): the sign bit of each
+    // half of rec - T is (q < t), of rec - (T + 1) is (q <= t); the two differ exactly on a tie.
+    // A tie is counted as +1 here and corrected by the fix-up.  NI subtracts from the record with
+    // the flip bit masked.  INT subtracts from the raw record: the flip S sits in the y half's sign
+    // position, so that half's sign bit comes out as (qy < ty) ^ S and bit 31 of dI ^ (dI << 16) is
+    // the sample's INT bit sbx ^ sby ^ S -- contribution (2S - 1) sx sy = +1 exactly when it is set.
+    const uint32_t TN = qNx | (qNy << 16), TI = qIx | (qIy << 16);
+    const uint32_t TN1 = TN + 0x00010001u, TI1 = TI + 0x00010001u;
+    auto fix_fast = [&](int64_t i, uint32_t w, int& cx, int& cy, int& cc) {
+      const uint32_t qx = w & 0x7fffu, qy = (w >> 16) & 0x7fffu;
+      if (!(force_exact || qx == qNx || qy == qNy || qx == qIx || qy == qIy)) return;
+      const int f = (w >> 31) ? 1 : -1;
+      const int fNx = qx < qNx ? -1 : 1, fNy = qy < qNy ? -1 : 1;
+      const int fIx = qx < qIx ? -1 : 1, fIy = qy < qIy ? -1 : 1;
+      int nx, ny, ix, iy;
+      exact_signs<DGP>(c, s, (uint32_t)i, rep, nx, ny, ix, iy, bad_ni, bad_int);
+      cx += nx - fNx;
+      cy += ny - fNy;
+      cc += f * (ix * iy - fIx * fIy);
+    };
+    // the count triple (cx, cy, cc) of batch j from its two 16-B record loads
+    auto decide = [&](int64_t j, const uint4& lo, const uint4& hi, int& cx, int& cy, int& cc) {
+      const U4 w0{lo.x, lo.y, lo.z, lo.w}, w1{hi.x, hi.y, hi.z, hi.w};
+      uint32_t neg = 0, tie = 0, par = 0;
 #pragma unroll
-    for (int d = 0; d < DCOR_P2_DEPTH; ++d) {
-      const int64_t jd = j + (int64_t)d * NT;
-      a0[d] = a1[d] = make_uint4(0, 0, 0, 0);
-      if (jd < c.k) {
-        a0[d] = *reinterpret_cast<const uint4*>(slab + 8 * jd);
-        a1[d] = *reinterpret_cast<const uint4*>(slab + 8 * jd + 4);
+      for (int q = 0; q < 8; ++q) {
+        const uint32_t w = word(q < 4 ? w0 : w1, q & 3);
+        const uint32_t r = w & 0x7fff7fffu;
+        const uint32_t dN = pk_sub16(r, TN), dN1 = pk_sub16(r, TN1);
+        const uint32_t dI = pk_sub16(w, TI), dI1 = pk_sub16(w, TI1);
+        tie |= (dN ^ dN1) | (dI ^ dI1);
+        neg += pk_sign_bits(dN);                                     // halves count to <= 8
+        par = __builtin_amdgcn_alignbit(par, dI ^ (dI << 16), 31u);  // (par << 1) | INT bit
       }
-    }
-    for (; j < c.k; j += NT) {
-      const int64_t jn = j + (int64_t)DCOR_P2_DEPTH * NT;
-      const U4 w0{a0[0].x, a0[0].y, a0[0].z, a0[0].w}, w1{a1[0].x, a1[0].y, a1[0].z, a1[0].w};
-#pragma unroll
-      for (int d = 0; d + 1 < DCOR_P2_DEPTH; ++d) { a0[d] = a0[d + 1]; a1[d] = a1[d + 1]; }
-      if (jn < c.k) {
-        a0[DCOR_P2_DEPTH - 1] = *reinterpret_cast<const uint4*>(slab + 8 * jn);
-        a1[DCOR_P2_DEPTH - 1] = *reinterpret_cast<const uint4*>(slab + 8 * jn + 4);
-      }
-      int cx = 0, cy = 0, cc = 0;
-      uint32_t tie = 0;
-#pragma unroll
-      for (int q = 0; q < 8; ++q) tie |= (fast(word(q < 4 ? w0 : w1, q & 3), cx, cy, cc) ? 1u : 0u) << q;
-      if (force_exact) tie = 0xFFu;
-      if (tie) {
+      cx = 8 - 2 * (int)(neg & 0xffffu);
+      cy = 8 - 2 * (int)(neg >> 16);
+      cc = 2 * __popc(par) - 8;
+      if ((tie & 0x80008000u) || force_exact) {
 #pragma unroll 1
         for (int q = 0; q < 8; ++q)  // re-read the record (L2-hot): no dynamically indexed registers
-          if ((tie >> q) & 1u) fixup(8 * j + q, slab[8 * j + q], cx, cy, cc, bad_ni);
+          fix_fast(8 * j + q, slab[8 * j + q], cx, cy, cc);
       }
-      core += cc;
-      batch_T(j, cx, cy, std::true_type());
+    };
+    // Two batches' records in flight per thread in two register sets, used in place (a move of a
+    // register with a load pending waits for the load): batch j is decided while j + NT loads, j +
+    // 2 NT is issued into j's registers, then j + NT is decided.  Batch j + NT is computed even past
+    // the last batch (on the last batch's records) and dropped, so the body has no branch the
+    // compiler could merge the two copies across.  Loads past the end re-read the last batch.
+    auto load = [&](int64_t jj, uint4& lo, uint4& hi) {
+      const int64_t jc = jj < c.k ? jj : c.k - 1;
+      lo = *reinterpret_cast<const uint4*>(slab + 8 * jc);
+      hi = *reinterpret_cast<const uint4*>(slab + 8 * jc + 4);
+    };
+    if (c.k > 0) {
+      uint4 a0, a1, b0, b1;
+      load(tid, a0, a1);
+      load(tid + NT, b0, b1);
+      for (int64_t j = tid; j < c.k; j += 2 * NT) {
+        const bool vb = j + NT < c.k;
+        const int64_t jb = vb ? j + NT : c.k - 1;
+        int cxa, cya, cca, cxb, cyb, ccb;
+        decide(j, a0, a1, cxa, cya, cca);
+        load(j + 2 * NT, a0, a1);
+        __builtin_amdgcn_sched_barrier(0);  // keep j + NT's decisions after j + 2 NT's loads
+        decide(jb, b0, b1, cxb, cyb, ccb);
+        load(j + 3 * NT, b0, b1);
+        __builtin_amdgcn_sched_barrier(0);
+        core += cca + (vb ? ccb : 0);
+        batch_T(j, cxa, cya, std::true_type());
+        batch_T_if(jb, cxb, cyb, vb);
+      }
     }
   } else {
     for (int64_t j = tid; j < c.k; j += NT) {
@@ -708,7 +764,10 @@ __device__ __forceinline__ void sign_pass2_body(const SignConst& c, uint32_t rep
                                                 const uint32_t* __restrict__ slab,
                                                 const double* __restrict__ sums_in,
                                                 SignPartial* __restrict__ part_out) {
-  const P2Result r = sign_pass2_core<DGP, false>(c, rep, slab, sums_in);
+  __shared__ double2 lt[256];
+  log_tab_to_lds(lt, DCOR_BLOCK);
+  __syncthreads();
+  const P2Result r = sign_pass2_core<DGP, false>(c, rep, slab, sums_in, lt);
   if (threadIdx.x == 0) {
     SignPartial p;
     p.sT[0] = r.sT.hi; p.sT[1] = r.sT.lo; p.sT2[0] = r.sT2.hi; p.sT2[1] = r.sT2.lo;
@@ -806,8 +865,9 @@ __global__ __launch_bounds__(DCOR_BLOCK) void k_sign_pass1_w(SignConst c, int64_
 // Pass 2 alone, one wave per replicate, writing the SignPartial the wave epilogue reads.
 template <int DGP>
 __device__ __forceinline__ void sign_pass2_wave_part(const SignConst& c, uint32_t rep, const uint32_t* slab,
-                                                     const double* sums_in, SignPartial* part_out) {
-  const P2Result r = sign_pass2_core<DGP, true>(c, rep, slab, sums_in);
+                                                     const double* sums_in, SignPartial* part_out,
+                                                     const double2* lt) {
+  const P2Result r = sign_pass2_core<DGP, true>(c, rep, slab, sums_in, lt);
   if ((threadIdx.x & 63) == 0) {
     SignPartial p;
     p.sT[0] = r.sT.hi; p.sT[1] = r.sT.lo; p.sT2[0] = r.sT2.hi; p.sT2[1] = r.sT2.lo;
@@ -822,10 +882,13 @@ __global__ __launch_bounds__(DCOR_BLOCK) void k_sign_pass2_w(SignConst c, int64_
                                                              const uint32_t* __restrict__ scratch,
                                                              const double* __restrict__ sums,
                                                              SignPartial* __restrict__ part) {
+  __shared__ double2 lt[256];
+  log_tab_to_lds(lt, DCOR_BLOCK);
+  __syncthreads();
   const int64_t r = (int64_t)blockIdx.x * DCOR_WAVES + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   if (r >= nreps) return;
   sign_pass2_wave_part<DGP>(c, (uint32_t)(c.rep_begin + r), scratch + (size_t)r * (size_t)c.n,
-                            sums + SIGN_SUMS * (size_t)r, part + r);
+                            sums + SIGN_SUMS * (size_t)r, part + r, lt);
 }
 
 template <int DGP, int VPL>
@@ -834,12 +897,15 @@ __global__ __launch_bounds__(DCOR_BLOCK, DCOR_P2E_WPE) void k_sign_p2e_w(SignCon
                                                            const double* __restrict__ sums,
                                                            dcor_rep_out* out) {
   __shared__ WaveMix<VPL> wsel[DCOR_WAVES];
+  __shared__ double2 lt[256];
+  log_tab_to_lds(lt, DCOR_BLOCK);
+  __syncthreads();
   const int wv = threadIdx.x >> 6;
   const int64_t r = (int64_t)blockIdx.x * DCOR_WAVES + __builtin_amdgcn_readfirstlane(wv);
   if (r >= nreps) return;  // whole waves only
   const uint32_t rep = (uint32_t)(c.rep_begin + r);
   const P2Result p = sign_pass2_core<DGP, true>(c, rep, scratch + (size_t)r * (size_t)c.n,
-                                                sums + SIGN_SUMS * (size_t)r);
+                                                sums + SIGN_SUMS * (size_t)r, lt);
   sign_finish_wave<VPL>(c, rep, p, out + r, &wsel[wv]);
 }
 
@@ -1420,10 +1486,14 @@ __global__ __launch_bounds__(DCOR_BLOCK) void k_grid_sign_pass2_w(const SignCons
                                                                   const uint32_t* __restrict__ scratch,
                                                                   const double* __restrict__ sums,
                                                                   SignPartial* __restrict__ part) {
+  __shared__ double2 lt[256];
+  log_tab_to_lds(lt, DCOR_BLOCK);
+  __syncthreads();
   const int64_t r = wave_item();
   if (r >= nitems) return;
   const GridItem it = items[r];
-  sign_pass2_wave_part<DGP>(cells[it.cell], it.rep, scratch + it.scratch, sums + SIGN_SUMS * (size_t)r, part + r);
+  sign_pass2_wave_part<DGP>(cells[it.cell], it.rep, scratch + it.scratch, sums + SIGN_SUMS * (size_t)r, part + r,
+                            lt);
 }
 
 template <int DGP, int VPL>
@@ -1434,11 +1504,14 @@ __global__ __launch_bounds__(DCOR_BLOCK, DCOR_P2E_WPE) void k_grid_sign_p2e_w(co
                                                                 const double* __restrict__ sums,
                                                                 dcor_rep_out* out) {
   __shared__ WaveMix<VPL> wsel[DCOR_WAVES];
+  __shared__ double2 lt[256];
+  log_tab_to_lds(lt, DCOR_BLOCK);
+  __syncthreads();
   const int64_t r = wave_item();
   if (r >= nitems) return;  // whole waves only
   const GridItem it = items[r];
   const SignConst& c = cells[it.cell];
-  const P2Result p = sign_pass2_core<DGP, true>(c, it.rep, scratch + it.scratch, sums + SIGN_SUMS * (size_t)r);
+  const P2Result p = sign_pass2_core<DGP, true>(c, it.rep, scratch + it.scratch, sums + SIGN_SUMS * (size_t)r, lt);
   sign_finish_wave<VPL>(c, it.rep, p, out + it.out, &wsel[threadIdx.x >> 6]);
 }
 
