@@ -482,6 +482,7 @@ __global__ __launch_bounds__(DICT_THREADS) void k_panel_dict(const double* __res
 #define DICT_NW (DICT_NT / 64)
 typedef double dv2 __attribute__((ext_vector_type(2)));
 typedef int iv4 __attribute__((ext_vector_type(4)));
+typedef int iv2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ int64_t share(int64_t total, int t, int S) { return total * t / S; }
 
@@ -568,27 +569,34 @@ __global__ __launch_bounds__(DICT_NT, WPE) void k_premat_subg_dict(PrematSubgCon
       ks_acc(sU, U0 + U1);
       ks_acc(sU2, U0 * U0 + U1 * U1);
     };
-    // INT stream: sample pairs (h + 2q, h + 2q + 1); h = 1 when the replicate's noise row
-    // starts off a 16-B boundary (odd n).  Slice 0 takes the head sample, slice S-1 the tail.
+    // INT stream: sample pairs (2q, 2q + 1) whatever the row's alignment, so a replicate's sums
+    // never depend on where its row sits in the launch (odd n: every other row starts 8 B off a
+    // 16-B boundary and reads its pairs as two 8-B loads).  Slice S-1 takes the odd tail sample.
     {
-      const int64_t h = (reinterpret_cast<uintptr_t>(ll) & 15) ? 1 : 0;
-      const int64_t np = (c.n - h) >> 1;
+      const bool al16 = (reinterpret_cast<uintptr_t>(ll) & 15) == 0;
+      const int64_t np = c.n >> 1;
       const int64_t q0 = share(np, t, S), q1 = share(np, t + 1, S);
-      const dv2* l2 = reinterpret_cast<const dv2*>(ll + h);
+      const dv2* l2 = reinterpret_cast<const dv2*>(ll);
+      auto ldp = [&](int64_t qq) -> dv2 {
+        if (al16) return __builtin_nontemporal_load(l2 + qq);
+        dv2 v;
+        v.x = __builtin_nontemporal_load(ll + 2 * qq);
+        v.y = __builtin_nontemporal_load(ll + 2 * qq + 1);
+        return v;
+      };
       int64_t q = q0 + tid;
       for (; q + (DUNR - 1) * DICT_NT < q1; q += DUNR * DICT_NT) {
         dv2 v[DUNR];
 #pragma unroll
-        for (int u = 0; u < DUNR; ++u) v[u] = __builtin_nontemporal_load(l2 + q + u * DICT_NT);
+        for (int u = 0; u < DUNR; ++u) v[u] = ldp(q + u * DICT_NT);
 #pragma unroll
-        for (int u = 0; u < DUNR; ++u) uterm2(h + 2 * (q + u * DICT_NT), v[u].x, v[u].y);
+        for (int u = 0; u < DUNR; ++u) uterm2(2 * (q + u * DICT_NT), v[u].x, v[u].y);
       }
       for (; q < q1; q += DICT_NT) {
-        const dv2 v = __builtin_nontemporal_load(l2 + q);
-        uterm2(h + 2 * q, v.x, v.y);
+        const dv2 v = ldp(q);
+        uterm2(2 * q, v.x, v.y);
       }
-      if (tid == 0 && t == 0 && h) uterm(0, ll[0]);
-      if (tid == DICT_NT - 1 && t == S - 1 && h + 2 * np < c.n) uterm(c.n - 1, ll[c.n - 1]);
+      if (tid == DICT_NT - 1 && t == S - 1 && (c.n & 1)) uterm(c.n - 1, ll[c.n - 1]);
     }
     // workgroup sums: wave sums into a scratch half alternating per item (a wave can run at
     // most one barrier ahead), then lane v < 5 folds sum v over the waves in wave order.  The
@@ -623,38 +631,47 @@ __global__ __launch_bounds__(DICT_NT, WPE) void k_premat_subg_dict(PrematSubgCon
         ks_acc(sT, T0 + T1);
         ks_acc(sT2, T0 * T0 + T1 * T1);
       };
+      // two batches (2q, 2q + 1) per lane whatever the rows' alignment (odd k: every other row
+      // is 8 B off a 16-B boundary and reads int2 / double pairs instead of int4 / double2)
       const bool al = ((reinterpret_cast<uintptr_t>(pm) | reinterpret_cast<uintptr_t>(lx) |
                         reinterpret_cast<uintptr_t>(ly)) & 15) == 0;
-      if (al) {  // two batches per lane: int4 of indices, double2 of each noise row
-        const int64_t np = c.k >> 1;
-        const int64_t q0 = share(np, t, S), q1 = share(np, t + 1, S);
-        const iv4* p4 = reinterpret_cast<const iv4*>(pm);
-        const dv2* x2 = reinterpret_cast<const dv2*>(lx);
-        const dv2* y2 = reinterpret_cast<const dv2*>(ly);
-        int64_t q = q0 + tid;
-        for (; q + (DUNR / 2 - 1) * DICT_NT < q1; q += (DUNR / 2) * DICT_NT) {
-          iv4 pr[DUNR / 2];
-          dv2 ax[DUNR / 2], ay[DUNR / 2];
-#pragma unroll
-          for (int u = 0; u < DUNR / 2; ++u) {
-            pr[u] = __builtin_nontemporal_load(p4 + q + u * DICT_NT);
-            ax[u] = __builtin_nontemporal_load(x2 + q + u * DICT_NT);
-            ay[u] = __builtin_nontemporal_load(y2 + q + u * DICT_NT);
-          }
-#pragma unroll
-          for (int u = 0; u < DUNR / 2; ++u) pair2(pr[u], ax[u], ay[u]);
+      const int64_t np = c.k >> 1;
+      const int64_t q0 = share(np, t, S), q1 = share(np, t + 1, S);
+      const iv4* p4 = reinterpret_cast<const iv4*>(pm);
+      const dv2* x2 = reinterpret_cast<const dv2*>(lx);
+      const dv2* y2 = reinterpret_cast<const dv2*>(ly);
+      auto ldb = [&](int64_t qq, iv4& pr, dv2& ax, dv2& ay) {
+        if (al) {
+          pr = __builtin_nontemporal_load(p4 + qq);
+          ax = __builtin_nontemporal_load(x2 + qq);
+          ay = __builtin_nontemporal_load(y2 + qq);
+        } else {
+          const iv2* p2 = reinterpret_cast<const iv2*>(pm);  // rows of 2k int32: 8-B aligned
+          const iv2 a = __builtin_nontemporal_load(p2 + 2 * qq), b = __builtin_nontemporal_load(p2 + 2 * qq + 1);
+          pr.x = a.x; pr.y = a.y; pr.z = b.x; pr.w = b.y;
+          ax.x = __builtin_nontemporal_load(lx + 2 * qq);
+          ax.y = __builtin_nontemporal_load(lx + 2 * qq + 1);
+          ay.x = __builtin_nontemporal_load(ly + 2 * qq);
+          ay.y = __builtin_nontemporal_load(ly + 2 * qq + 1);
         }
-        for (; q < q1; q += DICT_NT) {
-          const iv4 pr = __builtin_nontemporal_load(p4 + q);
-          const dv2 ax = __builtin_nontemporal_load(x2 + q), ay = __builtin_nontemporal_load(y2 + q);
-          pair2(pr, ax, ay);
-        }
-        if (tid == DICT_NT - 1 && t == S - 1 && (c.k & 1))
-          pair(pm[2 * (c.k - 1)], pm[2 * (c.k - 1) + 1], lx[c.k - 1], ly[c.k - 1]);
-      } else {
-        for (int64_t j = share(c.k, t, S) + tid; j < share(c.k, t + 1, S); j += DICT_NT)
-          pair(pm[2 * j], pm[2 * j + 1], lx[j], ly[j]);
+      };
+      int64_t q = q0 + tid;
+      for (; q + (DUNR / 2 - 1) * DICT_NT < q1; q += (DUNR / 2) * DICT_NT) {
+        iv4 pr[DUNR / 2];
+        dv2 ax[DUNR / 2], ay[DUNR / 2];
+#pragma unroll
+        for (int u = 0; u < DUNR / 2; ++u) ldb(q + u * DICT_NT, pr[u], ax[u], ay[u]);
+#pragma unroll
+        for (int u = 0; u < DUNR / 2; ++u) pair2(pr[u], ax[u], ay[u]);
       }
+      for (; q < q1; q += DICT_NT) {
+        iv4 pr;
+        dv2 ax, ay;
+        ldb(q, pr, ax, ay);
+        pair2(pr, ax, ay);
+      }
+      if (tid == DICT_NT - 1 && t == S - 1 && (c.k & 1))
+        pair(pm[2 * (c.k - 1)], pm[2 * (c.k - 1) + 1], lx[c.k - 1], ly[c.k - 1]);
     } else {
       for (int64_t j = share(c.k, t, S) + tid; j < share(c.k, t + 1, S); j += DICT_NT) {
         DD bx{0, 0}, by{0, 0};
@@ -748,11 +765,19 @@ __global__ __launch_bounds__(NT, WPE) void k_premat_subg_tiled(PrematSubgConst p
       ks_acc(sU[0], U0 + U1);
       ks_acc(sU2[0], U0 * U0 + U1 * U1);
     };
-    // INT sample pairs (h + 2q, h + 2q + 1), as in the L2 kernel; the head sample (h = 1) joins
-    // tile 0, the odd tail sample the last tile.
-    const uint32_t h = (reinterpret_cast<uintptr_t>(ll) & 15) ? 1u : 0u;
-    const uint32_t np = (n - h) >> 1;
-    const dv2* __restrict__ l2 = reinterpret_cast<const dv2*>(ll + h);
+    // INT sample pairs (2q, 2q + 1) whatever the row's alignment, as in the L2 kernel (a row 8 B off
+    // a 16-B boundary reads its pairs as two 8-B loads); the odd tail sample joins the last tile.
+    const bool al16 = (reinterpret_cast<uintptr_t>(ll) & 15) == 0;
+    const uint32_t h = 0u;
+    const uint32_t np = n >> 1;
+    const dv2* __restrict__ l2 = reinterpret_cast<const dv2*>(ll);
+    auto ldp = [&](uint32_t qq) -> dv2 {
+      if (al16) return __builtin_nontemporal_load(l2 + qq);
+      dv2 v;
+      v.x = __builtin_nontemporal_load(ll + 2 * qq);
+      v.y = __builtin_nontemporal_load(ll + 2 * qq + 1);
+      return v;
+    };
     const uint32_t ntiles = np > 0 ? (np + tile_pairs - 1) / tile_pairs : 1u;
     double* rb = red + (((it - blockIdx.x) / gridDim.x) & 1) * (10 * NW);
     auto wave_put = [&](int v, DD a) {
@@ -796,7 +821,7 @@ __global__ __launch_bounds__(NT, WPE) void k_premat_subg_tiled(PrematSubgConst p
             a0[u] = xy[i]; a1[u] = xy[i + 1];
             if (first) {
               s0[u] = so[i]; s1[u] = so[i + 1];
-              lv[u] = __builtin_nontemporal_load(l2 + (q + u * NT));
+              lv[u] = ldp(q + u * NT);
             }
           }
 #pragma unroll
@@ -819,7 +844,7 @@ __global__ __launch_bounds__(NT, WPE) void k_premat_subg_tiled(PrematSubgConst p
           tile[i - lo] = xy[i];
           tile[i + 1 - lo] = xy[i + 1];
           if (first) {
-            const dv2 l = __builtin_nontemporal_load(l2 + q);
+            const dv2 l = ldp(q);
             if (PG) {
               uterm2(so[i], l.x, so[i + 1], l.y);
             } else {
@@ -828,7 +853,6 @@ __global__ __launch_bounds__(NT, WPE) void k_premat_subg_tiled(PrematSubgConst p
             }
           }
         }
-        if (tp == 0 && h && tid == 0) tile[0] = xy[0];
         if (tp == ntiles - 1 && h + 2 * np < n && tid == NT - 1) tile[n - 1 - lo] = xy[n - 1];
         if (tid == 0) tile[tn] = make_double2(-0.0, -0.0);  // the out-of-tile sentinel
         __syncthreads();
@@ -848,7 +872,6 @@ __global__ __launch_bounds__(NT, WPE) void k_premat_subg_tiled(PrematSubgConst p
         }
       }
       if (first) {
-        if (tid == 0 && h) uterm(so[0], ll[0], 0);
         if (tid == NT - 1 && h + 2 * np < n) uterm(so[n - 1], ll[n - 1], 1);
         wave_put(3, merged(sU));
         wave_put(4, merged(sU2));
