@@ -103,6 +103,24 @@ def test_hrs_replicates_split_invariant(panel):
     np.testing.assert_array_equal(whole.view(np.int64), parts.view(np.int64))
 
 
+@pytest.mark.parametrize("kind,n", [("coded", 3003), ("continuous", 3003), ("continuous", 3001)])
+def test_premat_replicate_independent_of_row_position(kind, n):
+    """Odd n (odd k): every other noise row of a launch starts 8 B off a 16-B boundary.  INT sample
+    pairs and NI batch pairs are formed by index whatever the row's alignment, so a replicate run as
+    row 0 of its own launch equals the same replicate run as row 1..5 of a six-row launch, bit for
+    bit -- on the coded kernel (k odd), the L2-gather kernel (k odd) and the tiled kernel (k even)."""
+    from dcor import hrs
+    if kind == "coded":
+        age, bmi = hrs.standin_panel(n, -0.3, seed=7)
+        z = hrs.standardize_panel(age, bmi, lap=np.array([0.1, 0.2, -0.3, 0.05]))
+    else:
+        z = _continuous(n, seed=n)
+    args = (z["age_z"], z["bmi_z"], z["lambda_age_z"], z["lambda_bmi_z"], 2.0)
+    whole = hrs.hrs_replicates(*args, 6, rep_begin=1, chunk=6)
+    ones = np.concatenate([hrs.hrs_replicates(*args, 1, rep_begin=1 + r, chunk=1) for r in range(6)])
+    np.testing.assert_array_equal(whole.view(np.int64), ones.view(np.int64))
+
+
 def test_eps_sweep_summaries(panel):
     from dcor import hrs
     z = panel
