@@ -330,9 +330,11 @@ thread_local ThreadCtx t_ctx;
 void ctx_free(Ctx* c) {
   if (c->pipe.s) {
     (void)hipStreamSynchronize(c->pipe.s);
+    (void)hipStreamSynchronize(c->pipe.s2);
     (void)hipStreamDestroy(c->pipe.s);
-    (void)hipEventDestroy(c->pipe.fork);
-    (void)hipEventDestroy(c->pipe.join);
+    (void)hipStreamDestroy(c->pipe.s2);
+    for (hipEvent_t e : {c->pipe.fork, c->pipe.join, c->pipe.entry, c->pipe.end[0], c->pipe.end[1]})
+      (void)hipEventDestroy(e);
   }
   for (Pinned* b : {&c->stage[0], &c->stage[1], &c->hrec, &c->hacc}) {
     if (b->done) { (void)hipEventSynchronize(b->done); (void)hipEventDestroy(b->done); }
@@ -380,8 +382,9 @@ int pipe_get(Pipe** out) {
   Pipe& p = c->pipe;
   if (!p.s) {
     HIPCHK(hipStreamCreateWithFlags(&p.s, hipStreamNonBlocking));
-    HIPCHK(hipEventCreateWithFlags(&p.fork, hipEventDisableTiming));
-    HIPCHK(hipEventCreateWithFlags(&p.join, hipEventDisableTiming));
+    HIPCHK(hipStreamCreateWithFlags(&p.s2, hipStreamNonBlocking));
+    for (hipEvent_t* e : {&p.fork, &p.join, &p.entry, &p.end[0], &p.end[1]})
+      HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
   }
   *out = &p;
   return DCOR_OK;
@@ -666,6 +669,9 @@ int dcor_sim_launch(const dcor_cell* cell, int64_t rep_begin, int64_t rep_count,
       const size_t plane_bytes = ((size_t)chunk * (per_rep - 64) + 255) / 256 * 256;
       void* scratch = nullptr;
       if (int st = arena_get(plane_bytes + (size_t)chunk * 64, &scratch)) return st;
+      Ctx* cx = nullptr;
+      if (int st = ctx_get(&cx)) return st;
+      cx->pipe.sig = 0;  // the codes arena's last user is now the caller's stream
       rc = launch_sign_bern(k, rep_count, chunk, (uint64_t*)scratch,
                             (SignPartial*)((char*)scratch + plane_bytes), d_out, stream);
     } else if ((cp.kind != GK_SIGN_CODES && cp.kind != GK_SIGN_CODES_W) || rep_count == 0) {
@@ -694,12 +700,24 @@ int dcor_sim_launch(const dcor_cell* cell, int64_t rep_begin, int64_t rep_count,
         bf.slab[b] = (uint32_t*)(base + bb * slab_b);
         bf.sums[b] = (double*)(base + nbuf * slab_b + bb * sums_b);
       }
-      bf.aux = bf.ev_fork = bf.ev_join = nullptr;
+      bf.lib[0] = bf.lib[1] = bf.ev_entry = bf.ev_end[0] = bf.ev_end[1] = nullptr;
+      bf.cross = false;
       const char* pv = std::getenv("DCOR_SIGN_PIPELINE");
+      Pipe* pp = nullptr;
+      if (int st = pipe_get(&pp)) return st;
       if (nbuf == 2 && !(pv && std::strcmp(pv, "0") == 0)) {
-        Pipe* pp = nullptr;
-        if (int st = pipe_get(&pp)) return st;
-        bf.aux = pp->s; bf.ev_fork = pp->fork; bf.ev_join = pp->join;
+        bf.lib[0] = pp->s2; bf.lib[1] = pp->s;
+        bf.ev_entry = pp->entry; bf.ev_end[0] = pp->end[0]; bf.ev_end[1] = pp->end[1];
+        // calls of the same layout back to back: the next call's first chunks may start while
+        // the previous call's last chunk finishes (DCOR_SIGN_XCALL=0 orders every call after the
+        // caller's stream)
+        const uint64_t sig = ((uint64_t)(uintptr_t)scratch * 1000003u) ^ ((uint64_t)slab_b * 31u) ^
+                             ((uint64_t)sums_b << 1) ^ 1u;
+        const char* xv = std::getenv("DCOR_SIGN_XCALL");
+        bf.cross = sig == pp->sig && !(xv && std::strcmp(xv, "0") == 0);
+        pp->sig = sig;
+      } else {
+        pp->sig = 0;
       }
       rc = launch_sign_fused_codes(k, rep_count, chunk, bf, d_out, stream);
     }

@@ -125,12 +125,17 @@ int launch_sign_bern(SignConst c, int64_t reps, int64_t chunk, uint64_t* scratch
 // One-pass sign engine buffers: two slabs (chunk * n * 4 B) and two sums/partials areas
 // (chunk * 80 B), an auxiliary stream and two events (fork / join) for the two-stream
 // chunk pipeline; aux == nullptr runs every chunk on the caller's stream.
+// lib[0], lib[1]: the library streams the chunks alternate on (null: everything on the caller's
+// stream).  cross: the previous call ran on the same streams and scratch layout, so passes 1 and 2
+// start without waiting for the caller's stream (they touch library memory only); every kernel that
+// writes `out` waits for ev_entry, the caller's stream at this call.
 struct CodesBufs {
   uint32_t* slab[2];
   double* sums[2];
-  void* aux;
-  void* ev_fork;
-  void* ev_join;
+  void* lib[2];
+  void* ev_entry;
+  void* ev_end[2];
+  bool cross;
 };
 int launch_sign_fused_codes(const SignConst& c, int64_t reps, int64_t chunk, const CodesBufs& bf,
                             dcor_rep_out* out, void* stream);

@@ -1756,12 +1756,23 @@ template <int DGP>
 static int launch_codes_t(SignConst c, int64_t reps, int64_t chunk, const CodesBufs& bf,
                           dcor_rep_out* out, void* stream) {
   const int64_t rep0 = c.rep_begin;
-  hipStream_t st[2] = {(hipStream_t)stream, (hipStream_t)bf.aux};
-  const bool two = reps > chunk && bf.aux != nullptr;
+  const bool two = reps > chunk && bf.lib[0] != nullptr;
+  hipStream_t st[2] = {(hipStream_t)stream, (hipStream_t)stream};
+  bool waited[2] = {true, true};  // this stream's `out` writers are ordered after the caller's work
   if (two) {
-    if (hipEventRecord((hipEvent_t)bf.ev_fork, st[0]) != hipSuccess) return last_err();
-    if (hipStreamWaitEvent(st[1], (hipEvent_t)bf.ev_fork, 0) != hipSuccess) return last_err();
+    st[0] = (hipStream_t)bf.lib[0];
+    st[1] = (hipStream_t)bf.lib[1];
+    if (hipEventRecord((hipEvent_t)bf.ev_entry, (hipStream_t)stream) != hipSuccess) return last_err();
+    for (int b = 0; b < 2; ++b) {
+      waited[b] = !bf.cross;
+      if (!bf.cross && hipStreamWaitEvent(st[b], (hipEvent_t)bf.ev_entry, 0) != hipSuccess) return last_err();
+    }
   }
+  auto before_out = [&](int b) -> int {  // the first kernel writing `out` on stream b
+    if (waited[b]) return 0;
+    waited[b] = true;
+    return hipStreamWaitEvent(st[b], (hipEvent_t)bf.ev_entry, 0) != hipSuccess ? last_err() : 0;
+  };
   int64_t t = 0;
   for (int64_t r = 0; r < reps; r += chunk, ++t) {
     const int64_t nr = (reps - r < chunk) ? reps - r : chunk;
@@ -1770,6 +1781,7 @@ static int launch_codes_t(SignConst c, int64_t reps, int64_t chunk, const CodesB
     if (c.n <= SIGN_W_NMAX) {   // small cells: the wave-per-replicate kernels (as the grid runs them)
       hipLaunchKernelGGL(k_sign_pass1_w<DGP>, dim3(persistent_groups(nr)), dim3(DCOR_BLOCK), 0, st[b], c, nr,
                          bf.slab[b], bf.sums[b]);
+      if (int e = before_out(b)) return e;
       if (!p2e_fused()) {
         SignPartial* part = reinterpret_cast<SignPartial*>(bf.sums[b] + SIGN_SUMS * chunk);
         hipLaunchKernelGGL(k_sign_pass2_w<DGP>, dim3(wave_groups(nr)), dim3(DCOR_BLOCK), 0, st[b], c, nr,
@@ -1789,12 +1801,15 @@ static int launch_codes_t(SignConst c, int64_t reps, int64_t chunk, const CodesB
                        bf.slab[b], bf.sums[b]);
     hipLaunchKernelGGL(k_sign_pass2<DGP>, dim3((unsigned)nr), dim3(DCOR_BLOCK), 0, st[b], c,
                        bf.slab[b], bf.sums[b], part);
+    if (int e = before_out(b)) return e;
     launch_sign_epilogue(c, nr, part, out + r, st[b]);
     if (int e = last_err()) return e;
   }
-  if (two) {
-    if (hipEventRecord((hipEvent_t)bf.ev_join, st[1]) != hipSuccess) return last_err();
-    if (hipStreamWaitEvent(st[0], (hipEvent_t)bf.ev_join, 0) != hipSuccess) return last_err();
+  if (two) {  // the caller's stream continues after both library streams
+    for (int b = 0; b < 2; ++b) {
+      if (hipEventRecord((hipEvent_t)bf.ev_end[b], st[b]) != hipSuccess) return last_err();
+      if (hipStreamWaitEvent((hipStream_t)stream, (hipEvent_t)bf.ev_end[b], 0) != hipSuccess) return last_err();
+    }
   }
   return 0;
 }

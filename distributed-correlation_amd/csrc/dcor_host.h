@@ -29,7 +29,15 @@ double r_min(double a, double b);
 double r_max(double a, double b);
 
 struct Arena { void* p = nullptr; size_t bytes = 0; };
-struct Pipe { hipStream_t s = nullptr; hipEvent_t fork = nullptr, join = nullptr; };
+// s: the auxiliary stream of the two-stream pipelines (fork / join with the caller's stream).  The
+// one-pass sign path runs its chunks on two library streams (s2, s) instead: entry marks the
+// caller's stream at the call, end[] the two library streams at its end, and sig the scratch layout
+// of the last call that ran there (0: the arena's last user was the caller's stream).
+struct Pipe {
+  hipStream_t s = nullptr, s2 = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr, entry = nullptr, end[2] = {nullptr, nullptr};
+  uint64_t sig = 0;
+};
 // Pinned host memory with the event that marks the end of the last copy that read or wrote it.
 struct Pinned { void* p = nullptr; size_t bytes = 0; hipEvent_t done = nullptr; };
 // The library's state for one (host thread, device): scratch arenas, the auxiliary stream of the

@@ -95,3 +95,37 @@ def test_s_subg_launch_shape(dc, orc):
     got_all = simulate(cell, 4096).cpu().numpy()
     idx = [0, 1, 2047, 2048, 4094, 4095]
     assert_close(got_all[idx], _oracle_at(orc, cell, 0, idx), what="S launch shape")
+
+
+def test_back_to_back_calls_share_library_streams(dc):
+    """Pipelined sign calls run their chunks on two library streams and, when the previous call
+    used the same scratch layout, start before the caller's stream reaches them (their passes 1 and
+    2 touch library memory only; every kernel that writes `out` waits for the caller's stream).  A
+    sequence of calls enqueued back to back -- same layout twice, a Bernoulli call that reuses the
+    scratch arena on the caller's stream, a different n (new layout), the first layout again --
+    must give every call's records bit for bit as the same calls separated by device syncs."""
+    import dataclasses
+    import torch
+    from dcor.sim import headline_cell, simulate
+    base = headline_cell()
+    bern = dataclasses.replace(base, dgp="bernoulli", n=20_000, mu=(0.0, 0.0), sigma=(1.0, 1.0))
+    calls = [(base, 4096, 0), (base, 4096, 4096), (bern, 3000, 0), (headline_cell(60_000), 2048, 7),
+             (base, 4096, 9000)]
+    stream = torch.cuda.current_stream()
+
+    def run(sync):
+        outs = []
+        for cell, R, r0 in calls:
+            buf = torch.full((R, 6), float("nan"), dtype=torch.float64, device="cuda")
+            simulate(cell, R, r0, out=buf, stream=stream)
+            outs.append(buf)
+            if sync:
+                torch.cuda.synchronize()
+        torch.cuda.synchronize()
+        return [o.cpu().numpy() for o in outs]
+
+    ref = run(True)
+    got = run(False)
+    for (cell, R, r0), a, b in zip(calls, ref, got):
+        assert np.all(np.isfinite(b)), (cell.dgp, cell.n, R, r0)
+        np.testing.assert_array_equal(a.view(np.int64), b.view(np.int64))
