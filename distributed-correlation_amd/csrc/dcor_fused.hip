@@ -1341,20 +1341,40 @@ __device__ __forceinline__ void subg_fused_core(const SubgConst& c, uint32_t rep
     lapz = unit_laplace(u53(w.w0, w.w1));
   }
   DD sP{0, 0}, sT{0, 0}, sT2{0, 0}, sU{0, 0}, sU2{0, 0};
-  auto int_term = [&](double x, double y, double l) {
+  auto uc_of = [&](double x, double y, double l) {
     const double S = c.sender_is_X ? x : y, O = c.sender_is_X ? y : x;
-    const double Uc = rclip_fin((rclip_fin(S, c.ls) + c.bs * l) * O, c.lr);  // ver-cor-subG.R:88-90
+    return rclip_fin((rclip_fin(S, c.ls) + c.bs * l) * O, c.lr);          // ver-cor-subG.R:88-90
+  };
+  auto int_term = [&](double x, double y, double l) {
+    const double Uc = uc_of(x, y, l);
     ks_acc(sU, Uc);  // compensated sums (error ~ n 2^-106): the mean / sd of Uc
     ks_acc(sU2, Uc * Uc);
+  };
+  // two samples' INT terms added plainly and the pair sum compensated: half the TwoSum chains of
+  // per-term sums (as the HRS kernels do), sums that differ from per-term ones in the low bits only
+  auto int_term2 = [&](double U0, double U1) {
+    ks_acc(sU, U0 + U1);
+    ks_acc(sU2, U0 * U0 + U1 * U1);
   };
   for (int64_t j = tid; j < c.k; j += NT) {
     double sx = 0.0, sy = 0.0;
     const int64_t i0 = j * c.m;
-    for (int r = 0; r < c.m; ++r) {
+    int r = 0;
+    for (; r + 1 < c.m; r += 2) {
+      double x0, y0, l0, x1, y1, l1;
+      sample_lap<DGP>(c.g, (uint32_t)(i0 + r), rep, c.k0, c.k1, x0, y0, l0);
+      sample_lap<DGP>(c.g, (uint32_t)(i0 + r + 1), rep, c.k0, c.k1, x1, y1, l1);
+      sx += rclip_fin(x0, c.l1);                                         // :33
+      sy += rclip_fin(y0, c.l2);                                         // :34
+      sx += rclip_fin(x1, c.l1);
+      sy += rclip_fin(y1, c.l2);
+      int_term2(uc_of(x0, y0, l0), uc_of(x1, y1, l1));
+    }
+    if (r < c.m) {
       double x, y, l;
       sample_lap<DGP>(c.g, (uint32_t)(i0 + r), rep, c.k0, c.k1, x, y, l);
-      sx += rclip_fin(x, c.l1);                                          // :33
-      sy += rclip_fin(y, c.l2);                                          // :34
+      sx += rclip_fin(x, c.l1);
+      sy += rclip_fin(y, c.l2);
       int_term(x, y, l);
     }
     const U4 w = draw((uint32_t)j, rep, DCOR_SITE_NI_LAP, c.k0, c.k1);

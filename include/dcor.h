@@ -129,7 +129,12 @@ double dcor_qnorm(double p);
  * replicate: Philox DGP -> clip -> reduce -> Laplace -> NI + INT estimate + CI.
  * Replaces run_sim_one's loop body (vert-cor.R:392-419; ver-cor-subG.R:174-198).
  * d_out: rep_count device records.  Per-replicate results depend only on
- * (seed, rep), never on the range split, so any sharding over GPUs is exact. */
+ * (seed, rep), never on the range split, so any sharding over GPUs is exact.
+ * Asynchronous with stream semantics for d_out: every kernel that writes d_out runs after the
+ * work enqueued on `stream` before the call, and work enqueued on `stream` after the call runs
+ * after all of this call's kernels.  Kernels that only touch library scratch (the one-pass sign
+ * path's passes 1 and 2, on two library streams) may start earlier, beside the previous call's
+ * tail. */
 int dcor_sim_launch(const dcor_cell* cell, int64_t rep_begin, int64_t rep_count,
                     dcor_rep_out* d_out, void* stream);
 /* Deterministic per-method accumulation of `count` records into d_acc[0] (NI)
