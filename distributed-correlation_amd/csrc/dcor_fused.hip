@@ -637,6 +637,20 @@ __device__ __forceinline__ P2Result sign_pass2_core(const SignConst& c, uint32_t
     sT2.hi = valid ? sT2.hi : h2;
     sT2.lo = valid ? sT2.lo : l2;
   };
+  const uint32_t TN = qNx | (qNy << 16), TI = qIx | (qIy << 16);
+  const uint32_t TN1 = TN + 0x00010001u, TI1 = TI + 0x00010001u;
+  auto fix_fast = [&](int64_t i, uint32_t w, int& cx, int& cy, int& cc) {
+    const uint32_t qx = w & 0x7fffu, qy = (w >> 16) & 0x7fffu;
+    if (!(force_exact || qx == qNx || qy == qNy || qx == qIx || qy == qIy)) return;
+    const int f = (w >> 31) ? 1 : -1;
+    const int fNx = qx < qNx ? -1 : 1, fNy = qy < qNy ? -1 : 1;
+    const int fIx = qx < qIx ? -1 : 1, fIy = qy < qIy ? -1 : 1;
+    int nx, ny, ix, iy;
+    exact_signs<DGP>(c, s, (uint32_t)i, rep, nx, ny, ix, iy, bad_ni, bad_int);
+    cx += nx - fNx;
+    cy += ny - fNy;
+    cc += f * (ix * iy - fIx * fIy);
+  };
   if (c.m == 8) {
     // headline geometry: one thread = one batch = two 16-B loads.
     // Signs by packed 16-bit subtraction of the threshold pairs T = (tx, ty): the sign bit of each
@@ -645,20 +659,6 @@ __device__ __forceinline__ P2Result sign_pass2_core(const SignConst& c, uint32_t
     // the flip bit masked.  INT subtracts from the raw record: the flip S sits in the y half's sign
     // position, so that half's sign bit comes out as (qy < ty) ^ S and bit 31 of dI ^ (dI << 16) is
     // the sample's INT bit sbx ^ sby ^ S -- contribution (2S - 1) sx sy = +1 exactly when it is set.
-    const uint32_t TN = qNx | (qNy << 16), TI = qIx | (qIy << 16);
-    const uint32_t TN1 = TN + 0x00010001u, TI1 = TI + 0x00010001u;
-    auto fix_fast = [&](int64_t i, uint32_t w, int& cx, int& cy, int& cc) {
-      const uint32_t qx = w & 0x7fffu, qy = (w >> 16) & 0x7fffu;
-      if (!(force_exact || qx == qNx || qy == qNy || qx == qIx || qy == qIy)) return;
-      const int f = (w >> 31) ? 1 : -1;
-      const int fNx = qx < qNx ? -1 : 1, fNy = qy < qNy ? -1 : 1;
-      const int fIx = qx < qIx ? -1 : 1, fIy = qy < qIy ? -1 : 1;
-      int nx, ny, ix, iy;
-      exact_signs<DGP>(c, s, (uint32_t)i, rep, nx, ny, ix, iy, bad_ni, bad_int);
-      cx += nx - fNx;
-      cy += ny - fNy;
-      cc += f * (ix * iy - fIx * fIy);
-    };
     // the count triple (cx, cy, cc) of batch j from its two 16-B record loads
     auto decide = [&](int64_t j, const uint4& lo, const uint4& hi, int& cx, int& cy, int& cc) {
       const U4 w0{lo.x, lo.y, lo.z, lo.w}, w1{hi.x, hi.y, hi.z, hi.w};
@@ -712,7 +712,40 @@ __device__ __forceinline__ P2Result sign_pass2_core(const SignConst& c, uint32_t
       }
     }
   } else {
-    for (int64_t j = tid; j < c.k; j += NT) {
+    // any other m < 32768 (the reference grids' 11, 32, 200): the same packed decisions, four records
+    // per 16-B load when batches start on 16-B boundaries (m % 4 == 0), the counts per batch
+    if (c.m < 32768) {
+      const bool vec = (c.m & 3) == 0;
+      for (int64_t j = tid; j < c.k; j += NT) {
+        const int64_t i0 = j * c.m;
+        uint32_t neg = 0, tie = 0, pc = 0;
+        auto one = [&](uint32_t w) {
+          const uint32_t r = w & 0x7fff7fffu;
+          const uint32_t dN = pk_sub16(r, TN), dN1 = pk_sub16(r, TN1);
+          const uint32_t dI = pk_sub16(w, TI), dI1 = pk_sub16(w, TI1);
+          tie |= (dN ^ dN1) | (dI ^ dI1);
+          neg += pk_sign_bits(dN);           // halves count to <= m < 32768
+          pc += (dI ^ (dI << 16)) >> 31;     // the INT bit sbx ^ sby ^ S
+        };
+        if (vec) {
+          const uint4* __restrict__ p4 = reinterpret_cast<const uint4*>(slab + i0);
+          for (int q = 0; q < (c.m >> 2); ++q) {
+            const uint4 v = p4[q];
+            one(v.x); one(v.y); one(v.z); one(v.w);
+          }
+        } else {
+          for (int r = 0; r < c.m; ++r) one(slab[i0 + r]);
+        }
+        int cx = c.m - 2 * (int)(neg & 0xffffu), cy = c.m - 2 * (int)(neg >> 16);
+        int cc = 2 * (int)pc - c.m;
+        if ((tie & 0x80008000u) || force_exact) {
+#pragma unroll 1
+          for (int r = 0; r < c.m; ++r) fix_fast(i0 + r, slab[i0 + r], cx, cy, cc);
+        }
+        core += cc;
+        batch_T(j, cx, cy, std::false_type());
+      }
+    } else for (int64_t j = tid; j < c.k; j += NT) {
       int cx = 0, cy = 0, cc = 0;
       const int64_t i0 = j * c.m;
       bool any = false;
