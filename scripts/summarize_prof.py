@@ -127,6 +127,15 @@ if os.path.exists(trace):
     if spans:
         out["simulate_call_span_ms"] = {"calls": len(spans), "avg": sum(spans) / len(spans),
                                         "min": min(spans), "max": max(spans)}
+    # steady state: back-to-back calls overlap (the next call's first chunks start beside the previous
+    # call's tail), so the GPU time per call is the whole run's sign-kernel span over the calls --
+    # what bench.py's kernel_ms_avg measures (first call's start to last call's end, / K)
+    sk = [(int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in rows
+          if "k_sign_" in short(r["Kernel_Name"]) or "k_subg_" in short(r["Kernel_Name"])]
+    ncalls = len(spans) + (1 if cur else 0)
+    if sk and ncalls:
+        out["simulate_steady_ms"] = {"calls": ncalls,
+                                     "per_call": (max(e for _, e in sk) - min(t for t, _ in sk)) / 1e6 / ncalls}
 
 json.dump(out, open(os.path.join(dst, f"{tag}_summary.json"), "w"), indent=1, sort_keys=True)
 lines = [f"# rocprofv3 summary `{tag}`", "",
@@ -145,6 +154,11 @@ if "simulate_call_span_ms" in out:
     sp = out["simulate_call_span_ms"]
     lines += ["", f"simulate() call span from the trace (first sign-kernel start to last end, "
                   f"{sp['calls']} calls): avg {sp['avg']:.3f} ms, min {sp['min']:.3f}, max {sp['max']:.3f} "
-                  "-- compare bench.py roofline.kernel_ms_avg (HIP events around the same call)."]
+                  "(a call's own kernels, overlapping its neighbours')."]
+if "simulate_steady_ms" in out:
+    st = out["simulate_steady_ms"]
+    lines += ["", f"Steady-state GPU time per call (first sign-kernel start to last end over {st['calls']} "
+                  f"back-to-back calls, / calls): {st['per_call']:.3f} ms -- compare bench.py "
+                  "roofline.kernel_ms_avg (HIP events, first call's start to last call's end, / K)."]
 open(os.path.join(dst, f"{tag}_summary.md"), "w").write("\n".join(lines) + "\n")
 print("\n".join(lines))
