@@ -513,8 +513,9 @@ int prepare_cell(const dcor_cell& c, CellPlan& p) {
     }
     code_map(cx, rx, 32768.0, &k.cbase_x, &k.cinv_x);
     code_map(cy, ry, 32768.0, &k.cbase_y, &k.cinv_y);
-    k.cinv_xf = (float)k.cinv_x; k.cnb_xf = (float)(-k.cbase_x * k.cinv_x);
-    k.cinv_yf = (float)k.cinv_y; k.cnb_yf = (float)(-k.cbase_y * k.cinv_y);
+    // code_pair's unorm16 maps t in [0, 1] to [0, 65535]: the fp32 map is the code map / 65535
+    k.cinv_xf = (float)(k.cinv_x / 65535.0); k.cnb_xf = (float)(-k.cbase_x * k.cinv_x / 65535.0);
+    k.cinv_yf = (float)(k.cinv_y / 65535.0); k.cnb_yf = (float)(-k.cbase_y * k.cinv_y / 65535.0);
     if (c.dgp == DCOR_DGP_BERNOULLI && !force_regen)
       p.kind = c.n <= GRID_BERN_W_NMAX ? GK_SIGN_BERN_W : GK_SIGN_BERN;
     else if (force_regen || !c.normalise)

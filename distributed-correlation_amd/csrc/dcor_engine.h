@@ -49,7 +49,7 @@ struct SignConst {
   double inv_md;
   double scale_Z, coefZ, q2, ratio, inv_sqrt_n, eps_r, w_laplace;
   double cbase_x, cinv_x, cbase_y, cinv_y;    // monotone code maps of clip(x), clip(y)
-  float cinv_xf, cnb_xf, cinv_yf, cnb_yf;     // the same maps in fp32: q = fma(v, inv, -base*inv)
+  float cinv_xf, cnb_xf, cinv_yf, cnb_yf;     // the same maps in fp32 / 65535: t = fma(v, inv, -base*inv)
 };
 
 // Sub-G family: correlation_NI_subG + ci_INT_subG (ver-cor-subG.R:25-108).

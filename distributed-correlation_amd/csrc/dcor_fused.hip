@@ -281,13 +281,12 @@ __device__ __forceinline__ void sign_finish(const SignConst& c, uint32_t rep, DD
 // threshold's code.  Results equal the two-pass algorithm's exactly.  Each thread
 // generates groups of 4 consecutive samples (one flip block per group, 16-B slab stores).
 // Two launches per replicate chunk (pass 1, pass 2); scratch = chunk * n * 4 B.
-// q(v) = clamp(fma(float(v), inv, -base*inv), 0, top) in fp32: every step (round to float,
-// fma with inv > 0, clamp, truncation) is monotone non-decreasing, which is all the sign
-// decision needs; the 2^15-2^16 code levels sit far above fp32 resolution.
-__device__ __forceinline__ uint32_t code16(double v, float inv, float nb, float top) {
-  const float t = fmaf((float)v, inv, nb);
-  return (uint32_t)__builtin_amdgcn_fmed3f(t, 0.0f, top);  // NaN -> 0 (a NaN mu is flagged)
-}
+// The code pair of (x, y) is one record word: q(v) = min(unorm16(fma(float(v), inv, nb)), 32767)
+// per half, inv = levels / (2 R 65535), nb = -base inv.  Every step (round to float, fma with
+// inv > 0, v_cvt_pknorm_u16_f32's clamp to [0, 1] and round to nearest, the min) is monotone
+// non-decreasing, which is all the sign decision needs; the 2^15 code levels sit far above fp32
+// resolution.  Both codes come from one v_pk_fma_f32 and one v_cvt_pknorm_u16_f32 (a NaN codes
+// as 0; a NaN threshold is flagged), and bit 15 of each half is 0 (code_pair, below).
 __device__ __forceinline__ int sgnq(uint32_t q, uint32_t qm) { return (q > qm) - (q < qm); }
 // sign(q - qm) for 16-bit codes as one subtract + one v_med3_i32 (clamp to [-1, 1]); asm
 // keeps the compiler from expanding the clamp into compare/select pairs.
@@ -307,6 +306,14 @@ __device__ __forceinline__ uint32_t pk_sub16(uint32_t a, uint32_t b) {
 __device__ __forceinline__ uint32_t pk_sign_bits(uint32_t a) {
   const dcor_u16x2 v = __builtin_bit_cast(dcor_u16x2, a);
   return __builtin_bit_cast(uint32_t, (dcor_u16x2)(v >> (dcor_u16x2){15, 15}));
+}
+typedef float dcor_f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t code_pair(double x, double y, float ix, float iy, float bx,
+                                              float by) {
+  const dcor_f32x2 v = {(float)x, (float)y};
+  const dcor_f32x2 t = __builtin_elementwise_fma(v, dcor_f32x2{ix, iy}, dcor_f32x2{bx, by});
+  const dcor_u16x2 q = __builtin_amdgcn_cvt_pknorm_u16(t.x, t.y);
+  return __builtin_bit_cast(uint32_t, __builtin_elementwise_min(q, (dcor_u16x2){32767, 32767}));
 }
 
 template <int DGP>
@@ -336,7 +343,8 @@ __device__ __forceinline__ void exact_signs(const SignConst& c, const SignStd& s
 // Gaussian DGP in pass 1: the ziggurat's fast path inline; a sample with a normal that misses it
 // (1.6 % of samples) is queued in a per-wave LDS list and generated in full later by the whole
 // wave at once (zig_slow would otherwise run under divergence nearly every iteration).  The
-// queued sample's record is rewritten and its clipped values enter the sums at the drain.
+// queued sample's record is rewritten and its clipped values replace its placeholder's in the
+// sums at the drain.
 #define ZQ_CAP 512  // per-wave queue; a group iteration adds at most 256 entries per wave
 
 // WAVE = false: one 256-thread workgroup per replicate; WAVE = true: one wave per replicate (the
@@ -350,34 +358,45 @@ __device__ __forceinline__ void sign_pass1_core(const SignConst& c, uint32_t rep
   constexpr int NT = WAVE ? 64 : DCOR_BLOCK;
   const int tid = WAVE ? (int)(threadIdx.x & 63) : (int)threadIdx.x;
   DD sx{0.0, 0.0}, sy{0.0, 0.0};
+  const float cix = c.cinv_xf, ciy = c.cinv_yf, cbx = c.cnb_xf, cby = c.cnb_yf;
   auto record = [&](double xc, double yc, uint32_t fl) {
-    const uint32_t qx = code16(xc, c.cinv_xf, c.cnb_xf, 32767.0f);
-    const uint32_t qy = code16(yc, c.cinv_yf, c.cnb_yf, 32767.0f);
-    return qx | (qy << 16) | (fl << 31);
+    return code_pair(xc, yc, cix, ciy, cbx, cby) | (fl << 31);
   };
   // each thread runs its groups in increasing order; the partial last group (n % 4) is the last
   // group of its thread
   const int64_t nfull = c.n / 4;
   if constexpr (DGP == DCOR_DGP_GAUSSIAN) {
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    // the fast path's clipped sample from its Philox block; false: a normal missed the fast path
+    // (the values are then a finite placeholder in [-L, L])
+    auto fast_xy = [&](const U4& w, double& xc, double& yc) -> bool {
+      const double2 t1 = zt[zig_j1(w.w2)], t2 = zt[zig_j2(w.w2)];
+      const double z1 = fma(zig_d(w.w0, zig_y1(w.w2)), t1.x, -t1.x);
+      const double z2 = fma(zig_d(w.w1, zig_y2(w.w2)), t2.x, -t2.x);
+      const bool ok = ((int)(fabs(z1) < t1.y) & (int)(fabs(z2) < t2.y)) != 0;
+      double x, y;
+      mvn_z(z1, z2, c.g.mu0, c.g.mu1, c.g.a00, c.g.a01, c.g.a10, c.g.a11, &x, &y);
+      xc = rclip_fin(x, c.L);
+      yc = rclip_fin(y, c.L);
+      return ok;
+    };
+    // Every valid sample enters the group sums, a queued one with its placeholder: the drain
+    // takes the placeholder out and adds the true values (both compensated), so the hot loop
+    // selects nothing.
     auto group = [&](int64_t g4, auto full_tag) {
       constexpr bool FULL = decltype(full_tag)::value;
       const uint32_t i0 = (uint32_t)(4 * g4);
       uint32_t rec[4], pend = 0;
-      double gx = 0.0, gy = 0.0;
+      double gx, gy;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const U4 w = draw(i0 + q, rep, DCOR_SITE_DGP_A, c.k0, c.k1);
-        const double2 t1 = zt[zig_j1(w.w2)], t2 = zt[zig_j2(w.w2)];
-        const double z1 = fma(zig_d(w.w0, zig_y1(w.w2)), t1.x, -t1.x);
-        const double z2 = fma(zig_d(w.w1, zig_y2(w.w2)), t2.x, -t2.x);
-        const bool ok = ((int)(fabs(z1) < t1.y) & (int)(fabs(z2) < t2.y)) != 0;
-        double x, y;
-        mvn_z(z1, z2, c.g.mu0, c.g.mu1, c.g.a00, c.g.a01, c.g.a10, c.g.a11, &x, &y);
-        const double xc = rclip_fin(x, c.L), yc = rclip_fin(y, c.L);
+        double xc, yc;
+        const bool ok = fast_xy(w, xc, yc);
         const bool valid = FULL || (int64_t)(i0 + q) < c.n;
-        gx += (valid && ok) ? xc : 0.0;
-        gy += (valid && ok) ? yc : 0.0;
+        const double ax = valid ? xc : 0.0, ay = valid ? yc : 0.0;
+        gx = q == 0 ? ax : gx + ax;
+        gy = q == 0 ? ay : gy + ay;
         pend |= (valid && !ok) ? (1u << q) : 0u;
         rec[q] = record(xc, yc, ((uint64_t)w.w3 < c.flipT) ? 1u : 0u);
       }
@@ -400,6 +419,10 @@ __device__ __forceinline__ void sign_pass1_core(const SignConst& c, uint32_t rep
       __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the placeholder records have landed
       for (uint32_t k = (uint32_t)lane; k < cnt; k += 64) {
         const uint32_t i = zq[k];
+        double px, py;
+        fast_xy(draw(i, rep, DCOR_SITE_DGP_A, c.k0, c.k1), px, py);
+        ks_acc(sx, -px);
+        ks_acc(sy, -py);
         double x, y;
         uint32_t w3;
         Dgp<DGP>::one_w3(c.g, i, rep, c.k0, c.k1, x, y, w3);
@@ -579,10 +602,9 @@ __device__ __forceinline__ P2Result sign_pass2_core(const SignConst& c, uint32_t
   // sign(d/sd) == sign(d) needs sd < 2^900 (no underflow of the quotient); else exact path.
   const bool force_exact = !(s.sdNx < 0x1p900 && s.sdNy < 0x1p900 && s.sdIx < 0x1p900 &&
                              s.sdIy < 0x1p900);
-  const uint32_t qNx = code16(s.muNx, c.cinv_xf, c.cnb_xf, 32767.0f);
-  const uint32_t qIx = code16(s.muIx, c.cinv_xf, c.cnb_xf, 32767.0f);
-  const uint32_t qNy = code16(s.muNy, c.cinv_yf, c.cnb_yf, 32767.0f);
-  const uint32_t qIy = code16(s.muIy, c.cinv_yf, c.cnb_yf, 32767.0f);
+  const uint32_t TN = code_pair(s.muNx, s.muNy, c.cinv_xf, c.cinv_yf, c.cnb_xf, c.cnb_yf);
+  const uint32_t TI = code_pair(s.muIx, s.muIy, c.cinv_xf, c.cinv_yf, c.cnb_xf, c.cnb_yf);
+  const uint32_t qNx = TN & 0xffffu, qNy = TN >> 16, qIx = TI & 0xffffu, qIy = TI >> 16;
   bool bad_ni = thr_nan, bad_int = thr_nan;
   DD sT{0.0, 0.0}, sT2{0.0, 0.0};
   long long core = 0;
@@ -637,7 +659,6 @@ __device__ __forceinline__ P2Result sign_pass2_core(const SignConst& c, uint32_t
     sT2.hi = valid ? sT2.hi : h2;
     sT2.lo = valid ? sT2.lo : l2;
   };
-  const uint32_t TN = qNx | (qNy << 16), TI = qIx | (qIy << 16);
   const uint32_t TN1 = TN + 0x00010001u, TI1 = TI + 0x00010001u;
   auto fix_fast = [&](int64_t i, uint32_t w, int& cx, int& cy, int& cc) {
     const uint32_t qx = w & 0x7fffu, qy = (w >> 16) & 0x7fffu;
