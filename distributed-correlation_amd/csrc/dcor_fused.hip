@@ -307,12 +307,28 @@ __device__ __forceinline__ uint32_t pk_sign_bits(uint32_t a) {
   const dcor_u16x2 v = __builtin_bit_cast(dcor_u16x2, a);
   return __builtin_bit_cast(uint32_t, (dcor_u16x2)(v >> (dcor_u16x2){15, 15}));
 }
+__device__ __forceinline__ uint32_t pk_min16(uint32_t a, uint32_t b) {
+  return __builtin_bit_cast(uint32_t, __builtin_elementwise_min(__builtin_bit_cast(dcor_u16x2, a),
+                                                                __builtin_bit_cast(dcor_u16x2, b)));
+}
+__device__ __forceinline__ bool has_zero16(uint32_t a) { return (a & 0xffffu) == 0u || (a >> 16) == 0u; }
+// bit 31: dI[31] ^ dI[15] ^ w[31] (one v_bitop3 after the shift)
+__device__ __forceinline__ uint32_t int_bit31(uint32_t dI, uint32_t w) {
+  return __builtin_amdgcn_bitop3_b32(dI, dI << 16, w, 0x96);
+}
 typedef float dcor_f32x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint32_t code_pair(double x, double y, float ix, float iy, float bx,
                                               float by) {
   const dcor_f32x2 v = {(float)x, (float)y};
   const dcor_f32x2 t = __builtin_elementwise_fma(v, dcor_f32x2{ix, iy}, dcor_f32x2{bx, by});
   const dcor_u16x2 q = __builtin_amdgcn_cvt_pknorm_u16(t.x, t.y);
+  return __builtin_bit_cast(uint32_t, __builtin_elementwise_min(q, (dcor_u16x2){32767, 32767}));
+}
+// the same codes from two scalar fmas (fma rounds exactly either way): the thresholds' form, which
+// keeps the kernel-argument fields out of a vector build
+__device__ __forceinline__ uint32_t code_pair_s(double x, double y, float ix, float iy, float bx,
+                                                float by) {
+  const dcor_u16x2 q = __builtin_amdgcn_cvt_pknorm_u16(fmaf((float)x, ix, bx), fmaf((float)y, iy, by));
   return __builtin_bit_cast(uint32_t, __builtin_elementwise_min(q, (dcor_u16x2){32767, 32767}));
 }
 
@@ -359,8 +375,10 @@ __device__ __forceinline__ void sign_pass1_core(const SignConst& c, uint32_t rep
   const int tid = WAVE ? (int)(threadIdx.x & 63) : (int)threadIdx.x;
   DD sx{0.0, 0.0}, sy{0.0, 0.0};
   const float cix = c.cinv_xf, ciy = c.cinv_yf, cbx = c.cnb_xf, cby = c.cnb_yf;
-  auto record = [&](double xc, double yc, uint32_t fl) {
-    return code_pair(xc, yc, cix, ciy, cbx, cby) | (fl << 31);
+  // the INT flip from its 32-bit word: u < flipT (flipT <= 2^32) as a 32-bit compare
+  const uint32_t ftm1 = (uint32_t)(c.flipT - 1u), fbit = c.flipT != 0 ? 0x80000000u : 0u;
+  auto record_w = [&](double xc, double yc, uint32_t u) {
+    return code_pair(xc, yc, cix, ciy, cbx, cby) | (u <= ftm1 ? fbit : 0u);
   };
   // each thread runs its groups in increasing order; the partial last group (n % 4) is the last
   // group of its thread
@@ -398,7 +416,7 @@ __device__ __forceinline__ void sign_pass1_core(const SignConst& c, uint32_t rep
         gx = q == 0 ? ax : gx + ax;
         gy = q == 0 ? ay : gy + ay;
         pend |= (valid && !ok) ? (1u << q) : 0u;
-        rec[q] = record(xc, yc, ((uint64_t)w.w3 < c.flipT) ? 1u : 0u);
+        rec[q] = record_w(xc, yc, w.w3);
       }
       ks_acc(sx, gx);
       ks_acc(sy, gy);
@@ -429,7 +447,7 @@ __device__ __forceinline__ void sign_pass1_core(const SignConst& c, uint32_t rep
         const double xc = rclip_fin(x, c.L), yc = rclip_fin(y, c.L);
         ks_acc(sx, xc);
         ks_acc(sy, yc);
-        slab[i] = record(xc, yc, ((uint64_t)w3 < c.flipT) ? 1u : 0u);
+        slab[i] = record_w(xc, yc, w3);
       }
       wave_sync();
       if (lane == 0) *zqn = 0u;
@@ -447,17 +465,17 @@ __device__ __forceinline__ void sign_pass1_core(const SignConst& c, uint32_t rep
       constexpr bool FULL = decltype(full_tag)::value;
       const uint32_t i0 = (uint32_t)(4 * g4);
       double x[4], y[4];
-      uint32_t fl[4];  // INT flip bits (vert-cor.R:175)
+      uint32_t fl[4];  // INT flip bits (vert-cor.R:175), in bit 31
       if constexpr (Dgp<DGP>::flip_src == FLIP_SPARE24) {
         uint32_t u24[4];
         Dgp<DGP>::quad_u24(c.g, i0, rep, c.k0, c.k1, x, y, u24);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) fl[q] = u24[q] < c.flipT24 ? 1u : 0u;
+        for (int q = 0; q < 4; ++q) fl[q] = u24[q] < c.flipT24 ? 0x80000000u : 0u;
       } else {
         const U4 fw = draw((uint32_t)g4, rep, DCOR_SITE_FLIP, c.k0, c.k1);
         Dgp<DGP>::quad(c.g, i0, rep, c.k0, c.k1, x, y);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) fl[q] = ((uint64_t)word(fw, q) < c.flipT) ? 1u : 0u;
+        for (int q = 0; q < 4; ++q) fl[q] = word(fw, q) <= ftm1 ? fbit : 0u;
       }
       uint32_t rec[4];
       double gx = 0.0, gy = 0.0;
@@ -465,7 +483,7 @@ __device__ __forceinline__ void sign_pass1_core(const SignConst& c, uint32_t rep
       for (int q = 0; q < 4; ++q) {
         const double xc = rclip_fin(x[q], c.L), yc = rclip_fin(y[q], c.L);
         if (FULL || (int64_t)(i0 + q) < c.n) { gx += xc; gy += yc; }
-        rec[q] = record(xc, yc, fl[q]);
+        rec[q] = code_pair(xc, yc, cix, ciy, cbx, cby) | fl[q];
       }
       ks_acc(sx, gx);
       ks_acc(sy, gy);
@@ -602,8 +620,8 @@ __device__ __forceinline__ P2Result sign_pass2_core(const SignConst& c, uint32_t
   // sign(d/sd) == sign(d) needs sd < 2^900 (no underflow of the quotient); else exact path.
   const bool force_exact = !(s.sdNx < 0x1p900 && s.sdNy < 0x1p900 && s.sdIx < 0x1p900 &&
                              s.sdIy < 0x1p900);
-  const uint32_t TN = code_pair(s.muNx, s.muNy, c.cinv_xf, c.cinv_yf, c.cnb_xf, c.cnb_yf);
-  const uint32_t TI = code_pair(s.muIx, s.muIy, c.cinv_xf, c.cinv_yf, c.cnb_xf, c.cnb_yf);
+  const uint32_t TN = code_pair_s(s.muNx, s.muNy, c.cinv_xf, c.cinv_yf, c.cnb_xf, c.cnb_yf);
+  const uint32_t TI = code_pair_s(s.muIx, s.muIy, c.cinv_xf, c.cinv_yf, c.cnb_xf, c.cnb_yf);
   const uint32_t qNx = TN & 0xffffu, qNy = TN >> 16, qIx = TI & 0xffffu, qIy = TI >> 16;
   bool bad_ni = thr_nan, bad_int = thr_nan;
   DD sT{0.0, 0.0}, sT2{0.0, 0.0};
@@ -659,7 +677,6 @@ __device__ __forceinline__ P2Result sign_pass2_core(const SignConst& c, uint32_t
     sT2.hi = valid ? sT2.hi : h2;
     sT2.lo = valid ? sT2.lo : l2;
   };
-  const uint32_t TN1 = TN + 0x00010001u, TI1 = TI + 0x00010001u;
   auto fix_fast = [&](int64_t i, uint32_t w, int& cx, int& cy, int& cc) {
     const uint32_t qx = w & 0x7fffu, qy = (w >> 16) & 0x7fffu;
     if (!(force_exact || qx == qNx || qy == qNy || qx == qIx || qy == qIy)) return;
@@ -674,30 +691,29 @@ __device__ __forceinline__ P2Result sign_pass2_core(const SignConst& c, uint32_t
   };
   if (c.m == 8) {
     // headline geometry: one thread = one batch = two 16-B loads.
-    // Signs by packed 16-bit subtraction of the threshold pairs T = (tx, ty): the sign bit of each
-    // half of rec - T is (q < t), of rec - (T + 1) is (q <= t); the two differ exactly on a tie.
-    // A tie is counted as +1 here and corrected by the fix-up.  NI subtracts from the record with
-    // the flip bit masked.  INT subtracts from the raw record: the flip S sits in the y half's sign
-    // position, so that half's sign bit comes out as (qy < ty) ^ S and bit 31 of dI ^ (dI << 16) is
-    // the sample's INT bit sbx ^ sby ^ S -- contribution (2S - 1) sx sy = +1 exactly when it is set.
+    // Signs by packed 16-bit subtraction of the threshold pairs T = (tx, ty) from the record with the
+    // flip bit masked: the sign bit of each half of d = rec - T is (q < t), and a half of d is zero
+    // exactly on a tie, so the running packed minimum of the d's has a zero half iff the batch holds
+    // a tie.  A tie is counted as +1 here and corrected by the fix-up.  Bit 31 of
+    // dI ^ (dI << 16) ^ rec is the sample's INT bit sbx ^ sby ^ S (the flip S is the record's bit
+    // 31) -- contribution (2S - 1) sx sy = +1 exactly when it is set.
     // the count triple (cx, cy, cc) of batch j from its two 16-B record loads
     auto decide = [&](int64_t j, const uint4& lo, const uint4& hi, int& cx, int& cy, int& cc) {
       const U4 w0{lo.x, lo.y, lo.z, lo.w}, w1{hi.x, hi.y, hi.z, hi.w};
-      uint32_t neg = 0, tie = 0, par = 0;
+      uint32_t neg = 0, par = 0, mn = 0xffffffffu;
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
         const uint32_t w = word(q < 4 ? w0 : w1, q & 3);
         const uint32_t r = w & 0x7fff7fffu;
-        const uint32_t dN = pk_sub16(r, TN), dN1 = pk_sub16(r, TN1);
-        const uint32_t dI = pk_sub16(w, TI), dI1 = pk_sub16(w, TI1);
-        tie |= (dN ^ dN1) | (dI ^ dI1);
+        const uint32_t dN = pk_sub16(r, TN), dI = pk_sub16(r, TI);
+        mn = pk_min16(pk_min16(mn, dN), dI);                         // a zero half is a tie
         neg += pk_sign_bits(dN);                                     // halves count to <= 8
-        par = __builtin_amdgcn_alignbit(par, dI ^ (dI << 16), 31u);  // (par << 1) | INT bit
+        par = __builtin_amdgcn_alignbit(par, int_bit31(dI, w), 31u); // (par << 1) | INT bit
       }
       cx = 8 - 2 * (int)(neg & 0xffffu);
       cy = 8 - 2 * (int)(neg >> 16);
       cc = 2 * __popc(par) - 8;
-      if ((tie & 0x80008000u) || force_exact) {
+      if (has_zero16(mn) || force_exact) {
 #pragma unroll 1
         for (int q = 0; q < 8; ++q)  // re-read the record (L2-hot): no dynamically indexed registers
           fix_fast(8 * j + q, slab[8 * j + q], cx, cy, cc);
@@ -739,14 +755,13 @@ __device__ __forceinline__ P2Result sign_pass2_core(const SignConst& c, uint32_t
       const bool vec = (c.m & 3) == 0;
       for (int64_t j = tid; j < c.k; j += NT) {
         const int64_t i0 = j * c.m;
-        uint32_t neg = 0, tie = 0, pc = 0;
+        uint32_t neg = 0, pc = 0, mn = 0xffffffffu;
         auto one = [&](uint32_t w) {
           const uint32_t r = w & 0x7fff7fffu;
-          const uint32_t dN = pk_sub16(r, TN), dN1 = pk_sub16(r, TN1);
-          const uint32_t dI = pk_sub16(w, TI), dI1 = pk_sub16(w, TI1);
-          tie |= (dN ^ dN1) | (dI ^ dI1);
+          const uint32_t dN = pk_sub16(r, TN), dI = pk_sub16(r, TI);
+          mn = pk_min16(pk_min16(mn, dN), dI);
           neg += pk_sign_bits(dN);           // halves count to <= m < 32768
-          pc += (dI ^ (dI << 16)) >> 31;     // the INT bit sbx ^ sby ^ S
+          pc += int_bit31(dI, w) >> 31;      // the INT bit sbx ^ sby ^ S
         };
         if (vec) {
           const uint4* __restrict__ p4 = reinterpret_cast<const uint4*>(slab + i0);
@@ -759,7 +774,7 @@ __device__ __forceinline__ P2Result sign_pass2_core(const SignConst& c, uint32_t
         }
         int cx = c.m - 2 * (int)(neg & 0xffffu), cy = c.m - 2 * (int)(neg >> 16);
         int cc = 2 * (int)pc - c.m;
-        if ((tie & 0x80008000u) || force_exact) {
+        if (has_zero16(mn) || force_exact) {
 #pragma unroll 1
           for (int r = 0; r < c.m; ++r) fix_fast(i0 + r, slab[i0 + r], cx, cy, cc);
         }

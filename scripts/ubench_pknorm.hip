@@ -20,6 +20,16 @@ __global__ void k_mono(uint32_t ubegin, uint32_t count, uint32_t* bad) {
   if (n.x != 0 || n.y != 0) bad[1] = u;
 }
 
+// code resolution: t = (k + f) / 65535 must code as k (f = 0, 0.3) and k + 1 (f = 0.7)
+__global__ void k_levels(uint32_t* bad) {
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= 65535u) return;
+  const float a = (float)k / 65535.0f, b = ((float)k + 0.3f) / 65535.0f, c = ((float)k + 0.7f) / 65535.0f;
+  const u16x2 q = __builtin_amdgcn_cvt_pknorm_u16(a, b);
+  const u16x2 r = __builtin_amdgcn_cvt_pknorm_u16(c, c);
+  if (q.x != k || q.y != k || r.x != k + 1u) atomicAdd(&bad[0], 1u);
+}
+
 __global__ void k_special(uint32_t* out) {
   if (threadIdx.x != 0) return;
   const float nan = __uint_as_float(0x7fc00000u);
@@ -40,10 +50,12 @@ int main() {
     hipLaunchKernelGGL(k_mono, dim3((cnt + 255) / 256), dim3(256), 0, 0, b, cnt, d);
   }
   hipLaunchKernelGGL(k_special, dim3(1), dim3(64), 0, 0, d + 2);
+  hipLaunchKernelGGL(k_levels, dim3(256), dim3(256), 0, 0, d + 6);
   uint32_t h[8];
   if (hipMemcpy(h, d, sizeof(h), hipMemcpyDeviceToHost) != hipSuccess) return 2;
   std::printf("monotone violations: %s (first u 0x%08x); negative nonzero: %s\n",
               h[0] == 0xffffffffu ? "none" : "FOUND", h[0], h[1] == 0xffffffffu ? "none" : "FOUND");
+  std::printf("code levels off by rounding: %u of 65535\n", h[6]);
   std::printf("pknorm(NaN) = %u, pknorm(1) = %u, pknorm(0.5) = %u, pknorm(32767/65535) = %u\n",
               h[2], h[3], h[4], h[5]);
   hipFree(d);
