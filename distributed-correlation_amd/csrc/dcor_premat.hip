@@ -260,35 +260,51 @@ __global__ __launch_bounds__(DCOR_BLOCK) void k_premat_subg_stream(PrematSubgCon
 
 
 // NI result, INT estimate, mixquant, INT CI of replicate `rep` from its five sums
-// (ver-cor-subG.R:51-59, 91-103; real-data-sims.R:233-243).  quant(c*) is the mixquant
-// (workgroup- or wave-level); `writer` is the one thread that stores the record.
+// (ver-cor-subG.R:51-59, 91-103; real-data-sims.R:233-243), in two halves around the mixquant:
+// premat_subg_pre gives the NI triple, the INT point estimate, sd and c* (and whether the CI takes
+// a mixquant at all: the HRS sd == 0 branch does not); premat_subg_post the CI from quant(c*).
+struct SubgPre {
+  double o[3];
+  double rho, sd, cstar;
+  bool quant;
+};
+__device__ __forceinline__ SubgPre premat_subg_pre(const PrematSubgConst& p, const DD (&d5)[5],
+                                                   double lapc) {
+  const SubgConst& c = p.s;
+  SubgPre r;
+  ni_subg_result(c, d5[0], d5[1], d5[2], r.o);
+  const DD mU = dd_div_d(d5[3], c.nd);
+  r.rho = (mU.hi + mU.lo) + c.s_central * lapc;
+  r.sd = sqrt(dd_var(d5[3], d5[4], c.nd));
+  r.quant = !p.hrs || r.sd != 0.0;
+  r.cstar = !p.hrs ? 2.0 / (c.sqrt_n * r.sd * c.eps_r) : (2.0 * c.lr) / (c.sqrt_n * r.sd * c.eps_r);
+  return r;
+}
+__device__ __forceinline__ dcor_rep_out premat_subg_post(const PrematSubgConst& p, const SubgPre& r,
+                                                         double qq) {
+  const SubgConst& c = p.s;
+  double width;
+  if (!p.hrs) {
+    const double se_norm = sqrt(r.sd * r.sd + c.sn2x2);
+    width = qq * se_norm / c.sqrt_n;
+  } else if (r.sd == 0.0) {
+    width = p.crit_sqrt2_s;
+  } else {
+    width = qq * (r.sd / c.sqrt_n);
+  }
+  return dcor_rep_out{r.o[0], r.o[1], r.o[2], r.rho, rmax(r.rho - width, -1.0), rmin(r.rho + width, 1.0)};
+}
+
+// quant(c*) is the mixquant (workgroup- or wave-level, called uniformly); `writer` is the one
+// thread that stores the record.
 template <class Quant>
 __device__ __forceinline__ void premat_subg_finish_q(const PrematSubgConst& p, int64_t rep,
                                                      const DD (&d5)[5], Quant&& quant, bool writer,
                                                      dcor_rep_out* out, double lapc) {
-  const SubgConst& c = p.s;
-  double o[6];
-  ni_subg_result(c, d5[0], d5[1], d5[2], o);
-  const DD mU = dd_div_d(d5[3], c.nd);
-  const double rho = (mU.hi + mU.lo) + c.s_central * lapc;
-  const double sd = sqrt(dd_var(d5[3], d5[4], c.nd));
-  double width;
-  if (!p.hrs) {
-    const double se_norm = sqrt(sd * sd + c.sn2x2);
-    const double cstar = 2.0 / (c.sqrt_n * sd * c.eps_r);
-    const double qq = quant(cstar);
-    width = qq * se_norm / c.sqrt_n;
-  } else if (sd == 0.0) {
-    width = p.crit_sqrt2_s;
-  } else {
-    const double cstar = (2.0 * c.lr) / (c.sqrt_n * sd * c.eps_r);
-    const double qq = quant(cstar);
-    width = qq * (sd / c.sqrt_n);
-  }
-  o[3] = rho;
-  o[4] = rmax(rho - width, -1.0);
-  o[5] = rmin(rho + width, 1.0);
-  if (writer) out[rep] = dcor_rep_out{o[0], o[1], o[2], o[3], o[4], o[5]};
+  const SubgPre r = premat_subg_pre(p, d5, lapc);
+  const double qq = r.quant ? quant(r.cstar) : 0.0;
+  const dcor_rep_out o = premat_subg_post(p, r, qq);
+  if (writer) out[rep] = o;
 }
 
 __device__ __forceinline__ void premat_subg_finish(const PrematSubgConst& p, int64_t rep,
@@ -342,18 +358,27 @@ __global__ __launch_bounds__(DCOR_BLOCK) void k_premat_subg_epilogue_w(PrematSub
 }
 
 // Epilogue of the streaming kernels that hand their sums over through SubgPartial.
+// The scalar half (sums, NI triple, sd, c*) runs in wave 0 only and c* reaches the other waves
+// through LDS: the four waves computed it redundantly before, a quarter of the kernel's fp64 work.
 __global__ __launch_bounds__(DCOR_BLOCK) void k_premat_subg_epilogue(PrematSubgConst p,
                                                                      const SubgPartial* __restrict__ part,
                                                                      dcor_rep_out* out) {
   __shared__ SelScratch sel;
+  __shared__ double bc[2];  // c*, and 1.0 when the CI takes a mixquant
   const int64_t rep = blockIdx.x;
   const MixConst& mx = p.s.mix;
   double zv[SEL_VPT], lv[SEL_VPT];  // the mixquant draws do not depend on c*: load them first
   mixquant_prefetch(mx, p.mix_z + rep * mx.nsim, p.mix_l + rep * mx.nsim, zv, lv);
-  DD d5[5];
-  load_partials(p, part, rep, d5);
-  premat_subg_finish_q(p, rep, d5, [&](double cs) { return mixquant_regs(mx, cs, zv, lv, &sel); },
-                       threadIdx.x == 0, out, p.lap_central[rep]);
+  SubgPre r{};
+  if (threadIdx.x < 64) {
+    DD d5[5];
+    load_partials(p, part, rep, d5);
+    r = premat_subg_pre(p, d5, p.lap_central[rep]);
+    if (threadIdx.x == 0) { bc[0] = r.cstar; bc[1] = r.quant ? 1.0 : 0.0; }
+  }
+  __syncthreads();
+  const double qq = bc[1] != 0.0 ? mixquant_regs(mx, bc[0], zv, lv, &sel) : 0.0;
+  if (threadIdx.x == 0) out[rep] = premat_subg_post(p, r, qq);
 }
 
 // ------------------------------------------- dictionary-coded shared panel (HRS) ---
@@ -1603,13 +1628,20 @@ __global__ __launch_bounds__(DCOR_BLOCK) void k_hrs_fused_epilogue(PrematSubgCon
       lv[2 * s + 1] = unit_laplace(u53(wl.w2, wl.w3));
     }
   }
-  const U4 wc = draw(0u, rep, HRS_SITE_CENTRAL, hk.in0, hk.in1);
-  const double lapc = unit_laplace(u53(wc.w0, wc.w1));
-  DD d5[5];
-  load_partials(p, part, r, d5);
-  premat_subg_finish_q(p, r, d5, [&](double cs) {
-    if (threadIdx.x == 0) sel.nan_cnt = 0;
-    __syncthreads();
+  // the scalar half in wave 0 only (as k_premat_subg_epilogue); c* reaches the others through LDS
+  __shared__ double bc[2];
+  SubgPre pre{};
+  if (threadIdx.x < 64) {
+    const U4 wc = draw(0u, rep, HRS_SITE_CENTRAL, hk.in0, hk.in1);
+    DD d5[5];
+    load_partials(p, part, r, d5);
+    pre = premat_subg_pre(p, d5, unit_laplace(u53(wc.w0, wc.w1)));
+    if (threadIdx.x == 0) { bc[0] = pre.cstar; bc[1] = pre.quant ? 1.0 : 0.0; sel.nan_cnt = 0; }
+  }
+  __syncthreads();
+  double qq = 0.0;
+  if (bc[1] != 0.0) {
+    const double cs = bc[0];
     double val[SEL_VPT];
     int nn = 0;
 #pragma unroll
@@ -1622,8 +1654,9 @@ __global__ __launch_bounds__(DCOR_BLOCK) void k_hrs_fused_epilogue(PrematSubgCon
     }
     if (nn) atomicAdd(&sel.nan_cnt, nn);
     __syncthreads();
-    return value_select(val, mx.pos, mx.nsim - sel.nan_cnt, &sel);
-  }, threadIdx.x == 0, out, lapc);
+    qq = value_select(val, mx.pos, mx.nsim - sel.nan_cnt, &sel);
+  }
+  if (threadIdx.x == 0) out[r] = premat_subg_post(p, pre, qq);
 }
 
 int launch_hrs_fused(const PrematSubgConst& c, uint64_t seed_ni, uint64_t seed_int,
