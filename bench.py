@@ -92,7 +92,11 @@ def cpu_baseline(cell, seconds: float = 12.0):
             "multi_core_value": done / elm, "multi_core_cores": workers,
             "multi_core_sample": f"{workers} threads x {Bw} replicates, each its own headline-config "
                                  f"cell (seed 1e6 + i), in {elm:.1f} s: the mclapply grid's "
-                                 "detectCores() - 1 workers, capped at this box's CPU share"}
+                                 "detectCores() - 1 workers, capped at this box's CPU share",
+            "whole_host_projected_value": done / elm / workers * max(1, usable - 1),
+            "whole_host_projected_note": f"multi_core_value per thread x {max(1, usable - 1)} "
+                                         "(detectCores() - 1 on this host): a linear projection, "
+                                         "not a measurement; an upper bound for the host"}
 
 
 def src_sha16(root: str = ROOT) -> str:
