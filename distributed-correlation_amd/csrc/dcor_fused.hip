@@ -275,11 +275,11 @@ __device__ __forceinline__ void sign_finish(const SignConst& c, uint32_t rep, DD
 // ======================================== fused sign family, one pass (hot) ===
 // Pass 1 generates each sample once: the DP-mean sums of clip(x), clip(y) (vert-cor.R:
 // 328-340) and a 4-byte record per sample in a per-workgroup slab -- monotone 15-bit codes
-// of clip(x) (bits 0-14) and clip(y) (bits 16-30) and the INT flip bit (31); bit 15 is 0.  q(v) = clamp(floor(
-// (v - base) * inv)) is monotone non-decreasing, so q(xc) != q(mu) proves sign(xc - mu);
-// pass 2 decides every sign from codes and regenerates only samples whose code ties a
-// threshold's code.  Results equal the two-pass algorithm's exactly.  Each thread
-// generates groups of 4 consecutive samples (one flip block per group, 16-B slab stores).
+// of clip(x) (bits 0-14) and clip(y) (bits 16-30) and the INT flip bit (31); bit 15 is 0.  The
+// code map q (below) is monotone non-decreasing, so q(xc) != q(mu) proves sign(xc - mu); pass 2
+// decides every sign from codes and regenerates only samples whose code ties a threshold's code.
+// Results equal the two-pass algorithm's exactly.  Each thread generates groups of 4 consecutive
+// samples (16-B slab stores).
 // Two launches per replicate chunk (pass 1, pass 2); scratch = chunk * n * 4 B.
 // The code pair of (x, y) is one record word: q(v) = min(unorm16(fma(float(v), inv, nb)), 32767)
 // per half, inv = levels / (2 R 65535), nb = -base inv.  Every step (round to float, fma with
