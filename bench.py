@@ -123,7 +123,7 @@ def profile_stamp(path):
 
 
 def _profile(name):
-    for tag in ("r03", "r02", "r01"):
+    for tag in ("r04", "r03", "r02", "r01"):
         p = os.path.join(ROOT, "profiles", f"{tag}_{name}_summary.json")
         if os.path.exists(p):
             return p
@@ -140,39 +140,105 @@ def pmc_traffic(path=_profile("headline")):
         tot = sum((v["hbm_read_bytes_corrected"] + v["hbm_write_bytes"]) * v["calls"]
                   for name, v in ks.items() if "k_sign_" in name)
         return tot / calls
-    except (OSError, KeyError, ValueError, ZeroDivisionError):
+    except (OSError, KeyError, ValueError, ZeroDivisionError, TypeError):
         return None
 
 
-def issue_frac(path=_profile("serial")):
-    """Hardware-measured VALU roofline of the sign kernels from the committed rocprofv3 profile
-    (chunks profiled serially, so no kernel shares the SIMDs): rocprof's VALUBusy,
-    SQ_ACTIVE_INST_VALU x 4 / (1024 SIMDs x GRBM_GUI_ACTIVE / 8), the fraction of SIMD-cycles the
-    vector ALU was executing (scripts/summarize_prof.py valu_busy; <= 1 by construction).
-    -> (time-weighted fraction over pass 1 + pass 2 + epilogue, per kernel, source) or Nones."""
-    try:
-        ks = json.load(open(path))["kernels"]
-        per, num, den = {}, 0.0, 0.0
-        for name, v in ks.items():
-            if "k_sign_" in name and "valu_busy" in v:
-                per[name.split("::")[1].split("(")[0]] = round(v["valu_busy"], 3)
-                num += v["valu_busy"] * v["avg_ns"] * v["calls"]
-                den += v["avg_ns"] * v["calls"]
-        return (num / den if den else None), (per or None), os.path.relpath(path, ROOT)
-    except (OSError, KeyError, ValueError, IndexError, TypeError):
-        return None, None, None
+def measure_passes(cell, reps: int = 2048, rep_begin: int = 0, iters: int = 5) -> dict:
+    """Live per-pass times of the one-pass sign path and their measured issue ceilings, on this
+    GPU, now (dcor_diag_sign_pass): each pass over `reps` replicates as one chunk on the current
+    stream, alone on the device, median of `iters` launches timed with HIP events on that stream.
+
+      pass1 / pass2 / epilogue   the real kernels (k_sign_pass1, k_sign_pass2, k_sign_epilogue_w)
+      pass1_ceiling              k_sign_pass1's own hot loop -- Philox, ziggurat fast path, mvrnorm
+                                 transform, clips, record codes, group sums -- with the slab store
+                                 and the slow-normal queue removed, at pass 1's waves per SIMD
+      pass1_ceiling_own_occ      the same at the ceiling kernel's own (higher) occupancy
+      pass2_ceiling              k_sign_pass2's decision loop with its records held in registers
+                                 (no slab stream, no tie fix-up), at pass 2's occupancy
+
+    A ceiling is the time the pass's own instruction stream takes when nothing but issue limits
+    it: pass / ceiling is how far memory, queueing and fix-ups keep the pass from it."""
+    import ctypes as C
+
+    import torch
+    from dcor import _lib
+    c = cell.to_c()
+    st = torch.cuda.current_stream()
+
+    def run(which):
+        _lib.check(_lib.lib.dcor_diag_sign_pass(C.byref(c), rep_begin, reps, which, C.c_void_p(st.cuda_stream)))
+
+    def timed(which):
+        run(which)
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(iters)]
+        for a, b in ev:
+            a.record(st)
+            run(which)
+            b.record(st)
+        torch.cuda.synchronize()
+        return sorted(a.elapsed_time(b) for a, b in ev)[iters // 2]
+
+    out = {"pass1": timed(1), "pass2": timed(2), "epilogue": timed(3),
+           "pass1_ceiling": timed(11), "pass1_ceiling_own_occ": timed(13), "pass2_ceiling": timed(12)}
+    return {k: round(v, 5) for k, v in out.items()}
+
+
+def _free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n: int, argv) -> int:
+    """`bench.py --gpus N` without a launcher: start N rank processes of this script (RANK,
+    LOCAL_RANK, WORLD_SIZE, MASTER_ADDR/PORT set; rank r on GPU r) and return the worst exit code.
+    Called before anything touches the GPU (no HIP state to inherit); rank 0 prints the line."""
+    import subprocess
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env))
+    rcs = [p.wait() for p in procs]
+    bad = [rc for rc in rcs if rc != 0]
+    if bad:
+        print(f"bench.py: rank exit codes {rcs}", file=sys.stderr)
+    return bad[0] if bad else 0
 
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs (ranks); without a launcher's WORLD_SIZE, N > 1 starts N rank processes")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--reps", type=int, default=8192, help="replicates per GPU per step")
     ap.add_argument("--n", type=int, default=100_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-ceilings", action="store_true", help="skip the live pass ceilings (roofline.issue_frac)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher check on CPU: form the process group over gloo, exchange accumulators, "
+                         "print the world size formed; no GPU, no timing")
     args = ap.parse_args()
+
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None:
+        n = 1 if args.gpus is None else args.gpus
+        if n < 1:
+            sys.exit("bench.py: --gpus must be >= 1")
+        if n > 1:
+            if not args.dry_run:
+                import torch   # device_count() does not initialise HIP on this image
+                vis = torch.cuda.device_count()
+                if vis < n:
+                    sys.exit(f"bench.py: --gpus {n} but {vis} GPU(s) visible; refusing to measure fewer")
+            sys.exit(spawn_ranks(n, sys.argv[1:]))
+    elif args.gpus is not None and args.gpus != int(env_world):
+        sys.exit(f"bench.py: --gpus {args.gpus} but the launcher's WORLD_SIZE is {env_world}")
 
     import torch
     import torch.distributed as dist
@@ -180,6 +246,8 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.dry_run:
+        return dry_run(world, rank)
     cpu = None
     if world == 1 and not args.no_cpu_baseline:   # before the GPU is touched (the pool forks nothing)
         from dcor.sim import headline_cell as _hc
@@ -187,11 +255,14 @@ def main():
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        formed = dist.get_world_size()
+        if formed != world:
+            sys.exit(f"bench.py: process group formed {formed} ranks, expected {world}")
     else:
         torch.cuda.set_device(0)
+        formed = 1
 
     import dcor
-    from dcor import _lib
     from dcor.dist import gather_accums, merge_ranked
     from dcor.sim import accum_from_bytes, accumulate, finalize, headline_cell, simulate
 
@@ -249,31 +320,46 @@ def main():
     achieved = R * W * 2.0 / (kern_ms * 1e-3) / 1e12  # fp64-equivalent TFLOP/s per GPU
     summ = {"NI": finalize(merged[0], cell.rho), "INT": finalize(merged[1], cell.rho)}
 
-    ifrac, iper, isrc = issue_frac()
+    # live pass ceilings (after the timed region; untimed): the physical roofline of the VALU-bound path
+    chunk = 2048 if R >= 4096 else max(1, R // 2)
+    nch = -(-R // chunk)
+    passes = None
+    if rank == 0 and not args.no_ceilings and cell.n > 16384 and m == 8:
+        passes = measure_passes(cell, chunk, rep_begin=(args.steps + args.warmup) * world * R)
+    issue = None
+    if passes:
+        ceil_call = nch * (passes["pass1_ceiling"] + passes["pass2_ceiling"] + passes["epilogue"])
+        issue = {"call": ceil_call / kern_ms,
+                 "pass1": passes["pass1_ceiling"] / passes["pass1"],
+                 "pass2": passes["pass2_ceiling"] / passes["pass2"],
+                 "pass1_occupancy_gain": passes["pass1_ceiling"] / passes["pass1_ceiling_own_occ"],
+                 "chunk_reps": chunk, "chunks_per_call": nch, "ms": passes}
+    traffic = pmc_traffic()
     if rank == 0:
         res = {
-            "metric": METRIC, "value": value, "unit": "replicates/s", "n_gpus": world,
+            "metric": METRIC, "value": value, "unit": "replicates/s", "n_gpus": formed,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": el * 1e3 / args.steps,
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
             "data": "synthetic (on-device Philox draws of the reference DGP)",
             "config": {"workload": "vert-cor.R sign family, Gaussian mvrnorm mu=(.5,.5) sigma=(2,2), "
                                    "rho=.5, eps=(1,1), NI+INT CIs (mixquant)",
                        "n": cell.n, "m": m, "k": k, "replicates_per_gpu_per_step": R,
-                       "parallelism": f"replicate-shard x{world}"},
+                       "parallelism": f"replicate-shard x{formed}",
+                       "world_formed": formed, "backend": "nccl (RCCL)" if world > 1 else "single process"},
             "roofline": {"bound": "valu_fp64", "achieved": achieved, "peak": FP64_PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": achieved / FP64_PEAK_TFLOPS,
-                         "frac_convention": achieved / FP64_PEAK_TFLOPS,
-                         "frac_kind": "pinned-convention: SURVEY §8d work weights (fp64-FMA units) per "
+                         "frac_kind": "pinned convention: SURVEY §8d work weights (fp64-FMA units) per "
                                       "replicate x replicates / kernel time over the fp64 peak; > 1 means "
-                                      "the kernels issue fewer instructions than the weights assume",
-                         "issue_frac": ifrac, "issue_frac_per_kernel": iper,
-                         "issue_frac_kind": "measured: rocprofv3 VALUBusy (SQ_ACTIVE_INST_VALU x 4 / "
-                                            "SIMD-cycles), time-weighted over the sign kernels "
-                                            "profiled serially; the VALU-bound kernels' roofline",
-                         "issue_source": isrc,
-                         "issue_source_head": profile_stamp(os.path.join(ROOT, isrc))[0] if isrc else None,
-                         "issue_source_fresh": profile_stamp(os.path.join(ROOT, isrc))[1] if isrc else False,
-                         "traffic": pmc_traffic(),
+                                      "the kernels issue fewer instructions than the weights assume, so it "
+                                      "is not a physical fraction -- issue_frac is",
+                         "issue_frac": None if issue is None else issue["call"],
+                         "issue_frac_kind": "measured live on this GPU: the call's issue-bound time "
+                                            "(chunks x (pass-1 ceiling + pass-2 ceiling + epilogue), "
+                                            "dcor_diag_sign_pass 11/12/3: each pass's own instruction "
+                                            "stream with its memory side removed, at its occupancy) "
+                                            "over the call's kernel time",
+                         "issue": issue,
+                         "traffic": traffic,
                          "traffic_source": os.path.relpath(_profile("headline"), ROOT) if _profile("headline") else None,
                          "traffic_source_head": profile_stamp(_profile("headline"))[0] if _profile("headline") else None,
                          "traffic_source_fresh": profile_stamp(_profile("headline"))[1] if _profile("headline") else False,
@@ -288,6 +374,27 @@ def main():
         if cpu is not None:
             res["cpu_baseline"] = cpu
         print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def dry_run(world: int, rank: int) -> None:
+    """The launcher without a GPU: the ranks form a gloo group on the CPU, all-gather one
+    accumulator pair each and merge them in rank order -- the bench's only collective -- and rank 0
+    prints the world size formed (no value: nothing is measured)."""
+    import torch.distributed as dist
+
+    from dcor import _lib
+    from dcor.dist import gather_accums, merge_ranked
+    if world > 1:
+        dist.init_process_group("gloo")
+    formed = dist.get_world_size() if world > 1 else 1
+    mine = [_lib.Accum(), _lib.Accum()]
+    mine[0].n = rank + 1
+    merged = merge_ranked(gather_accums(mine)) if world > 1 else mine
+    if rank == 0:
+        print(json.dumps({"dry_run": True, "metric": METRIC, "value": None, "n_gpus": formed,
+                          "world_formed": formed, "merged_n": merged[0].n}), flush=True)
     if world > 1:
         dist.destroy_process_group()
 

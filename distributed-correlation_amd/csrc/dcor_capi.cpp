@@ -323,6 +323,9 @@ int make_subg(int64_t n, double eps1, double eps2, double eta1, double eta2, dou
 // worker threads release theirs when they finish.
 std::mutex g_ctx_mu;
 std::vector<Ctx*> g_ctxs;            // every live context (guarded by g_ctx_mu)
+// Bytes held by every live context's arenas (dcor_device_bytes): updated where an arena grows or
+// is freed, so a reader needs no access to another thread's context.
+std::atomic<int64_t> g_device_bytes{0};
 std::atomic<uint64_t> g_ctx_gen{1};  // bumped by dcor_shutdown: older thread caches are stale
 struct ThreadCtx { Ctx* c[64] = {}; uint64_t gen = 0; };
 thread_local ThreadCtx t_ctx;
@@ -342,7 +345,10 @@ void ctx_free(Ctx* c) {
   }
   if (c->work) { (void)hipStreamSynchronize(c->work); (void)hipStreamDestroy(c->work); }
   for (Arena* a : {&c->codes, &c->rs, &c->grid, &c->gpart, &c->out, &c->rsj})
-    if (a->p) (void)hipFree(a->p);
+    if (a->p) {
+      (void)hipFree(a->p);
+      g_device_bytes.fetch_sub((int64_t)a->bytes);
+    }
   delete c;
 }
 
@@ -396,7 +402,13 @@ void count_alloc() { g_alloc_count.fetch_add(1); }
 int arena_grow(Arena& a, size_t bytes, void** out) {
   if (a.bytes < bytes) {
     // the old block may still be read by work queued earlier: wait for the device
-    if (a.p) { HIPCHK(hipDeviceSynchronize()); HIPCHK(hipFree(a.p)); a.p = nullptr; a.bytes = 0; }
+    if (a.p) {
+      HIPCHK(hipDeviceSynchronize());
+      HIPCHK(hipFree(a.p));
+      g_device_bytes.fetch_sub((int64_t)a.bytes);
+      a.p = nullptr;
+      a.bytes = 0;
+    }
     if (hipMalloc(&a.p, bytes) != hipSuccess) {
       (void)hipGetLastError();
       a.p = nullptr;
@@ -404,6 +416,7 @@ int arena_grow(Arena& a, size_t bytes, void** out) {
     }
     count_alloc();
     a.bytes = bytes;
+    g_device_bytes.fetch_add((int64_t)bytes);
   }
   *out = a.p;
   return DCOR_OK;
@@ -428,10 +441,15 @@ int pinned_grow(Pinned& b, size_t bytes, void** out) {
   return DCOR_OK;
 }
 
+int codes_arena(Ctx* c, size_t bytes, void** out) {
+  c->pipe.sig = 0;
+  return arena_grow(c->codes, bytes, out);
+}
+
 int arena_get(size_t bytes, void** out) {
   Ctx* c = nullptr;
   if (int st = ctx_get(&c)) return st;
-  return arena_grow(c->codes, bytes, out);
+  return codes_arena(c, bytes, out);
 }
 
 int rs_arena_get(size_t bytes, void** out) {
@@ -447,9 +465,9 @@ int rsj_polys(int n, const uint32_t** poff, const uint32_t** pidx) {
   Ctx* c = nullptr;
   if (int st = ctx_get(&c)) return st;
   if (c->rsj_npoly < n) {
-    const uint64_t* table = nullptr;
+    std::vector<uint64_t> table;
     int words = 0;
-    if (int st = mt_segment_polys(RSJ_L, n, &table, &words)) return st;
+    if (int st = mt_segment_polys(RSJ_L, n, table, &words)) return st;
     if (words != RSJ_PW) return fail(DCOR_EINVAL, "jump polynomial width %d", words);
     const size_t head = (size_t)(n + 1 + 3) / 4 * 4;
     std::vector<uint32_t> buf(head, 0u);
@@ -669,10 +687,7 @@ int dcor_sim_launch(const dcor_cell* cell, int64_t rep_begin, int64_t rep_count,
       if (chunk > rep_count) chunk = rep_count;
       const size_t plane_bytes = ((size_t)chunk * (per_rep - 64) + 255) / 256 * 256;
       void* scratch = nullptr;
-      if (int st = arena_get(plane_bytes + (size_t)chunk * 64, &scratch)) return st;
-      Ctx* cx = nullptr;
-      if (int st = ctx_get(&cx)) return st;
-      cx->pipe.sig = 0;  // the codes arena's last user is now the caller's stream
+      if (int st = arena_get(plane_bytes + (size_t)chunk * 64, &scratch)) return st;  // clears pipe.sig
       rc = launch_sign_bern(k, rep_count, chunk, (uint64_t*)scratch,
                             (SignPartial*)((char*)scratch + plane_bytes), d_out, stream);
     } else if ((cp.kind != GK_SIGN_CODES && cp.kind != GK_SIGN_CODES_W) || rep_count == 0) {
@@ -692,6 +707,10 @@ int dcor_sim_launch(const dcor_cell* cell, int64_t rep_begin, int64_t rep_count,
       const size_t slab_b = ((size_t)chunk * per_rep + 255) / 256 * 256;
       const size_t sums_b = ((size_t)chunk * (8 * sizeof(double) + 48) + 255) / 256 * 256;
       const int nbuf = nch > 1 ? 2 : 1;
+      Ctx* cx = nullptr;
+      if (int st = ctx_get(&cx)) return st;
+      // the layout of the arena's last user, if that was this path (any other user cleared it)
+      const uint64_t prev_sig = cx->pipe.sig;
       void* scratch = nullptr;
       if (int st = arena_get(nbuf * (slab_b + sums_b), &scratch)) return st;
       CodesBufs bf;
@@ -715,7 +734,7 @@ int dcor_sim_launch(const dcor_cell* cell, int64_t rep_begin, int64_t rep_count,
         const uint64_t sig = ((uint64_t)(uintptr_t)scratch * 1000003u) ^ ((uint64_t)slab_b * 31u) ^
                              ((uint64_t)sums_b << 1) ^ 1u;
         const char* xv = std::getenv("DCOR_SIGN_XCALL");
-        bf.cross = sig == pp->sig && !(xv && std::strcmp(xv, "0") == 0);
+        bf.cross = sig == prev_sig && !(xv && std::strcmp(xv, "0") == 0);
         pp->sig = sig;
       } else {
         pp->sig = 0;
@@ -724,6 +743,49 @@ int dcor_sim_launch(const dcor_cell* cell, int64_t rep_begin, int64_t rep_count,
     }
   }
   if (rc) return hip_fail((hipError_t)rc, "sim kernel launch");
+  return DCOR_OK;
+}
+
+int dcor_diag_sign_pass(const dcor_cell* cell, int64_t rep_begin, int64_t reps, int which, void* stream) {
+  if (!cell || reps < 1 || reps > 65535 || rep_begin < 0 || rep_begin + reps > 0xffffffffLL)
+    return fail(DCOR_EINVAL, "diag_sign_pass: bad arguments");
+  if (which != 1 && which != 2 && which != 3 && which != 11 && which != 12 && which != 13)
+    return fail(DCOR_EINVAL, "diag_sign_pass: which must be 1, 2, 3, 11, 12 or 13");
+  if (int st = need_device()) return st;
+  CellPlan cp;
+  if (int st = prepare_cell(*cell, cp)) return st;
+  if (cp.kind != GK_SIGN_CODES || cp.nan_dgp)
+    return fail(DCOR_EINVAL, "diag_sign_pass: the cell does not run the one-pass sign kernels");
+  if (which > 10 && (cp.dgp != DCOR_DGP_GAUSSIAN || cp.sign.m != 8))
+    return fail(DCOR_EINVAL, "diag_sign_pass: the ceilings run the Gaussian DGP at m = 8");
+  SignConst k = cp.sign;
+  k.rep_begin = rep_begin;
+  const size_t slab_b = ((size_t)reps * (size_t)cell->n * sizeof(uint32_t) + 255) / 256 * 256;
+  const size_t sums_b = ((size_t)reps * SIGN_SUMS * sizeof(double) + 255) / 256 * 256;
+  const size_t part_b = ((size_t)reps * SIGN_PARTIAL_BYTES + 255) / 256 * 256;
+  void* scratch = nullptr;
+  if (int st = arena_get(slab_b + sums_b + part_b + (size_t)reps * sizeof(dcor_rep_out), &scratch)) return st;
+  char* b = (char*)scratch;
+  const int rc = launch_sign_diag(k, reps, which, (uint32_t*)b, (double*)(b + slab_b), b + slab_b + sums_b,
+                                  (dcor_rep_out*)(b + slab_b + sums_b + part_b), stream);
+  if (rc) return hip_fail((hipError_t)rc, "diag_sign_pass launch");
+  return DCOR_OK;
+}
+
+int dcor_diag_sign_ties(const dcor_cell* cell, int64_t rep_begin, int64_t reps, int64_t* h_ties) {
+  if (!h_ties) return fail(DCOR_EINVAL, "diag_sign_ties: null output");
+  if (int st = dcor_diag_sign_pass(cell, rep_begin, reps, 1, nullptr)) return st;
+  if (int st = dcor_diag_sign_pass(cell, rep_begin, reps, 2, nullptr)) return st;
+  void* scratch = nullptr;
+  if (int st = arena_get(0, &scratch)) return st;   // the same arena dcor_diag_sign_pass used
+  const size_t slab_b = ((size_t)reps * (size_t)cell->n * sizeof(uint32_t) + 255) / 256 * 256;
+  const size_t sums_b = ((size_t)reps * SIGN_SUMS * sizeof(double) + 255) / 256 * 256;
+  std::vector<long long> part((size_t)reps * SIGN_PARTIAL_BYTES / sizeof(long long));
+  HIPCHK(hipDeviceSynchronize());
+  HIPCHK(hipMemcpy(part.data(), (char*)scratch + slab_b + sums_b, (size_t)reps * SIGN_PARTIAL_BYTES,
+                   hipMemcpyDeviceToHost));
+  const size_t words = SIGN_PARTIAL_BYTES / sizeof(long long);
+  for (int64_t r = 0; r < reps; ++r) h_ties[r] = part[(size_t)r * words + words - 1] >> 8;
   return DCOR_OK;
 }
 
@@ -1298,13 +1360,7 @@ int dcor_perm_launch(uint64_t seed, int site, int64_t rep_begin, int64_t reps, i
 
 int64_t dcor_alloc_count(void) { return g_alloc_count.load(); }
 
-int64_t dcor_device_bytes(void) {
-  std::lock_guard<std::mutex> lk(g_ctx_mu);
-  int64_t b = 0;
-  for (const Ctx* c : g_ctxs)
-    for (const Arena* a : {&c->codes, &c->rs, &c->grid, &c->gpart, &c->out, &c->rsj}) b += (int64_t)a->bytes;
-  return b;
-}
+int64_t dcor_device_bytes(void) { return g_device_bytes.load(); }
 
 int dcor_shutdown(void) {
   const int owner = g_owner_pid.load();
@@ -1316,6 +1372,7 @@ int dcor_shutdown(void) {
     std::lock_guard<std::mutex> lk(g_ctx_mu);
     g_ctxs.clear();
     g_ctx_gen.fetch_add(1);
+    g_device_bytes.store(0);
     return fork_guard();
   }
   grid_workers_stop(false);   // idle workers first: their contexts are freed below

@@ -139,6 +139,9 @@ struct CodesBufs {
 };
 int launch_sign_fused_codes(const SignConst& c, int64_t reps, int64_t chunk, const CodesBufs& bf,
                             dcor_rep_out* out, void* stream);
+// One pass of the one-pass sign path as a single chunk (dcor_diag_sign_pass).
+int launch_sign_diag(const SignConst& c, int64_t reps, int which, uint32_t* slab, double* sums,
+                     void* part, dcor_rep_out* out, void* stream);
 int launch_subg_fused(const SubgConst& c, int64_t reps, dcor_rep_out* out, void* stream);
 int launch_dgp(const DgpConst& g, uint32_t k0, uint32_t k1, int64_t rep_begin, int64_t reps,
                int64_t n, double* X, double* Y, void* stream);

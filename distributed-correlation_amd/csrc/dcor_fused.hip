@@ -366,7 +366,11 @@ __device__ __forceinline__ void exact_signs(const SignConst& c, const SignStd& s
 // WAVE = false: one 256-thread workgroup per replicate; WAVE = true: one wave per replicate (the
 // caller's workgroup has loaded the ziggurat table `zt` into LDS once for all its replicates).
 // zq / zqn: the calling wave's slow-normal queue and its counter (LDS).
-template <int DGP, bool WAVE>
+// CEIL (Gaussian only; a measurement kernel, never a result): the same hot loop with its memory
+// side removed -- no slab store, no slow-normal queue or drain; an empty asm consumes the records
+// and the pending mask, so the compiler keeps every instruction that computes them.  Its time is
+// the loop's own VALU-issue ceiling (dcor_diag_sign_pass, bench.py roofline.issue_frac).
+template <int DGP, bool WAVE, bool CEIL = false>
 __device__ __forceinline__ void sign_pass1_core(const SignConst& c, uint32_t rep,
                                                 uint32_t* __restrict__ slab,
                                                 double* __restrict__ sums_out, const double2* zt,
@@ -420,6 +424,10 @@ __device__ __forceinline__ void sign_pass1_core(const SignConst& c, uint32_t rep
       }
       ks_acc(sx, gx);
       ks_acc(sy, gy);
+      if constexpr (CEIL) {
+        asm volatile("" ::"v"(rec[0]), "v"(rec[1]), "v"(rec[2]), "v"(rec[3]), "v"(pend));
+        return;
+      }
       if (FULL) {
         *reinterpret_cast<uint4*>(slab + i0) = make_uint4(rec[0], rec[1], rec[2], rec[3]);
       } else {
@@ -432,6 +440,7 @@ __device__ __forceinline__ void sign_pass1_core(const SignConst& c, uint32_t rep
     };
     // the whole wave, converged: each lane takes queued samples lane, lane + 64, ...
     auto drain = [&]() {
+      if constexpr (CEIL) return;
       const uint32_t cnt = __builtin_amdgcn_readfirstlane(*zqn);
       if (cnt == 0) return;
       __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the placeholder records have landed
@@ -455,11 +464,12 @@ __device__ __forceinline__ void sign_pass1_core(const SignConst& c, uint32_t rep
     };
     for (int64_t b = WAVE ? 0 : 64 * wv; b < nfull; b += NT) {  // trip count uniform per wave
       if (b + lane < nfull) group(b + lane, std::true_type());
-      if (__builtin_amdgcn_readfirstlane(*zqn) > ZQ_CAP - 256) drain();
+      if (!CEIL && __builtin_amdgcn_readfirstlane(*zqn) > ZQ_CAP - 256) drain();
     }
     if ((c.n & 3) && tid == (int)(nfull % NT)) group(nfull, std::false_type());
     drain();
   } else {
+    static_assert(!CEIL, "the ceiling kernel runs the Gaussian loop");
     // group g4 = samples 4 g4 .. 4 g4 + 3; FULL: all four exist (the hot loop has no guards)
     auto group = [&](int64_t g4, auto full_tag) {
       constexpr bool FULL = decltype(full_tag)::value;
@@ -510,7 +520,7 @@ __device__ __forceinline__ void sign_pass1_core(const SignConst& c, uint32_t rep
   }
 }
 
-template <int DGP>
+template <int DGP, bool CEIL = false>
 __device__ __forceinline__ void sign_pass1_body(const SignConst& c, uint32_t rep,
                                                 uint32_t* __restrict__ slab,
                                                 double* __restrict__ sums_out) {
@@ -523,7 +533,7 @@ __device__ __forceinline__ void sign_pass1_body(const SignConst& c, uint32_t rep
       zt[e] = make_double2(dcor_zig_tab[e][0], dcor_zig_tab[e][1]);
     if (tid < DCOR_WAVES) zqn[tid] = 0u;
     __syncthreads();
-    sign_pass1_core<DGP, false>(c, rep, slab, sums_out, zt, zq[wv], &zqn[wv]);
+    sign_pass1_core<DGP, false, CEIL>(c, rep, slab, sums_out, zt, zq[wv], &zqn[wv]);
   } else {
     sign_pass1_core<DGP, false>(c, rep, slab, sums_out, nullptr, nullptr, nullptr);
   }
@@ -543,6 +553,12 @@ __global__ __launch_bounds__(DCOR_BLOCK, DCOR_P1_WPE) void k_sign_pass1(SignCons
   sign_pass1_body<DGP>(c, (uint32_t)(c.rep_begin + blockIdx.x),
                        scratch + (size_t)blockIdx.x * (size_t)c.n, sums + SIGN_SUMS * (size_t)blockIdx.x);
 }
+// The pass-1 ceiling (CEIL above): same grid, registers and occupancy target as k_sign_pass1.
+__global__ __launch_bounds__(DCOR_BLOCK, DCOR_P1_WPE) void k_sign_pass1_ceil(SignConst c,
+                                                                         double* __restrict__ sums) {
+  sign_pass1_body<DCOR_DGP_GAUSSIAN, true>(c, (uint32_t)(c.rep_begin + blockIdx.x), nullptr,
+                                           sums + SIGN_SUMS * (size_t)blockIdx.x);
+}
 
 // The private centres and scales from pass 1's sums (vert-cor.R:335-344): mean(xc) is the
 // double-double sum divided by n, rounded once.
@@ -557,7 +573,7 @@ __device__ __forceinline__ void sign_std_from_pass1(const SignConst& c, const do
 struct SignPartial {
   double sT[2], sT2[2];  // double-double sum of T_j and T_j^2 (vert-cor.R:233-239)
   long long core;        // sum of (2S-1) sign(X) sign(Y) (vert-cor.R:178-183)
-  long long flags;       // bit 0: NI saw NaN, bit 1: INT saw NaN
+  long long flags;       // bit 0: NI saw NaN, bit 1: INT saw NaN; bits 8-: tie batches (k_sign_pass2)
 };
 static_assert(sizeof(SignPartial) == SIGN_PARTIAL_BYTES, "dcor_engine.h SIGN_PARTIAL_BYTES");
 
@@ -569,6 +585,7 @@ struct P2Result {
   long long core;
   bool bad_ni, bad_int;
   double lapz;   // SITE_SCALAR block 4's first draw: the INT estimate's Z (vert-cor.R:188)
+  long long ties;  // NI batches that took the exact fix-up (workgroup form only; 0 in the wave form)
 };
 
 // The 10 SITE_SCALAR draws of one replicate in every lane of a wave (lanes 0-4 draw, shuffles).
@@ -590,7 +607,11 @@ __device__ __forceinline__ void scalar_laplace_wave(uint32_t rep, uint32_t k0, u
 
 // WAVE = false: one 256-thread workgroup per replicate (barriers, LDS reductions); WAVE = true:
 // one wave per replicate (wave reductions only) -- the same arithmetic per batch and sample.
-template <int DGP, bool WAVE>
+// CEIL (m = 8 only; a measurement kernel, never a result): the decision loop with each thread's
+// first two batches' records loaded once and then held in registers (an empty asm redefines them
+// every step, so nothing is hoisted), and no tie fix-up (1e-4 of samples): the loop's own
+// VALU-issue ceiling without the slab stream (dcor_diag_sign_pass, bench.py roofline.issue_frac).
+template <int DGP, bool WAVE, bool CEIL = false>
 __device__ __forceinline__ P2Result sign_pass2_core(const SignConst& c, uint32_t rep,
                                                     const uint32_t* __restrict__ slab,
                                                     const double* __restrict__ sums_in,
@@ -626,6 +647,7 @@ __device__ __forceinline__ P2Result sign_pass2_core(const SignConst& c, uint32_t
   bool bad_ni = thr_nan, bad_int = thr_nan;
   DD sT{0.0, 0.0}, sT2{0.0, 0.0};
   long long core = 0;
+  int ties = 0;   // batches whose codes tie a threshold (diagnostic: dcor_diag_sign_ties)
   // Fast path: signs from codes (branch-free).  A sample whose code ties a threshold's
   // code is flagged and fixed up afterwards by exact regeneration (rolled loop, rare).
   // sign(xc - mu) from codes: sgnd in {-1, 0, 1}; 0 is a tie (the code cannot decide).
@@ -713,7 +735,14 @@ __device__ __forceinline__ P2Result sign_pass2_core(const SignConst& c, uint32_t
       cx = 8 - 2 * (int)(neg & 0xffffu);
       cy = 8 - 2 * (int)(neg >> 16);
       cc = 2 * __popc(par) - 8;
+      if constexpr (CEIL) {
+        uint32_t tie = has_zero16(mn) || force_exact;
+        asm volatile("" : "+v"(tie));
+        cc += (int)tie;
+        return;
+      }
       if (has_zero16(mn) || force_exact) {
+        ++ties;
 #pragma unroll 1
         for (int q = 0; q < 8; ++q)  // re-read the record (L2-hot): no dynamically indexed registers
           fix_fast(8 * j + q, slab[8 * j + q], cx, cy, cc);
@@ -724,15 +753,22 @@ __device__ __forceinline__ P2Result sign_pass2_core(const SignConst& c, uint32_t
     // 2 NT is issued into j's registers, then j + NT is decided.  Batch j + NT is computed even past
     // the last batch (on the last batch's records) and dropped, so the body has no branch the
     // compiler could merge the two copies across.  Loads past the end re-read the last batch.
-    auto load = [&](int64_t jj, uint4& lo, uint4& hi) {
+    auto load_mem = [&](int64_t jj, uint4& lo, uint4& hi) {
       const int64_t jc = jj < c.k ? jj : c.k - 1;
       lo = *reinterpret_cast<const uint4*>(slab + 8 * jc);
       hi = *reinterpret_cast<const uint4*>(slab + 8 * jc + 4);
     };
+    auto load = [&](int64_t jj, uint4& lo, uint4& hi) {
+      if constexpr (CEIL)
+        asm volatile("" : "+v"(lo.x), "+v"(lo.y), "+v"(lo.z), "+v"(lo.w), "+v"(hi.x), "+v"(hi.y),
+                     "+v"(hi.z), "+v"(hi.w));
+      else
+        load_mem(jj, lo, hi);
+    };
     if (c.k > 0) {
       uint4 a0, a1, b0, b1;
-      load(tid, a0, a1);
-      load(tid + NT, b0, b1);
+      load_mem(tid, a0, a1);
+      load_mem(tid + NT, b0, b1);
       for (int64_t j = tid; j < c.k; j += 2 * NT) {
         const bool vb = j + NT < c.k;
         const int64_t jb = vb ? j + NT : c.k - 1;
@@ -748,7 +784,7 @@ __device__ __forceinline__ P2Result sign_pass2_core(const SignConst& c, uint32_t
         batch_T_if(jb, cxb, cyb, vb);
       }
     }
-  } else {
+  } else if constexpr (!CEIL) {
     // any other m < 32768 (the reference grids' 11, 32, 200): the same packed decisions, four records
     // per 16-B load when batches start on 16-B boundaries (m % 4 == 0), the counts per batch
     if (c.m < 32768) {
@@ -775,6 +811,7 @@ __device__ __forceinline__ P2Result sign_pass2_core(const SignConst& c, uint32_t
         int cx = c.m - 2 * (int)(neg & 0xffffu), cy = c.m - 2 * (int)(neg >> 16);
         int cc = 2 * (int)pc - c.m;
         if (has_zero16(mn) || force_exact) {
+          ++ties;
 #pragma unroll 1
           for (int r = 0; r < c.m; ++r) fix_fast(i0 + r, slab[i0 + r], cx, cy, cc);
         }
@@ -798,7 +835,7 @@ __device__ __forceinline__ P2Result sign_pass2_core(const SignConst& c, uint32_t
       batch_T(j, cx, cy, std::false_type());
     }
   }
-  for (int64_t i = c.k * c.m + tid; i < c.n; i += NT) {  // tail: INT only
+  for (int64_t i = c.k * c.m + tid; !CEIL && i < c.n; i += NT) {  // tail: INT only
     int dx = 0, dy = 0, cc = 0;
     bool ignore = false;  // NI never reads the tail
     const uint32_t w = slab[i];
@@ -807,6 +844,7 @@ __device__ __forceinline__ P2Result sign_pass2_core(const SignConst& c, uint32_t
   }
   P2Result r;
   r.lapz = lap[8];
+  r.ties = 0;
   if constexpr (WAVE) {
     r.sT = wave_sum_dd(sT);
     r.sT2 = wave_sum_dd(sT2);
@@ -821,14 +859,16 @@ __device__ __forceinline__ P2Result sign_pass2_core(const SignConst& c, uint32_t
     r.sT = d2[0];
     r.sT2 = d2[1];
     r.core = block_sum_i(core, redi);
-    const long long nbad = block_sum_i((bad_ni ? 1LL : 0LL) + (bad_int ? (1LL << 20) : 0LL), redi);
+    const long long nbad = block_sum_i((bad_ni ? 1LL : 0LL) + (bad_int ? (1LL << 20) : 0LL) +
+                                       ((long long)ties << 40), redi);
     r.bad_ni = (nbad & 0xFFFFF) != 0;
-    r.bad_int = (nbad >> 20) != 0;
+    r.bad_int = ((nbad >> 20) & 0xFFFFF) != 0;
+    r.ties = nbad >> 40;
   }
   return r;
 }
 
-template <int DGP>
+template <int DGP, bool CEIL = false>
 __device__ __forceinline__ void sign_pass2_body(const SignConst& c, uint32_t rep,
                                                 const uint32_t* __restrict__ slab,
                                                 const double* __restrict__ sums_in,
@@ -836,12 +876,12 @@ __device__ __forceinline__ void sign_pass2_body(const SignConst& c, uint32_t rep
   __shared__ double2 lt[256];
   log_tab_to_lds(lt, DCOR_BLOCK);
   __syncthreads();
-  const P2Result r = sign_pass2_core<DGP, false>(c, rep, slab, sums_in, lt);
+  const P2Result r = sign_pass2_core<DGP, false, CEIL>(c, rep, slab, sums_in, lt);
   if (threadIdx.x == 0) {
     SignPartial p;
     p.sT[0] = r.sT.hi; p.sT[1] = r.sT.lo; p.sT2[0] = r.sT2.hi; p.sT2[1] = r.sT2.lo;
     p.core = r.core;
-    p.flags = (r.bad_ni ? 1 : 0) | (r.bad_int ? 2 : 0);
+    p.flags = (r.bad_ni ? 1 : 0) | (r.bad_int ? 2 : 0) | (r.ties << 8);
     *part_out = p;
   }
 }
@@ -856,6 +896,15 @@ __global__ __launch_bounds__(DCOR_BLOCK, DCOR_P2_WPE) void k_sign_pass2(SignCons
   sign_pass2_body<DGP>(c, (uint32_t)(c.rep_begin + blockIdx.x),
                        scratch + (size_t)blockIdx.x * (size_t)c.n,
                        sums + SIGN_SUMS * (size_t)blockIdx.x, part + blockIdx.x);
+}
+// The pass-2 ceiling (CEIL above, m = 8): same grid, registers and occupancy target as k_sign_pass2.
+__global__ __launch_bounds__(DCOR_BLOCK, DCOR_P2_WPE) void k_sign_pass2_ceil(SignConst c,
+                                                                         const uint32_t* __restrict__ scratch,
+                                                                         const double* __restrict__ sums,
+                                                                         SignPartial* __restrict__ part) {
+  sign_pass2_body<DCOR_DGP_GAUSSIAN, true>(c, (uint32_t)(c.rep_begin + blockIdx.x),
+                                           scratch + (size_t)blockIdx.x * (size_t)c.n,
+                                           sums + SIGN_SUMS * (size_t)blockIdx.x, part + blockIdx.x);
 }
 
 // The INT side and the record of one replicate from its pass-2 result, one wave: NI estimate/CI,
@@ -941,7 +990,7 @@ __device__ __forceinline__ void sign_pass2_wave_part(const SignConst& c, uint32_
     SignPartial p;
     p.sT[0] = r.sT.hi; p.sT[1] = r.sT.lo; p.sT2[0] = r.sT2.hi; p.sT2[1] = r.sT2.lo;
     p.core = r.core;
-    p.flags = (r.bad_ni ? 1 : 0) | (r.bad_int ? 2 : 0);
+    p.flags = (r.bad_ni ? 1 : 0) | (r.bad_int ? 2 : 0) | (r.ties << 8);
     *part_out = p;
   }
 }
@@ -1912,6 +1961,54 @@ int launch_sign_fused_codes(const SignConst& c, int64_t reps, int64_t chunk, con
     case DCOR_DGP_MIX_GAUSSIAN: return launch_codes_t<DCOR_DGP_MIX_GAUSSIAN>(c, reps, chunk, bf, out, stream);
     default: return launch_codes_t<DCOR_DGP_BOUNDED_FACTOR>(c, reps, chunk, bf, out, stream);
   }
+}
+
+// One pass of the one-pass sign path over `reps` replicates as a single chunk on `stream`, for
+// timing (dcor_diag_sign_pass): 1 pass 1, 2 pass 2, 3 the epilogue; 11 / 12 the pass-1 / pass-2
+// ceilings (Gaussian DGP, m = 8) at the real passes' occupancy, 13 the pass-1 ceiling at its own.  slab / sums / part / out as launch_codes_t lays them out.
+int launch_sign_diag(const SignConst& c, int64_t reps, int which, uint32_t* slab, double* sums,
+                     void* part_v, dcor_rep_out* out, void* stream) {
+  if (reps <= 0) return 0;
+  SignPartial* part = reinterpret_cast<SignPartial*>(part_v);
+  const hipStream_t st = (hipStream_t)stream;
+  const dim3 g((unsigned)reps), b(DCOR_BLOCK);
+  switch (which) {
+    case 1:
+      switch (c.g.dgp) {
+        case DCOR_DGP_GAUSSIAN: hipLaunchKernelGGL(k_sign_pass1<DCOR_DGP_GAUSSIAN>, g, b, 0, st, c, slab, sums); break;
+        case DCOR_DGP_MIX_GAUSSIAN: hipLaunchKernelGGL(k_sign_pass1<DCOR_DGP_MIX_GAUSSIAN>, g, b, 0, st, c, slab, sums); break;
+        default: hipLaunchKernelGGL(k_sign_pass1<DCOR_DGP_BOUNDED_FACTOR>, g, b, 0, st, c, slab, sums);
+      }
+      break;
+    case 2:
+      switch (c.g.dgp) {
+        case DCOR_DGP_GAUSSIAN: hipLaunchKernelGGL(k_sign_pass2<DCOR_DGP_GAUSSIAN>, g, b, 0, st, c, slab, sums, part); break;
+        case DCOR_DGP_MIX_GAUSSIAN: hipLaunchKernelGGL(k_sign_pass2<DCOR_DGP_MIX_GAUSSIAN>, g, b, 0, st, c, slab, sums, part); break;
+        default: hipLaunchKernelGGL(k_sign_pass2<DCOR_DGP_BOUNDED_FACTOR>, g, b, 0, st, c, slab, sums, part);
+      }
+      break;
+    case 3: launch_sign_epilogue(c, reps, part, out, st); break;
+    case 11: case 13: {
+      // 11: at pass 1's occupancy (pass 1 holds more VGPRs and LDS than its ceiling: pad the
+      // ceiling's LDS until no more of its workgroups fit per CU than of pass 1's); 13: its own
+      size_t pad = 0;
+      if (which == 11) {
+        int want = 0, have = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&want, k_sign_pass1<DCOR_DGP_GAUSSIAN>, DCOR_BLOCK, 0) != hipSuccess)
+          return last_err();
+        for (;; pad += 256) {
+          if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&have, k_sign_pass1_ceil, DCOR_BLOCK, pad) != hipSuccess)
+            return last_err();
+          if (have <= want || pad > 64 * 1024) break;
+        }
+      }
+      hipLaunchKernelGGL(k_sign_pass1_ceil, g, b, pad, st, c, sums);
+      break;
+    }
+    case 12: hipLaunchKernelGGL(k_sign_pass2_ceil, g, b, 0, st, c, slab, sums, part); break;
+    default: return (int)hipErrorInvalidValue;
+  }
+  return last_err();
 }
 
 int launch_sign_bern(SignConst c, int64_t reps, int64_t chunk, uint64_t* scratch,

@@ -226,7 +226,7 @@ int exec_ranges(const dcor_cell* cells, const std::vector<CellPlan>& cp, const s
   void* scr = nullptr;
   const size_t slab_one = al256(max_scr_b);
   if (max_scr_b > 0)
-    if (int st = arena_grow(ctx->codes, (size_t)nslot * slab_one, &scr)) return st;
+    if (int st = codes_arena(ctx, (size_t)nslot * slab_one, &scr)) return st;
   // ---- upload through a pinned staging slot (its previous upload finished long ago in steady
   // state: the slots alternate, and each synchronous call ends with a stream sync)
   Pinned& stg = ctx->stage[ctx->stage_next];
@@ -529,6 +529,10 @@ struct Worker {
   }
 };
 std::mutex g_workers_mu;
+// Held across the whole worker section of dcor_grid_run_multi: a worker holds one job at a time,
+// so two host threads running multi-device grids at once take turns (each still runs its shards in
+// parallel over its devices) instead of overwriting each other's jobs.
+std::mutex g_multi_mu;
 std::map<std::pair<int, int>, Worker*>* g_workers = new std::map<std::pair<int, int>, Worker*>();
 int g_workers_pid = 0;
 
@@ -601,6 +605,7 @@ int dcor_grid_run_multi(const dcor_cell* cells, int ncells, int64_t B, const int
     (void)hipSetDevice(cur);
     if (s.status) return s.status;
   } else {       // one persistent worker per (device, listing): several may share a device
+    std::lock_guard<std::mutex> run_lk(g_multi_mu);
     std::map<int, int> seen;
     std::vector<Worker*> ws;
     for (int g = 0; g < G; ++g) {

@@ -6,6 +6,7 @@
 
 #include <cstddef>
 #include <cstdint>
+#include <vector>
 
 #include "../../include/dcor.h"
 #include "dcor_engine.h"
@@ -62,6 +63,10 @@ void ctx_release_thread();       // free every context of the calling thread
 int pipe_get(Pipe** out);
 // Device arena of at least `bytes` (grows, never shrinks; counted by dcor_alloc_count()).
 int arena_grow(Arena& a, size_t bytes, void** out);
+// The codes arena of `c`: every user but the one-pass sign path's pipelined chunks hands it to
+// kernels on the caller's stream, so taking it clears the pipe signature (the next sign call then
+// orders its library streams after the caller's stream instead of overlapping this user's work).
+int codes_arena(Ctx* c, size_t bytes, void** out);
 // Pinned host buffer of at least `bytes`, after its previous copy finished (counted likewise).
 int pinned_grow(Pinned& b, size_t bytes, void** out);
 void count_alloc();
@@ -70,9 +75,9 @@ void grid_workers_stop(bool forked);              // one more device or pinned a
 
 // MT19937 jump-ahead (dcor_mtjump.cpp): the degree of the characteristic polynomial found by
 // Berlekamp-Massey (19937); the cached table of nseg polynomials x^((s + 1) L - 624) mod phi,
-// words 64-bit words each; the host-side jumped window (test reference).
+// words 64-bit words each (copied into `table`); the host-side jumped window (test reference).
 int mt_charpoly_degree();
-int mt_segment_polys(int64_t L, int nseg, const uint64_t** table, int* words);
+int mt_segment_polys(int64_t L, int nseg, std::vector<uint64_t>& table, int* words);
 int mt_jump_window(int32_t seed, int64_t J, uint32_t out[624]);
 
 // All constants of one fused cell and the kernel family that runs it.

@@ -111,6 +111,20 @@ int dcor_shutdown(void);
 int64_t dcor_alloc_count(void);
 /* Device bytes held by the library's scratch arenas over every live context. */
 int64_t dcor_device_bytes(void);
+/* Measurement only (bench.py's roofline, not part of the reference surface): one pass of the
+ * one-pass sign path (the kernels dcor_sim_launch runs for cells with n > 16384 and
+ * normalise = TRUE) over replicates rep_begin .. rep_begin + reps - 1 as ONE chunk, on `stream`, in
+ * the calling thread's scratch arena.  which: 1 pass 1 (writes the slab and the clipped sums),
+ * 2 pass 2 (reads them), 3 the epilogue (reads pass 2's partials); 11 the pass-1 ceiling and 12 the
+ * pass-2 ceiling (Gaussian DGP, m = 8): the same loops with their memory side removed, at the real
+ * passes' waves per SIMD -- their time is the instruction stream's own issue-bound time on this
+ * GPU; 13 the pass-1 ceiling at its own (higher) occupancy.  Run 1, 2, 3 in that order
+ * on the same cell and reps (12 after 1).  No result is returned; time them with events. */
+int dcor_diag_sign_pass(const dcor_cell* cell, int64_t rep_begin, int64_t reps, int which, void* stream);
+/* Measurement only: passes 1 and 2 (as dcor_diag_sign_pass 1, 2, on the null stream) and, per
+ * replicate, the number of NI batches whose record codes tied a private centre's code and took the
+ * exact regeneration fix-up (the rare path of the one-pass sign kernels) into h_ties[reps]. */
+int dcor_diag_sign_ties(const dcor_cell* cell, int64_t rep_begin, int64_t reps, int64_t* h_ties);
 
 /* ---- calibration scalars (host closed forms) ----------------------------- */
 /* lambda_n, ver-cor-subG.R:1 (= real-data-sims.R:109). */

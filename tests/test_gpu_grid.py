@@ -194,3 +194,33 @@ def test_grid_memory_bounded_in_B(dc, monkeypatch):
     # only the block partials may grow (<= 512 per cell, 2 x 160 B each), never the record buffer
     assert _lib.lib.dcor_device_bytes() - held <= 3 * 512 * 2 * 160
     assert all(r["accum"][0].n == 80_000 for r in res4)
+
+
+def test_two_host_threads_run_multi_concurrently(dc):
+    """dcor_grid_run_multi from two host threads at once, each with two shards on
+    device 0 (persistent workers): every thread's accumulators and records equal its serial run."""
+    from dcor.sim import CellSpec, run_grid
+    grids = [_mixed_cells()[:4],
+             [CellSpec(n=4000, rho=0.3, eps1=1.0, eps2=1.0, family="subG", dgp="bounded_factor", seed=1_000_201),
+              CellSpec(n=6000, rho=-0.5, eps1=1.5, eps2=0.5, mu=(0.5, 0.5), sigma=(2.0, 2.0), seed=1_000_202)]]
+    ref = [run_grid(g, 257, detail=True, devices=[0, 0]) for g in grids]
+    got = [None, None]
+    err = []
+
+    def work(i):
+        try:
+            for _ in range(3):
+                got[i] = run_grid(grids[i], 257, detail=True, devices=[0, 0])
+        except Exception as e:  # noqa: BLE001 -- reported below
+            err.append(e)
+
+    th = [threading.Thread(target=work, args=(i,)) for i in range(2)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not err, err
+    for g, r in zip(got, ref):
+        for a, b in zip(g, r):
+            assert np.array_equal(_bits(a["records"]), _bits(b["records"]))
+            assert [bytes(x) for x in a["accum"]] == [bytes(x) for x in b["accum"]]
