@@ -2,9 +2,9 @@
 
 C1  vert-cor.R sign family n=1000 rho=.5 eps=(1,1), 1000 reps: GPU vs CPU oracle (1 and nproc-1 threads)
 C2  Bernoulli sign-family grid n=1e4, 8 rho x 3 eps, 1e4 reps/cell (fused kernels)
-C3  Gaussian + mixquant grid n=1e6, 8 rho x 3 eps (1e5 reps/cell in the config; --c3-reps here)
+C3  Gaussian + mixquant grid n=1e6, 8 rho x 3 eps, 1e5 reps/cell (the config's size; --c3-reps)
 C4  legacy paper sweep: {sign: gaussian, bernoulli; sub-G: gaussian, bounded factor} x rho {0,.3,.8}
-    x 5 eps pairs x n {200..3200, 1e4, 1e5, 1e6}, B=1000
+    x 5 eps pairs x n {200..3200, 1e4, 1e5, 1e6}, B=1000 (vert-cor.R:40) and 1e5 at n=1e6
 C5  HRS BMI-vs-Age pre-materialised streaming (synthetic stand-in panel n=19,433, eps=2): noise
     generated on device into HBM, then the streaming kernel is timed -> replicates/s and HBM GB/s
 S   sub-G fused, bounded factor, n=1e5, rho=.5, eps=(1,1)
@@ -83,37 +83,22 @@ def run_grid_gpu(cells, B, chunk=1 << 15):
     return acc
 
 
-# config line -> (committed rocprofv3 summary, kernel-name filter of the line's own launches)
-PROFILE_OF = {"VG": ("r03_vg", "k_grid_"), "SG": ("r03_sg", "k_grid_"), "C2": ("r03_c2", "k_grid_"),
-              "C3": ("r03_c3", "k_grid_"), "C5": ("r03_c5", "k_premat_subg_dict"),
-              "C5-continuous": ("r03_c5c", "k_premat_subg_tiled"), "C5-fused": ("r03_c5f", "k_hrs_fused"),
-              "S": ("r03_s", "k_subg_fused")}
+# config line -> its committed rocprofv3 summary (per-kernel times and counters)
+PROFILE_OF = {"VG": "vg", "SG": "sg", "C2": "c2", "C3": "c3", "C5": "c5", "C5-continuous": "c5c",
+              "C5-fused": "c5f", "S": "sg"}
 
 
 def measured(name):
-    """The line's hardware counters from its committed profile (scripts/summarize_prof.py):
-    issue_frac = VALUBusy time-weighted over the line's kernels, the HBM bytes they moved per
-    call (FETCH_SIZE x2 + WRITE_SIZE), and whether the profile was taken on this tree's sources."""
-    from bench import profile_stamp
+    """Where the line's per-kernel counters are (scripts/summarize_prof.py) and whether that
+    profile was taken on this tree's sources."""
+    from bench import _profile, profile_stamp
     if name not in PROFILE_OF:
         return {}
-    tag, filt = PROFILE_OF[name]
-    path = os.path.join(ROOT, "profiles", f"{tag}_summary.json")
-    try:
-        ks = json.load(open(path))["kernels"]
-    except (OSError, ValueError, KeyError):
+    path = _profile(PROFILE_OF[name])
+    if path is None:
         return {}
-    num = den = 0.0
-    per = {}
-    for kname, v in ks.items():
-        if filt in kname and "valu_busy" in v and v.get("avg_ns"):
-            w = v["avg_ns"] * v.get("calls", 1)
-            num += v["valu_busy"] * w
-            den += w
-            per[kname.split("::")[-1]] = round(v["valu_busy"], 3)
     head, fresh = profile_stamp(path)
-    return {"issue_frac": (num / den) if den else None, "issue_frac_per_kernel": per or None,
-            "issue_source": os.path.relpath(path, ROOT), "issue_source_head": head, "issue_source_fresh": fresh}
+    return {"profile": os.path.relpath(path, ROOT), "profile_head": head, "profile_fresh": fresh}
 
 
 def line(name, **kw):
@@ -158,14 +143,14 @@ def c3(reps):
                         mu=(0.5, 0.5), sigma=(2.0, 2.0))
     t = timed(grid_call(cells, reps), reps=1)
     u = grid_units(cells, reps)
-    rps = len(cells) * reps / t
-    line("C3", cells=len(cells), reps_per_cell=reps, seconds=t, reps_per_s=rps,
+    line("C3", cells=len(cells), reps_per_cell=reps, seconds=t, reps_per_s=len(cells) * reps / t,
          roofline_frac=u / t / FP64_PEAK_UNITS,
-         projected_full_config_seconds_1gpu=len(cells) * 1e5 / rps,
-         projected_full_config_seconds_8gpu=len(cells) * 1e5 / rps / 8)
+         note="one dcor_grid_run_multi call on one GPU over every cell's reps_per_cell replicates, measured")
 
 
-def c4(B):
+def c4(B, B_big):
+    """The paper sweep at its stated sizes: B replicates per cell (vert-cor.R:40), B_big for the
+    n = 1e6 cells: two grid calls (one per B), timed together."""
     from dcor.sim import paper_grid
     cells = paper_grid(n_grid=(200, 400, 800, 1600, 3200, 10_000, 100_000, 1_000_000))
     ok = []
@@ -174,12 +159,24 @@ def c4(B):
         if c.family == "sign" and c.n // m < 1:
             continue
         ok.append(c)
-    t = timed(grid_call(ok, B), reps=1)
-    tl = timed(lambda: run_grid_gpu(ok, B), reps=1)
-    u = grid_units(ok, B)
-    line("C4", cells=len(ok), cells_skipped_k_lt_1=len(cells) - len(ok), reps_per_cell=B, seconds=t,
-         reps_per_s=len(ok) * B / t, roofline_frac=u / t / FP64_PEAK_UNITS,
-         per_cell_loop_seconds=tl, per_cell_loop_reps_per_s=len(ok) * B / tl)
+    small = [c for c in ok if c.n < 1_000_000]
+    big = [c for c in ok if c.n >= 1_000_000]
+    g_small, g_big = grid_call(small, B), grid_call(big, B_big)
+
+    def both():
+        g_small()
+        g_big()
+    t = timed(both, reps=1)
+    ts = timed(g_small, reps=1)
+    tl = timed(lambda: run_grid_gpu(small, B), reps=1)
+    reps = len(small) * B + len(big) * B_big
+    u = grid_units(small, B) + grid_units(big, B_big)
+    line("C4", cells=len(ok), cells_skipped_k_lt_1=len(cells) - len(ok), reps_per_cell=B,
+         reps_per_cell_n1e6=B_big, cells_n1e6=len(big), replicates=reps, seconds=t, reps_per_s=reps / t,
+         roofline_frac=u / t / FP64_PEAK_UNITS, small_cells_seconds=ts,
+         small_cells_per_cell_loop_seconds=tl, small_cells_per_cell_loop_reps_per_s=len(small) * B / tl,
+         note="measured at the stated sizes: one dcor_grid_run_multi call for the n < 1e6 cells at B, one for "
+              "the n = 1e6 cells at B_big; the per-cell launch loop (A/B reference) on the n < 1e6 cells")
 
 
 def grid_call(cells, B):
@@ -424,8 +421,9 @@ def rstream_hrs():
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--only", default="C1,C2,C3,C4,VG,SG,C5,C5c,C5e,C5f,C5fc,S,R1,RG,RH")
-    ap.add_argument("--c3-reps", type=int, default=2000)
+    ap.add_argument("--c3-reps", type=int, default=100_000)
     ap.add_argument("--c4-B", type=int, default=1000)
+    ap.add_argument("--c4-B-big", type=int, default=100_000)
     ap.add_argument("--c5-R", type=int, default=8192)
     ap.add_argument("--c5e-R", type=int, default=1_000_000)
     a = ap.parse_args()
@@ -435,7 +433,7 @@ def main():
     if "C1" in which: c1()
     if "C2" in which: c2()
     if "C3" in which: c3(a.c3_reps)
-    if "C4" in which: c4(a.c4_B)
+    if "C4" in which: c4(a.c4_B, a.c4_B_big)
     if "VG" in which:
         from dcor.sim import vert_cor_grid
         ref_grid("VG", vert_cor_grid())

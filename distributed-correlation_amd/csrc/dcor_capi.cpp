@@ -501,6 +501,15 @@ void code_map(double center, double R, double levels, double* base, double* inv)
   *inv = levels / (2.0 * R);
 }
 
+// E[clip(X, -L, L)] for X ~ N(m, s^2): the centre of a Gaussian cell's code window.
+static double clipped_normal_mean(double m, double s, double L) {
+  if (!(s > 0) || !std::isfinite(s)) return r_min(r_max(m, -L), L);
+  const double a = (-L - m) / s, b = (L - m) / s;
+  auto Phi = [](double t) { return 0.5 * std::erfc(-t / std::sqrt(2.0)); };
+  auto phi = [](double t) { return std::exp(-0.5 * t * t) / std::sqrt(2.0 * M_PI); };
+  return m * (Phi(b) - Phi(a)) + s * (phi(a) - phi(b)) + L * (1.0 - Phi(b)) - L * Phi(a);
+}
+
 // Every data-independent constant of one fused cell (R operation order) and the kernel family
 // that runs it.  The status is the one the reference raises for the cell (stopifnot, k < 1).
 int prepare_cell(const dcor_cell& c, CellPlan& p) {
@@ -519,9 +528,26 @@ int prepare_cell(const dcor_cell& c, CellPlan& p) {
     // code windows centred on the DGP's location (speed only)
     double cx = 0.0, cy = 0.0, rx = 1.0, ry = 1.0;
     if (c.dgp == DCOR_DGP_GAUSSIAN) {
-      cx = r_min(r_max(c.mu[0], -k.L), k.L); cy = r_min(r_max(c.mu[1], -k.L), k.L);
-      rx = 2.0 * std::sqrt(g.a00 * g.a00 + g.a01 * g.a01);
-      ry = 2.0 * std::sqrt(g.a10 * g.a10 + g.a11 * g.a11);
+      // The private centres are mean(clip(x)) + Laplace(s_mu) (vert-cor.R:335-336): within
+      // 12 sd(mean) + 40 noise scales of E[clip(x)] but with probability ~1e-17 per replicate.  A
+      // window that narrow spends the 2^15 code levels where the thresholds fall, so few samples
+      // tie one (each tie costs an exact regeneration in pass 2); samples outside it clamp to the
+      // end codes, still decided exactly while the thresholds lie inside.  DCOR_CODE_WINDOW=wide:
+      // the round-3 window, 2 sd of the sample around mu.
+      const double sx = std::sqrt(g.a00 * g.a00 + g.a01 * g.a01);
+      const double sy = std::sqrt(g.a10 * g.a10 + g.a11 * g.a11);
+      const char* wv = std::getenv("DCOR_CODE_WINDOW");
+      if (wv && std::strcmp(wv, "wide") == 0) {
+        cx = r_min(r_max(c.mu[0], -k.L), k.L); cy = r_min(r_max(c.mu[1], -k.L), k.L);
+        rx = 2.0 * sx;
+        ry = 2.0 * sy;
+      } else {
+        const double rn = 1.0 / std::sqrt((double)c.n);
+        cx = clipped_normal_mean(c.mu[0], sx, k.L);
+        cy = clipped_normal_mean(c.mu[1], sy, k.L);
+        rx = r_min(2.0 * sx, 12.0 * sx * rn + 40.0 * k.s_mu_x);
+        ry = r_min(2.0 * sy, 12.0 * sy * rn + 40.0 * k.s_mu_y);
+      }
     } else if (c.dgp == DCOR_DGP_BERNOULLI) {
       cx = cy = 0.5; rx = ry = 1.0;
     } else if (c.dgp == DCOR_DGP_MIX_GAUSSIAN) {

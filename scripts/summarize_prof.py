@@ -1,18 +1,28 @@
-"""Summarise a rocprofv3 run (gpurun_out/prof_*) into profiles/<tag>_*.
+"""Summarise a rocprofv3 run (scripts/prof.sh -> gpurun_out/prof_<tag>/prof_*) into profiles/<tag>_*.
 
-Copies the kernel-trace stats CSV and writes <tag>_summary.json / .md with, per kernel:
-average duration, PMC counters per dispatch (FETCH_SIZE doubled for gfx950's 1/2 under-
-report of wide streaming reads, MI355X_MICROARCH.md §HBM), effective clock, VALU
-activity and the fp64 instruction mix.
-VALU busy: rocprof's derived VALUBusy, SQ_ACTIVE_INST_VALU x 4 (quad-cycles -> cycles) over the
-SIMD-cycles of the dispatch (1024 SIMDs x GRBM_GUI_ACTIVE / 8 XCDs): the fraction of SIMD time
-the vector ALU was executing, <= 1 by construction -- the hardware-measured roofline fraction
-of a VALU-bound kernel (bench.py roofline.issue_frac).
-VALU time (cross-check): each instruction class of the mix weighted by its measured issue cost on gfx950
-(SIMD cycles per wave64 instruction, scripts/ubench_issue.hip -> profiles/<costs>.json), over
-the SIMD-cycles the dispatch had (1024 SIMDs x GRBM_GUI_ACTIVE / 8): the physically grounded
-roofline fraction of a VALU-bound kernel.
-Usage: python scripts/summarize_prof.py <tag> [gpurun_out] [issue-costs json]
+Copies the kernel-trace stats CSV and writes <tag>_summary.json / .md with, per kernel: average
+duration, PMC counters per dispatch (FETCH_SIZE doubled for gfx950's 1/2 under-report of wide
+streaming reads, MI355X_MICROARCH.md §HBM), effective clock, VALU activity and the fp64
+instruction mix, and the command that produced it (PROF_CMD, set by scripts/prof.sh).
+
+VALU counters, and what they are not:
+- valu_busy_4cyc: rocprof's derived VALUBusy, SQ_ACTIVE_INST_VALU x 4 over the dispatch's SIMD-cycles
+  (1024 SIMDs x GRBM_GUI_ACTIVE / 8 XCDs).  SQ_ACTIVE_INST_VALU equals SQ_INSTS_VALU here to ~2 %,
+  so this is the instruction count priced at 4 cycles per wave64 instruction.  gfx950 issues a
+  wave64 fp32 / int32 instruction in 2 cycles (MI355X_MICROARCH.md §Wave scheduling), so it is NOT
+  bounded by 1 and is not a physical fraction (kernels read up to 1.09).  Kept for comparison with
+  earlier rounds only.
+- cycles_per_valu_inst: the dispatch's SIMD-cycles per VALU wave-instruction it issued (lower =
+  denser issue); a stream of 2-cycle instructions cannot go below 2.
+- wait_inst_frac / wait_any_frac: SQ_WAIT_INST_ANY / SQ_WAIT_ANY over SQ_WAVE_CYCLES: the share of
+  wave-cycles a wave waited for its next instruction's issue / for anything (memory included).
+- valu_time_frac: each instruction class of the mix priced at its measured issue cost (SIMD cycles
+  per wave64 instruction, scripts/ubench_issue.hip -> profiles/<costs>.json) over the dispatch's
+  SIMD-cycles; physical only when the costs file is absolute ("calibration": "absolute").
+The physical ceiling of the headline's VALU-bound passes is measured directly instead: bench.py
+roofline.issue (dcor_diag_sign_pass ceilings).
+L2 -> CU traffic (pass "tcp"): TCP_TCC_READ_REQ_sum x 128 B (gfx950 L1 line) per dispatch.
+Usage: python scripts/summarize_prof.py <tag> [prof dir] [issue-costs json]
 """
 import collections
 import csv
@@ -26,8 +36,15 @@ src = sys.argv[2] if len(sys.argv) > 2 else "gpurun_out"
 root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 dst = os.path.join(root, "profiles")
 os.makedirs(dst, exist_ok=True)
-costs_path = sys.argv[3] if len(sys.argv) > 3 else os.path.join(dst, "r02_issue_costs.json")
-COSTS = json.load(open(costs_path))["cycles_per_wave_instruction"] if os.path.exists(costs_path) else None
+costs_path = sys.argv[3] if len(sys.argv) > 3 else None
+if costs_path is None:
+    for t in ("r04", "r02"):
+        costs_path = os.path.join(dst, f"{t}_issue_costs.json")
+        if os.path.exists(costs_path):
+            break
+_costs = json.load(open(costs_path)) if os.path.exists(costs_path) else {}
+COSTS = _costs.get("cycles_per_wave_instruction")
+COSTS_ABSOLUTE = _costs.get("calibration") == "absolute"
 # instruction class of the mix counters -> the measured instruction that represents it
 CLASS_COST = {"SQ_INSTS_VALU_ADD_F64": "v_add_f64", "SQ_INSTS_VALU_MUL_F64": "v_mul_f64",
               "SQ_INSTS_VALU_FMA_F64": "v_fma_f64", "SQ_INSTS_VALU_TRANS_F64": "v_rsq_f64",
@@ -57,7 +74,9 @@ except (OSError, subprocess.CalledProcessError):
     head = None
 # the tree this summary describes: the committed head it was profiled at and the hash of the engine
 # sources (bench.py compares the hash with its own tree's: roofline.*_source_fresh)
-out = {"kernels": {}, "git_head": os.environ.get("PROF_HEAD", head), "src_sha16": src_sha16(root)}
+out = {"kernels": {}, "git_head": os.environ.get("PROF_HEAD", head), "src_sha16": src_sha16(root),
+       "command": os.environ.get("PROF_CMD"), "issue_costs": os.path.relpath(costs_path, root) if COSTS else None,
+       "issue_costs_absolute": COSTS_ABSOLUTE}
 stats = os.path.join(src, "prof_trace", "run_kernel_stats.csv")
 if os.path.exists(stats):
     shutil.copy(stats, os.path.join(dst, f"{tag}_kernel_stats.csv"))
@@ -68,7 +87,7 @@ if os.path.exists(stats):
         k["pct_time"] = float(r["Percentage"])
 
 counters = collections.defaultdict(lambda: collections.defaultdict(list))
-for sub in ("prof_fetch", "prof_write", "prof_sq", "prof_mix"):
+for sub in ("prof_fetch", "prof_write", "prof_sq", "prof_mix", "prof_tcp"):
     f = os.path.join(src, sub, "run_counter_collection.csv")
     if not os.path.exists(f):
         continue
@@ -91,19 +110,23 @@ for kname, cs in counters.items():
         k["vgpr"] = avg["_vgpr"]
         k["lds_bytes"] = avg["_lds"]
         k["grid_threads"] = avg["_grid"]
-    if "SQ_ACTIVE_INST_VALU" in avg and "SQ_WAVE_CYCLES" in avg and avg["SQ_WAVE_CYCLES"]:
-        k["valu_active_frac_of_wave_cycles"] = avg["SQ_ACTIVE_INST_VALU"] / avg["SQ_WAVE_CYCLES"]
+    if "SQ_WAVE_CYCLES" in avg and avg["SQ_WAVE_CYCLES"]:
+        for c, nm in (("SQ_WAIT_INST_ANY", "wait_inst_frac"), ("SQ_WAIT_ANY", "wait_any_frac")):
+            if c in avg:
+                k[nm] = avg[c] / avg["SQ_WAVE_CYCLES"]
+    if "TCP_TCC_READ_REQ_sum" in avg:
+        k["l2_to_cu_read_bytes"] = avg["TCP_TCC_READ_REQ_sum"] * 128
+    if "TCC_HIT_sum" in avg and "TCC_MISS_sum" in avg and avg["TCC_HIT_sum"] + avg["TCC_MISS_sum"]:
+        k["l2_hit_rate"] = avg["TCC_HIT_sum"] / (avg["TCC_HIT_sum"] + avg["TCC_MISS_sum"])
     if "GRBM_GUI_ACTIVE" in avg and k.get("avg_ns"):
         k["effective_clock_ghz"] = avg["GRBM_GUI_ACTIVE"] / 8 / k["avg_ns"]
-        # VALU issue ceiling: one wave64 VALU instruction per 4 cycles per SIMD = 1 per cycle
-        # per CU (256 CUs); meaningful for kernels profiled without overlap (PIPE=0 runs)
+        simd_cycles = 1024 * avg["GRBM_GUI_ACTIVE"] / 8   # meaningful for kernels profiled alone (SERIAL=1)
         if "SQ_ACTIVE_INST_VALU" in avg:
-            k["valu_busy"] = avg["SQ_ACTIVE_INST_VALU"] * 4 / (1024 * avg["GRBM_GUI_ACTIVE"] / 8)
-        if "SQ_INSTS_VALU" in avg:
-            k["valu_issue_util"] = avg["SQ_INSTS_VALU"] / (256 * avg["GRBM_GUI_ACTIVE"] / 8)
+            k["valu_busy_4cyc"] = avg["SQ_ACTIVE_INST_VALU"] * 4 / simd_cycles
+        if "SQ_INSTS_VALU" in avg and avg["SQ_INSTS_VALU"]:
+            k["cycles_per_valu_inst"] = simd_cycles / avg["SQ_INSTS_VALU"]
             if COSTS and all(c in avg for c in CLASS_COST):
-                # VALU time over the SIMD-cycles of the dispatch (1024 SIMDs)
-                k["valu_time_frac"] = valu_cycles(avg) / (1024 * avg["GRBM_GUI_ACTIVE"] / 8)
+                k["valu_time_frac"] = valu_cycles(avg) / simd_cycles
                 k["valu_cycles_per_dispatch"] = valu_cycles(avg)
     mix = {c: avg[c] for c in avg if c.startswith("SQ_INSTS_VALU_")}
     if mix:
@@ -139,17 +162,25 @@ if os.path.exists(trace):
 
 json.dump(out, open(os.path.join(dst, f"{tag}_summary.json"), "w"), indent=1, sort_keys=True)
 lines = [f"# rocprofv3 summary `{tag}`", "",
-         f"Profiled at git head `{out['git_head']}` (engine sources sha256 `{out['src_sha16']}`).", "",
-         "| kernel | calls | avg µs | % time | VGPR | HBM read B (corr.) | HBM write B | VALU active / wave-cycles | VALU instr / CU-cycle | VALU time / SIMD-cycles | VALUBusy | clock GHz |",
-         "|---|---|---|---|---|---|---|---|---|---|---|---|"]
+         f"Profiled at git head `{out['git_head']}` (engine sources sha256 `{out['src_sha16']}`).",
+         f"Command: `{out['command']}`." if out.get("command") else "", "",
+         "| kernel | calls | avg µs | % time | VGPR | HBM read B (corr.) | HBM write B | L2->CU read B | "
+         "SIMD-cycles / VALU inst | wait-inst / wave-cycles | wait-any / wave-cycles | VALU time / SIMD-cycles | "
+         "VALUBusy (4-cycle) | clock GHz |",
+         "|---|---|---|---|---|---|---|---|---|---|---|---|---|---|"]
 for kname, k in sorted(out["kernels"].items(), key=lambda kv: -kv[1].get("pct_time", 0)):
     def f(x, fmt="{:.3g}"):
         return fmt.format(x) if isinstance(x, (int, float)) else "—"
     lines.append(f"| {kname} | {k.get('calls', '—')} | {f(k.get('avg_ns', 0) / 1e3)} | {f(k.get('pct_time'))} | "
                  f"{f(k.get('vgpr'))} | {f(k.get('hbm_read_bytes_corrected'))} | {f(k.get('hbm_write_bytes'))} | "
-                 f"{f(k.get('valu_active_frac_of_wave_cycles'))} | {f(k.get('valu_issue_util'))} | "
-                 f"{f(k.get('valu_time_frac'))} | {f(k.get('valu_busy'))} | "
+                 f"{f(k.get('l2_to_cu_read_bytes'))} | {f(k.get('cycles_per_valu_inst'))} | "
+                 f"{f(k.get('wait_inst_frac'))} | {f(k.get('wait_any_frac'))} | "
+                 f"{f(k.get('valu_time_frac'))} | {f(k.get('valu_busy_4cyc'))} | "
                  f"{f(k.get('effective_clock_ghz'))} |")
+lines += ["", "VALUBusy (4-cycle) prices every VALU wave-instruction at 4 SIMD-cycles; gfx950 issues int32 / "
+              "fp32 ones in 2, so it is not bounded by 1 (see scripts/summarize_prof.py).  VALU time is "
+              + ("priced at absolute measured costs" if out["issue_costs_absolute"] else
+                 "priced at RELATIVE issue costs (not a physical fraction)") + "."]
 if "simulate_call_span_ms" in out:
     sp = out["simulate_call_span_ms"]
     lines += ["", f"simulate() call span from the trace (first sign-kernel start to last end, "

@@ -1,18 +1,19 @@
 // ubench_issue.hip -- measured VALU issue cost (SIMD cycles per wave64 instruction) of the
 // instruction classes the fused kernels issue on gfx950, with 8 waves per SIMD each running 8
-// independent chains (throughput, not latency).  Cycles come from s_memtime (shader clock)
-// around each wave's loop; cost = wave cycles / (waves per SIMD x instructions per wave).
-// s_memtime does not tick at the shader clock on gfx950 (its per-XCD bases also differ), so the
-// costs are relative: v_fma_f64 costs 2.3x v_fma_f32 and 1.8x v_add_u32.  They weight the
-// instruction-mix cross-check in scripts/summarize_prof.py (valu_time_frac); the roofline
-// fraction the bench line reports is the hardware's own VALUBusy (roofline.issue_frac).
+// independent chains (throughput, not latency).  One kernel per instruction.
+// Relative costs (printed): s_memtime around each wave's loop, cost = wave ticks / (waves per
+// SIMD x instructions per wave); s_memtime does not tick at the shader clock on gfx950, so these
+// are relative only.
+// Absolute costs: run under rocprofv3 --pmc SQ_INSTS_VALU GRBM_GUI_ACTIVE and let
+// scripts/issue_costs.py divide each dispatch's SIMD-cycles (1024 x GRBM_GUI_ACTIVE / 8) by its
+// VALU wave-instructions -> profiles/<tag>_issue_costs.json ("calibration": "absolute").
 // Build: hipcc --offload-arch=gfx950 -O3 -o ubench_issue ubench_issue.hip
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
 #include <cstdio>
 
-#define N_ITER 512
+#define N_ITER 2048
 #define CH 8
 
 #define ASM8(op)                                                                          \
@@ -58,6 +59,12 @@ KERNEL(k_cndmask, uint32_t, uint32_t, "v_cndmask_b32 %0, %0, %1, vcc")
 KERNEL(k_med3_i32, uint32_t, uint32_t, "v_med3_i32 %0, %0, %1, %2")
 KERNEL(k_pk_fma_f32, uint64_t, uint64_t, "v_pk_fma_f32 %0, %0, %1, %2")
 KERNEL(k_mul_u32_u24, uint32_t, uint32_t, "v_mul_u32_u24 %0, %0, %1")
+KERNEL(k_pk_sub_u16, uint32_t, uint32_t, "v_pk_sub_u16 %0, %0, %1")
+KERNEL(k_pk_min_u16, uint32_t, uint32_t, "v_pk_min_u16 %0, %0, %1")
+KERNEL(k_bcnt, uint32_t, uint32_t, "v_bcnt_u32_b32 %0, %0, %1")
+KERNEL(k_cvt_f32_f64, uint32_t, double, "v_cvt_f32_f64 %0, %1")
+KERNEL(k_cvt_pknorm, uint32_t, uint32_t, "v_cvt_pknorm_u16_f32 %0, %0, %1")
+KERNEL(k_min_f64, double, double, "v_min_f64 %0, %0, %1")
 
 typedef void (*Fn)(unsigned long long*, void*);
 
@@ -78,7 +85,10 @@ int main() {
       {"v_cvt_f64_i32", (Fn)k_cvt_f64_i32}, {"v_rsq_f64", (Fn)k_rsq_f64}, {"v_rcp_f64", (Fn)k_rcp_f64},
       {"v_ldexp_f64", (Fn)k_ldexp_f64}, {"v_max_f64", (Fn)k_max_f64}, {"v_fract_f64", (Fn)k_fract_f64},
       {"v_cndmask_b32", (Fn)k_cndmask}, {"v_med3_i32", (Fn)k_med3_i32},
-      {"v_pk_fma_f32", (Fn)k_pk_fma_f32}, {"v_mul_u32_u24", (Fn)k_mul_u32_u24}};
+      {"v_pk_fma_f32", (Fn)k_pk_fma_f32}, {"v_mul_u32_u24", (Fn)k_mul_u32_u24},
+      {"v_pk_sub_u16", (Fn)k_pk_sub_u16}, {"v_pk_min_u16", (Fn)k_pk_min_u16},
+      {"v_bcnt_u32_b32", (Fn)k_bcnt}, {"v_cvt_f32_f64", (Fn)k_cvt_f32_f64},
+      {"v_cvt_pknorm_u16_f32", (Fn)k_cvt_pknorm}, {"v_min_f64", (Fn)k_min_f64}};
   unsigned long long* h = new unsigned long long[blocks * 4];
   printf("{\"waves_per_simd\": 8, \"instructions_per_wave\": %d, \"cycles_per_wave_instruction\": {", N_ITER * CH);
   const int nk = sizeof(ks) / sizeof(ks[0]);

@@ -196,3 +196,30 @@ def test_headline_bench_step_every_replicate(dc, orc):
     print(f"tie batches in the step: {int(ties.sum())} over {int((ties > 0).sum())} replicates")
     assert ties.sum() > 0
     assert (ties > 0).sum() < R        # rare: most replicates have none
+
+
+def test_headline_wide_code_window(dc, orc, monkeypatch):
+    """The record codes' window only decides how many samples tie a private centre's code (each tie
+    is regenerated exactly), never a result: with round 3's wide window (DCOR_CODE_WINDOW=wide,
+    ~20x the ties of the default) 2048 headline replicates equal the default window's bit for bit
+    and the oracle at 1e-12, and tie more often."""
+    import ctypes as C
+    from dcor import _lib
+    from dcor.sim import headline_cell, simulate
+    cell = headline_cell()
+    R, r0 = 2048, 3 * 8192
+    c = cell.to_c()
+
+    def ties():
+        t = np.zeros(R, dtype=np.int64)
+        _lib.check(_lib.lib.dcor_diag_sign_ties(C.byref(c), r0, R, t.ctypes.data_as(C.POINTER(C.c_int64))))
+        return int(t.sum())
+
+    narrow, t_narrow = simulate(cell, R, r0).cpu().numpy(), ties()
+    monkeypatch.setenv("DCOR_CODE_WINDOW", "wide")
+    wide, t_wide = simulate(cell, R, r0).cpu().numpy(), ties()
+    assert np.array_equal(narrow.view(np.int64), wide.view(np.int64))
+    assert_close(wide, orc.sim_reps(c, r0, r0 + R, threads=min(16, os.cpu_count() or 1)),
+                 what="headline, wide code window")
+    print(f"tie batches over {R} replicates: default window {t_narrow}, wide {t_wide}")
+    assert t_wide > 4 * max(t_narrow, 1)
