@@ -361,6 +361,14 @@ __device__ __forceinline__ void exact_signs(const SignConst& c, const SignStd& s
 // wave at once (zig_slow would otherwise run under divergence nearly every iteration).  The
 // queued sample's record is rewritten and its clipped values replace its placeholder's in the
 // sums at the drain.
+// Pass 1 folds two sample groups' plain sums per compensated add; pass 2 (m = 8) pair-groups the
+// T sums of a thread's two batches in flight (build with 0 for the per-group / per-batch sums).
+#ifndef DCOR_P1_FOLD8
+#define DCOR_P1_FOLD8 1
+#endif
+#ifndef DCOR_P2_PAIRT
+#define DCOR_P2_PAIRT 1
+#endif
 #define ZQ_CAP 512  // per-wave queue; a group iteration adds at most 256 entries per wave
 
 // WAVE = false: one 256-thread workgroup per replicate; WAVE = true: one wave per replicate (the
@@ -404,8 +412,9 @@ __device__ __forceinline__ void sign_pass1_core(const SignConst& c, uint32_t rep
     };
     // Every valid sample enters the group sums, a queued one with its placeholder: the drain
     // takes the placeholder out and adds the true values (both compensated), so the hot loop
-    // selects nothing.
-    auto group = [&](int64_t g4, auto full_tag) {
+    // selects nothing.  The group's plain sums are added into (hx, hy); the caller folds them
+    // into the compensated sums (with DCOR_P1_FOLD8, once per two groups).
+    auto group = [&](int64_t g4, auto full_tag, double& hx, double& hy) {
       constexpr bool FULL = decltype(full_tag)::value;
       const uint32_t i0 = (uint32_t)(4 * g4);
       uint32_t rec[4], pend = 0;
@@ -422,8 +431,8 @@ __device__ __forceinline__ void sign_pass1_core(const SignConst& c, uint32_t rep
         pend |= (valid && !ok) ? (1u << q) : 0u;
         rec[q] = record_w(xc, yc, w.w3);
       }
-      ks_acc(sx, gx);
-      ks_acc(sy, gy);
+      hx += gx;
+      hy += gy;
       if constexpr (CEIL) {
         asm volatile("" ::"v"(rec[0]), "v"(rec[1]), "v"(rec[2]), "v"(rec[3]), "v"(pend));
         return;
@@ -462,11 +471,34 @@ __device__ __forceinline__ void sign_pass1_core(const SignConst& c, uint32_t rep
       if (lane == 0) *zqn = 0u;
       wave_sync();
     };
+#if DCOR_P1_FOLD8
+    // two groups per step (wave groups b + lane and b + NT + lane), one compensated fold of their
+    // plain 8-sample sums: half the TwoSum chains of a fold per group (the low bits of the sums
+    // differ from per-group folds; the private centres they decide are unchanged in practice)
+    for (int64_t b = WAVE ? 0 : 64 * wv; b < nfull; b += 2 * NT) {  // trip count uniform per wave
+      double hx = 0.0, hy = 0.0;
+      if (b + lane < nfull) group(b + lane, std::true_type(), hx, hy);
+      if (!CEIL && __builtin_amdgcn_readfirstlane(*zqn) > ZQ_CAP - 256) drain();
+      if (b + NT + lane < nfull) group(b + NT + lane, std::true_type(), hx, hy);
+      if (!CEIL && __builtin_amdgcn_readfirstlane(*zqn) > ZQ_CAP - 256) drain();
+      ks_acc(sx, hx);
+      ks_acc(sy, hy);
+    }
+#else
     for (int64_t b = WAVE ? 0 : 64 * wv; b < nfull; b += NT) {  // trip count uniform per wave
-      if (b + lane < nfull) group(b + lane, std::true_type());
+      double hx = 0.0, hy = 0.0;
+      if (b + lane < nfull) group(b + lane, std::true_type(), hx, hy);
+      ks_acc(sx, hx);
+      ks_acc(sy, hy);
       if (!CEIL && __builtin_amdgcn_readfirstlane(*zqn) > ZQ_CAP - 256) drain();
     }
-    if ((c.n & 3) && tid == (int)(nfull % NT)) group(nfull, std::false_type());
+#endif
+    if ((c.n & 3) && tid == (int)(nfull % NT)) {
+      double hx = 0.0, hy = 0.0;
+      group(nfull, std::false_type(), hx, hy);
+      ks_acc(sx, hx);
+      ks_acc(sy, hy);
+    }
     drain();
   } else {
     static_assert(!CEIL, "the ceiling kernel runs the Gaussian loop");
@@ -690,6 +722,13 @@ __device__ __forceinline__ P2Result sign_pass2_core(const SignConst& c, uint32_t
     ks_acc(sT, T);  // compensated (error ~ k 2^-106): the T mean / sd inputs
     ks_acc(sT2, T * T);
   };
+  // T_j alone (no accumulation): the pair-grouped form below
+  auto batch_T_val = [&](int64_t j, int cx, int cy) -> double {
+    const U4 w = draw((uint32_t)j, rep, DCOR_SITE_NI_LAP, c.k0, c.k1);   // vert-cor.R:230-231
+    const double xt = (double)cx * 0.125 + c.bx * unit_laplace_t(u53(w.w0, w.w1), lt);
+    const double yt = (double)cy * 0.125 + c.by * unit_laplace_t(u53(w.w2, w.w3), lt);
+    return 8.0 * xt * yt;                                                 // vert-cor.R:233
+  };
   // the same, kept only when `valid` (a batch computed past the last one is dropped exactly)
   auto batch_T_if = [&](int64_t j, int cx, int cy, bool valid) {
     const double h1 = sT.hi, l1 = sT.lo, h2 = sT2.hi, l2 = sT2.lo;  // scalars: no aggregate select
@@ -780,8 +819,17 @@ __device__ __forceinline__ P2Result sign_pass2_core(const SignConst& c, uint32_t
         load(j + 3 * NT, b0, b1);
         __builtin_amdgcn_sched_barrier(0);
         core += cca + (vb ? ccb : 0);
+#if DCOR_P2_PAIRT
+        // the two batches' T and T^2 added plainly, the pair sums compensated: half the TwoSum
+        // chains (the low bits differ from per-batch sums, within the oracle's 1e-12)
+        const double Ta = batch_T_val(j, cxa, cya);
+        const double Tb = vb ? batch_T_val(jb, cxb, cyb) : 0.0;
+        ks_acc(sT, Ta + Tb);
+        ks_acc(sT2, Ta * Ta + Tb * Tb);
+#else
         batch_T(j, cxa, cya, std::true_type());
         batch_T_if(jb, cxb, cyb, vb);
+#endif
       }
     }
   } else if constexpr (!CEIL) {
