@@ -945,8 +945,9 @@ __global__ __launch_bounds__(DCOR_BLOCK, DCOR_P2_WPE) void k_sign_pass2(SignCons
                        scratch + (size_t)blockIdx.x * (size_t)c.n,
                        sums + SIGN_SUMS * (size_t)blockIdx.x, part + blockIdx.x);
 }
-// The pass-2 ceiling (CEIL above, m = 8): same grid, registers and occupancy target as k_sign_pass2.
-__global__ __launch_bounds__(DCOR_BLOCK, DCOR_P2_WPE) void k_sign_pass2_ceil(SignConst c,
+// The pass-2 ceiling (CEIL above, m = 8): same grid as k_sign_pass2, compiled for 4 waves per SIMD
+// (its register-held records would otherwise take it to 3) and launched at k_sign_pass2's occupancy.
+__global__ __launch_bounds__(DCOR_BLOCK, 4) void k_sign_pass2_ceil(SignConst c,
                                                                          const uint32_t* __restrict__ scratch,
                                                                          const double* __restrict__ sums,
                                                                          SignPartial* __restrict__ part) {
@@ -2011,6 +2012,16 @@ int launch_sign_fused_codes(const SignConst& c, int64_t reps, int64_t chunk, con
   }
 }
 
+// Dynamic LDS that brings kernel `ceil`'s workgroups per CU down to kernel `real`'s (256 threads).
+static int occupancy_pad(const void* real, const void* ceil, size_t* pad) {
+  int want = 0, have = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&want, real, DCOR_BLOCK, 0) != hipSuccess) return last_err();
+  for (*pad = 0;; *pad += 256) {
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&have, ceil, DCOR_BLOCK, *pad) != hipSuccess) return last_err();
+    if (have <= want || *pad > 64 * 1024) return 0;
+  }
+}
+
 // One pass of the one-pass sign path over `reps` replicates as a single chunk on `stream`, for
 // timing (dcor_diag_sign_pass): 1 pass 1, 2 pass 2, 3 the epilogue; 11 / 12 the pass-1 / pass-2
 // ceilings (Gaussian DGP, m = 8) at the real passes' occupancy, 13 the pass-1 ceiling at its own.  slab / sums / part / out as launch_codes_t lays them out.
@@ -2037,23 +2048,22 @@ int launch_sign_diag(const SignConst& c, int64_t reps, int which, uint32_t* slab
       break;
     case 3: launch_sign_epilogue(c, reps, part, out, st); break;
     case 11: case 13: {
-      // 11: at pass 1's occupancy (pass 1 holds more VGPRs and LDS than its ceiling: pad the
-      // ceiling's LDS until no more of its workgroups fit per CU than of pass 1's); 13: its own
+      // 11: at pass 1's occupancy (pass 1 holds more VGPRs and LDS than its ceiling); 13: its own
       size_t pad = 0;
       if (which == 11) {
-        int want = 0, have = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&want, k_sign_pass1<DCOR_DGP_GAUSSIAN>, DCOR_BLOCK, 0) != hipSuccess)
-          return last_err();
-        for (;; pad += 256) {
-          if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&have, k_sign_pass1_ceil, DCOR_BLOCK, pad) != hipSuccess)
-            return last_err();
-          if (have <= want || pad > 64 * 1024) break;
-        }
+        const int e = occupancy_pad((const void*)k_sign_pass1<DCOR_DGP_GAUSSIAN>, (const void*)k_sign_pass1_ceil, &pad);
+        if (e) return e;
       }
       hipLaunchKernelGGL(k_sign_pass1_ceil, g, b, pad, st, c, sums);
       break;
     }
-    case 12: hipLaunchKernelGGL(k_sign_pass2_ceil, g, b, 0, st, c, slab, sums, part); break;
+    case 12: {
+      size_t pad = 0;
+      const int e = occupancy_pad((const void*)k_sign_pass2<DCOR_DGP_GAUSSIAN>, (const void*)k_sign_pass2_ceil, &pad);
+      if (e) return e;
+      hipLaunchKernelGGL(k_sign_pass2_ceil, g, b, pad, st, c, slab, sums, part);
+      break;
+    }
     default: return (int)hipErrorInvalidValue;
   }
   return last_err();
