@@ -369,6 +369,28 @@ __device__ __forceinline__ void exact_signs(const SignConst& c, const SignStd& s
 #ifndef DCOR_P2_PAIRT
 #define DCOR_P2_PAIRT 1
 #endif
+// Slab layout.  For m = 8 cells (DCOR_SLAB_WAVE) the records of every full block of 512 samples
+// (64 batches) are stored half-batch-major: the first four records of the block's 64 batches
+// (1 KB), then their last four (1 KB).  Pass 2's wave then loads its 64 consecutive batches' first
+// halves as one contiguous 1-KB row and their second halves as another -- 8 whole cache lines per
+// load instead of 16 half lines -- and pass 1's 16-B group stores stay two contiguous 512-B runs
+// per wave.  Samples past the last full block (and every other m) keep position i.  Tail samples
+// (i >= 8 k) always lie past the full blocks, since 8 floor(n / 8) >= 512 floor(n / 512).
+#ifndef DCOR_SLAB_WAVE
+#define DCOR_SLAB_WAVE 1
+#endif
+struct SlabMap {
+  bool on;
+  uint32_t nfb;   // samples in full 512-sample blocks
+  __device__ explicit SlabMap(const SignConst& c)
+      : on(DCOR_SLAB_WAVE && c.m == 8), nfb((uint32_t)(c.n >> 9) << 9) {}
+  __device__ __forceinline__ uint32_t pos(uint32_t i) const {
+    if (!on || i >= nfb) return i;
+    const uint32_t g4 = i >> 2;
+    return ((g4 >> 7) << 9) | ((g4 & 1u) << 8) | (((g4 >> 1) & 63u) << 2) | (i & 3u);
+  }
+};
+
 #define ZQ_CAP 512  // per-wave queue; a group iteration adds at most 256 entries per wave
 
 // WAVE = false: one 256-thread workgroup per replicate; WAVE = true: one wave per replicate (the
@@ -385,6 +407,7 @@ __device__ __forceinline__ void sign_pass1_core(const SignConst& c, uint32_t rep
                                                 uint32_t* zq, uint32_t* zqn) {
   constexpr int NT = WAVE ? 64 : DCOR_BLOCK;
   const int tid = WAVE ? (int)(threadIdx.x & 63) : (int)threadIdx.x;
+  const SlabMap sm(c);
   DD sx{0.0, 0.0}, sy{0.0, 0.0};
   const float cix = c.cinv_xf, ciy = c.cinv_yf, cbx = c.cnb_xf, cby = c.cnb_yf;
   // the INT flip from its 32-bit word: u < flipT (flipT <= 2^32) as a 32-bit compare
@@ -438,7 +461,7 @@ __device__ __forceinline__ void sign_pass1_core(const SignConst& c, uint32_t rep
         return;
       }
       if (FULL) {
-        *reinterpret_cast<uint4*>(slab + i0) = make_uint4(rec[0], rec[1], rec[2], rec[3]);
+        *reinterpret_cast<uint4*>(slab + sm.pos(i0)) = make_uint4(rec[0], rec[1], rec[2], rec[3]);
       } else {
         for (int q = 0; q < 4; ++q) if ((int64_t)(i0 + q) < c.n) slab[i0 + q] = rec[q];
       }
@@ -465,7 +488,7 @@ __device__ __forceinline__ void sign_pass1_core(const SignConst& c, uint32_t rep
         const double xc = rclip_fin(x, c.L), yc = rclip_fin(y, c.L);
         ks_acc(sx, xc);
         ks_acc(sy, yc);
-        slab[i] = record_w(xc, yc, w3);
+        slab[sm.pos(i)] = record_w(xc, yc, w3);
       }
       wave_sync();
       if (lane == 0) *zqn = 0u;
@@ -530,7 +553,7 @@ __device__ __forceinline__ void sign_pass1_core(const SignConst& c, uint32_t rep
       ks_acc(sx, gx);
       ks_acc(sy, gy);
       if (FULL) {
-        *reinterpret_cast<uint4*>(slab + i0) = make_uint4(rec[0], rec[1], rec[2], rec[3]);
+        *reinterpret_cast<uint4*>(slab + sm.pos(i0)) = make_uint4(rec[0], rec[1], rec[2], rec[3]);
       } else {
         for (int q = 0; q < 4; ++q) if ((int64_t)(i0 + q) < c.n) slab[i0 + q] = rec[q];
       }
@@ -650,6 +673,7 @@ __device__ __forceinline__ P2Result sign_pass2_core(const SignConst& c, uint32_t
                                                     const double2* lt) {
   constexpr int NT = WAVE ? 64 : DCOR_BLOCK;   // threads sharing the replicate
   const int tid = WAVE ? (int)(threadIdx.x & 63) : (int)threadIdx.x;
+  const SlabMap sm(c);
   double lap[10];
   if constexpr (WAVE) {
     scalar_laplace_wave(rep, c.k0, c.k1, lap);
@@ -784,7 +808,7 @@ __device__ __forceinline__ P2Result sign_pass2_core(const SignConst& c, uint32_t
         ++ties;
 #pragma unroll 1
         for (int q = 0; q < 8; ++q)  // re-read the record (L2-hot): no dynamically indexed registers
-          fix_fast(8 * j + q, slab[8 * j + q], cx, cy, cc);
+          fix_fast(8 * j + q, slab[sm.pos((uint32_t)(8 * j + q))], cx, cy, cc);
       }
     };
     // Two batches' records in flight per thread in two register sets, used in place (a move of a
@@ -794,8 +818,8 @@ __device__ __forceinline__ P2Result sign_pass2_core(const SignConst& c, uint32_t
     // compiler could merge the two copies across.  Loads past the end re-read the last batch.
     auto load_mem = [&](int64_t jj, uint4& lo, uint4& hi) {
       const int64_t jc = jj < c.k ? jj : c.k - 1;
-      lo = *reinterpret_cast<const uint4*>(slab + 8 * jc);
-      hi = *reinterpret_cast<const uint4*>(slab + 8 * jc + 4);
+      lo = *reinterpret_cast<const uint4*>(slab + sm.pos((uint32_t)(8 * jc)));
+      hi = *reinterpret_cast<const uint4*>(slab + sm.pos((uint32_t)(8 * jc + 4)));
     };
     auto load = [&](int64_t jj, uint4& lo, uint4& hi) {
       if constexpr (CEIL)
@@ -886,7 +910,7 @@ __device__ __forceinline__ P2Result sign_pass2_core(const SignConst& c, uint32_t
   for (int64_t i = c.k * c.m + tid; !CEIL && i < c.n; i += NT) {  // tail: INT only
     int dx = 0, dy = 0, cc = 0;
     bool ignore = false;  // NI never reads the tail
-    const uint32_t w = slab[i];
+    const uint32_t w = slab[sm.pos((uint32_t)i)];
     if (fast(w, dx, dy, cc) || force_exact) fixup(i, w, dx, dy, cc, ignore);
     core += cc;
   }
