@@ -830,8 +830,12 @@ __device__ __forceinline__ P2Result sign_pass2_core(const SignConst& c, uint32_t
     };
     if (c.k > 0) {
       uint4 a0, a1, b0, b1;
+      // issued in this order (a older than b), as in the loop, so the loop header's wait for
+      // a's records is vmcnt(2) on every incoming path
       load_mem(tid, a0, a1);
+      __builtin_amdgcn_sched_barrier(0);
       load_mem(tid + NT, b0, b1);
+      __builtin_amdgcn_sched_barrier(0);
       for (int64_t j = tid; j < c.k; j += 2 * NT) {
         const bool vb = j + NT < c.k;
         const int64_t jb = vb ? j + NT : c.k - 1;
