@@ -156,6 +156,8 @@ def measure_passes(cell, reps: int = 2048, rep_begin: int = 0, iters: int = 5) -
       pass1_ceiling_own_occ      the same at the ceiling kernel's own (higher) occupancy
       pass2_ceiling              k_sign_pass2's decision loop with its records held in registers
                                  (no slab stream, no tie fix-up), at pass 2's occupancy
+      pass1_ceiling_plus_stores  the pass-1 ceiling with its slab stores put back
+      pass1_ceiling_plus_queue   the pass-1 ceiling with its slow-normal queue and drain put back
 
     A ceiling is the time the pass's own instruction stream takes when nothing but issue limits
     it: pass / ceiling is how far memory, queueing and fix-ups keep the pass from it."""
@@ -180,7 +182,8 @@ def measure_passes(cell, reps: int = 2048, rep_begin: int = 0, iters: int = 5) -
         return sorted(a.elapsed_time(b) for a, b in ev)[iters // 2]
 
     out = {"pass1": timed(1), "pass2": timed(2), "epilogue": timed(3),
-           "pass1_ceiling": timed(11), "pass1_ceiling_own_occ": timed(13), "pass2_ceiling": timed(12)}
+           "pass1_ceiling": timed(11), "pass1_ceiling_own_occ": timed(13), "pass2_ceiling": timed(12),
+           "pass1_ceiling_plus_stores": timed(14), "pass1_ceiling_plus_queue": timed(15)}
     return {k: round(v, 5) for k, v in out.items()}
 
 

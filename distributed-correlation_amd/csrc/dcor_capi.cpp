@@ -775,8 +775,8 @@ int dcor_sim_launch(const dcor_cell* cell, int64_t rep_begin, int64_t rep_count,
 int dcor_diag_sign_pass(const dcor_cell* cell, int64_t rep_begin, int64_t reps, int which, void* stream) {
   if (!cell || reps < 1 || reps > 65535 || rep_begin < 0 || rep_begin + reps > 0xffffffffLL)
     return fail(DCOR_EINVAL, "diag_sign_pass: bad arguments");
-  if (which != 1 && which != 2 && which != 3 && which != 11 && which != 12 && which != 13)
-    return fail(DCOR_EINVAL, "diag_sign_pass: which must be 1, 2, 3, 11, 12 or 13");
+  if (which != 1 && which != 2 && which != 3 && (which < 11 || which > 15))
+    return fail(DCOR_EINVAL, "diag_sign_pass: which must be 1, 2, 3 or 11-15");
   if (int st = need_device()) return st;
   CellPlan cp;
   if (int st = prepare_cell(*cell, cp)) return st;

@@ -376,8 +376,10 @@ __device__ __forceinline__ void exact_signs(const SignConst& c, const SignStd& s
 // load instead of 16 half lines -- and pass 1's 16-B group stores stay two contiguous 512-B runs
 // per wave.  Samples past the last full block (and every other m) keep position i.  Tail samples
 // (i >= 8 k) always lie past the full blocks, since 8 floor(n / 8) >= 512 floor(n / 512).
+// Measured (round 4, headline, one box): pass 2 181 us with it, 177 us without; pass 1 533 vs 531
+// (the address arithmetic costs more than the fuller cache lines save), so it is off by default.
 #ifndef DCOR_SLAB_WAVE
-#define DCOR_SLAB_WAVE 1
+#define DCOR_SLAB_WAVE 0
 #endif
 struct SlabMap {
   bool on;
@@ -399,8 +401,9 @@ struct SlabMap {
 // CEIL (Gaussian only; a measurement kernel, never a result): the same hot loop with its memory
 // side removed -- no slab store, no slow-normal queue or drain; an empty asm consumes the records
 // and the pending mask, so the compiler keeps every instruction that computes them.  Its time is
-// the loop's own VALU-issue ceiling (dcor_diag_sign_pass, bench.py roofline.issue_frac).
-template <int DGP, bool WAVE, bool CEIL = false>
+// the loop's own VALU-issue ceiling (dcor_diag_sign_pass, bench.py roofline.issue_frac).  CEIL = 2
+// keeps the slab stores only, CEIL = 3 the slow-normal queue and drain only (the cost of each).
+template <int DGP, bool WAVE, int CEIL = 0>
 __device__ __forceinline__ void sign_pass1_core(const SignConst& c, uint32_t rep,
                                                 uint32_t* __restrict__ slab,
                                                 double* __restrict__ sums_out, const double2* zt,
@@ -456,15 +459,20 @@ __device__ __forceinline__ void sign_pass1_core(const SignConst& c, uint32_t rep
       }
       hx += gx;
       hy += gy;
-      if constexpr (CEIL) {
-        asm volatile("" ::"v"(rec[0]), "v"(rec[1]), "v"(rec[2]), "v"(rec[3]), "v"(pend));
-        return;
+      if constexpr (CEIL == 1 || CEIL == 3)
+        asm volatile("" ::"v"(rec[0]), "v"(rec[1]), "v"(rec[2]), "v"(rec[3]));
+      if constexpr (CEIL == 1 || CEIL == 2) {
+        asm volatile("" ::"v"(pend));
+        if constexpr (CEIL == 1) return;
       }
-      if (FULL) {
-        *reinterpret_cast<uint4*>(slab + sm.pos(i0)) = make_uint4(rec[0], rec[1], rec[2], rec[3]);
-      } else {
-        for (int q = 0; q < 4; ++q) if ((int64_t)(i0 + q) < c.n) slab[i0 + q] = rec[q];
+      if constexpr (CEIL == 0 || CEIL == 2) {
+        if (FULL) {
+          *reinterpret_cast<uint4*>(slab + sm.pos(i0)) = make_uint4(rec[0], rec[1], rec[2], rec[3]);
+        } else {
+          for (int q = 0; q < 4; ++q) if ((int64_t)(i0 + q) < c.n) slab[i0 + q] = rec[q];
+        }
       }
+      if constexpr (CEIL == 2) return;
       if (pend) {
         uint32_t pos = atomicAdd(zqn, (uint32_t)__popc(pend));
         for (; pend; pend &= pend - 1u) zq[pos++] = i0 + (uint32_t)(__ffs(pend) - 1);
@@ -472,7 +480,7 @@ __device__ __forceinline__ void sign_pass1_core(const SignConst& c, uint32_t rep
     };
     // the whole wave, converged: each lane takes queued samples lane, lane + 64, ...
     auto drain = [&]() {
-      if constexpr (CEIL) return;
+      if constexpr (CEIL == 1 || CEIL == 2) return;
       const uint32_t cnt = __builtin_amdgcn_readfirstlane(*zqn);
       if (cnt == 0) return;
       __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the placeholder records have landed
@@ -488,7 +496,12 @@ __device__ __forceinline__ void sign_pass1_core(const SignConst& c, uint32_t rep
         const double xc = rclip_fin(x, c.L), yc = rclip_fin(y, c.L);
         ks_acc(sx, xc);
         ks_acc(sy, yc);
-        slab[sm.pos(i)] = record_w(xc, yc, w3);
+        if constexpr (CEIL == 3) {
+          const uint32_t r = record_w(xc, yc, w3);
+          asm volatile("" ::"v"(r));
+        } else {
+          slab[sm.pos(i)] = record_w(xc, yc, w3);
+        }
       }
       wave_sync();
       if (lane == 0) *zqn = 0u;
@@ -501,9 +514,9 @@ __device__ __forceinline__ void sign_pass1_core(const SignConst& c, uint32_t rep
     for (int64_t b = WAVE ? 0 : 64 * wv; b < nfull; b += 2 * NT) {  // trip count uniform per wave
       double hx = 0.0, hy = 0.0;
       if (b + lane < nfull) group(b + lane, std::true_type(), hx, hy);
-      if (!CEIL && __builtin_amdgcn_readfirstlane(*zqn) > ZQ_CAP - 256) drain();
+      if ((CEIL == 0 || CEIL == 3) && __builtin_amdgcn_readfirstlane(*zqn) > ZQ_CAP - 256) drain();
       if (b + NT + lane < nfull) group(b + NT + lane, std::true_type(), hx, hy);
-      if (!CEIL && __builtin_amdgcn_readfirstlane(*zqn) > ZQ_CAP - 256) drain();
+      if ((CEIL == 0 || CEIL == 3) && __builtin_amdgcn_readfirstlane(*zqn) > ZQ_CAP - 256) drain();
       ks_acc(sx, hx);
       ks_acc(sy, hy);
     }
@@ -513,7 +526,7 @@ __device__ __forceinline__ void sign_pass1_core(const SignConst& c, uint32_t rep
       if (b + lane < nfull) group(b + lane, std::true_type(), hx, hy);
       ks_acc(sx, hx);
       ks_acc(sy, hy);
-      if (!CEIL && __builtin_amdgcn_readfirstlane(*zqn) > ZQ_CAP - 256) drain();
+      if ((CEIL == 0 || CEIL == 3) && __builtin_amdgcn_readfirstlane(*zqn) > ZQ_CAP - 256) drain();
     }
 #endif
     if ((c.n & 3) && tid == (int)(nfull % NT)) {
@@ -524,7 +537,7 @@ __device__ __forceinline__ void sign_pass1_core(const SignConst& c, uint32_t rep
     }
     drain();
   } else {
-    static_assert(!CEIL, "the ceiling kernel runs the Gaussian loop");
+    static_assert(CEIL == 0, "the ceiling kernel runs the Gaussian loop");
     // group g4 = samples 4 g4 .. 4 g4 + 3; FULL: all four exist (the hot loop has no guards)
     auto group = [&](int64_t g4, auto full_tag) {
       constexpr bool FULL = decltype(full_tag)::value;
@@ -575,7 +588,7 @@ __device__ __forceinline__ void sign_pass1_core(const SignConst& c, uint32_t rep
   }
 }
 
-template <int DGP, bool CEIL = false>
+template <int DGP, int CEIL = 0>
 __device__ __forceinline__ void sign_pass1_body(const SignConst& c, uint32_t rep,
                                                 uint32_t* __restrict__ slab,
                                                 double* __restrict__ sums_out) {
@@ -609,10 +622,13 @@ __global__ __launch_bounds__(DCOR_BLOCK, DCOR_P1_WPE) void k_sign_pass1(SignCons
                        scratch + (size_t)blockIdx.x * (size_t)c.n, sums + SIGN_SUMS * (size_t)blockIdx.x);
 }
 // The pass-1 ceiling (CEIL above): same grid, registers and occupancy target as k_sign_pass1.
+template <int CM>
 __global__ __launch_bounds__(DCOR_BLOCK, DCOR_P1_WPE) void k_sign_pass1_ceil(SignConst c,
+                                                                         uint32_t* __restrict__ scratch,
                                                                          double* __restrict__ sums) {
-  sign_pass1_body<DCOR_DGP_GAUSSIAN, true>(c, (uint32_t)(c.rep_begin + blockIdx.x), nullptr,
-                                           sums + SIGN_SUMS * (size_t)blockIdx.x);
+  sign_pass1_body<DCOR_DGP_GAUSSIAN, CM>(c, (uint32_t)(c.rep_begin + blockIdx.x),
+                                         scratch + (size_t)blockIdx.x * (size_t)c.n,
+                                         sums + SIGN_SUMS * (size_t)blockIdx.x);
 }
 
 // The private centres and scales from pass 1's sums (vert-cor.R:335-344): mean(xc) is the
@@ -2079,10 +2095,19 @@ int launch_sign_diag(const SignConst& c, int64_t reps, int which, uint32_t* slab
       // 11: at pass 1's occupancy (pass 1 holds more VGPRs and LDS than its ceiling); 13: its own
       size_t pad = 0;
       if (which == 11) {
-        const int e = occupancy_pad((const void*)k_sign_pass1<DCOR_DGP_GAUSSIAN>, (const void*)k_sign_pass1_ceil, &pad);
+        const int e = occupancy_pad((const void*)k_sign_pass1<DCOR_DGP_GAUSSIAN>, (const void*)k_sign_pass1_ceil<1>, &pad);
         if (e) return e;
       }
-      hipLaunchKernelGGL(k_sign_pass1_ceil, g, b, pad, st, c, sums);
+      hipLaunchKernelGGL(k_sign_pass1_ceil<1>, g, b, pad, st, c, slab, sums);
+      break;
+    }
+    case 14: case 15: {   // the ceiling plus the slab stores / plus the slow-normal queue
+      size_t pad = 0;
+      const void* k = which == 14 ? (const void*)k_sign_pass1_ceil<2> : (const void*)k_sign_pass1_ceil<3>;
+      const int e = occupancy_pad((const void*)k_sign_pass1<DCOR_DGP_GAUSSIAN>, k, &pad);
+      if (e) return e;
+      if (which == 14) hipLaunchKernelGGL(k_sign_pass1_ceil<2>, g, b, pad, st, c, slab, sums);
+      else hipLaunchKernelGGL(k_sign_pass1_ceil<3>, g, b, pad, st, c, slab, sums);
       break;
     }
     case 12: {

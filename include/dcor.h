@@ -118,7 +118,8 @@ int64_t dcor_device_bytes(void);
  * 2 pass 2 (reads them), 3 the epilogue (reads pass 2's partials); 11 the pass-1 ceiling and 12 the
  * pass-2 ceiling (Gaussian DGP, m = 8): the same loops with their memory side removed, at the real
  * passes' waves per SIMD -- their time is the instruction stream's own issue-bound time on this
- * GPU; 13 the pass-1 ceiling at its own (higher) occupancy.  Run 1, 2, 3 in that order
+ * GPU; 13 the pass-1 ceiling at its own (higher) occupancy; 14 / 15 the pass-1 ceiling plus
+ * only its slab stores / plus only its slow-normal queue (what each costs).  Run 1, 2, 3 in that order
  * on the same cell and reps (12 after 1).  No result is returned; time them with events. */
 int dcor_diag_sign_pass(const dcor_cell* cell, int64_t rep_begin, int64_t reps, int which, void* stream);
 /* Measurement only: passes 1 and 2 (as dcor_diag_sign_pass 1, 2, on the null stream) and, per
