@@ -381,6 +381,24 @@ __device__ __forceinline__ void exact_signs(const SignConst& c, const SignStd& s
 #ifndef DCOR_SLAB_WAVE
 #define DCOR_SLAB_WAVE 0
 #endif
+// DCOR_SLAB_NT: the slab's 16-B record stores (pass 1) and loads (pass 2, m = 8) non-temporal.
+#ifndef DCOR_SLAB_NT
+#define DCOR_SLAB_NT 0
+#endif
+typedef uint32_t dcor_u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void slab_st4(uint32_t* p, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+  if (DCOR_SLAB_NT)
+    __builtin_nontemporal_store((dcor_u32x4){a, b, c, d}, reinterpret_cast<dcor_u32x4*>(p));
+  else
+    *reinterpret_cast<uint4*>(p) = make_uint4(a, b, c, d);
+}
+__device__ __forceinline__ uint4 slab_ld4(const uint32_t* p) {
+  if (DCOR_SLAB_NT) {
+    const dcor_u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const dcor_u32x4*>(p));
+    return make_uint4(v.x, v.y, v.z, v.w);
+  }
+  return *reinterpret_cast<const uint4*>(p);
+}
 struct SlabMap {
   bool on;
   uint32_t nfb;   // samples in full 512-sample blocks
@@ -467,7 +485,7 @@ __device__ __forceinline__ void sign_pass1_core(const SignConst& c, uint32_t rep
       }
       if constexpr (CEIL == 0 || CEIL == 2) {
         if (FULL) {
-          *reinterpret_cast<uint4*>(slab + sm.pos(i0)) = make_uint4(rec[0], rec[1], rec[2], rec[3]);
+          slab_st4(slab + sm.pos(i0), rec[0], rec[1], rec[2], rec[3]);
         } else {
           for (int q = 0; q < 4; ++q) if ((int64_t)(i0 + q) < c.n) slab[i0 + q] = rec[q];
         }
@@ -566,7 +584,7 @@ __device__ __forceinline__ void sign_pass1_core(const SignConst& c, uint32_t rep
       ks_acc(sx, gx);
       ks_acc(sy, gy);
       if (FULL) {
-        *reinterpret_cast<uint4*>(slab + sm.pos(i0)) = make_uint4(rec[0], rec[1], rec[2], rec[3]);
+        slab_st4(slab + sm.pos(i0), rec[0], rec[1], rec[2], rec[3]);
       } else {
         for (int q = 0; q < 4; ++q) if ((int64_t)(i0 + q) < c.n) slab[i0 + q] = rec[q];
       }
@@ -834,8 +852,8 @@ __device__ __forceinline__ P2Result sign_pass2_core(const SignConst& c, uint32_t
     // compiler could merge the two copies across.  Loads past the end re-read the last batch.
     auto load_mem = [&](int64_t jj, uint4& lo, uint4& hi) {
       const int64_t jc = jj < c.k ? jj : c.k - 1;
-      lo = *reinterpret_cast<const uint4*>(slab + sm.pos((uint32_t)(8 * jc)));
-      hi = *reinterpret_cast<const uint4*>(slab + sm.pos((uint32_t)(8 * jc + 4)));
+      lo = slab_ld4(slab + sm.pos((uint32_t)(8 * jc)));
+      hi = slab_ld4(slab + sm.pos((uint32_t)(8 * jc + 4)));
     };
     auto load = [&](int64_t jj, uint4& lo, uint4& hi) {
       if constexpr (CEIL)
