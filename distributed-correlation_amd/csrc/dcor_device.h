@@ -172,15 +172,20 @@ __device__ __forceinline__ uint32_t zig_j2(uint32_t w2) { return w2 >> 22; }
 // The full draw from attempt 0's (A, H): fast test, then the wedge test (L >= 1) against
 // f(x) = exp(-x^2/2) compared in logs, or the base layer's tail (L = 0: Marsaglia's x = -log(U1)/r,
 // accepted when -2 log(U2) > x^2), and otherwise a new attempt from block (i, rep, ZIG, 2a + which).
+// Entry j of the layer table: from the caller's LDS copy `zt` when it has one (pass 1's drain:
+// a global load there would wait behind every slab store the wave has in flight), else global.
+__device__ __forceinline__ double2 zig_entry(const double2* zt, uint32_t j) {
+  return zt ? zt[j] : make_double2(dcor_zig_tab[j][0], dcor_zig_tab[j][1]);
+}
 __device__ __forceinline__ double zig_slow(uint32_t i, uint32_t which, uint32_t rep, uint32_t k0,
-                                        uint32_t k1, uint32_t A, uint32_t H) {
+                                        uint32_t k1, uint32_t A, uint32_t H, const double2* zt = nullptr) {
   for (uint32_t a = 0;; ++a) {
     const U4 q = philox(i, rep, DCOR_SITE_ZIG, 2u * a + which, k0, k1);
     if (a > 0) { A = q.w0; H = q.w1 & 0xffffu; }
     const uint32_t j = H >> 6, L = j >> 1;
-    const double sx = dcor_zig_tab[j][0];
-    const double x = fma(zig_d(A, zig_y_lo(H)), sx, -sx);
-    if (fabs(x) < dcor_zig_tab[j][1]) return x;
+    const double2 t = zig_entry(zt, j);
+    const double x = fma(zig_d(A, zig_y_lo(H)), t.x, -t.x);
+    if (fabs(x) < t.y) return x;
     if (L == 0) {
       for (uint32_t t = 0;; ++t) {
         const U4 b = philox(i, rep, DCOR_SITE_ZIG_TAIL, 2u * t + which, k0, k1);
@@ -196,12 +201,12 @@ __device__ __forceinline__ double zig_slow(uint32_t i, uint32_t which, uint32_t 
 
 // One draw: the fast path inline, the rest out of line.
 __device__ __forceinline__ double zig_draw(uint32_t i, uint32_t which, uint32_t rep, uint32_t k0,
-                                           uint32_t k1, uint32_t A, uint32_t H) {
+                                           uint32_t k1, uint32_t A, uint32_t H, const double2* zt = nullptr) {
   const uint32_t j = H >> 6;
-  const double sx = dcor_zig_tab[j][0];
-  const double x = fma(zig_d(A, zig_y_lo(H)), sx, -sx);
-  if (fabs(x) < dcor_zig_tab[j][1]) return x;
-  return zig_slow(i, which, rep, k0, k1, A, H);
+  const double2 t = zig_entry(zt, j);
+  const double x = fma(zig_d(A, zig_y_lo(H)), t.x, -t.x);
+  if (fabs(x) < t.y) return x;
+  return zig_slow(i, which, rep, k0, k1, A, H, zt);
 }
 
 // mu + A z of MASS::mvrnorm (vert-cor.R:389-394) for z = (z1, z2) (same code as oracle/orc_mvn_z).

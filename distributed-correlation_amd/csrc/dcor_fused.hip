@@ -28,10 +28,10 @@ template <> struct Dgp<DCOR_DGP_GAUSSIAN> {  // MASS::mvrnorm (vert-cor.R:389-39
   static constexpr int flip_src = FLIP_SPARE32;
   static __device__ __forceinline__ void one_w3(const DgpConst& g, uint32_t i, uint32_t rep,
                                                 uint32_t k0, uint32_t k1, double& x, double& y,
-                                                uint32_t& w3) {
+                                                uint32_t& w3, const double2* zt = nullptr) {
     const U4 w = draw(i, rep, DCOR_SITE_DGP_A, k0, k1);
-    const double z1 = zig_draw(i, 0u, rep, k0, k1, w.w0, w.w2 & 0xffffu);
-    const double z2 = zig_draw(i, 1u, rep, k0, k1, w.w1, w.w2 >> 16);
+    const double z1 = zig_draw(i, 0u, rep, k0, k1, w.w0, w.w2 & 0xffffu, zt);
+    const double z2 = zig_draw(i, 1u, rep, k0, k1, w.w1, w.w2 >> 16, zt);
     mvn_z(z1, z2, g.mu0, g.mu1, g.a00, g.a01, g.a10, g.a11, &x, &y);
     w3 = w.w3;
   }
@@ -411,7 +411,16 @@ struct SlabMap {
   }
 };
 
-#define ZQ_CAP 512  // per-wave queue; a group iteration adds at most 256 entries per wave
+// per-wave queue; a group adds at most 256 entries per wave and the loop drains above ZQ_CAP - 256,
+// so at C's n the queue (about 1.6 % of a wave's samples) is usually drained once, at the end.
+// 768: the workgroup's LDS (28.7 KB with the table) still fits five workgroups per CU.
+#ifndef DCOR_ZQ_CAP
+#define DCOR_ZQ_CAP 768
+#endif
+#define ZQ_CAP DCOR_ZQ_CAP
+#ifndef DCOR_DRAIN_LDS
+#define DCOR_DRAIN_LDS 1
+#endif
 
 // WAVE = false: one 256-thread workgroup per replicate; WAVE = true: one wave per replicate (the
 // caller's workgroup has loaded the ziggurat table `zt` into LDS once for all its replicates).
@@ -510,7 +519,9 @@ __device__ __forceinline__ void sign_pass1_core(const SignConst& c, uint32_t rep
         ks_acc(sy, -py);
         double x, y;
         uint32_t w3;
-        Dgp<DGP>::one_w3(c.g, i, rep, c.k0, c.k1, x, y, w3);
+        // the table from LDS in the workgroup kernel (the wave kernel keeps the global table: the
+        // LDS pointer costs it six VGPRs and a wave per SIMD)
+        Dgp<DGP>::one_w3(c.g, i, rep, c.k0, c.k1, x, y, w3, (WAVE || !DCOR_DRAIN_LDS) ? nullptr : zt);
         const double xc = rclip_fin(x, c.L), yc = rclip_fin(y, c.L);
         ks_acc(sx, xc);
         ks_acc(sy, yc);
