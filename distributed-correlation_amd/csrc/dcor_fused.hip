@@ -418,6 +418,9 @@ struct SlabMap {
 #define DCOR_ZQ_CAP 768
 #endif
 #define ZQ_CAP DCOR_ZQ_CAP
+#ifndef DCOR_ZQ_BALLOT
+#define DCOR_ZQ_BALLOT 1
+#endif
 #ifndef DCOR_DRAIN_LDS
 #define DCOR_DRAIN_LDS 1
 #endif
@@ -467,10 +470,13 @@ __device__ __forceinline__ void sign_pass1_core(const SignConst& c, uint32_t rep
     // takes the placeholder out and adds the true values (both compensated), so the hot loop
     // selects nothing.  The group's plain sums are added into (hx, hy); the caller folds them
     // into the compensated sums (with DCOR_P1_FOLD8, once per two groups).
-    auto group = [&](int64_t g4, auto full_tag, double& hx, double& hy) {
+    // The group's slow samples (pend bit q: sample i0 + q) are queued by the caller (enqueue),
+    // outside the lanes' divergent group branch.
+    auto group = [&](int64_t g4, auto full_tag, double& hx, double& hy, uint32_t& pend) {
       constexpr bool FULL = decltype(full_tag)::value;
       const uint32_t i0 = (uint32_t)(4 * g4);
-      uint32_t rec[4], pend = 0;
+      uint32_t rec[4];
+      pend = 0;
       double gx, gy;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
@@ -499,16 +505,44 @@ __device__ __forceinline__ void sign_pass1_core(const SignConst& c, uint32_t rep
           for (int q = 0; q < 4; ++q) if ((int64_t)(i0 + q) < c.n) slab[i0 + q] = rec[q];
         }
       }
-      if constexpr (CEIL == 2) return;
+    };
+    // Queue the slow samples of every lane's group (converged; pend = 0 in lanes without a group).
+    // DCOR_ZQ_BALLOT: slots from a wave prefix sum of the lanes' counts (three ballots and mbcnts)
+    // and the queue length kept wave-uniform in a register -- no LDS atomic to wait for, and the
+    // drain test is a scalar compare; else an LDS atomic per group and an LDS length.
+    uint32_t zc = 0;   // queue length (DCOR_ZQ_BALLOT)
+    auto enqueue = [&](uint32_t pend, uint32_t i0) {
+      if constexpr (CEIL == 1 || CEIL == 2) {
+        asm volatile("" ::"v"(pend));
+        return;
+      }
+#if DCOR_ZQ_BALLOT
+      const uint32_t cnt = (uint32_t)__popc(pend);   // 0..4
+      const uint64_t B0 = __ballot(cnt & 1u), B1 = __ballot(cnt & 2u), B2 = __ballot(cnt & 4u);
+      auto below = [](uint64_t m) {
+        return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+      };
+      uint32_t pos = zc + below(B0) + 2u * below(B1) + 4u * below(B2);
+      for (; pend; pend &= pend - 1u) zq[pos++] = i0 + (uint32_t)(__ffs(pend) - 1);
+      zc = __builtin_amdgcn_readfirstlane(zc + (uint32_t)(__popcll(B0) + 2 * __popcll(B1) + 4 * __popcll(B2)));
+#else
       if (pend) {
         uint32_t pos = atomicAdd(zqn, (uint32_t)__popc(pend));
         for (; pend; pend &= pend - 1u) zq[pos++] = i0 + (uint32_t)(__ffs(pend) - 1);
       }
+#endif
+    };
+    auto queued = [&]() -> uint32_t {
+#if DCOR_ZQ_BALLOT
+      return zc;
+#else
+      return __builtin_amdgcn_readfirstlane(*zqn);
+#endif
     };
     // the whole wave, converged: each lane takes queued samples lane, lane + 64, ...
     auto drain = [&]() {
       if constexpr (CEIL == 1 || CEIL == 2) return;
-      const uint32_t cnt = __builtin_amdgcn_readfirstlane(*zqn);
+      const uint32_t cnt = queued();
       if (cnt == 0) return;
       __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the placeholder records have landed
       for (uint32_t k = (uint32_t)lane; k < cnt; k += 64) {
@@ -533,7 +567,11 @@ __device__ __forceinline__ void sign_pass1_core(const SignConst& c, uint32_t rep
         }
       }
       wave_sync();
+#if DCOR_ZQ_BALLOT
+      zc = 0;
+#else
       if (lane == 0) *zqn = 0u;
+#endif
       wave_sync();
     };
 #if DCOR_P1_FOLD8
@@ -542,27 +580,37 @@ __device__ __forceinline__ void sign_pass1_core(const SignConst& c, uint32_t rep
     // differ from per-group folds; the private centres they decide are unchanged in practice)
     for (int64_t b = WAVE ? 0 : 64 * wv; b < nfull; b += 2 * NT) {  // trip count uniform per wave
       double hx = 0.0, hy = 0.0;
-      if (b + lane < nfull) group(b + lane, std::true_type(), hx, hy);
-      if ((CEIL == 0 || CEIL == 3) && __builtin_amdgcn_readfirstlane(*zqn) > ZQ_CAP - 256) drain();
-      if (b + NT + lane < nfull) group(b + NT + lane, std::true_type(), hx, hy);
-      if ((CEIL == 0 || CEIL == 3) && __builtin_amdgcn_readfirstlane(*zqn) > ZQ_CAP - 256) drain();
+      uint32_t pa = 0, pb = 0;
+      if (b + lane < nfull) group(b + lane, std::true_type(), hx, hy, pa);
+      enqueue(pa, (uint32_t)(4 * (b + lane)));
+      if ((CEIL == 0 || CEIL == 3) && queued() > ZQ_CAP - 256) drain();
+      if (b + NT + lane < nfull) group(b + NT + lane, std::true_type(), hx, hy, pb);
+      enqueue(pb, (uint32_t)(4 * (b + NT + lane)));
+      if ((CEIL == 0 || CEIL == 3) && queued() > ZQ_CAP - 256) drain();
       ks_acc(sx, hx);
       ks_acc(sy, hy);
     }
 #else
     for (int64_t b = WAVE ? 0 : 64 * wv; b < nfull; b += NT) {  // trip count uniform per wave
       double hx = 0.0, hy = 0.0;
-      if (b + lane < nfull) group(b + lane, std::true_type(), hx, hy);
+      uint32_t pa = 0;
+      if (b + lane < nfull) group(b + lane, std::true_type(), hx, hy, pa);
+      enqueue(pa, (uint32_t)(4 * (b + lane)));
       ks_acc(sx, hx);
       ks_acc(sy, hy);
-      if ((CEIL == 0 || CEIL == 3) && __builtin_amdgcn_readfirstlane(*zqn) > ZQ_CAP - 256) drain();
+      if ((CEIL == 0 || CEIL == 3) && queued() > ZQ_CAP - 256) drain();
     }
 #endif
-    if ((c.n & 3) && tid == (int)(nfull % NT)) {
+    {  // the partial last group (n % 4), converged around its enqueue
       double hx = 0.0, hy = 0.0;
-      group(nfull, std::false_type(), hx, hy);
-      ks_acc(sx, hx);
-      ks_acc(sy, hy);
+      uint32_t pa = 0;
+      const bool last = (c.n & 3) && tid == (int)(nfull % NT);
+      if (last) group(nfull, std::false_type(), hx, hy, pa);
+      enqueue(pa, (uint32_t)(4 * nfull));
+      if (last) {
+        ks_acc(sx, hx);
+        ks_acc(sy, hy);
+      }
     }
     drain();
   } else {
