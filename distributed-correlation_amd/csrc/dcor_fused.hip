@@ -411,17 +411,14 @@ struct SlabMap {
   }
 };
 
-// per-wave queue; a group adds at most 256 entries per wave and the loop drains above ZQ_CAP - 256,
-// so at C's n the queue (about 1.6 % of a wave's samples) is usually drained once, at the end.
-// 768: the workgroup's LDS (28.7 KB with the table) still fits five workgroups per CU.
+// Per-wave slow-normal queue: a loop step adds at most 512 entries per wave (two groups), so the loop
+// drains above ZQ_CAP - 512; about 1.6 % of a wave's samples are queued, so at the headline's n a
+// wave drains one to three times per replicate.  768: the workgroup's LDS (28.7 KB with the table)
+// still fits five workgroups per CU.
 #ifndef DCOR_ZQ_CAP
 #define DCOR_ZQ_CAP 768
 #endif
 #define ZQ_CAP DCOR_ZQ_CAP
-// DCOR_ZQ_BALLOT=1: queue slots from ballots (measured slower than the LDS atomic: 535 vs 523 us)
-#ifndef DCOR_ZQ_BALLOT
-#define DCOR_ZQ_BALLOT 0
-#endif
 // Diagnostic builds only: the CEIL = 3 kernel queues but skips the regeneration in its drain.
 #ifndef DCOR_DIAG_NODRAIN
 #define DCOR_DIAG_NODRAIN 0
@@ -511,48 +508,33 @@ __device__ __forceinline__ void sign_pass1_core(const SignConst& c, uint32_t rep
         }
       }
     };
-    // Queue the slow samples of every lane's group (converged; pend = 0 in lanes without a group).
-    // DCOR_ZQ_BALLOT: slots from a wave prefix sum of the lanes' counts (three ballots and mbcnts)
-    // and the queue length kept wave-uniform in a register -- no LDS atomic to wait for, and the
-    // drain test is a scalar compare; else an LDS atomic per group and an LDS length.
-    uint32_t zc = 0;   // queue length (DCOR_ZQ_BALLOT)
-    auto enqueue = [&](uint32_t pend, uint32_t i0) {
+    // Queue the slow samples of a step's groups (pa: samples ia + q, pb: ib + q; 0 in lanes without
+    // a group) with one LDS atomic per step, and report whether the queue passed `limit`: the lanes'
+    // reserved ranges [pos, pos + cnt) tile [old length, new length), so the largest end among them
+    // is the new length -- one compare and a ballot, no read of the length back from LDS.
+    auto enqueue = [&](uint32_t pa, uint32_t ia, uint32_t pb, uint32_t ib, uint32_t limit) -> bool {
       if constexpr (CEIL == 1 || CEIL == 2) {
-        asm volatile("" ::"v"(pend));
-        return;
+        asm volatile("" ::"v"(pa), "v"(pb));
+        return false;
       }
-#if DCOR_ZQ_BALLOT
-      const uint32_t cnt = (uint32_t)__popc(pend);   // 0..4
-      const uint64_t B0 = __ballot(cnt & 1u), B1 = __ballot(cnt & 2u), B2 = __ballot(cnt & 4u);
-      auto below = [](uint64_t m) {
-        return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-      };
-      uint32_t pos = zc + below(B0) + 2u * below(B1) + 4u * below(B2);
-      for (; pend; pend &= pend - 1u) zq[pos++] = i0 + (uint32_t)(__ffs(pend) - 1);
-      zc = __builtin_amdgcn_readfirstlane(zc + (uint32_t)(__popcll(B0) + 2 * __popcll(B1) + 4 * __popcll(B2)));
-#else
-      if (pend) {
-        uint32_t pos = atomicAdd(zqn, (uint32_t)__popc(pend));
-        for (; pend; pend &= pend - 1u) zq[pos++] = i0 + (uint32_t)(__ffs(pend) - 1);
+      bool over = false;
+      if (pa | pb) {
+        const uint32_t cnt = (uint32_t)(__popc(pa) + __popc(pb));
+        uint32_t pos = atomicAdd(zqn, cnt);
+        over = pos + cnt > limit;
+        for (; pa; pa &= pa - 1u) zq[pos++] = ia + (uint32_t)(__ffs(pa) - 1);
+        for (; pb; pb &= pb - 1u) zq[pos++] = ib + (uint32_t)(__ffs(pb) - 1);
       }
-#endif
-    };
-    auto queued = [&]() -> uint32_t {
-#if DCOR_ZQ_BALLOT
-      return zc;
-#else
-      return __builtin_amdgcn_readfirstlane(*zqn);
-#endif
+      return __ballot(over) != 0;
     };
     // the whole wave, converged: each lane takes queued samples lane, lane + 64, ...
     auto drain = [&]() {
       if constexpr (CEIL == 1 || CEIL == 2) return;
-      const uint32_t cnt = queued();
+      const uint32_t cnt = __builtin_amdgcn_readfirstlane(*zqn);
       if (cnt == 0) return;
       if constexpr (CEIL == 3 && DCOR_DIAG_NODRAIN) {
         wave_sync();
         if (lane == 0) *zqn = 0u;
-        zc = 0;
         wave_sync();
         return;
       }
@@ -579,38 +561,31 @@ __device__ __forceinline__ void sign_pass1_core(const SignConst& c, uint32_t rep
         }
       }
       wave_sync();
-#if DCOR_ZQ_BALLOT
-      zc = 0;
-#else
       if (lane == 0) *zqn = 0u;
-#endif
       wave_sync();
     };
 #if DCOR_P1_FOLD8
     // two groups per step (wave groups b + lane and b + NT + lane), one compensated fold of their
     // plain 8-sample sums: half the TwoSum chains of a fold per group (the low bits of the sums
-    // differ from per-group folds; the private centres they decide are unchanged in practice)
+    // differ from per-group folds; the private centres they decide are unchanged in practice).  A
+    // step queues at most 512 entries per wave, so the queue drains above ZQ_CAP - 512.
     for (int64_t b = WAVE ? 0 : 64 * wv; b < nfull; b += 2 * NT) {  // trip count uniform per wave
       double hx = 0.0, hy = 0.0;
       uint32_t pa = 0, pb = 0;
       if (b + lane < nfull) group(b + lane, std::true_type(), hx, hy, pa);
-      enqueue(pa, (uint32_t)(4 * (b + lane)));
-      if ((CEIL == 0 || CEIL == 3) && queued() > ZQ_CAP - 256) drain();
       if (b + NT + lane < nfull) group(b + NT + lane, std::true_type(), hx, hy, pb);
-      enqueue(pb, (uint32_t)(4 * (b + NT + lane)));
-      if ((CEIL == 0 || CEIL == 3) && queued() > ZQ_CAP - 256) drain();
       ks_acc(sx, hx);
       ks_acc(sy, hy);
+      if (enqueue(pa, (uint32_t)(4 * (b + lane)), pb, (uint32_t)(4 * (b + NT + lane)), ZQ_CAP - 512)) drain();
     }
 #else
     for (int64_t b = WAVE ? 0 : 64 * wv; b < nfull; b += NT) {  // trip count uniform per wave
       double hx = 0.0, hy = 0.0;
       uint32_t pa = 0;
       if (b + lane < nfull) group(b + lane, std::true_type(), hx, hy, pa);
-      enqueue(pa, (uint32_t)(4 * (b + lane)));
       ks_acc(sx, hx);
       ks_acc(sy, hy);
-      if ((CEIL == 0 || CEIL == 3) && queued() > ZQ_CAP - 256) drain();
+      if (enqueue(pa, (uint32_t)(4 * (b + lane)), 0u, 0u, ZQ_CAP - 256)) drain();
     }
 #endif
     {  // the partial last group (n % 4), converged around its enqueue
@@ -618,7 +593,7 @@ __device__ __forceinline__ void sign_pass1_core(const SignConst& c, uint32_t rep
       uint32_t pa = 0;
       const bool last = (c.n & 3) && tid == (int)(nfull % NT);
       if (last) group(nfull, std::false_type(), hx, hy, pa);
-      enqueue(pa, (uint32_t)(4 * nfull));
+      (void)enqueue(pa, (uint32_t)(4 * nfull), 0u, 0u, ZQ_CAP);   // the final drain follows
       if (last) {
         ks_acc(sx, hx);
         ks_acc(sy, hy);
