@@ -26,13 +26,19 @@ template <> struct Dgp<DCOR_DGP_GAUSSIAN> {  // MASS::mvrnorm (vert-cor.R:389-39
   // 0xffff), z2 = zig(w1, w2 >> 16) (dcor_device.h), x = mu + A z; the sign family's INT flip is
   // w3 < ceil(p 2^32).
   static constexpr int flip_src = FLIP_SPARE32;
-  static __device__ __forceinline__ void one_w3(const DgpConst& g, uint32_t i, uint32_t rep,
-                                                uint32_t k0, uint32_t k1, double& x, double& y,
-                                                uint32_t& w3, const double2* zt = nullptr) {
-    const U4 w = draw(i, rep, DCOR_SITE_DGP_A, k0, k1);
+  // sample i from its DGP_A block w (= draw(i, rep, DGP_A))
+  static __device__ __forceinline__ void from_block(const DgpConst& g, uint32_t i, uint32_t rep, uint32_t k0,
+                                                    uint32_t k1, const U4& w, double& x, double& y,
+                                                    const double2* zt = nullptr) {
     const double z1 = zig_draw(i, 0u, rep, k0, k1, w.w0, w.w2 & 0xffffu, zt);
     const double z2 = zig_draw(i, 1u, rep, k0, k1, w.w1, w.w2 >> 16, zt);
     mvn_z(z1, z2, g.mu0, g.mu1, g.a00, g.a01, g.a10, g.a11, &x, &y);
+  }
+  static __device__ __forceinline__ void one_w3(const DgpConst& g, uint32_t i, uint32_t rep,
+                                                uint32_t k0, uint32_t k1, double& x, double& y,
+                                                uint32_t& w3) {
+    const U4 w = draw(i, rep, DCOR_SITE_DGP_A, k0, k1);
+    from_block(g, i, rep, k0, k1, w, x, y);
     w3 = w.w3;
   }
   static __device__ __forceinline__ void one(const DgpConst& g, uint32_t i, uint32_t rep,
@@ -541,15 +547,16 @@ __device__ __forceinline__ void sign_pass1_core(const SignConst& c, uint32_t rep
       __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the placeholder records have landed
       for (uint32_t k = (uint32_t)lane; k < cnt; k += 64) {
         const uint32_t i = zq[k];
+        const U4 w = draw(i, rep, DCOR_SITE_DGP_A, c.k0, c.k1);   // one block: placeholder and sample
         double px, py;
-        fast_xy(draw(i, rep, DCOR_SITE_DGP_A, c.k0, c.k1), px, py);
+        fast_xy(w, px, py);
         ks_acc(sx, -px);
         ks_acc(sy, -py);
         double x, y;
-        uint32_t w3;
+        const uint32_t w3 = w.w3;
         // the table from LDS in the workgroup kernel (the wave kernel keeps the global table: the
         // LDS pointer costs it six VGPRs and a wave per SIMD)
-        Dgp<DGP>::one_w3(c.g, i, rep, c.k0, c.k1, x, y, w3, (WAVE || !DCOR_DRAIN_LDS) ? nullptr : zt);
+        Dgp<DGP>::from_block(c.g, i, rep, c.k0, c.k1, w, x, y, (WAVE || !DCOR_DRAIN_LDS) ? nullptr : zt);
         const double xc = rclip_fin(x, c.L), yc = rclip_fin(y, c.L);
         ks_acc(sx, xc);
         ks_acc(sy, yc);
