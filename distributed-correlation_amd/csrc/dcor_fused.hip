@@ -417,10 +417,10 @@ struct SlabMap {
   }
 };
 
-// Per-wave slow-normal queue: a loop step adds at most 512 entries per wave (two groups), so the loop
-// drains above ZQ_CAP - 512; about 1.6 % of a wave's samples are queued, so at the headline's n a
-// wave drains one to three times per replicate.  768: the workgroup's LDS (28.7 KB with the table)
-// still fits five workgroups per CU.
+// Per-wave slow-normal queue: a group adds at most 256 entries per wave and the loop drains above
+// ZQ_CAP - 256; about 1.6 % of a wave's samples are queued, so at the headline's n a wave usually
+// drains once, at the end of its replicate.  768: the workgroup's LDS (28.7 KB with the table) still
+// fits five workgroups per CU.
 #ifndef DCOR_ZQ_CAP
 #define DCOR_ZQ_CAP 768
 #endif
@@ -514,25 +514,21 @@ __device__ __forceinline__ void sign_pass1_core(const SignConst& c, uint32_t rep
         }
       }
     };
-    // Queue the slow samples of a step's groups (pa: samples ia + q, pb: ib + q; 0 in lanes without
-    // a group) with one LDS atomic per step, and report whether the queue passed `limit`: the lanes'
-    // reserved ranges [pos, pos + cnt) tile [old length, new length), so the largest end among them
-    // is the new length -- one compare and a ballot, no read of the length back from LDS.
-    auto enqueue = [&](uint32_t pa, uint32_t ia, uint32_t pb, uint32_t ib, uint32_t limit) -> bool {
+    // Queue one group's slow samples (pend bit q: sample i0 + q; 0 in lanes without a group), one
+    // LDS atomic per group.  (Measured against: one atomic per two-group step with the drain test
+    // taken from the reservations -- its drain threshold has to be 512 lower, so the queue drains
+    // more often, 513 vs 497 us for the queue-only ceiling; ballot-allocated slots, 535 vs 523 us.)
+    auto enqueue = [&](uint32_t pend, uint32_t i0) {
       if constexpr (CEIL == 1 || CEIL == 2) {
-        asm volatile("" ::"v"(pa), "v"(pb));
-        return false;
+        asm volatile("" ::"v"(pend));
+        return;
       }
-      bool over = false;
-      if (pa | pb) {
-        const uint32_t cnt = (uint32_t)(__popc(pa) + __popc(pb));
-        uint32_t pos = atomicAdd(zqn, cnt);
-        over = pos + cnt > limit;
-        for (; pa; pa &= pa - 1u) zq[pos++] = ia + (uint32_t)(__ffs(pa) - 1);
-        for (; pb; pb &= pb - 1u) zq[pos++] = ib + (uint32_t)(__ffs(pb) - 1);
+      if (pend) {
+        uint32_t pos = atomicAdd(zqn, (uint32_t)__popc(pend));
+        for (; pend; pend &= pend - 1u) zq[pos++] = i0 + (uint32_t)(__ffs(pend) - 1);
       }
-      return __ballot(over) != 0;
     };
+    auto full = [&]() { return (CEIL == 0 || CEIL == 3) && __builtin_amdgcn_readfirstlane(*zqn) > ZQ_CAP - 256; };
     // the whole wave, converged: each lane takes queued samples lane, lane + 64, ...
     auto drain = [&]() {
       if constexpr (CEIL == 1 || CEIL == 2) return;
@@ -574,25 +570,28 @@ __device__ __forceinline__ void sign_pass1_core(const SignConst& c, uint32_t rep
 #if DCOR_P1_FOLD8
     // two groups per step (wave groups b + lane and b + NT + lane), one compensated fold of their
     // plain 8-sample sums: half the TwoSum chains of a fold per group (the low bits of the sums
-    // differ from per-group folds; the private centres they decide are unchanged in practice).  A
-    // step queues at most 512 entries per wave, so the queue drains above ZQ_CAP - 512.
+    // differ from per-group folds; the private centres they decide are unchanged in practice)
     for (int64_t b = WAVE ? 0 : 64 * wv; b < nfull; b += 2 * NT) {  // trip count uniform per wave
       double hx = 0.0, hy = 0.0;
       uint32_t pa = 0, pb = 0;
       if (b + lane < nfull) group(b + lane, std::true_type(), hx, hy, pa);
+      enqueue(pa, (uint32_t)(4 * (b + lane)));
+      if (full()) drain();
       if (b + NT + lane < nfull) group(b + NT + lane, std::true_type(), hx, hy, pb);
+      enqueue(pb, (uint32_t)(4 * (b + NT + lane)));
+      if (full()) drain();
       ks_acc(sx, hx);
       ks_acc(sy, hy);
-      if (enqueue(pa, (uint32_t)(4 * (b + lane)), pb, (uint32_t)(4 * (b + NT + lane)), ZQ_CAP - 512)) drain();
     }
 #else
     for (int64_t b = WAVE ? 0 : 64 * wv; b < nfull; b += NT) {  // trip count uniform per wave
       double hx = 0.0, hy = 0.0;
       uint32_t pa = 0;
       if (b + lane < nfull) group(b + lane, std::true_type(), hx, hy, pa);
+      enqueue(pa, (uint32_t)(4 * (b + lane)));
       ks_acc(sx, hx);
       ks_acc(sy, hy);
-      if (enqueue(pa, (uint32_t)(4 * (b + lane)), 0u, 0u, ZQ_CAP - 256)) drain();
+      if (full()) drain();
     }
 #endif
     {  // the partial last group (n % 4), converged around its enqueue
@@ -600,7 +599,7 @@ __device__ __forceinline__ void sign_pass1_core(const SignConst& c, uint32_t rep
       uint32_t pa = 0;
       const bool last = (c.n & 3) && tid == (int)(nfull % NT);
       if (last) group(nfull, std::false_type(), hx, hy, pa);
-      (void)enqueue(pa, (uint32_t)(4 * nfull), 0u, 0u, ZQ_CAP);   // the final drain follows
+      enqueue(pa, (uint32_t)(4 * nfull));   // the final drain follows
       if (last) {
         ks_acc(sx, hx);
         ks_acc(sy, hy);
