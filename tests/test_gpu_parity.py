@@ -235,3 +235,25 @@ def test_fused_split_invariance_n1e6(dc):
     assert np.array_equal(a, b)
     assert np.all(np.isfinite(a))
     assert np.all((a[:, 1] <= a[:, 2]) & (a[:, 4] <= a[:, 5]))
+
+
+# Clip-saturated and degenerate Gaussian cells: the record-code window sits on E[clip(x)], the
+# private centres beside it, so samples pinned at the clip bound L tie a centre's code far more
+# often (each tie is regenerated exactly).  mu far outside [-L, L] clips every sample to +-L; a
+# near-zero sigma puts every sample at mu; sigma_x != sigma_y and rho = -1 stress the window per
+# coordinate.  Both kernel forms: the wave kernel (n <= 16384) and the workgroup kernel.
+SATURATED_CELLS = [
+    dict(n=20_000, rho=0.5, eps1=1.0, eps2=1.0, mu=(10.0, -10.0), sigma=(1.0, 1.0)),
+    dict(n=4_000, rho=0.5, eps1=1.0, eps2=1.0, mu=(10.0, 0.5), sigma=(1.0, 2.0)),
+    dict(n=30_000, rho=0.0, eps1=1.0, eps2=1.0, mu=(0.25, 0.25), sigma=(1e-9, 1e-9)),
+    dict(n=25_000, rho=-1.0, eps1=1.5, eps2=0.5, mu=(0.0, 3.0), sigma=(3.0, 0.5)),
+]
+
+
+@pytest.mark.parametrize("spec", SATURATED_CELLS)
+def test_saturated_cells_vs_oracle(dc, orc, spec):
+    from dcor.sim import CellSpec, simulate
+    cell = CellSpec(seed=3_000_011 + spec["n"], **spec)
+    got = simulate(cell, 6, rep_begin=2).cpu().numpy()
+    ref = orc.sim_reps(cell.to_c(), 2, 8)
+    assert_close(got, ref, what=f"saturated {spec}")
