@@ -85,7 +85,7 @@ def run_grid_gpu(cells, B, chunk=1 << 15):
 
 # config line -> its committed rocprofv3 summary (per-kernel times and counters)
 PROFILE_OF = {"VG": "vg", "SG": "sg", "C2": "c2", "C3": "c3", "C5": "c5", "C5-continuous": "c5c",
-              "C5-fused": "c5f", "S": "sg"}
+              "C5-fused": "c5f"}
 
 
 def measured(name):
@@ -265,7 +265,8 @@ def c5(R, panel="coded"):
          algorithmic_bytes_per_rep=per_rep, input_bytes_per_rep=read_rep,
          hbm_gbps=per_rep * R / t / 1e9, hbm_frac=per_rep * R / t / HBM_PEAK,
          input_gbps=read_rep * R / t / 1e9, panel=panel, **cpu,
-         kernel="dictionary-coded LDS panel" if ok.value else "L2-gather packed panel",
+         kernel=("dictionary-coded LDS panel (k_premat_subg_dict)" if ok.value else
+                 "uncoded panel: LDS tiles (k_premat_subg_tiled) for m = 2, else L2 gathers"),
          note="synthetic stand-in panel; noise pre-generated on device (dcor_draws_launch / "
               "dcor_perm_launch); timed = one dcor_premat_subg_panel_launch (stream + epilogue) over a panel "
               "encoded once by dcor_panel_create")
