@@ -205,7 +205,24 @@ def spawn_ranks(n: int, argv) -> int:
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env))
-    rcs = [p.wait() for p in procs]
+    # a rank that fails leaves the others blocked in the rendezvous or a collective: stop them
+    rcs = [None] * n
+    while any(rc is None for rc in rcs):
+        for r, p in enumerate(procs):
+            if rcs[r] is None:
+                rcs[r] = p.poll()
+        if any(rc not in (None, 0) for rc in rcs):
+            for p in procs:
+                if p.poll() is None:
+                    p.terminate()
+            for r, p in enumerate(procs):
+                try:
+                    rcs[r] = p.wait(timeout=30)
+                except subprocess.TimeoutExpired:
+                    p.kill()
+                    rcs[r] = p.wait()
+            break
+        time.sleep(0.2)
     bad = [rc for rc in rcs if rc != 0]
     if bad:
         print(f"bench.py: rank exit codes {rcs}", file=sys.stderr)
@@ -250,6 +267,8 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if args.dry_run:
+        if os.environ.get("DCOR_BENCH_FAIL_RANK") == str(rank):   # launcher test: a rank that dies
+            sys.exit(3)
         return dry_run(world, rank)
     cpu = None
     if world == 1 and not args.no_cpu_baseline:   # before the GPU is touched (the pool forks nothing)

@@ -45,3 +45,13 @@ def test_more_gpus_than_visible_is_refused():
     p = _run(["--gpus", "2", "--no-cpu-baseline"], env={"HIP_VISIBLE_DEVICES": ""})
     assert p.returncode != 0
     assert "visible" in p.stderr
+
+
+def test_failing_rank_stops_the_others():
+    """A rank that dies before the rendezvous must not leave the other ranks waiting in it: the
+    launcher stops them and exits non-zero, promptly."""
+    import time
+    t0 = time.time()
+    p = _run(["--gpus", "2", "--dry-run"], env={"DCOR_BENCH_FAIL_RANK": "1"})
+    assert p.returncode != 0
+    assert time.time() - t0 < 120
