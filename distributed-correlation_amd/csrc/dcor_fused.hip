@@ -417,10 +417,10 @@ struct SlabMap {
   }
 };
 
-// Per-wave slow-normal queue: a group adds at most 256 entries per wave and the loop drains above
-// ZQ_CAP - 256; about 1.6 % of a wave's samples are queued, so at the headline's n a wave usually
-// drains once, at the end of its replicate.  768: the workgroup's LDS (28.7 KB with the table) still
-// fits five workgroups per CU.
+// Per-wave slow-normal queue: a group adds at most 256 entries per wave (about 1.6 % of a wave's
+// samples are queued).  With DCOR_DRAIN_AT = 0 the loop drains the whole queue above ZQ_CAP - 256,
+// so at the headline's n a wave usually drains once, at the end of its replicate; 768: the
+// workgroup's LDS (28.7 KB with the table) still fits five workgroups per CU.
 #ifndef DCOR_ZQ_CAP
 #define DCOR_ZQ_CAP 768
 #endif
@@ -431,6 +431,15 @@ struct SlabMap {
 #endif
 #ifndef DCOR_DRAIN_LDS
 #define DCOR_DRAIN_LDS 1
+#endif
+// DCOR_DRAIN_AT > 0: a wave drains whole 64-entry rounds of its queue as soon as it holds
+// DCOR_DRAIN_AT entries (the rest stays queued for later), so its regenerations interleave with
+// the other waves' hot loops instead of all coinciding at the replicates' ends.  Measured (round 4,
+// headline, one box, two runs each): pass 1 506-511 us per chunk at 64, 510-511 at 128, 517-535
+// at 256, 514-519 draining at the end (0); 2.85e6-2.86e6 replicates/s against 2.81e6-2.83e6.
+// The drain order only moves the low bits of the compensated sums.
+#ifndef DCOR_DRAIN_AT
+#define DCOR_DRAIN_AT 64
 #endif
 
 // WAVE = false: one 256-thread workgroup per replicate; WAVE = true: one wave per replicate (the
@@ -528,20 +537,26 @@ __device__ __forceinline__ void sign_pass1_core(const SignConst& c, uint32_t rep
         for (; pend; pend &= pend - 1u) zq[pos++] = i0 + (uint32_t)(__ffs(pend) - 1);
       }
     };
-    auto full = [&]() { return (CEIL == 0 || CEIL == 3) && __builtin_amdgcn_readfirstlane(*zqn) > ZQ_CAP - 256; };
+    auto full = [&]() {
+      return (CEIL == 0 || CEIL == 3) &&
+             __builtin_amdgcn_readfirstlane(*zqn) > (DCOR_DRAIN_AT > 0 ? DCOR_DRAIN_AT - 1 : ZQ_CAP - 256);
+    };
     // the whole wave, converged: each lane takes queued samples lane, lane + 64, ...
-    auto drain = [&]() {
+    // part: the loop's early drains take the queue's top 64 floor(cnt / 64) entries; the final
+    // drain takes all
+    auto drain = [&](bool part) {
       if constexpr (CEIL == 1 || CEIL == 2) return;
       const uint32_t cnt = __builtin_amdgcn_readfirstlane(*zqn);
-      if (cnt == 0) return;
+      const uint32_t keep = (DCOR_DRAIN_AT > 0 && part) ? (cnt & 63u) : 0u;
+      if (cnt == keep) return;
       if constexpr (CEIL == 3 && DCOR_DIAG_NODRAIN) {
         wave_sync();
-        if (lane == 0) *zqn = 0u;
+        if (lane == 0) *zqn = keep;
         wave_sync();
         return;
       }
       __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the placeholder records have landed
-      for (uint32_t k = (uint32_t)lane; k < cnt; k += 64) {
+      for (uint32_t k = keep + (uint32_t)lane; k < cnt; k += 64) {
         const uint32_t i = zq[k];
         const U4 w = draw(i, rep, DCOR_SITE_DGP_A, c.k0, c.k1);   // one block: placeholder and sample
         double px, py;
@@ -564,7 +579,7 @@ __device__ __forceinline__ void sign_pass1_core(const SignConst& c, uint32_t rep
         }
       }
       wave_sync();
-      if (lane == 0) *zqn = 0u;
+      if (lane == 0) *zqn = keep;
       wave_sync();
     };
 #if DCOR_P1_FOLD8
@@ -576,10 +591,10 @@ __device__ __forceinline__ void sign_pass1_core(const SignConst& c, uint32_t rep
       uint32_t pa = 0, pb = 0;
       if (b + lane < nfull) group(b + lane, std::true_type(), hx, hy, pa);
       enqueue(pa, (uint32_t)(4 * (b + lane)));
-      if (full()) drain();
+      if (full()) drain(true);
       if (b + NT + lane < nfull) group(b + NT + lane, std::true_type(), hx, hy, pb);
       enqueue(pb, (uint32_t)(4 * (b + NT + lane)));
-      if (full()) drain();
+      if (full()) drain(true);
       ks_acc(sx, hx);
       ks_acc(sy, hy);
     }
@@ -591,7 +606,7 @@ __device__ __forceinline__ void sign_pass1_core(const SignConst& c, uint32_t rep
       enqueue(pa, (uint32_t)(4 * (b + lane)));
       ks_acc(sx, hx);
       ks_acc(sy, hy);
-      if (full()) drain();
+      if (full()) drain(true);
     }
 #endif
     {  // the partial last group (n % 4), converged around its enqueue
@@ -605,7 +620,7 @@ __device__ __forceinline__ void sign_pass1_core(const SignConst& c, uint32_t rep
         ks_acc(sy, hy);
       }
     }
-    drain();
+    drain(false);
   } else {
     static_assert(CEIL == 0, "the ceiling kernel runs the Gaussian loop");
     // group g4 = samples 4 g4 .. 4 g4 + 3; FULL: all four exist (the hot loop has no guards)
