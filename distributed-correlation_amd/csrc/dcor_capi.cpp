@@ -1160,7 +1160,12 @@ static int premat_subg_run(const dcor_premat_subg* d, const dcor_panel* panel, d
     if (!rc && hipEventRecord(pp->join, pp->s) != hipSuccess) rc = (int)hipGetLastError();
     if (!rc && hipStreamWaitEvent((hipStream_t)stream, pp->join, 0) != hipSuccess) rc = (int)hipGetLastError();
   } else {
-    rc = launch_premat_subg(p, d->reps, part, d_out, stream);
+    // the tiled path's INT kernel may run on the auxiliary stream (DCOR_TILED_INT=2)
+    Pipe* pp = nullptr;
+    const char* iv = std::getenv("DCOR_TILED_INT");
+    if (iv && std::strcmp(iv, "2") == 0 && pipe_get(&pp) != 0) pp = nullptr;
+    rc = launch_premat_subg(p, d->reps, part, d_out, stream, nullptr, nullptr, pp ? pp->s : nullptr,
+                            pp ? pp->fork : nullptr, pp ? pp->join : nullptr);
   }
   (void)hipFreeAsync(part, (hipStream_t)stream);
   if (rc) return hip_fail((hipError_t)rc, "premat_subg launch");

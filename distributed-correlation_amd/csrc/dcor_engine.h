@@ -230,8 +230,11 @@ int launch_premat_sign(const PrematSignConst& c, int64_t reps, dcor_rep_out* out
 // scratch the launch packs; n <= DCOR_DICT_NMAX); part: reps * 80 B.
 int launch_hrs_fused(const PrematSubgConst& c, uint64_t seed_ni, uint64_t seed_int,
                      int64_t rep_begin, int64_t reps, void* part, dcor_rep_out* out, void* stream);
+// int_stream / ev_fork / ev_join: an auxiliary stream and two events for the tiled path's INT kernel
+// (DCOR_TILED_INT=2); without them that mode runs the INT sums inside the tiled kernel.
 int launch_premat_subg(const PrematSubgConst& c, int64_t reps, void* part, dcor_rep_out* out,
-                       void* stream, void* epi_stream = nullptr, void* ev = nullptr);
+                       void* stream, void* epi_stream = nullptr, void* ev = nullptr,
+                       void* int_stream = nullptr, void* ev_fork = nullptr, void* ev_join = nullptr);
 int launch_accumulate(const dcor_rep_out* d_out, int64_t count, double rho, dcor_accum* acc,
                       void* stream);
 int launch_mixquant(const double* z, const double* l, int32_t nsim, double c, int32_t pos,

@@ -743,13 +743,21 @@ __global__ __launch_bounds__(DICT_NT, WPE) void k_premat_subg_dict(PrematSubgCon
 // tiles (NI only).  Threads own INT pairs and NI batch pairs q = tid (mod NT), ascending, as in
 // the L2 kernel; PG adds the two terms of an INT pair (of a batch pair) plainly and compensates
 // the pair sums, as the L2 kernel does, so with NT = 512 and NA = 1 the sums are its bit for bit.
-// Measured (C5-continuous, 8192 replicates): 1.08 ms against 1.28 ms for the L2 kernel.  The
-// HBM stream is not what binds: with every load removed the kernel still takes 0.6 ms (fp64
-// compensated sums at one or two workgroups per CU, behind the tile barriers), and each class
-// of loads removed (noise, panel, permutations, gathers) takes off 0.1-0.3 ms.
+// Measured (C5-continuous, 8192 replicates, round 4, with the epilogue): 1.05 ms with the INT
+// stream in the first round's fills; without it (timing ablations, DCOR_TILED_ABL) 0.68 ms, without
+// the gathers 0.91, without the NI noise 0.93.  The INT stream therefore runs in a kernel of its
+// own by default (k_premat_subg_int; tiled_kernel() below).  A round issues all its batch-index
+// loads, and later all its noise loads, before it waits for any: one HBM round trip each per
+// round (a per-pair branch around each load had made them five).
 // NT threads per workgroup; NQ batch pairs per thread per round; FU fill pairs per loop trip; GB
 // batch pairs gathered per scheduling group; NA accumulator sets; WPE waves per SIMD.
-template <int NT, int NQ, int FU, int GB, int NA, int WPE, bool PG = false>
+// DCOR_TILED_ABL (timing ablations, wrong results): 1 no INT stream, 2 no gathers, 3 no NI noise.
+#ifndef DCOR_TILED_ABL
+#define DCOR_TILED_ABL 0
+#endif
+// INTK = false: the INT sums are left to k_premat_subg_int (s[6..9] of each partial); the kernel
+// then streams no INT bytes, writes s[0..5] only and needs 106 VGPRs instead of 128.
+template <int NT, int NQ, int FU, int GB, int NA, int WPE, bool PG = false, bool INTK = true>
 __global__ __launch_bounds__(NT, WPE) void k_premat_subg_tiled(PrematSubgConst p,
                                                               const int* __restrict__ dict_ok,
                                                               int64_t reps, int64_t tile_pairs_,
@@ -814,17 +822,24 @@ __global__ __launch_bounds__(NT, WPE) void k_premat_subg_tiled(PrematSubgConst p
     };
     // rounds of NQ * NT batch pairs; the INT terms ride along the first round's fills
     for (uint32_t qb = 0; qb == 0 || qb < nbp; qb += (uint32_t)NQ * NT) {
-      const bool first = qb == 0;
+      const bool first = INTK && qb == 0 && DCOR_TILED_ABL != 1;
       uint32_t sa[NQ], sb[NQ];  // (a | b << 16) of the pair's two batches
       double ax[NQ][2], ay[NQ][2];
+      // every load of the round first (a pair past the last re-reads the last), then the packing:
+      // one HBM round trip per round instead of one per batch pair
+      iv4 pr[NQ];
+#pragma unroll
+      for (int u = 0; u < NQ; ++u) {
+        const uint32_t q = qb + tid + (uint32_t)u * NT;
+        pr[u] = __builtin_nontemporal_load(p4 + (q < nbp ? q : nbp - 1));
+      }
 #pragma unroll
       for (int u = 0; u < NQ; ++u) {
         const uint32_t q = qb + tid + (uint32_t)u * NT;
         sa[u] = sb[u] = 0xFFFFFFFFu;  // 65535 is never a sample index (n < 65536)
         if (q < nbp) {
-          const iv4 pr = __builtin_nontemporal_load(p4 + q);
-          sa[u] = (uint32_t)pr.x | ((uint32_t)pr.y << 16);
-          sb[u] = (uint32_t)pr.z | ((uint32_t)pr.w << 16);
+          sa[u] = (uint32_t)pr[u].x | ((uint32_t)pr[u].y << 16);
+          sb[u] = (uint32_t)pr[u].z | ((uint32_t)pr[u].w << 16);
         }
         ax[u][0] = ax[u][1] = ay[u][0] = ay[u][1] = -0.0;
       }
@@ -883,7 +898,7 @@ __global__ __launch_bounds__(NT, WPE) void k_premat_subg_tiled(PrematSubgConst p
         __syncthreads();
         // gather: every index of this thread's batch pairs against the tile
 #pragma unroll
-        for (int u = 0; u < NQ; ++u) {
+        for (int u = 0; u < (DCOR_TILED_ABL == 2 ? 0 : NQ); ++u) {
           const uint32_t i0 = sa[u] & 0xFFFFu, i1 = sa[u] >> 16, i2 = sb[u] & 0xFFFFu, i3 = sb[u] >> 16;
           const double2 t0 = tile[min(i0 - lo, tn)], t1 = tile[min(i1 - lo, tn)];
           const double2 t2 = tile[min(i2 - lo, tn)], t3 = tile[min(i3 - lo, tn)];
@@ -901,12 +916,23 @@ __global__ __launch_bounds__(NT, WPE) void k_premat_subg_tiled(PrematSubgConst p
         wave_put(3, merged(sU));
         wave_put(4, merged(sU2));
       }
-      // NI terms of this round's batch pairs, ascending q (real-data-sims.R:131-137)
+      // NI terms of this round's batch pairs, ascending q (real-data-sims.R:131-137); the noise
+      // of every pair loaded first (past the last pair: the last pair's), one round trip per round
+      dv2 nx[NQ], ny[NQ];
+#pragma unroll
+      for (int u = 0; u < NQ; ++u) {
+        const uint32_t q = qb + tid + (uint32_t)u * NT, qc = q < nbp ? q : nbp - 1;
+        if (DCOR_TILED_ABL == 3) {
+          nx[u] = dv2{(double)sa[u], (double)sb[u]}; ny[u] = nx[u];
+        } else {
+          nx[u] = __builtin_nontemporal_load(x2 + qc); ny[u] = __builtin_nontemporal_load(y2 + qc);
+        }
+      }
 #pragma unroll
       for (int u = 0; u < NQ; ++u) {
         const uint32_t q = qb + tid + (uint32_t)u * NT;
         if (q < nbp) {
-          const dv2 lx = __builtin_nontemporal_load(x2 + q), ly = __builtin_nontemporal_load(y2 + q);
+          const dv2 lx = nx[u], ly = ny[u];
           if (PG) {  // the pair's two batch terms added plainly, the pair sums compensated
             const double xt0 = ax[u][0] * 0.5 + c.bx * lx[0], yt0 = ay[u][0] * 0.5 + c.by * ly[0];
             const double xt1 = ax[u][1] * 0.5 + c.bx * lx[1], yt1 = ay[u][1] * 0.5 + c.by * ly[1];
@@ -932,13 +958,100 @@ __global__ __launch_bounds__(NT, WPE) void k_premat_subg_tiled(PrematSubgConst p
     wave_put(1, merged(sT));
     wave_put(2, merged(sT2));
     __syncthreads();
-    if (tid < 5) {
+    if (tid < (INTK ? 5u : 3u)) {
       DD a{rb[(2 * tid) * NW], rb[(2 * tid + 1) * NW]};
 #pragma unroll
       for (int w = 1; w < NW; ++w)
         a = dd_add(a, DD{rb[(2 * tid) * NW + w], rb[(2 * tid + 1) * NW + w]});
       part[it].s[2 * tid] = a.hi;
       part[it].s[2 * tid + 1] = a.lo;
+    }
+  }
+}
+
+// The INT sums of the tiled kernel's replicates in a kernel of their own (real-data-sims.R:
+// 176-252; ver-cor-subG.R:88-90): the packed clipped (S, O) panel and each replicate's local noise
+// streamed once, R replicates per workgroup sharing every panel load, with no tile phases or
+// barriers between the loads.  The work split and summation order are the tiled kernel's (INT
+// pairs q = t (mod 512) ascending in logical thread t, the odd tail sample last in thread 511,
+// wave sums folded over the 8 logical waves in order): 256 threads stand for the 512 logical
+// threads t and t + 256, so the sums are the tiled and L2 kernels' bit for bit.  Writes s[6..9]
+// of each replicate's partial; k_premat_subg_tiled<.., INTK = false> writes s[0..5].
+#ifndef DCOR_INT_WPE
+#define DCOR_INT_WPE 1
+#endif
+template <int R>
+__global__ __launch_bounds__(256, DCOR_INT_WPE) void k_premat_subg_int(PrematSubgConst p, int64_t reps,
+                                                         SubgPartial* __restrict__ part) {
+  constexpr int LNW = 8;                 // logical waves (512 logical threads)
+  __shared__ double red[R][4][LNW];      // [replicate][sU.hi, sU.lo, sU2.hi, sU2.lo][logical wave]
+  const SubgConst& c = p.s;
+  const uint32_t tid = threadIdx.x;
+  const uint32_t n = (uint32_t)c.n, np = n >> 1;
+  const double2* __restrict__ so = p.soc;
+  const int64_t r0 = (int64_t)blockIdx.x * R;
+  const double* ll[R];
+  bool al[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int64_t rep = r0 + r < reps ? r0 + r : reps - 1;  // a short last group recomputes, never writes
+    ll[r] = p.lap_local + rep * c.n;
+    al[r] = (reinterpret_cast<uintptr_t>(ll[r]) & 15) == 0;
+  }
+  auto ldp = [&](int r, uint32_t q) -> dv2 {
+    if (al[r]) return __builtin_nontemporal_load(reinterpret_cast<const dv2*>(ll[r]) + q);
+    dv2 v;
+    v.x = __builtin_nontemporal_load(ll[r] + 2 * q);
+    v.y = __builtin_nontemporal_load(ll[r] + 2 * q + 1);
+    return v;
+  };
+  DD sU[R][2] = {}, sU2[R][2] = {};      // [replicate][logical thread tid, tid + 256]
+  auto pair = [&](uint32_t q, DD (&a)[R][2], DD (&a2)[R][2], int set) {
+    const double2 v0 = so[2 * q], v1 = so[2 * q + 1];
+    dv2 l[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) l[r] = ldp(r, q);
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const double U0 = rclip((v0.x + c.bs * l[r].x) * v0.y, c.lr);
+      const double U1 = rclip((v1.x + c.bs * l[r].y) * v1.y, c.lr);
+      ks_acc(a[r][set], U0 + U1);
+      ks_acc(a2[r][set], U0 * U0 + U1 * U1);
+    }
+  };
+  for (uint32_t q = tid; q < np; q += 512) {
+    pair(q, sU, sU2, 0);
+    if (q + 256 < np) pair(q + 256, sU, sU2, 1);
+  }
+  if (tid == 255 && 2 * np < n) {        // logical thread 511: the odd tail sample
+    const double2 v = so[n - 1];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const double Uc = rclip((v.x + c.bs * ll[r][n - 1]) * v.y, c.lr);
+      ks_acc(sU[r][1], Uc);
+      ks_acc(sU2[r][1], Uc * Uc);
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < R; ++r)
+#pragma unroll
+    for (int set = 0; set < 2; ++set) {
+      const DD a = wave_sum_dd(sU[r][set]), a2 = wave_sum_dd(sU2[r][set]);
+      if ((tid & 63) == 0) {
+        const int w = set * 4 + (int)(tid >> 6);
+        red[r][0][w] = a.hi; red[r][1][w] = a.lo;
+        red[r][2][w] = a2.hi; red[r][3][w] = a2.lo;
+      }
+    }
+  __syncthreads();
+  if (tid < 2 * R) {
+    const int r = (int)tid >> 1, v = (int)tid & 1;
+    DD a{red[r][2 * v][0], red[r][2 * v + 1][0]};
+#pragma unroll
+    for (int w = 1; w < LNW; ++w) a = dd_add(a, DD{red[r][2 * v][w], red[r][2 * v + 1][w]});
+    if (r0 + r < reps) {
+      part[r0 + r].s[6 + 2 * v] = a.hi;
+      part[r0 + r].s[7 + 2 * v] = a.lo;
     }
   }
 }
@@ -1769,26 +1882,54 @@ static DictKernel l2_kernel() {
 }
 
 // Tiled uncoded-panel kernel variants (threads, batch pairs per thread per round, fill unroll,
-// gather group, accumulator sets, waves per SIMD, pair-grouped sums) and the LDS each workgroup
-// may give its tile.  Default: two 512-thread workgroups per CU, four 80-KB tiles and two rounds
-// at C5's n (C5-continuous: 1.08 ms per 8192 replicates against 1.28 ms for the L2-gather
-// kernel; 1.15 ms with per-term sums); its sums are the L2-gather kernel's bit for bit.  For A/B
-// (DCOR_TILED_VARIANT=1): one 1024-thread workgroup per CU with two 156-KB tiles (1.11 ms).
-// DCOR_TILED=0 runs the L2-gather kernel.
+// gather group, accumulator sets, waves per SIMD, pair-grouped sums, INT sums in the kernel) and
+// the LDS each workgroup may give its tile.  C5-continuous, 8192 replicates per launch (call incl.
+// the epilogue; round 4, one box):
+//   in-kernel INT sums, two 512-thread workgroups per CU, four 80-KB tiles   1.05 ms (0.39 of 8 TB/s)
+//   INT sums in k_premat_subg_int (serial), same tiled kernel               0.87 ms (0.47)
+//   INT sums in k_premat_subg_int, one 1024-thread workgroup per CU with
+//     two 156-KB tiles and one round of batch pairs (default)               0.82 ms (0.50)
+// Without the INT stream the tiled kernel needs 116 VGPRs instead of 128 (and no spills), and its
+// tile fills read the L2-resident panel only.  The 512-thread variant's sums are the L2-gather
+// kernel's bit for bit in every INT mode; the 1024-thread variant splits the batch pairs over
+// 1024 threads, so its NI sums differ from those in the low bits.  Measured and dropped: one
+// 512-thread workgroup per CU with ten batch pairs per thread (one round; 200 VGPRs, 0.38-0.40),
+// L2 warm-up loads of the noise phase during the last tile (0.39), barriers that wait for LDS
+// traffic only (no change), a wider fill unroll (no change), the INT kernel on the auxiliary
+// stream beside the tiled kernel (DCOR_TILED_INT=2: the two share the CUs' issue and memory
+// pipelines, 0.47).  DCOR_TILED_VARIANT=0 selects the 512-thread variant; DCOR_TILED=0 the
+// L2-gather kernel.
 struct TiledKernel {
   void (*k)(PrematSubgConst, const int*, int64_t, int64_t, SubgPartial*);
   int nt;
   size_t lds_budget;
 };
-static TiledKernel tiled_kernel() {
-  static const TiledKernel ks[2] = {{k_premat_subg_tiled<512, 5, 1, 1, 1, 4, true>, 512, 80 * 1024},
-                                    {k_premat_subg_tiled<1024, 5, 1, 1, 1, 4, true>, 1024, 160 * 1024}};
+// Where the tiled path's INT sums run (DCOR_TILED_INT): 0 inside the tiled kernel's first round of
+// tile fills; 1 (default) in k_premat_subg_int before it on the same stream; 2 in
+// k_premat_subg_int on the library's auxiliary stream beside it.
+static int tiled_int_mode() {
+  static const int m = [] {
+    const char* e = std::getenv("DCOR_TILED_INT");
+    const int x = e ? std::atoi(e) : 1;
+    return (x >= 0 && x <= 2) ? x : 1;
+  }();
+  return m;
+}
+#ifndef DCOR_INT_R
+#define DCOR_INT_R 2
+#endif
+static TiledKernel tiled_kernel(bool intk) {
+  static const TiledKernel ks[2][2] = {
+      {{k_premat_subg_tiled<512, 5, 1, 1, 1, 4, true>, 512, 80 * 1024},
+       {k_premat_subg_tiled<512, 5, 1, 1, 1, 4, true, false>, 512, 80 * 1024}},
+      {{k_premat_subg_tiled<1024, 5, 1, 1, 1, 4, true>, 1024, 160 * 1024},
+       {k_premat_subg_tiled<1024, 5, 1, 1, 1, 4, true, false>, 1024, 160 * 1024}}};
   static const int v = [] {
     const char* e = std::getenv("DCOR_TILED_VARIANT");
-    const int x = e ? std::atoi(e) : 0;
-    return (x >= 0 && x < 2) ? x : 0;
+    const int x = e ? std::atoi(e) : 1;
+    return (x >= 0 && x < 2) ? x : 1;
   }();
-  return ks[v];
+  return ks[v][intk ? 0 : 1];
 }
 static bool tiled_enabled() {
   static const bool on = [] {
@@ -1817,7 +1958,8 @@ static int premat_dict_slots(int64_t n, int* slots) {
 }
 
 int launch_premat_subg(const PrematSubgConst& c0, int64_t reps, void* part, dcor_rep_out* out,
-                       void* stream, void* epi_stream, void* ev) {
+                       void* stream, void* epi_stream, void* ev, void* int_stream, void* ev_fork,
+                       void* ev_join) {
   if (reps <= 0) return 0;
   PrematSubgConst c = c0;
   c.slices = 1;
@@ -1850,7 +1992,19 @@ int launch_premat_subg(const PrematSubgConst& c0, int64_t reps, void* part, dcor
                        dim3(DCOR_BLOCK), 0, (hipStream_t)stream, c, (double2*)c.xyc,
                        (double2*)c.soc);
     if (tiled) {
-      const TiledKernel tk = tiled_kernel();
+      // the INT sums in k_premat_subg_int: on the auxiliary stream when the caller gave one
+      const int im = tiled_int_mode();
+      const bool conc = im == 2 && int_stream != nullptr && ev_fork != nullptr && ev_join != nullptr;
+      const bool intk = im == 0 || (im == 2 && !conc);
+      // serial: before the tiled kernel; concurrent: submitted after it, so the tiled kernel's
+      // persistent workgroups are resident first and the INT workgroups fill what they leave
+      auto launch_int = [&](hipStream_t is) {
+        hipLaunchKernelGGL(k_premat_subg_int<DCOR_INT_R>, dim3((unsigned)((reps + DCOR_INT_R - 1) / DCOR_INT_R)),
+                           dim3(256), 0, is, c, reps, (SubgPartial*)part);
+      };
+      if (conc && hipEventRecord((hipEvent_t)ev_fork, (hipStream_t)stream) != hipSuccess) return last_err();
+      if (!intk && !conc) launch_int((hipStream_t)stream);
+      const TiledKernel tk = tiled_kernel(intk);
       const int64_t np = c.s.n >> 1;  // INT pairs (at most; h = 1 rows have (n - 1) / 2)
       const size_t red_b = (size_t)(20 * (tk.nt / 64)) * sizeof(double);
       const int64_t tp_max = (int64_t)((tk.lds_budget - red_b) / 16 - 3) / 2;
@@ -1870,6 +2024,12 @@ int launch_premat_subg(const PrematSubgConst& c0, int64_t reps, void* part, dcor
       const int64_t grid = reps < slots ? reps : slots;
       hipLaunchKernelGGL(tk.k, dim3((unsigned)grid), dim3((unsigned)tk.nt), lds, (hipStream_t)stream, c,
                          (const int*)c.dict_ok, reps, tile_pairs, (SubgPartial*)part);
+      if (conc) {
+        if (hipStreamWaitEvent((hipStream_t)int_stream, (hipEvent_t)ev_fork, 0) != hipSuccess) return last_err();
+        launch_int((hipStream_t)int_stream);
+        if (hipEventRecord((hipEvent_t)ev_join, (hipStream_t)int_stream) != hipSuccess) return last_err();
+        if (hipStreamWaitEvent((hipStream_t)stream, (hipEvent_t)ev_join, 0) != hipSuccess) return last_err();
+      }
     } else if (c.dict_built != 2) {
       const DictKernel kl = l2_kernel();
       const size_t lds = (size_t)(20 * DICT_NW) * sizeof(double);

@@ -333,13 +333,15 @@ def _premat_continuous_runs():
 
 
 def test_premat_tiled_kernel_matches_l2_kernel():
-    """Continuous panels, m = 2 (and one m > 2 case, which keeps the L2-gather kernel): the tiled
-    LDS kernel (default) returns the L2-gather kernel's bits (DCOR_TILED=0: same work split, same
-    pair-grouped sums), and the 1024-thread variant agrees within the estimator tolerance.
-    n = 1001 is one tile, 19,433 four (default) or two; 30,001 takes two rounds of batch pairs
-    in both variants, 19,433 in the default; odd n puts every other replicate's noise row off a
-    16-B boundary (the head-sample path).  The estimators against the oracle on this path:
-    test_gpu_more.py::test_premat_subg_hrs_shared_panel."""
+    """Continuous panels, m = 2 (and one m > 2 case, which keeps the L2-gather kernel).  The
+    512-thread tiled kernel (DCOR_TILED_VARIANT=0) returns the L2-gather kernel's bits (DCOR_TILED=0:
+    same work split, same pair-grouped sums) whether its INT sums run in k_premat_subg_int on the
+    same stream (default), on the auxiliary stream (DCOR_TILED_INT=2) or inside the tiled kernel
+    (DCOR_TILED_INT=0); the default 1024-thread variant splits the NI batch pairs over 1024 threads
+    and agrees within the estimator tolerance.  n = 1001 is one tile, 19,433 four (512 threads) or
+    two (1024); 30,001 takes two rounds of batch pairs in both variants, 19,433 in the 512-thread
+    one; odd n puts every other replicate's noise row off a 16-B boundary (the head-sample path).
+    The estimators against the oracle on this path: test_gpu_more.py::test_premat_subg_hrs_shared_panel."""
     import os
     import subprocess
     import sys
@@ -350,7 +352,10 @@ def test_premat_tiled_kernel_matches_l2_kernel():
     code = ("import sys, numpy as np; sys.path[:0] = %r; import test_gpu_hrs as t; "
             "np.savez(sys.argv[1], **t._premat_continuous_runs())") % (paths,)
     runs = {}
-    for name, env_over in (("l2", {"DCOR_TILED": "0"}), ("v1", {"DCOR_TILED_VARIANT": "1"})):
+    variants = (("l2", {"DCOR_TILED": "0"}), ("v0", {"DCOR_TILED_VARIANT": "0"}),
+                ("v0_aux", {"DCOR_TILED_VARIANT": "0", "DCOR_TILED_INT": "2"}),
+                ("v0_in", {"DCOR_TILED_VARIANT": "0", "DCOR_TILED_INT": "0"}))
+    for name, env_over in variants:
         with tempfile.TemporaryDirectory() as d:
             env = dict(os.environ, **env_over)
             subprocess.run([sys.executable, "-c", code, os.path.join(d, "o.npz")], check=True, env=env,
@@ -359,7 +364,8 @@ def test_premat_tiled_kernel_matches_l2_kernel():
             runs[name] = {key: o[key] for key in o.files}
     for key, v in got.items():
         assert np.isfinite(v).all()
-        np.testing.assert_array_equal(v.view(np.int64), runs["l2"][key].view(np.int64),
-                                      err_msg=f"{key}: tiled vs L2 kernel")
+        for name in ("v0", "v0_aux", "v0_in"):
+            np.testing.assert_array_equal(runs[name][key].view(np.int64), runs["l2"][key].view(np.int64),
+                                          err_msg=f"{key}: 512-thread tiled ({name}) vs L2 kernel")
         for r in range(len(v)):
-            assert_close(v[r], runs["v1"][key][r], what=f"{key} rep {r} default vs 1024-thread variant")
+            assert_close(v[r], runs["l2"][key][r], what=f"{key} rep {r} default vs L2 kernel")
