@@ -980,6 +980,9 @@ __global__ __launch_bounds__(NT, WPE) void k_premat_subg_tiled(PrematSubgConst p
 #ifndef DCOR_INT_WPE
 #define DCOR_INT_WPE 1
 #endif
+#ifndef DCOR_INT_PU
+#define DCOR_INT_PU 2
+#endif
 template <int R>
 __global__ __launch_bounds__(256, DCOR_INT_WPE) void k_premat_subg_int(PrematSubgConst p, int64_t reps,
                                                          SubgPartial* __restrict__ part) {
@@ -1006,22 +1009,32 @@ __global__ __launch_bounds__(256, DCOR_INT_WPE) void k_premat_subg_int(PrematSub
     return v;
   };
   DD sU[R][2] = {}, sU2[R][2] = {};      // [replicate][logical thread tid, tid + 256]
-  auto pair = [&](uint32_t q, DD (&a)[R][2], DD (&a2)[R][2], int set) {
-    const double2 v0 = so[2 * q], v1 = so[2 * q + 1];
-    dv2 l[R];
+  // PU pair slots per trip, q + 256 j (logical set j & 1): every load of the trip first (a slot past
+  // the last pair re-reads pair q), then the terms of the slots that exist, in ascending q
+  constexpr int PU = DCOR_INT_PU;
+  for (uint32_t q = tid; q < np; q += 256 * PU) {
+    double2 v0[PU], v1[PU];
+    dv2 l[PU][R];
 #pragma unroll
-    for (int r = 0; r < R; ++r) l[r] = ldp(r, q);
+    for (int j = 0; j < PU; ++j) {
+      const uint32_t qj = q + 256u * j < np ? q + 256u * j : q;
+      v0[j] = so[2 * qj];
+      v1[j] = so[2 * qj + 1];
 #pragma unroll
-    for (int r = 0; r < R; ++r) {
-      const double U0 = rclip((v0.x + c.bs * l[r].x) * v0.y, c.lr);
-      const double U1 = rclip((v1.x + c.bs * l[r].y) * v1.y, c.lr);
-      ks_acc(a[r][set], U0 + U1);
-      ks_acc(a2[r][set], U0 * U0 + U1 * U1);
+      for (int r = 0; r < R; ++r) l[j][r] = ldp(r, qj);
     }
-  };
-  for (uint32_t q = tid; q < np; q += 512) {
-    pair(q, sU, sU2, 0);
-    if (q + 256 < np) pair(q + 256, sU, sU2, 1);
+#pragma unroll
+    for (int j = 0; j < PU; ++j) {
+      if (j == 0 || q + 256u * j < np) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const double U0 = rclip((v0[j].x + c.bs * l[j][r].x) * v0[j].y, c.lr);
+          const double U1 = rclip((v1[j].x + c.bs * l[j][r].y) * v1[j].y, c.lr);
+          ks_acc(sU[r][j & 1], U0 + U1);
+          ks_acc(sU2[r][j & 1], U0 * U0 + U1 * U1);
+        }
+      }
+    }
   }
   if (tid == 255 && 2 * np < n) {        // logical thread 511: the odd tail sample
     const double2 v = so[n - 1];

@@ -1,7 +1,7 @@
 # rocprofv3 recipe for any workload: a kernel trace, then PMC passes (each in its own run, as the
 # guide prescribes), then profiles/<tag>_summary.{json,md} + <tag>_kernel_stats.csv.
 #   bash scripts/prof.sh <tag> <passes> -- <python args...>
-# passes: comma list of trace, fetch, write, sq, mix, tcp (default trace,fetch,write,sq,mix)
+# passes: comma list of trace, fetch, write, sq, mix, tcp, lds (default trace,fetch,write,sq,mix)
 # env: SERIAL=1 runs the sign path's chunks on one stream (DCOR_SIGN_PIPELINE=0: clean per-kernel
 #      counters); PROF_HEAD=<git head> is stamped into the summary (the GPU box has no .git).
 # Example: bash scripts/prof.sh r04_serial trace,sq,mix -- bench.py --steps 5 --warmup 1 --no-cpu-baseline
@@ -25,6 +25,7 @@ for p in ${PASSES//,/ }; do
     write) pmc write WRITE_SIZE ;;
     sq) pmc sq SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY SQ_WAIT_ANY GRBM_GUI_ACTIVE ;;
     mix) pmc mix SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_INSTS_VALU_CVT SQ_INSTS_SALU ;;
+    lds) pmc lds SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_INSTS_VALU SQ_WAVE_CYCLES GRBM_GUI_ACTIVE ;;
     tcp) pmc tcp TCP_TCC_READ_REQ_sum TCP_TOTAL_CACHE_ACCESSES_sum TCC_HIT_sum TCC_MISS_sum GRBM_GUI_ACTIVE ;;
     *) echo "unknown pass $p"; exit 2 ;;
   esac
