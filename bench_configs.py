@@ -266,7 +266,7 @@ def c5(R, panel="coded"):
          hbm_gbps=per_rep * R / t / 1e9, hbm_frac=per_rep * R / t / HBM_PEAK,
          input_gbps=read_rep * R / t / 1e9, panel=panel, **cpu,
          kernel=("dictionary-coded LDS panel (k_premat_subg_dict)" if ok.value else
-                 "uncoded panel: LDS tiles (k_premat_subg_tiled) for m = 2, else L2 gathers"),
+                 "uncoded panel: INT stream (k_premat_subg_int) + NI LDS tiles (k_premat_subg_tiled) for m = 2, else L2 gathers"),
          note="synthetic stand-in panel; noise pre-generated on device (dcor_draws_launch / "
               "dcor_perm_launch); timed = one dcor_premat_subg_panel_launch (stream + epilogue) over a panel "
               "encoded once by dcor_panel_create")
