@@ -775,6 +775,8 @@ __global__ __launch_bounds__(NT, WPE) void k_premat_subg_tiled(PrematSubgConst p
   const uint32_t n = (uint32_t)c.n;
   const uint32_t nbp = (uint32_t)(c.k >> 1);  // batch pairs (k even)
   const uint32_t tile_pairs = (uint32_t)tile_pairs_;
+  // the panel tile in LDS (its index; the panel is every replicate's) and the sweep direction
+  uint32_t held = 0xFFFFFFFFu, dir = 0u;
   for (int64_t it = blockIdx.x; it < reps; it += gridDim.x) {
     const int64_t rep = it;
     const double* __restrict__ ll = p.lap_local + rep * c.n;
@@ -843,59 +845,65 @@ __global__ __launch_bounds__(NT, WPE) void k_premat_subg_tiled(PrematSubgConst p
         }
         ax[u][0] = ax[u][1] = ay[u][0] = ay[u][1] = -0.0;
       }
-      for (uint32_t tp = 0; tp < ntiles; ++tp) {
+      for (uint32_t ti = 0; ti < ntiles; ++ti) {
+        // NI-only kernel: every other round sweeps the tiles in reverse, so it starts on the tile
+        // the previous round (of this replicate or the last) ended on, still in LDS
+        const uint32_t tp = (!INTK && dir) ? ntiles - 1 - ti : ti;
         const uint32_t pa = tp * tile_pairs;
         const uint32_t pb = pa + tile_pairs < np ? pa + tile_pairs : np;
         const uint32_t lo = tp == 0 ? 0u : h + 2 * pa;
         const uint32_t hi = tp == ntiles - 1 ? n : h + 2 * pb;
         const uint32_t tn = hi - lo;
-        __syncthreads();  // the previous tile's readers are done
-        // fill: this thread's INT pairs q = tid (mod NT) in [pa, pb), FU per loop trip
-        uint32_t q = pa + ((tid + NT - pa % NT) % NT);
-        for (; q + (FU - 1) * NT < pb; q += FU * NT) {
-          double2 a0[FU], a1[FU], s0[FU], s1[FU];
-          dv2 lv[FU];
+        if (INTK || tp != held) {
+          __syncthreads();  // the previous tile's readers are done
+          // fill: this thread's INT pairs q = tid (mod NT) in [pa, pb), FU per loop trip
+          uint32_t q = pa + ((tid + NT - pa % NT) % NT);
+          for (; q + (FU - 1) * NT < pb; q += FU * NT) {
+            double2 a0[FU], a1[FU], s0[FU], s1[FU];
+            dv2 lv[FU];
 #pragma unroll
-          for (int u = 0; u < FU; ++u) {
-            const uint32_t i = h + 2 * (q + u * NT);
-            a0[u] = xy[i]; a1[u] = xy[i + 1];
-            if (first) {
-              s0[u] = so[i]; s1[u] = so[i + 1];
-              lv[u] = ldp(q + u * NT);
+            for (int u = 0; u < FU; ++u) {
+              const uint32_t i = h + 2 * (q + u * NT);
+              a0[u] = xy[i]; a1[u] = xy[i + 1];
+              if (first) {
+                s0[u] = so[i]; s1[u] = so[i + 1];
+                lv[u] = ldp(q + u * NT);
+              }
             }
-          }
 #pragma unroll
-          for (int u = 0; u < FU; ++u) {
-            const uint32_t i = h + 2 * (q + u * NT);
-            tile[i - lo] = a0[u];
-            tile[i + 1 - lo] = a1[u];
-            if (first) {
-              if (PG) {
-                uterm2(s0[u], lv[u].x, s1[u], lv[u].y);
-              } else {
-                uterm(s0[u], lv[u].x, 0);
-                uterm(s1[u], lv[u].y, 1);
+            for (int u = 0; u < FU; ++u) {
+              const uint32_t i = h + 2 * (q + u * NT);
+              tile[i - lo] = a0[u];
+              tile[i + 1 - lo] = a1[u];
+              if (first) {
+                if (PG) {
+                  uterm2(s0[u], lv[u].x, s1[u], lv[u].y);
+                } else {
+                  uterm(s0[u], lv[u].x, 0);
+                  uterm(s1[u], lv[u].y, 1);
+                }
               }
             }
           }
-        }
-        for (; q < pb; q += NT) {
-          const uint32_t i = h + 2 * q;
-          tile[i - lo] = xy[i];
-          tile[i + 1 - lo] = xy[i + 1];
-          if (first) {
-            const dv2 l = ldp(q);
-            if (PG) {
-              uterm2(so[i], l.x, so[i + 1], l.y);
-            } else {
-              uterm(so[i], l.x, 0);
-              uterm(so[i + 1], l.y, 1);
+          for (; q < pb; q += NT) {
+            const uint32_t i = h + 2 * q;
+            tile[i - lo] = xy[i];
+            tile[i + 1 - lo] = xy[i + 1];
+            if (first) {
+              const dv2 l = ldp(q);
+              if (PG) {
+                uterm2(so[i], l.x, so[i + 1], l.y);
+              } else {
+                uterm(so[i], l.x, 0);
+                uterm(so[i + 1], l.y, 1);
+              }
             }
           }
+          if (tp == ntiles - 1 && h + 2 * np < n && tid == NT - 1) tile[n - 1 - lo] = xy[n - 1];
+          if (tid == 0) tile[tn] = make_double2(-0.0, -0.0);  // the out-of-tile sentinel
+          __syncthreads();
+          held = tp;
         }
-        if (tp == ntiles - 1 && h + 2 * np < n && tid == NT - 1) tile[n - 1 - lo] = xy[n - 1];
-        if (tid == 0) tile[tn] = make_double2(-0.0, -0.0);  // the out-of-tile sentinel
-        __syncthreads();
         // gather: every index of this thread's batch pairs against the tile
 #pragma unroll
         for (int u = 0; u < (DCOR_TILED_ABL == 2 ? 0 : NQ); ++u) {
@@ -911,6 +919,7 @@ __global__ __launch_bounds__(NT, WPE) void k_premat_subg_tiled(PrematSubgConst p
           if ((u + 1) % GB == 0) __builtin_amdgcn_sched_barrier(0);
         }
       }
+      dir ^= 1u;
       if (first) {
         if (tid == NT - 1 && h + 2 * np < n) uterm(so[n - 1], ll[n - 1], 1);
         wave_put(3, merged(sU));
