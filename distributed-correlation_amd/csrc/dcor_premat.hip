@@ -986,11 +986,15 @@ __global__ __launch_bounds__(NT, WPE) void k_premat_subg_tiled(PrematSubgConst p
 // wave sums folded over the 8 logical waves in order): 256 threads stand for the 512 logical
 // threads t and t + 256, so the sums are the tiled and L2 kernels' bit for bit.  Writes s[6..9]
 // of each replicate's partial; k_premat_subg_tiled<.., INTK = false> writes s[0..5].
+// The INT kernel's replicates per workgroup (R), pair slots per loop trip (PU) and minimum waves per
+// SIMD: 4, 1, 4 (100 VGPRs, 2048 workgroups at 8192 replicates) measured 0.54 of 8 TB/s for
+// C5-continuous against 0.53-0.54 for 2, 2, 1 and 2, 1, 1, 0.52 for 2, 1, 8 (spills) and 0.47 for
+// 2, 2, 6 (spills).
 #ifndef DCOR_INT_WPE
-#define DCOR_INT_WPE 1
+#define DCOR_INT_WPE 4
 #endif
 #ifndef DCOR_INT_PU
-#define DCOR_INT_PU 2
+#define DCOR_INT_PU 1
 #endif
 template <int R>
 __global__ __launch_bounds__(256, DCOR_INT_WPE) void k_premat_subg_int(PrematSubgConst p, int64_t reps,
@@ -1938,7 +1942,7 @@ static int tiled_int_mode() {
   return m;
 }
 #ifndef DCOR_INT_R
-#define DCOR_INT_R 2
+#define DCOR_INT_R 4
 #endif
 static TiledKernel tiled_kernel(bool intk) {
   static const TiledKernel ks[2][2] = {
