@@ -69,9 +69,9 @@ int arena_grow(Arena& a, size_t bytes, void** out);
 int codes_arena(Ctx* c, size_t bytes, void** out);
 // Pinned host buffer of at least `bytes`, after its previous copy finished (counted likewise).
 int pinned_grow(Pinned& b, size_t bytes, void** out);
-void count_alloc();
+void count_alloc();              // one more device or pinned allocation (dcor_alloc_count)
 // Stop the grid's persistent device workers (dcor_shutdown); `forked`: forget them unjoined.
-void grid_workers_stop(bool forked);              // one more device or pinned allocation (dcor_alloc_count)
+void grid_workers_stop(bool forked);
 
 // MT19937 jump-ahead (dcor_mtjump.cpp): the degree of the characteristic polynomial found by
 // Berlekamp-Massey (19937); the cached table of nseg polynomials x^((s + 1) L - 624) mod phi,
