@@ -369,3 +369,36 @@ def test_premat_tiled_kernel_matches_l2_kernel():
                                           err_msg=f"{key}: 512-thread tiled ({name}) vs L2 kernel")
         for r in range(len(v)):
             assert_close(v[r], runs["l2"][key][r], what=f"{key} rep {r} default vs L2 kernel")
+
+
+def test_premat_tiled_workgroup_runs_many_replicates():
+    """One launch with more replicates than the tiled kernel's resident workgroups: each
+    workgroup then runs several replicates in turn, starting each on the panel tile its previous
+    replicate left in LDS (every other sweep reversed), and the INT kernel groups four replicates
+    per workgroup with a short last group.  Sampled rows equal the same replicates run one per
+    launch (a fresh workgroup, every tile filled), bit for bit, and the oracle-checked 512-thread
+    variant's rows within the estimator tolerance."""
+    import os
+    import subprocess
+    import sys
+    import tempfile
+    from dcor import hrs
+    z = _continuous(3001, seed=11)
+    args = (z["age_z"], z["bmi_z"], z["lambda_age_z"], z["lambda_bmi_z"], 2.0)
+    R = 1203                     # > 256 CUs x 1 workgroup, and R % 4 == 3
+    whole = hrs.hrs_replicates(*args, R, rep_begin=5, chunk=R)
+    assert np.isfinite(whole).all()
+    for r in (0, 1, 255, 256, 257, 511, 767, 1023, 1200, 1201, 1202):
+        one = hrs.hrs_replicates(*args, 1, rep_begin=5 + r, chunk=1)
+        np.testing.assert_array_equal(whole[r:r + 1].view(np.int64), one.view(np.int64), err_msg=f"row {r}")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    paths = [root, os.path.join(root, "distributed-correlation_amd"), os.path.join(root, "tests")]
+    code = ("import sys, numpy as np; sys.path[:0] = %r; import test_gpu_hrs as t; from dcor import hrs; "
+            "z = t._continuous(3001, seed=11); np.save(sys.argv[1], hrs.hrs_replicates(z['age_z'], z['bmi_z'], "
+            "z['lambda_age_z'], z['lambda_bmi_z'], 2.0, %d, rep_begin=5, chunk=%d))") % (paths, R, R)
+    with tempfile.TemporaryDirectory() as d:
+        env = dict(os.environ, DCOR_TILED_VARIANT="0")
+        subprocess.run([sys.executable, "-c", code, os.path.join(d, "o.npy")], check=True, env=env, timeout=120)
+        v0 = np.load(os.path.join(d, "o.npy"))
+    for r in range(0, R, 97):
+        assert_close(whole[r], v0[r], what=f"row {r}: default vs 512-thread tiled kernel")
