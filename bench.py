@@ -123,7 +123,7 @@ def profile_stamp(path):
 
 
 def _profile(name):
-    for tag in ("r04", "r03", "r02", "r01"):
+    for tag in ("r05", "r04", "r03", "r02", "r01"):
         p = os.path.join(ROOT, "profiles", f"{tag}_{name}_summary.json")
         if os.path.exists(p):
             return p
@@ -185,6 +185,41 @@ def measure_passes(cell, reps: int = 2048, rep_begin: int = 0, iters: int = 5) -
            "pass1_ceiling": timed(11), "pass1_ceiling_own_occ": timed(13), "pass2_ceiling": timed(12),
            "pass1_ceiling_plus_stores": timed(14), "pass1_ceiling_plus_queue": timed(15)}
     return {k: round(v, 5) for k, v in out.items()}
+
+
+def sim_chunking(cell, reps: int):
+    """(chunk, chunks) of dcor_sim_launch for `reps` replicates of `cell`: the library's own plan,
+    so the live ceilings are timed at the launch shape the timed calls ran."""
+    import ctypes as C
+
+    from dcor import _lib
+    ch, nc = C.c_int64(), C.c_int64()
+    _lib.check(_lib.lib.dcor_sim_chunking(C.byref(cell.to_c()), reps, C.byref(ch), C.byref(nc)))
+    return ch.value, nc.value
+
+
+def serial_valu_time(names=("k_sign_pass1<0>", "k_sign_pass2<0>", "k_sign_epilogue_w<16>")):
+    """Hardware-anchored fraction per kernel from the committed serial profile (rocprofv3 PMC,
+    scripts/summarize_prof.py): VALU time / SIMD-cycles, each VALU wave-instruction priced at its
+    measured absolute issue cost -- the share of the SIMDs' cycles the kernel spends issuing VALU work
+    (1.0 = the SIMDs never idle).  Unlike issue_frac it does not depend on the kernel's own
+    instruction count."""
+    path = _profile("serial")
+    if path is None:
+        return None
+    try:
+        ks = json.load(open(path))["kernels"]
+    except (OSError, ValueError, KeyError):
+        return None
+    out = {}
+    for nm in names:
+        v = ks.get("dcor::" + nm)
+        if v is not None and v.get("valu_time_frac") is not None:
+            out[nm] = {"valu_time_frac": round(v["valu_time_frac"], 4),
+                       "wait_any_frac": round(v.get("wait_any_frac", float("nan")), 4),
+                       "simd_cycles_per_valu_inst": round(v.get("cycles_per_valu_inst", float("nan")), 3)}
+    head, fresh = profile_stamp(path)
+    return {"kernels": out, "source": os.path.relpath(path, ROOT), "source_head": head, "source_fresh": fresh}
 
 
 def _free_port() -> int:
@@ -251,11 +286,8 @@ def main():
         if n < 1:
             sys.exit("bench.py: --gpus must be >= 1")
         if n > 1:
-            if not args.dry_run:
-                import torch   # device_count() does not initialise HIP on this image
-                vis = torch.cuda.device_count()
-                if vis < n:
-                    sys.exit(f"bench.py: --gpus {n} but {vis} GPU(s) visible; refusing to measure fewer")
+            # the launcher itself loads no GPU library (no torch, no HIP, no amdsmi): each rank checks
+            # its own LOCAL_RANK against the GPUs it sees and exits non-zero, which stops the others
             sys.exit(spawn_ranks(n, sys.argv[1:]))
     elif args.gpus is not None and args.gpus != int(env_world):
         sys.exit(f"bench.py: --gpus {args.gpus} but the launcher's WORLD_SIZE is {env_world}")
@@ -275,6 +307,10 @@ def main():
         from dcor.sim import headline_cell as _hc
         cpu = cpu_baseline(_hc(args.n), args.cpu_seconds)
     if world > 1:
+        vis = torch.cuda.device_count()
+        if local >= vis:
+            sys.exit(f"bench.py: rank {rank}: LOCAL_RANK {local} but {vis} GPU(s) visible "
+                     f"(--gpus {world}); refusing to measure fewer")
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         formed = dist.get_world_size()
@@ -343,8 +379,7 @@ def main():
     summ = {"NI": finalize(merged[0], cell.rho), "INT": finalize(merged[1], cell.rho)}
 
     # live pass ceilings (after the timed region; untimed): the physical roofline of the VALU-bound path
-    chunk = 2048 if R >= 4096 else max(1, R // 2)
-    nch = -(-R // chunk)
+    chunk, nch = sim_chunking(cell, R)       # the launch shape dcor_sim_launch used for R replicates
     passes = None
     if rank == 0 and not args.no_ceilings and cell.n > 16384 and m == 8:
         passes = measure_passes(cell, chunk, rep_begin=(args.steps + args.warmup) * world * R)
@@ -381,6 +416,10 @@ def main():
                                             "stream with its memory side removed, at its occupancy) "
                                             "over the call's kernel time",
                          "issue": issue,
+                         "valu_time": serial_valu_time(),
+                         "valu_time_kind": "per kernel, from the serial rocprofv3 profile: VALU time at the "
+                                           "measured absolute issue costs / SIMD-cycles (hardware-anchored: "
+                                           "the SIMDs' busy share, not relative to the kernel's own stream)",
                          "traffic": traffic,
                          "traffic_source": os.path.relpath(_profile("headline"), ROOT) if _profile("headline") else None,
                          "traffic_source_head": profile_stamp(_profile("headline"))[0] if _profile("headline") else None,

@@ -136,14 +136,18 @@ def c2():
          roofline_frac=u / t / FP64_PEAK_UNITS)
 
 
-def c3(reps):
+C3_EPS = [(0.5, 0.5), (1.0, 1.0), (1.5, 0.5)]
+
+
+def c3(reps, eps=None):
+    """eps: a subset of the config's eps pairs (per-batch-size measurement: m = 32, 8, 11)."""
     from dcor.sim import expand_grid
     cells = expand_grid([1_000_000], [0, 0.15, 0.3, 0.4, 0.5, 0.65, 0.8, 0.9],
-                        [(0.5, 0.5), (1.0, 1.0), (1.5, 0.5)], family="sign", dgp="gaussian",
+                        eps or C3_EPS, family="sign", dgp="gaussian",
                         mu=(0.5, 0.5), sigma=(2.0, 2.0))
     t = timed(grid_call(cells, reps), reps=1)
     u = grid_units(cells, reps)
-    line("C3", cells=len(cells), reps_per_cell=reps, seconds=t, reps_per_s=len(cells) * reps / t,
+    line("C3", cells=len(cells), reps_per_cell=reps, eps_pairs=eps or C3_EPS, seconds=t, reps_per_s=len(cells) * reps / t,
          roofline_frac=u / t / FP64_PEAK_UNITS,
          note="one dcor_grid_run_multi call on one GPU over every cell's reps_per_cell replicates, measured")
 
@@ -423,6 +427,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--only", default="C1,C2,C3,C4,VG,SG,C5,C5c,C5e,C5f,C5fc,S,R1,RG,RH")
     ap.add_argument("--c3-reps", type=int, default=100_000)
+    ap.add_argument("--c3-eps", default=None, help="subset of C3's eps pairs, e.g. 0.5x0.5,1.5x0.5")
     ap.add_argument("--c4-B", type=int, default=1000)
     ap.add_argument("--c4-B-big", type=int, default=100_000)
     ap.add_argument("--c5-R", type=int, default=8192)
@@ -433,7 +438,8 @@ def main():
     which = a.only.split(",")
     if "C1" in which: c1()
     if "C2" in which: c2()
-    if "C3" in which: c3(a.c3_reps)
+    if "C3" in which:
+        c3(a.c3_reps, [tuple(float(v) for v in e.split("x")) for e in a.c3_eps.split(",")] if a.c3_eps else None)
     if "C4" in which: c4(a.c4_B, a.c4_B_big)
     if "VG" in which:
         from dcor.sim import vert_cor_grid

@@ -680,6 +680,22 @@ int dcor_batch_geometry(int64_t n, double eps1, double eps2, int family, int hrs
   return DCOR_OK;
 }
 
+// The one-pass sign path's replicate chunks: two slabs (two-stream chunk pipeline), each within a
+// budget of >= 1 GiB and >= 2048 replicates' codes, <= 8 GiB; equal chunks (no small tail launch).
+// dcor_sim_launch and dcor_sim_chunking (bench.py's live ceilings) share it.
+static void codes_chunking(int64_t n, int64_t rep_count, int64_t* chunk, int64_t* nchunks) {
+  const size_t per_rep = (size_t)n * sizeof(uint32_t);
+  size_t budget = (size_t)1 << 30;
+  if (budget < 2048 * per_rep) budget = 2048 * per_rep;
+  if (budget > ((size_t)8 << 30)) budget = (size_t)8 << 30;
+  int64_t maxchunk = (int64_t)(budget / per_rep);
+  if (maxchunk < 1) maxchunk = 1;
+  int64_t nch = (rep_count + maxchunk - 1) / maxchunk;
+  if (nch == 1 && rep_count >= 512) nch = 2;  // two chunks at least: pass 2 of one beside pass 1 of the other
+  *nchunks = nch;
+  *chunk = nch > 0 ? (rep_count + nch - 1) / nch : 0;
+}
+
 int dcor_sim_launch(const dcor_cell* cell, int64_t rep_begin, int64_t rep_count,
                     dcor_rep_out* d_out, void* stream) {
   if (!cell || (rep_count > 0 && !d_out)) return fail(DCOR_EINVAL, "null argument");
@@ -719,18 +735,10 @@ int dcor_sim_launch(const dcor_cell* cell, int64_t rep_begin, int64_t rep_count,
     } else if ((cp.kind != GK_SIGN_CODES && cp.kind != GK_SIGN_CODES_W) || rep_count == 0) {
       rc = launch_sign_fused(k, rep_count, d_out, stream);
     } else {
-      // two slabs (two-stream chunk pipeline), each within a budget of >= 1 GiB and
-      // >= 2048 replicates' codes, <= 8 GiB; equal chunks (no small tail launch)
       const size_t per_rep = (size_t)c.n * sizeof(uint32_t);
-      size_t budget = (size_t)1 << 30;
-      if (budget < 2048 * per_rep) budget = 2048 * per_rep;
-      if (budget > ((size_t)8 << 30)) budget = (size_t)8 << 30;
-      int64_t maxchunk = (int64_t)(budget / per_rep);
-      if (maxchunk < 1) maxchunk = 1;
-      int64_t nch = (rep_count + maxchunk - 1) / maxchunk;
-      if (nch == 1 && rep_count >= 512) nch = 2;  // two chunks at least: pass 2 of one beside pass 1 of the other
-      const int64_t chunk = (rep_count + nch - 1) / nch;
-      const size_t slab_b = ((size_t)chunk * per_rep + 255) / 256 * 256;
+      int64_t chunk = 0, nch = 0;
+      codes_chunking(c.n, rep_count, &chunk, &nch);
+      const size_t slab_b = ((size_t)chunk * per_rep + 255) / 256 * 256 + 256;  // + pass 2's over-read
       const size_t sums_b = ((size_t)chunk * (8 * sizeof(double) + 48) + 255) / 256 * 256;
       const int nbuf = nch > 1 ? 2 : 1;
       Ctx* cx = nullptr;
@@ -769,6 +777,19 @@ int dcor_sim_launch(const dcor_cell* cell, int64_t rep_begin, int64_t rep_count,
     }
   }
   if (rc) return hip_fail((hipError_t)rc, "sim kernel launch");
+  return DCOR_OK;
+}
+
+int dcor_sim_chunking(const dcor_cell* cell, int64_t rep_count, int64_t* chunk, int64_t* nchunks) {
+  if (!cell || !chunk || !nchunks || rep_count < 0) return fail(DCOR_EINVAL, "sim_chunking: bad arguments");
+  CellPlan cp;
+  if (int st = prepare_cell(*cell, cp)) return st;
+  if ((cp.kind != GK_SIGN_CODES && cp.kind != GK_SIGN_CODES_W) || cp.nan_dgp || rep_count == 0) {
+    *chunk = rep_count;
+    *nchunks = rep_count > 0 ? 1 : 0;
+    return DCOR_OK;
+  }
+  codes_chunking(cell->n, rep_count, chunk, nchunks);
   return DCOR_OK;
 }
 

@@ -367,55 +367,19 @@ __device__ __forceinline__ void exact_signs(const SignConst& c, const SignStd& s
 // wave at once (zig_slow would otherwise run under divergence nearly every iteration).  The
 // queued sample's record is rewritten and its clipped values replace its placeholder's in the
 // sums at the drain.
-// Pass 1 folds two sample groups' plain sums per compensated add; pass 2 (m = 8) pair-groups the
-// T sums of a thread's two batches in flight (build with 0 for the per-group / per-batch sums).
-#ifndef DCOR_P1_FOLD8
-#define DCOR_P1_FOLD8 1
-#endif
-#ifndef DCOR_P2_PAIRT
-#define DCOR_P2_PAIRT 1
-#endif
-// Slab layout.  For m = 8 cells (DCOR_SLAB_WAVE) the records of every full block of 512 samples
-// (64 batches) are stored half-batch-major: the first four records of the block's 64 batches
-// (1 KB), then their last four (1 KB).  Pass 2's wave then loads its 64 consecutive batches' first
-// halves as one contiguous 1-KB row and their second halves as another -- 8 whole cache lines per
-// load instead of 16 half lines -- and pass 1's 16-B group stores stay two contiguous 512-B runs
-// per wave.  Samples past the last full block (and every other m) keep position i.  Tail samples
-// (i >= 8 k) always lie past the full blocks, since 8 floor(n / 8) >= 512 floor(n / 512).
-// Measured (round 4, headline, one box): pass 2 181 us with it, 177 us without; pass 1 533 vs 531
-// (the address arithmetic costs more than the fuller cache lines save), so it is off by default.
-#ifndef DCOR_SLAB_WAVE
-#define DCOR_SLAB_WAVE 0
-#endif
-// DCOR_SLAB_NT: the slab's 16-B record stores (pass 1) and loads (pass 2, m = 8) non-temporal.
-#ifndef DCOR_SLAB_NT
-#define DCOR_SLAB_NT 0
-#endif
+// Pass 1 folds two sample groups' plain sums per compensated add (one TwoSum per 8 samples); pass 2
+// (m = 8) pair-groups the T sums of a thread's two batches in flight.  Measured (round 4): 11 and 4 us
+// per headline chunk against per-group / per-batch sums.
+// Slab layout: record i of a replicate at slab[i].  (Measured and dropped in round 4: a
+// wave-contiguous half-batch layout for m = 8, pass 2 181 vs 177 us; non-temporal slab stores and
+// loads, +-0.)
 typedef uint32_t dcor_u32x4 __attribute__((ext_vector_type(4)));
+// four records from any 4-B aligned position (global_load_dwordx4 takes dword alignment)
+typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
 __device__ __forceinline__ void slab_st4(uint32_t* p, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
-  if (DCOR_SLAB_NT)
-    __builtin_nontemporal_store((dcor_u32x4){a, b, c, d}, reinterpret_cast<dcor_u32x4*>(p));
-  else
-    *reinterpret_cast<uint4*>(p) = make_uint4(a, b, c, d);
+  *reinterpret_cast<uint4*>(p) = make_uint4(a, b, c, d);
 }
-__device__ __forceinline__ uint4 slab_ld4(const uint32_t* p) {
-  if (DCOR_SLAB_NT) {
-    const dcor_u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const dcor_u32x4*>(p));
-    return make_uint4(v.x, v.y, v.z, v.w);
-  }
-  return *reinterpret_cast<const uint4*>(p);
-}
-struct SlabMap {
-  bool on;
-  uint32_t nfb;   // samples in full 512-sample blocks
-  __device__ explicit SlabMap(const SignConst& c)
-      : on(DCOR_SLAB_WAVE && c.m == 8), nfb((uint32_t)(c.n >> 9) << 9) {}
-  __device__ __forceinline__ uint32_t pos(uint32_t i) const {
-    if (!on || i >= nfb) return i;
-    const uint32_t g4 = i >> 2;
-    return ((g4 >> 7) << 9) | ((g4 & 1u) << 8) | (((g4 >> 1) & 63u) << 2) | (i & 3u);
-  }
-};
+__device__ __forceinline__ uint4 slab_ld4(const uint32_t* p) { return *reinterpret_cast<const uint4*>(p); }
 
 // Per-wave slow-normal queue: a group adds at most 256 entries per wave (about 1.6 % of a wave's
 // samples are queued).  With DCOR_DRAIN_AT = 0 the loop drains the whole queue above ZQ_CAP - 256,
@@ -425,13 +389,6 @@ struct SlabMap {
 #define DCOR_ZQ_CAP 768
 #endif
 #define ZQ_CAP DCOR_ZQ_CAP
-// Diagnostic builds only: the CEIL = 3 kernel queues but skips the regeneration in its drain.
-#ifndef DCOR_DIAG_NODRAIN
-#define DCOR_DIAG_NODRAIN 0
-#endif
-#ifndef DCOR_DRAIN_LDS
-#define DCOR_DRAIN_LDS 1
-#endif
 // DCOR_DRAIN_AT > 0: a wave drains whole 64-entry rounds of its queue as soon as it holds
 // DCOR_DRAIN_AT entries (the rest stays queued for later), so its regenerations interleave with
 // the other waves' hot loops instead of all coinciding at the replicates' ends.  Measured (round 4,
@@ -457,7 +414,6 @@ __device__ __forceinline__ void sign_pass1_core(const SignConst& c, uint32_t rep
                                                 uint32_t* zq, uint32_t* zqn) {
   constexpr int NT = WAVE ? 64 : DCOR_BLOCK;
   const int tid = WAVE ? (int)(threadIdx.x & 63) : (int)threadIdx.x;
-  const SlabMap sm(c);
   DD sx{0.0, 0.0}, sy{0.0, 0.0};
   const float cix = c.cinv_xf, ciy = c.cinv_yf, cbx = c.cnb_xf, cby = c.cnb_yf;
   // the INT flip from its 32-bit word: u < flipT (flipT <= 2^32) as a 32-bit compare
@@ -486,7 +442,7 @@ __device__ __forceinline__ void sign_pass1_core(const SignConst& c, uint32_t rep
     // Every valid sample enters the group sums, a queued one with its placeholder: the drain
     // takes the placeholder out and adds the true values (both compensated), so the hot loop
     // selects nothing.  The group's plain sums are added into (hx, hy); the caller folds them
-    // into the compensated sums (with DCOR_P1_FOLD8, once per two groups).
+    // into the compensated sums, once per two groups.
     // The group's slow samples (pend bit q: sample i0 + q) are queued by the caller (enqueue),
     // outside the lanes' divergent group branch.
     auto group = [&](int64_t g4, auto full_tag, double& hx, double& hy, uint32_t& pend) {
@@ -517,7 +473,7 @@ __device__ __forceinline__ void sign_pass1_core(const SignConst& c, uint32_t rep
       }
       if constexpr (CEIL == 0 || CEIL == 2) {
         if (FULL) {
-          slab_st4(slab + sm.pos(i0), rec[0], rec[1], rec[2], rec[3]);
+          slab_st4(slab + i0, rec[0], rec[1], rec[2], rec[3]);
         } else {
           for (int q = 0; q < 4; ++q) if ((int64_t)(i0 + q) < c.n) slab[i0 + q] = rec[q];
         }
@@ -549,12 +505,6 @@ __device__ __forceinline__ void sign_pass1_core(const SignConst& c, uint32_t rep
       const uint32_t cnt = __builtin_amdgcn_readfirstlane(*zqn);
       const uint32_t keep = (DCOR_DRAIN_AT > 0 && part) ? (cnt & 63u) : 0u;
       if (cnt == keep) return;
-      if constexpr (CEIL == 3 && DCOR_DIAG_NODRAIN) {
-        wave_sync();
-        if (lane == 0) *zqn = keep;
-        wave_sync();
-        return;
-      }
       __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the placeholder records have landed
       for (uint32_t k = keep + (uint32_t)lane; k < cnt; k += 64) {
         const uint32_t i = zq[k];
@@ -567,7 +517,7 @@ __device__ __forceinline__ void sign_pass1_core(const SignConst& c, uint32_t rep
         const uint32_t w3 = w.w3;
         // the table from LDS in the workgroup kernel (the wave kernel keeps the global table: the
         // LDS pointer costs it six VGPRs and a wave per SIMD)
-        Dgp<DGP>::from_block(c.g, i, rep, c.k0, c.k1, w, x, y, (WAVE || !DCOR_DRAIN_LDS) ? nullptr : zt);
+        Dgp<DGP>::from_block(c.g, i, rep, c.k0, c.k1, w, x, y, WAVE ? nullptr : zt);
         const double xc = rclip_fin(x, c.L), yc = rclip_fin(y, c.L);
         ks_acc(sx, xc);
         ks_acc(sy, yc);
@@ -575,14 +525,13 @@ __device__ __forceinline__ void sign_pass1_core(const SignConst& c, uint32_t rep
           const uint32_t r = record_w(xc, yc, w3);
           asm volatile("" ::"v"(r));
         } else {
-          slab[sm.pos(i)] = record_w(xc, yc, w3);
+          slab[i] = record_w(xc, yc, w3);
         }
       }
       wave_sync();
       if (lane == 0) *zqn = keep;
       wave_sync();
     };
-#if DCOR_P1_FOLD8
     // two groups per step (wave groups b + lane and b + NT + lane), one compensated fold of their
     // plain 8-sample sums: half the TwoSum chains of a fold per group (the low bits of the sums
     // differ from per-group folds; the private centres they decide are unchanged in practice)
@@ -598,17 +547,6 @@ __device__ __forceinline__ void sign_pass1_core(const SignConst& c, uint32_t rep
       ks_acc(sx, hx);
       ks_acc(sy, hy);
     }
-#else
-    for (int64_t b = WAVE ? 0 : 64 * wv; b < nfull; b += NT) {  // trip count uniform per wave
-      double hx = 0.0, hy = 0.0;
-      uint32_t pa = 0;
-      if (b + lane < nfull) group(b + lane, std::true_type(), hx, hy, pa);
-      enqueue(pa, (uint32_t)(4 * (b + lane)));
-      ks_acc(sx, hx);
-      ks_acc(sy, hy);
-      if (full()) drain(true);
-    }
-#endif
     {  // the partial last group (n % 4), converged around its enqueue
       double hx = 0.0, hy = 0.0;
       uint32_t pa = 0;
@@ -651,7 +589,7 @@ __device__ __forceinline__ void sign_pass1_core(const SignConst& c, uint32_t rep
       ks_acc(sx, gx);
       ks_acc(sy, gy);
       if (FULL) {
-        slab_st4(slab + sm.pos(i0), rec[0], rec[1], rec[2], rec[3]);
+        slab_st4(slab + i0, rec[0], rec[1], rec[2], rec[3]);
       } else {
         for (int q = 0; q < 4; ++q) if ((int64_t)(i0 + q) < c.n) slab[i0 + q] = rec[q];
       }
@@ -774,7 +712,6 @@ __device__ __forceinline__ P2Result sign_pass2_core(const SignConst& c, uint32_t
                                                     const double2* lt) {
   constexpr int NT = WAVE ? 64 : DCOR_BLOCK;   // threads sharing the replicate
   const int tid = WAVE ? (int)(threadIdx.x & 63) : (int)threadIdx.x;
-  const SlabMap sm(c);
   double lap[10];
   if constexpr (WAVE) {
     scalar_laplace_wave(rep, c.k0, c.k1, lap);
@@ -854,15 +791,6 @@ __device__ __forceinline__ P2Result sign_pass2_core(const SignConst& c, uint32_t
     const double yt = (double)cy * 0.125 + c.by * unit_laplace_t(u53(w.w2, w.w3), lt);
     return 8.0 * xt * yt;                                                 // vert-cor.R:233
   };
-  // the same, kept only when `valid` (a batch computed past the last one is dropped exactly)
-  auto batch_T_if = [&](int64_t j, int cx, int cy, bool valid) {
-    const double h1 = sT.hi, l1 = sT.lo, h2 = sT2.hi, l2 = sT2.lo;  // scalars: no aggregate select
-    batch_T(j, cx, cy, std::true_type());
-    sT.hi = valid ? sT.hi : h1;
-    sT.lo = valid ? sT.lo : l1;
-    sT2.hi = valid ? sT2.hi : h2;
-    sT2.lo = valid ? sT2.lo : l2;
-  };
   auto fix_fast = [&](int64_t i, uint32_t w, int& cx, int& cy, int& cc) {
     const uint32_t qx = w & 0x7fffu, qy = (w >> 16) & 0x7fffu;
     if (!(force_exact || qx == qNx || qy == qNy || qx == qIx || qy == qIy)) return;
@@ -909,7 +837,7 @@ __device__ __forceinline__ P2Result sign_pass2_core(const SignConst& c, uint32_t
         ++ties;
 #pragma unroll 1
         for (int q = 0; q < 8; ++q)  // re-read the record (L2-hot): no dynamically indexed registers
-          fix_fast(8 * j + q, slab[sm.pos((uint32_t)(8 * j + q))], cx, cy, cc);
+          fix_fast(8 * j + q, slab[8 * j + q], cx, cy, cc);
       }
     };
     // Two batches' records in flight per thread in two register sets, used in place (a move of a
@@ -919,8 +847,8 @@ __device__ __forceinline__ P2Result sign_pass2_core(const SignConst& c, uint32_t
     // compiler could merge the two copies across.  Loads past the end re-read the last batch.
     auto load_mem = [&](int64_t jj, uint4& lo, uint4& hi) {
       const int64_t jc = jj < c.k ? jj : c.k - 1;
-      lo = slab_ld4(slab + sm.pos((uint32_t)(8 * jc)));
-      hi = slab_ld4(slab + sm.pos((uint32_t)(8 * jc + 4)));
+      lo = slab_ld4(slab + 8 * jc);
+      hi = slab_ld4(slab + 8 * jc + 4);
     };
     auto load = [&](int64_t jj, uint4& lo, uint4& hi) {
       if constexpr (CEIL)
@@ -948,52 +876,105 @@ __device__ __forceinline__ P2Result sign_pass2_core(const SignConst& c, uint32_t
         load(j + 3 * NT, b0, b1);
         __builtin_amdgcn_sched_barrier(0);
         core += cca + (vb ? ccb : 0);
-#if DCOR_P2_PAIRT
         // the two batches' T and T^2 added plainly, the pair sums compensated: half the TwoSum
         // chains (the low bits differ from per-batch sums, within the oracle's 1e-12)
         const double Ta = batch_T_val(j, cxa, cya);
         const double Tb = vb ? batch_T_val(jb, cxb, cyb) : 0.0;
         ks_acc(sT, Ta + Tb);
         ks_acc(sT2, Ta * Ta + Tb * Tb);
-#else
-        batch_T(j, cxa, cya, std::true_type());
-        batch_T_if(jb, cxb, cyb, vb);
-#endif
       }
     }
   } else if constexpr (!CEIL) {
-    // any other m < 32768 (the reference grids' 11, 32, 200): the same packed decisions, four records
-    // per 16-B load when batches start on 16-B boundaries (m % 4 == 0), the counts per batch
+    // any other m < 32768 (the reference grids' 11, 32, 200): the same packed decisions over a
+    // stream of 16-B units.  A thread's batches j = tid, tid + NT, ... are U = ceil(m / 4) units
+    // each, loaded 4-B aligned (one dwordx4 whatever m % 4; the last unit of a batch reads up to three
+    // records past it, which it replaces by PAD), four units in flight in four register sets used in
+    // place, as the m = 8 loop keeps two batches: the loop waits vmcnt(3), never for a unit it does
+    // not need yet.  PAD = (32767, 32767), flip 0, adds nothing to the counts (its halves are >= any
+    // threshold code, its INT bit 0) and ties only a threshold coded 32767, which the exact fix-up
+    // then settles.  The loop runs a multiple of four units; units past the thread's last batch
+    // re-read it and are dropped.  Counts and the per-batch T sums are the per-batch loop's, bit for
+    // bit (batch j's T is added after batch j - NT's).
     if (c.m < 32768) {
-      const bool vec = (c.m & 3) == 0;
-      for (int64_t j = tid; j < c.k; j += NT) {
-        const int64_t i0 = j * c.m;
-        uint32_t neg = 0, pc = 0, mn = 0xffffffffu;
-        auto one = [&](uint32_t w) {
-          const uint32_t r = w & 0x7fff7fffu;
-          const uint32_t dN = pk_sub16(r, TN), dI = pk_sub16(r, TI);
-          mn = pk_min16(pk_min16(mn, dN), dI);
-          neg += pk_sign_bits(dN);           // halves count to <= m < 32768
-          pc += int_bit31(dI, w) >> 31;      // the INT bit sbx ^ sby ^ S
-        };
-        if (vec) {
-          const uint4* __restrict__ p4 = reinterpret_cast<const uint4*>(slab + i0);
-          for (int q = 0; q < (c.m >> 2); ++q) {
-            const uint4 v = p4[q];
-            one(v.x); one(v.y); one(v.z); one(v.w);
-          }
-        } else {
-          for (int r = 0; r < c.m; ++r) one(slab[i0 + r]);
+      const uint32_t m = (uint32_t)c.m, U = (m + 3u) >> 2, rem = m & 3u;
+      const int64_t rounds = (c.k + NT - 1) / NT;       // batches per thread (the last one partial)
+      const int64_t nu = ((rounds * (int64_t)U) + 3) & ~(int64_t)3;
+      constexpr uint32_t PAD = 0x7fff7fffu;
+      // load cursor: round rl, unit ul of this thread's batch tid + NT rl (clamped to the last batch)
+      int64_t rl = 0;
+      uint32_t ul = 0;
+      auto load_next = [&](u32x4a4& v) {
+        const int64_t jj = tid + NT * rl;
+        const int64_t jc = jj < c.k ? jj : c.k - 1;
+        v = *reinterpret_cast<const u32x4a4*>(slab + jc * m + 4u * ul);
+        if (++ul == U) { ul = 0; ++rl; }
+      };
+      // decision cursor and the current batch's packed counts
+      int64_t rd = 0;
+      uint32_t ud = 0, neg = 0, pc = 0, par = 0, mn = 0xffffffffu;
+      auto one = [&](uint32_t w) {
+        const uint32_t r = w & 0x7fff7fffu;
+        const uint32_t dN = pk_sub16(r, TN), dI = pk_sub16(r, TI);
+        mn = pk_min16(pk_min16(mn, dN), dI);
+        neg += pk_sign_bits(dN);                                     // halves count to <= m < 32768
+        par = __builtin_amdgcn_alignbit(par, int_bit31(dI, w), 31u); // (par << 1) | INT bit
+      };
+      auto step = [&](const u32x4a4& v) {
+        const bool last = ud + 1u == U;
+        uint32_t w1 = v.y, w2 = v.z, w3 = v.w;
+        if (last && rem) {
+          w3 = PAD;
+          if (rem < 3u) w2 = PAD;
+          if (rem < 2u) w1 = PAD;
         }
-        int cx = c.m - 2 * (int)(neg & 0xffffu), cy = c.m - 2 * (int)(neg >> 16);
-        int cc = 2 * (int)pc - c.m;
-        if (has_zero16(mn) || force_exact) {
-          ++ties;
+        one(v.x); one(w1); one(w2); one(w3);
+        pc += __popc(par & 15u);
+        if (last) {
+          const int64_t j = tid + NT * rd;
+          const int64_t i0 = j * (int64_t)m;
+          int cx = (int)m - 2 * (int)(neg & 0xffffu), cy = (int)m - 2 * (int)(neg >> 16);
+          int cc = 2 * (int)pc - (int)m;
+          if (j < c.k) {
+            if (has_zero16(mn) || force_exact) {
+              ++ties;
 #pragma unroll 1
-          for (int r = 0; r < c.m; ++r) fix_fast(i0 + r, slab[i0 + r], cx, cy, cc);
+              for (uint32_t r = 0; r < m; ++r) fix_fast(i0 + r, slab[i0 + r], cx, cy, cc);
+            }
+            core += cc;
+            batch_T(j, cx, cy, std::false_type());
+          }
+          neg = pc = 0;
+          mn = 0xffffffffu;
+          ud = 0;
+          ++rd;
+        } else {
+          ++ud;
         }
-        core += cc;
-        batch_T(j, cx, cy, std::false_type());
+      };
+      if (nu > 0) {
+        u32x4a4 u0, u1, u2, u3;
+        load_next(u0);
+        __builtin_amdgcn_sched_barrier(0);
+        load_next(u1);
+        __builtin_amdgcn_sched_barrier(0);
+        load_next(u2);
+        __builtin_amdgcn_sched_barrier(0);
+        load_next(u3);
+        __builtin_amdgcn_sched_barrier(0);
+        for (int64_t t = 0; t < nu; t += 4) {
+          step(u0);
+          load_next(u0);
+          __builtin_amdgcn_sched_barrier(0);
+          step(u1);
+          load_next(u1);
+          __builtin_amdgcn_sched_barrier(0);
+          step(u2);
+          load_next(u2);
+          __builtin_amdgcn_sched_barrier(0);
+          step(u3);
+          load_next(u3);
+          __builtin_amdgcn_sched_barrier(0);
+        }
       }
     } else for (int64_t j = tid; j < c.k; j += NT) {
       int cx = 0, cy = 0, cc = 0;
@@ -1015,7 +996,7 @@ __device__ __forceinline__ P2Result sign_pass2_core(const SignConst& c, uint32_t
   for (int64_t i = c.k * c.m + tid; !CEIL && i < c.n; i += NT) {  // tail: INT only
     int dx = 0, dy = 0, cc = 0;
     bool ignore = false;  // NI never reads the tail
-    const uint32_t w = slab[sm.pos((uint32_t)i)];
+    const uint32_t w = slab[i];
     if (fast(w, dx, dy, cc) || force_exact) fixup(i, w, dx, dy, cc, ignore);
     core += cc;
   }

@@ -224,7 +224,7 @@ int exec_ranges(const dcor_cell* cells, const std::vector<CellPlan>& cp, const s
   void* garena = nullptr;
   if (int st = arena_grow(ctx->grid, total, &garena)) return st;
   void* scr = nullptr;
-  const size_t slab_one = al256(max_scr_b);
+  const size_t slab_one = al256(max_scr_b) + 256;   // + pass 2's 16-B over-read past the last record
   if (max_scr_b > 0)
     if (int st = codes_arena(ctx, (size_t)nslot * slab_one, &scr)) return st;
   // ---- upload through a pinned staging slot (its previous upload finished long ago in steady

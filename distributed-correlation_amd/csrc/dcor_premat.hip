@@ -744,17 +744,13 @@ __global__ __launch_bounds__(DICT_NT, WPE) void k_premat_subg_dict(PrematSubgCon
 // the L2 kernel; PG adds the two terms of an INT pair (of a batch pair) plainly and compensates
 // the pair sums, as the L2 kernel does, so with NT = 512 and NA = 1 the sums are its bit for bit.
 // Measured (C5-continuous, 8192 replicates, round 4, with the epilogue): 1.05 ms with the INT
-// stream in the first round's fills; without it (timing ablations, DCOR_TILED_ABL) 0.68 ms, without
-// the gathers 0.91, without the NI noise 0.93.  The INT stream therefore runs in a kernel of its
+// stream in the first round's fills; timing ablations (wrong results, round 4) took 0.68 ms without
+// it, 0.91 without the gathers, 0.93 without the NI noise.  The INT stream therefore runs in a kernel of its
 // own by default (k_premat_subg_int; tiled_kernel() below).  A round issues all its batch-index
 // loads, and later all its noise loads, before it waits for any: one HBM round trip each per
 // round (a per-pair branch around each load had made them five).
 // NT threads per workgroup; NQ batch pairs per thread per round; FU fill pairs per loop trip; GB
 // batch pairs gathered per scheduling group; NA accumulator sets; WPE waves per SIMD.
-// DCOR_TILED_ABL (timing ablations, wrong results): 1 no INT stream, 2 no gathers, 3 no NI noise.
-#ifndef DCOR_TILED_ABL
-#define DCOR_TILED_ABL 0
-#endif
 // INTK = false: the INT sums are left to k_premat_subg_int (s[6..9] of each partial); the kernel
 // then streams no INT bytes, writes s[0..5] only and needs 106 VGPRs instead of 128.
 template <int NT, int NQ, int FU, int GB, int NA, int WPE, bool PG = false, bool INTK = true>
@@ -780,9 +776,30 @@ __global__ __launch_bounds__(NT, WPE) void k_premat_subg_tiled(PrematSubgConst p
   for (int64_t it = blockIdx.x; it < reps; it += gridDim.x) {
     const int64_t rep = it;
     const double* __restrict__ ll = p.lap_local + rep * c.n;
-    const iv4* __restrict__ p4 = reinterpret_cast<const iv4*>(p.perm + rep * (c.k * 2));
-    const dv2* __restrict__ x2 = reinterpret_cast<const dv2*>(p.lap_ni_x + rep * c.k);
-    const dv2* __restrict__ y2 = reinterpret_cast<const dv2*>(p.lap_ni_y + rep * c.k);
+    // batch pair q's four indices and two noise pairs: 16-B loads when the caller's arrays are
+    // 16-B aligned (every row is then, k being even), element loads otherwise -- the same values,
+    // so the kernel (and every replicate's bits) does not depend on the buffers' alignment
+    const int* __restrict__ pr_row = p.perm + rep * (c.k * 2);
+    const double* __restrict__ x_row = p.lap_ni_x + rep * c.k;
+    const double* __restrict__ y_row = p.lap_ni_y + rep * c.k;
+    const bool al_ni = ((reinterpret_cast<uintptr_t>(p.perm) | reinterpret_cast<uintptr_t>(p.lap_ni_x) |
+                         reinterpret_cast<uintptr_t>(p.lap_ni_y)) & 15) == 0;
+    auto ld_pr = [&](uint32_t q) -> iv4 {
+      if (al_ni) return __builtin_nontemporal_load(reinterpret_cast<const iv4*>(pr_row) + q);
+      iv4 v;
+      v.x = __builtin_nontemporal_load(pr_row + 4 * q);
+      v.y = __builtin_nontemporal_load(pr_row + 4 * q + 1);
+      v.z = __builtin_nontemporal_load(pr_row + 4 * q + 2);
+      v.w = __builtin_nontemporal_load(pr_row + 4 * q + 3);
+      return v;
+    };
+    auto ld_nz = [&](const double* __restrict__ row, uint32_t q) -> dv2 {
+      if (al_ni) return __builtin_nontemporal_load(reinterpret_cast<const dv2*>(row) + q);
+      dv2 v;
+      v.x = __builtin_nontemporal_load(row + 2 * q);
+      v.y = __builtin_nontemporal_load(row + 2 * q + 1);
+      return v;
+    };
     // two independent accumulator sets (the first / second sample of an INT pair, the first /
     // second batch of a batch pair): twice the fp64 dependency chains in flight per thread at
     // two waves per SIMD; the sets are merged with dd_add before the wave reduction
@@ -824,7 +841,7 @@ __global__ __launch_bounds__(NT, WPE) void k_premat_subg_tiled(PrematSubgConst p
     };
     // rounds of NQ * NT batch pairs; the INT terms ride along the first round's fills
     for (uint32_t qb = 0; qb == 0 || qb < nbp; qb += (uint32_t)NQ * NT) {
-      const bool first = INTK && qb == 0 && DCOR_TILED_ABL != 1;
+      const bool first = INTK && qb == 0;
       uint32_t sa[NQ], sb[NQ];  // (a | b << 16) of the pair's two batches
       double ax[NQ][2], ay[NQ][2];
       // every load of the round first (a pair past the last re-reads the last), then the packing:
@@ -833,7 +850,7 @@ __global__ __launch_bounds__(NT, WPE) void k_premat_subg_tiled(PrematSubgConst p
 #pragma unroll
       for (int u = 0; u < NQ; ++u) {
         const uint32_t q = qb + tid + (uint32_t)u * NT;
-        pr[u] = __builtin_nontemporal_load(p4 + (q < nbp ? q : nbp - 1));
+        pr[u] = ld_pr(q < nbp ? q : nbp - 1);
       }
 #pragma unroll
       for (int u = 0; u < NQ; ++u) {
@@ -906,7 +923,7 @@ __global__ __launch_bounds__(NT, WPE) void k_premat_subg_tiled(PrematSubgConst p
         }
         // gather: every index of this thread's batch pairs against the tile
 #pragma unroll
-        for (int u = 0; u < (DCOR_TILED_ABL == 2 ? 0 : NQ); ++u) {
+        for (int u = 0; u < NQ; ++u) {
           const uint32_t i0 = sa[u] & 0xFFFFu, i1 = sa[u] >> 16, i2 = sb[u] & 0xFFFFu, i3 = sb[u] >> 16;
           const double2 t0 = tile[min(i0 - lo, tn)], t1 = tile[min(i1 - lo, tn)];
           const double2 t2 = tile[min(i2 - lo, tn)], t3 = tile[min(i3 - lo, tn)];
@@ -931,11 +948,8 @@ __global__ __launch_bounds__(NT, WPE) void k_premat_subg_tiled(PrematSubgConst p
 #pragma unroll
       for (int u = 0; u < NQ; ++u) {
         const uint32_t q = qb + tid + (uint32_t)u * NT, qc = q < nbp ? q : nbp - 1;
-        if (DCOR_TILED_ABL == 3) {
-          nx[u] = dv2{(double)sa[u], (double)sb[u]}; ny[u] = nx[u];
-        } else {
-          nx[u] = __builtin_nontemporal_load(x2 + qc); ny[u] = __builtin_nontemporal_load(y2 + qc);
-        }
+        nx[u] = ld_nz(x_row, qc);
+        ny[u] = ld_nz(y_row, qc);
       }
 #pragma unroll
       for (int u = 0; u < NQ; ++u) {
@@ -986,16 +1000,11 @@ __global__ __launch_bounds__(NT, WPE) void k_premat_subg_tiled(PrematSubgConst p
 // wave sums folded over the 8 logical waves in order): 256 threads stand for the 512 logical
 // threads t and t + 256, so the sums are the tiled and L2 kernels' bit for bit.  Writes s[6..9]
 // of each replicate's partial; k_premat_subg_tiled<.., INTK = false> writes s[0..5].
-// The INT kernel's replicates per workgroup (R), pair slots per loop trip (PU) and minimum waves per
+// The INT kernel's replicates per workgroup (R), pair slots loaded per step and minimum waves per
 // SIMD: 4, 1, 4 (100 VGPRs, 2048 workgroups at 8192 replicates) measured 0.54 of 8 TB/s for
-// C5-continuous against 0.53-0.54 for 2, 2, 1 and 2, 1, 1, 0.52 for 2, 1, 8 (spills) and 0.47 for
-// 2, 2, 6 (spills).
-#ifndef DCOR_INT_WPE
+// C5-continuous (round 4) against 0.53-0.54 for 2, 2, 1 and 2, 1, 1, 0.52 for 2, 1, 8 (spills) and
+// 0.47 for 2, 2, 6 (spills).
 #define DCOR_INT_WPE 4
-#endif
-#ifndef DCOR_INT_PU
-#define DCOR_INT_PU 1
-#endif
 template <int R>
 __global__ __launch_bounds__(256, DCOR_INT_WPE) void k_premat_subg_int(PrematSubgConst p, int64_t reps,
                                                          SubgPartial* __restrict__ part) {
@@ -1022,32 +1031,26 @@ __global__ __launch_bounds__(256, DCOR_INT_WPE) void k_premat_subg_int(PrematSub
     return v;
   };
   DD sU[R][2] = {}, sU2[R][2] = {};      // [replicate][logical thread tid, tid + 256]
-  // PU pair slots per trip, q + 256 j (logical set j & 1): every load of the trip first (a slot past
-  // the last pair re-reads pair q), then the terms of the slots that exist, in ascending q
-  constexpr int PU = DCOR_INT_PU;
-  for (uint32_t q = tid; q < np; q += 256 * PU) {
-    double2 v0[PU], v1[PU];
-    dv2 l[PU][R];
+  // Pair p belongs to logical thread p mod 512: a trip takes pair q (logical thread tid, set 0) and
+  // then pair q + 256 (logical thread tid + 256, set 1), so each set sums its pairs in ascending
+  // order, as the 512-thread kernels do.  The set is a compile-time index of each slot.
+  auto slot = [&](uint32_t qj, auto set_tag) {
+    constexpr int SET = decltype(set_tag)::value;
+    const double2 v0 = so[2 * qj], v1 = so[2 * qj + 1];
+    dv2 l[R];
 #pragma unroll
-    for (int j = 0; j < PU; ++j) {
-      const uint32_t qj = q + 256u * j < np ? q + 256u * j : q;
-      v0[j] = so[2 * qj];
-      v1[j] = so[2 * qj + 1];
+    for (int r = 0; r < R; ++r) l[r] = ldp(r, qj);
 #pragma unroll
-      for (int r = 0; r < R; ++r) l[j][r] = ldp(r, qj);
+    for (int r = 0; r < R; ++r) {
+      const double U0 = rclip((v0.x + c.bs * l[r].x) * v0.y, c.lr);
+      const double U1 = rclip((v1.x + c.bs * l[r].y) * v1.y, c.lr);
+      ks_acc(sU[r][SET], U0 + U1);
+      ks_acc(sU2[r][SET], U0 * U0 + U1 * U1);
     }
-#pragma unroll
-    for (int j = 0; j < PU; ++j) {
-      if (j == 0 || q + 256u * j < np) {
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-          const double U0 = rclip((v0[j].x + c.bs * l[j][r].x) * v0[j].y, c.lr);
-          const double U1 = rclip((v1[j].x + c.bs * l[j][r].y) * v1[j].y, c.lr);
-          ks_acc(sU[r][j & 1], U0 + U1);
-          ks_acc(sU2[r][j & 1], U0 * U0 + U1 * U1);
-        }
-      }
-    }
+  };
+  for (uint32_t q = tid; q < np; q += 512) {
+    slot(q, std::integral_constant<int, 0>());
+    if (q + 256 < np) slot(q + 256, std::integral_constant<int, 1>());
   }
   if (tid == 255 && 2 * np < n) {        // logical thread 511: the odd tail sample
     const double2 v = so[n - 1];
@@ -2008,12 +2011,12 @@ int launch_premat_subg(const PrematSubgConst& c0, int64_t reps, void* part, dcor
   }
   if (c.xyc != nullptr) {
     // shared panel, random batches, no dictionary (or the device probe may find none): the
-    // clipped panel packed once, then for m = 2 with every row 16-B aligned and u16 sample
-    // indices the tiled kernel, otherwise the persistent kernel gathering it from L2.
+    // clipped panel packed once, then for m = 2 (k even) and u16 sample indices the tiled kernel,
+    // otherwise the persistent kernel gathering it from L2.  The choice depends on the geometry
+    // only, never on the caller's buffer alignment (the tiled kernel reads unaligned rows element
+    // by element), so a replicate's bits do not either.
     const bool tiled = c.dict_built != 2 && tiled_enabled() && c.s.m == 2 && (c.s.k & 1) == 0 &&
-                       c.s.k >= 2 && c.s.n < 65536 &&
-                       ((reinterpret_cast<uintptr_t>(c.perm) | reinterpret_cast<uintptr_t>(c.lap_ni_x) |
-                         reinterpret_cast<uintptr_t>(c.lap_ni_y)) & 15) == 0;
+                       c.s.k >= 2 && c.s.n < 65536;
     hipLaunchKernelGGL(k_premat_xy_pack, dim3((unsigned)((c.s.n + DCOR_BLOCK - 1) / DCOR_BLOCK)),
                        dim3(DCOR_BLOCK), 0, (hipStream_t)stream, c, (double2*)c.xyc,
                        (double2*)c.soc);

@@ -108,6 +108,7 @@ SIGNATURES = {
     "dcor_shutdown": (C.c_int, []),
     "dcor_alloc_count": (C.c_int64, []),
     "dcor_device_bytes": (C.c_int64, []),
+    "dcor_sim_chunking": (C.c_int, [C.POINTER(Cell), C.c_int64, _I64, _I64]),
     "dcor_diag_sign_pass": (C.c_int, [C.POINTER(Cell), C.c_int64, C.c_int64, C.c_int, _P]),
     "dcor_diag_sign_ties": (C.c_int, [C.POINTER(Cell), C.c_int64, C.c_int64, _I64]),
     "dcor_lambda_n": (C.c_double, [C.c_double, C.c_double]),

@@ -111,6 +111,10 @@ int dcor_shutdown(void);
 int64_t dcor_alloc_count(void);
 /* Device bytes held by the library's scratch arenas over every live context. */
 int64_t dcor_device_bytes(void);
+/* How dcor_sim_launch splits rep_count replicates of `cell` into launches: *nchunks chunks of at
+ * most *chunk replicates (the one-pass sign path's slab chunks; 1 x rep_count for every other kernel
+ * family).  Planning only: no device work.  bench.py times its live pass ceilings at this chunk. */
+int dcor_sim_chunking(const dcor_cell* cell, int64_t rep_count, int64_t* chunk, int64_t* nchunks);
 /* Measurement only (bench.py's roofline, not part of the reference surface): one pass of the
  * one-pass sign path (the kernels dcor_sim_launch runs for cells with n > 16384 and
  * normalise = TRUE) over replicates rep_begin .. rep_begin + reps - 1 as ONE chunk, on `stream`, in

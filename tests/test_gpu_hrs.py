@@ -402,3 +402,54 @@ def test_premat_tiled_workgroup_runs_many_replicates():
         v0 = np.load(os.path.join(d, "o.npy"))
     for r in range(0, R, 97):
         assert_close(whole[r], v0[r], what=f"row {r}: default vs 512-thread tiled kernel")
+
+
+@pytest.mark.parametrize("off", [1, 2, 3])
+def test_premat_tiled_kernel_independent_of_buffer_alignment(off):
+    """The uncoded-panel dispatch depends on the geometry only: the caller's index and NI-noise
+    arrays placed `off` elements past a 16-B boundary (4-B / 8-B aligned) run the same tiled kernel,
+    reading rows element by element, and return the aligned launch's bits."""
+    import ctypes as C
+
+    import torch
+    from dcor import _lib, api, hrs
+    z = _continuous(3001, seed=5)
+    eps, R = 2.0, 5
+    args = (z["age_z"], z["bmi_z"], z["lambda_age_z"], z["lambda_bmi_z"], eps)
+    ref, noise, geo = hrs.hrs_replicates(*args, R, seed_ni=41, seed_int=42, keep_noise=True)
+    k, m = geo["k"], geo["m"]
+    assert m == 2 and k % 2 == 0
+    n = len(z["age_z"])
+
+    def dev(a, dtype, shift):
+        a = np.ascontiguousarray(a)
+        t = torch.empty(a.size + 4, dtype=dtype, device="cuda")
+        assert t.data_ptr() % 16 == 0
+        v = t[shift:shift + a.size]
+        v.copy_(torch.as_tensor(a.ravel()))
+        return v
+    perm = dev(noise["perm"], torch.int32, off)
+    lx = dev(noise["lap_x"], torch.float64, 1)
+    ly = dev(noise["lap_y"], torch.float64, 1)
+    ll = dev(noise["lap_local"], torch.float64, 0)
+    lc = dev(noise["lap_central"], torch.float64, 0)
+    mz = dev(noise["mix_z"], torch.float64, 0)
+    ml = dev(noise["mix_l"], torch.float64, 0)
+    X = torch.as_tensor(z["age_z"], device="cuda")
+    Y = torch.as_tensor(z["bmi_z"], device="cuda")
+    out = torch.empty((R, 6), dtype=torch.float64, device="cuda")
+    P = lambda t: C.c_void_p(t.data_ptr())
+    pn = C.c_void_p()
+    _lib.check(_lib.lib.dcor_panel_create(P(X), P(Y), n, None, C.byref(pn)))
+    try:
+        d = _lib.PrematSubg(n=n, reps=R, eps1=eps, eps2=eps, eta1=1.0, eta2=1.0, alpha=0.05, hrs=1,
+                            lam_x=args[2], lam_y=args[3], lam_s=args[2], lam_o=args[3], lam_r=geo["lam_r"],
+                            delta=geo["delta"], nsim=2000, X=X.data_ptr(), Y=Y.data_ptr(), xy_stride=0,
+                            perm=perm.data_ptr(), lap_ni_x=lx.data_ptr(), lap_ni_y=ly.data_ptr(),
+                            lap_local=ll.data_ptr(), lap_central=lc.data_ptr(), mix_z=mz.data_ptr(),
+                            mix_l=ml.data_ptr())
+        _lib.check(_lib.lib.dcor_premat_subg_panel_launch(C.byref(d), pn, P(out), None))
+        got = out.cpu().numpy()
+    finally:
+        _lib.lib.dcor_panel_destroy(pn)
+    np.testing.assert_array_equal(got.view(np.int64), ref.view(np.int64))

@@ -211,6 +211,7 @@ def test_fused_split_invariance(dc):
 C3_CELLS = [
     dict(rho=0.5, eps1=1.0, eps2=1.0, family="sign", dgp="gaussian", mu=(0.5, 0.5), sigma=(2.0, 2.0)),
     dict(rho=0.8, eps1=1.5, eps2=0.5, family="sign", dgp="gaussian", mu=(0.5, 0.5), sigma=(2.0, 2.0)),
+    dict(rho=0.15, eps1=0.5, eps2=0.5, family="sign", dgp="gaussian", mu=(0.5, 0.5), sigma=(2.0, 2.0)),  # m = 32
     dict(rho=0.3, eps1=1.0, eps2=1.0, family="sign", dgp="bernoulli"),
     dict(rho=0.65, eps1=0.5, eps2=1.5, family="subG", dgp="bounded_factor"),
     dict(rho=0.6, eps1=1.0, eps2=1.0, family="subG", dgp="mix_gaussian"),
@@ -247,6 +248,10 @@ SATURATED_CELLS = [
     dict(n=4_000, rho=0.5, eps1=1.0, eps2=1.0, mu=(10.0, 0.5), sigma=(1.0, 2.0)),
     dict(n=30_000, rho=0.0, eps1=1.0, eps2=1.0, mu=(0.25, 0.25), sigma=(1e-9, 1e-9)),
     dict(n=25_000, rho=-1.0, eps1=1.5, eps2=0.5, mu=(0.0, 3.0), sigma=(3.0, 0.5)),
+    # batch sizes off the m = 8 loop (the unit stream): m = 32 in the wave kernel, m = 11 in the
+    # workgroup kernel, both with clip-saturated coordinates
+    dict(n=6_000, rho=0.3, eps1=0.5, eps2=0.5, mu=(10.0, 0.5), sigma=(1.0, 2.0)),
+    dict(n=50_000, rho=0.5, eps1=1.5, eps2=0.5, mu=(-10.0, 10.0), sigma=(1.0, 1.0)),
 ]
 
 
