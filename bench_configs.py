@@ -17,6 +17,11 @@ RG  R-stream mode on vert-cor.R's own 144-cell sign-family grid, B = 250 (vert-c
 RH  R-stream HRS sweep: real-data-sims.R's 23 eps x 200 runs with its own per-run set.seed
     streams (4,600 NI + 4,600 INT runs) on a stand-in panel n = 19,433
 Run on one GPU: python bench_configs.py [--only C2,C5] > profiles/rNN_configs.jsonl
+Multi-GPU (C3, C4: the configs BASELINE names for 8 GPUs): python bench_configs.py --gpus N --only C3,C4
+starts N rank processes (one per GPU, torch.distributed over RCCL; or runs under torchrun), each
+running its contiguous replicate shard of every cell (dcor.dist.run_grid_distributed), the
+per-cell accumulators all-gathered once; total work is fixed (strong scaling) and the time is the
+max over ranks.  --dry-run forms the group over gloo on the CPU and prints the shard plan.
 """
 import argparse
 import ctypes as C
@@ -84,13 +89,16 @@ def run_grid_gpu(cells, B, chunk=1 << 15):
 
 
 # config line -> its committed rocprofv3 summary (per-kernel times and counters)
-PROFILE_OF = {"VG": "vg", "SG": "sg", "C2": "c2", "C3": "c3", "C5": "c5", "C5-continuous": "c5c",
-              "C5-fused": "c5f"}
+PROFILE_OF = {"VG": "vg", "SG": "sg", "C2": "c2", "C3": "c3", "C4": "c4", "S": "s", "C5": "c5",
+              "C5-continuous": "c5c", "C5-fused": "c5f"}
 
 
 def measured(name):
-    """Where the line's per-kernel counters are (scripts/summarize_prof.py) and whether that
-    profile was taken on this tree's sources."""
+    """Where the line's per-kernel counters are (scripts/summarize_prof.py), whether that profile
+    was taken on this tree's sources, and the physical fraction of each kernel that holds >= 5 % of
+    the profiled GPU time: VALU time (the mix priced at measured absolute issue costs) over the
+    SIMDs' cycles -- hardware-anchored, unlike the pinned convention `roofline_frac`, which prices
+    the reference's work units and exceeds 1 when the kernels issue fewer instructions."""
     from bench import _profile, profile_stamp
     if name not in PROFILE_OF:
         return {}
@@ -98,7 +106,25 @@ def measured(name):
     if path is None:
         return {}
     head, fresh = profile_stamp(path)
-    return {"profile": os.path.relpath(path, ROOT), "profile_head": head, "profile_fresh": fresh}
+    out = {"profile": os.path.relpath(path, ROOT), "profile_head": head, "profile_fresh": fresh}
+    try:
+        ks = json.load(open(path))["kernels"]
+    except (OSError, ValueError, KeyError):
+        return out
+    phys = {}
+    for k, v in sorted(ks.items(), key=lambda kv: -kv[1].get("pct_time", 0.0)):
+        if v.get("pct_time", 0.0) < 5.0:
+            continue
+        phys[k.replace("dcor::", "")] = {
+            "pct_time": v.get("pct_time"),
+            "valu_time_frac": None if v.get("valu_time_frac") is None else round(v["valu_time_frac"], 4),
+            "wait_any_frac": None if v.get("wait_any_frac") is None else round(v["wait_any_frac"], 4),
+            "simd_cycles_per_valu_inst": None if v.get("cycles_per_valu_inst") is None
+            else round(v["cycles_per_valu_inst"], 3),
+            "hbm_bytes_per_dispatch": None if v.get("hbm_read_bytes_corrected") is None
+            else v["hbm_read_bytes_corrected"] + (v.get("hbm_write_bytes") or 0.0)}
+    out["physical"] = phys
+    return out
 
 
 def line(name, **kw):
@@ -139,12 +165,16 @@ def c2():
 C3_EPS = [(0.5, 0.5), (1.0, 1.0), (1.5, 0.5)]
 
 
+def c3_cells(eps=None):
+    from dcor.sim import expand_grid
+    return expand_grid([1_000_000], [0, 0.15, 0.3, 0.4, 0.5, 0.65, 0.8, 0.9],
+                       eps or C3_EPS, family="sign", dgp="gaussian",
+                       mu=(0.5, 0.5), sigma=(2.0, 2.0))
+
+
 def c3(reps, eps=None):
     """eps: a subset of the config's eps pairs (per-batch-size measurement: m = 32, 8, 11)."""
-    from dcor.sim import expand_grid
-    cells = expand_grid([1_000_000], [0, 0.15, 0.3, 0.4, 0.5, 0.65, 0.8, 0.9],
-                        eps or C3_EPS, family="sign", dgp="gaussian",
-                        mu=(0.5, 0.5), sigma=(2.0, 2.0))
+    cells = c3_cells(eps)
     t = timed(grid_call(cells, reps), reps=1)
     u = grid_units(cells, reps)
     line("C3", cells=len(cells), reps_per_cell=reps, eps_pairs=eps or C3_EPS, seconds=t, reps_per_s=len(cells) * reps / t,
@@ -152,9 +182,8 @@ def c3(reps, eps=None):
          note="one dcor_grid_run_multi call on one GPU over every cell's reps_per_cell replicates, measured")
 
 
-def c4(B, B_big):
-    """The paper sweep at its stated sizes: B replicates per cell (vert-cor.R:40), B_big for the
-    n = 1e6 cells (SURVEY §8d C4): two grid calls (one per B), timed together."""
+def c4_cells():
+    """(every runnable cell, the n < 1e6 cells, the n = 1e6 cells, cells skipped for k < 1)."""
     from dcor.sim import paper_grid
     cells = paper_grid(n_grid=(200, 400, 800, 1600, 3200, 10_000, 100_000, 1_000_000))
     ok = []
@@ -163,8 +192,13 @@ def c4(B, B_big):
         if c.family == "sign" and c.n // m < 1:
             continue
         ok.append(c)
-    small = [c for c in ok if c.n < 1_000_000]
-    big = [c for c in ok if c.n >= 1_000_000]
+    return ok, [c for c in ok if c.n < 1_000_000], [c for c in ok if c.n >= 1_000_000], len(cells) - len(ok)
+
+
+def c4(B, B_big):
+    """The paper sweep at its stated sizes: B replicates per cell (vert-cor.R:40), B_big for the
+    n = 1e6 cells (SURVEY §8d C4): two grid calls (one per B), timed together."""
+    ok, small, big, nskip = c4_cells()
     g_small, g_big = grid_call(small, B), grid_call(big, B_big)
 
     def both():
@@ -175,7 +209,7 @@ def c4(B, B_big):
     tl = timed(lambda: run_grid_gpu(small, B), reps=1)
     reps = len(small) * B + len(big) * B_big
     u = grid_units(small, B) + grid_units(big, B_big)
-    line("C4", cells=len(ok), cells_skipped_k_lt_1=len(cells) - len(ok), reps_per_cell=B,
+    line("C4", cells=len(ok), cells_skipped_k_lt_1=nskip, reps_per_cell=B,
          reps_per_cell_n1e6=B_big, cells_n1e6=len(big), replicates=reps, seconds=t, reps_per_s=reps / t,
          roofline_frac=u / t / FP64_PEAK_UNITS, small_cells_seconds=ts,
          small_cells_per_cell_loop_seconds=tl, small_cells_per_cell_loop_reps_per_s=len(small) * B / tl,
@@ -423,6 +457,79 @@ def rstream_hrs():
          note="each run replays its own set.seed(10 + 37 rep + 1000 idx) / (20 + 41 rep + 1000 idx)")
 
 
+def dist_grid(name, groups, world, rank, dry_run=False, **extra):
+    """One config over the ranks: every rank runs its replicate shard of every (cells, B) group
+    (dcor.dist.run_grid_distributed: one batched launch sequence per group, the per-cell
+    accumulators all-gathered over RCCL), barrier + synchronize around the timed region, the time
+    the max over ranks.  Total replicates are fixed whatever the world size (strong scaling)."""
+    import torch
+    import torch.distributed as dist
+    from dcor.dist import shard
+    reps = sum(len(cells) * B for cells, B in groups)
+    shards = [[shard(B, r, world) for r in range(world)] for _, B in groups]
+    if dry_run:
+        if rank == 0:
+            print(json.dumps({"config": name, "dry_run": True, "world_formed": dist.get_world_size(),
+                              "replicates": reps, "shards": shards, **extra}), flush=True)
+        return
+    from dcor.dist import run_grid_distributed
+
+    def run():
+        return [run_grid_distributed(cells, B) for cells, B in groups]
+    run()                                  # warm-up (plans, arenas, RCCL communicator)
+    torch.cuda.synchronize()
+    dist.barrier()
+    t0 = time.perf_counter()
+    res = run()
+    torch.cuda.synchronize()
+    dist.barrier()
+    el = time.perf_counter() - t0
+    t = torch.tensor([el], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    el = float(t.item())
+    u = sum(grid_units(cells, B) for cells, B in groups)
+    n_ok = sum(1 for g in res for (ni, it) in g if ni.n > 0)
+    if rank == 0:
+        line(name, world_formed=dist.get_world_size(), backend=dist.get_backend(), scaling="strong",
+             replicates=reps, seconds=el, reps_per_s=reps / el, roofline_frac_per_gpu=u / el / FP64_PEAK_UNITS / world,
+             shards=shards, cells_with_results=n_ok,
+             note="one process per GPU: each rank's replicate shard of every cell in one batched launch "
+                  "sequence per group, accumulators all-gathered (RCCL); time = max over ranks", **extra)
+
+
+def main_dist(a, world, rank, local):
+    """bench_configs.py under N ranks: C3 and C4 (the configs defined as multi-GPU)."""
+    import torch.distributed as dist
+    which = a.only.split(",")
+    if a.dry_run:
+        dist.init_process_group("gloo")
+    else:
+        import torch
+        vis = torch.cuda.device_count()
+        if local >= vis:
+            sys.exit(f"bench_configs.py: rank {rank}: LOCAL_RANK {local} but {vis} GPU(s) visible "
+                     f"(--gpus {world}); refusing to measure fewer")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    formed = dist.get_world_size()
+    if formed != world:
+        sys.exit(f"bench_configs.py: process group formed {formed} ranks, expected {world}")
+    if "C3" in which:
+        eps = [tuple(float(v) for v in e.split("x")) for e in a.c3_eps.split(",")] if a.c3_eps else None
+        cells = c3_cells(eps)
+        dist_grid("C3", [(cells, a.c3_reps)], world, rank, a.dry_run, cells=len(cells), reps_per_cell=a.c3_reps,
+                  eps_pairs=eps or C3_EPS)
+    if "C4" in which:
+        ok, small, big, nskip = c4_cells()
+        dist_grid("C4", [(small, a.c4_B), (big, a.c4_B_big)], world, rank, a.dry_run, cells=len(ok),
+                  cells_skipped_k_lt_1=nskip, reps_per_cell=a.c4_B, reps_per_cell_n1e6=a.c4_B_big,
+                  cells_n1e6=len(big))
+    others = [w for w in which if w not in ("C3", "C4")]
+    if others and rank == 0:
+        print(json.dumps({"skipped": others, "reason": "single-GPU configs: run without --gpus"}), flush=True)
+    dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--only", default="C1,C2,C3,C4,VG,SG,C5,C5c,C5e,C5f,C5fc,S,R1,RG,RH")
@@ -432,7 +539,22 @@ def main():
     ap.add_argument("--c4-B-big", type=int, default=100_000)
     ap.add_argument("--c5-R", type=int, default=8192)
     ap.add_argument("--c5e-R", type=int, default=1_000_000)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="C3 / C4 over N ranks (one per GPU); without a launcher's WORLD_SIZE, N rank processes "
+                         "are started")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="with --gpus: form the group over gloo on the CPU and print the shard plan, no GPU")
     a = ap.parse_args()
+    env_world = os.environ.get("WORLD_SIZE")
+    if a.gpus is not None or env_world is not None:
+        if env_world is None:
+            if a.gpus < 1:
+                sys.exit("bench_configs.py: --gpus must be >= 1")
+            from bench import spawn_ranks     # the launcher loads no GPU library
+            sys.exit(spawn_ranks(a.gpus, sys.argv[1:], script=os.path.abspath(__file__)))
+        if a.gpus is not None and a.gpus != int(env_world):
+            sys.exit(f"bench_configs.py: --gpus {a.gpus} but the launcher's WORLD_SIZE is {env_world}")
+        return main_dist(a, int(env_world), int(os.environ.get("RANK", "0")), int(os.environ.get("LOCAL_RANK", "0")))
     import torch
     torch.cuda.set_device(0)
     which = a.only.split(",")

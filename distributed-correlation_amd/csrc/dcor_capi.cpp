@@ -735,7 +735,7 @@ int dcor_sim_launch(const dcor_cell* cell, int64_t rep_begin, int64_t rep_count,
     } else if ((cp.kind != GK_SIGN_CODES && cp.kind != GK_SIGN_CODES_W) || rep_count == 0) {
       rc = launch_sign_fused(k, rep_count, d_out, stream);
     } else {
-      const size_t per_rep = (size_t)c.n * sizeof(uint32_t);
+      const size_t per_rep = (size_t)sign_item_words(c.n, c.dgp) * sizeof(uint32_t);   // records + bitmap
       int64_t chunk = 0, nch = 0;
       codes_chunking(c.n, rep_count, &chunk, &nch);
       const size_t slab_b = ((size_t)chunk * per_rep + 255) / 256 * 256 + 256;  // + pass 2's over-read
@@ -796,8 +796,8 @@ int dcor_sim_chunking(const dcor_cell* cell, int64_t rep_count, int64_t* chunk, 
 int dcor_diag_sign_pass(const dcor_cell* cell, int64_t rep_begin, int64_t reps, int which, void* stream) {
   if (!cell || reps < 1 || reps > 65535 || rep_begin < 0 || rep_begin + reps > 0xffffffffLL)
     return fail(DCOR_EINVAL, "diag_sign_pass: bad arguments");
-  if (which != 1 && which != 2 && which != 3 && (which < 11 || which > 15))
-    return fail(DCOR_EINVAL, "diag_sign_pass: which must be 1, 2, 3 or 11-15");
+  if ((which < 1 || which > 4) && (which < 11 || which > 15))
+    return fail(DCOR_EINVAL, "diag_sign_pass: which must be 1-4 or 11-15");
   if (int st = need_device()) return st;
   CellPlan cp;
   if (int st = prepare_cell(*cell, cp)) return st;
@@ -807,7 +807,7 @@ int dcor_diag_sign_pass(const dcor_cell* cell, int64_t rep_begin, int64_t reps, 
     return fail(DCOR_EINVAL, "diag_sign_pass: the ceilings run the Gaussian DGP at m = 8");
   SignConst k = cp.sign;
   k.rep_begin = rep_begin;
-  const size_t slab_b = ((size_t)reps * (size_t)cell->n * sizeof(uint32_t) + 255) / 256 * 256;
+  const size_t slab_b = ((size_t)reps * sign_item_words(cell->n, cell->dgp) * sizeof(uint32_t) + 255) / 256 * 256;
   const size_t sums_b = ((size_t)reps * SIGN_SUMS * sizeof(double) + 255) / 256 * 256;
   const size_t part_b = ((size_t)reps * SIGN_PARTIAL_BYTES + 255) / 256 * 256;
   void* scratch = nullptr;
@@ -822,10 +822,11 @@ int dcor_diag_sign_pass(const dcor_cell* cell, int64_t rep_begin, int64_t reps, 
 int dcor_diag_sign_ties(const dcor_cell* cell, int64_t rep_begin, int64_t reps, int64_t* h_ties) {
   if (!h_ties) return fail(DCOR_EINVAL, "diag_sign_ties: null output");
   if (int st = dcor_diag_sign_pass(cell, rep_begin, reps, 1, nullptr)) return st;
+  if (int st = dcor_diag_sign_pass(cell, rep_begin, reps, 4, nullptr)) return st;
   if (int st = dcor_diag_sign_pass(cell, rep_begin, reps, 2, nullptr)) return st;
   void* scratch = nullptr;
   if (int st = arena_get(0, &scratch)) return st;   // the same arena dcor_diag_sign_pass used
-  const size_t slab_b = ((size_t)reps * (size_t)cell->n * sizeof(uint32_t) + 255) / 256 * 256;
+  const size_t slab_b = ((size_t)reps * sign_item_words(cell->n, cell->dgp) * sizeof(uint32_t) + 255) / 256 * 256;
   const size_t sums_b = ((size_t)reps * SIGN_SUMS * sizeof(double) + 255) / 256 * 256;
   std::vector<long long> part((size_t)reps * SIGN_PARTIAL_BYTES / sizeof(long long));
   HIPCHK(hipDeviceSynchronize());

@@ -381,7 +381,28 @@ __device__ __forceinline__ void slab_st4(uint32_t* p, uint32_t a, uint32_t b, ui
 }
 __device__ __forceinline__ uint4 slab_ld4(const uint32_t* p) { return *reinterpret_cast<const uint4*>(p); }
 
-// Per-wave slow-normal queue: a group adds at most 256 entries per wave (about 1.6 % of a wave's
+// The Gaussian DGP's ziggurat fast path for one sample's Philox block (pass 1 and k_sign_drain
+// compute it alike): the clipped sample, true = both normals took the fast path (otherwise the
+// values are a finite placeholder in [-L, L] that pass 1 adds and the drain takes out again).
+__device__ __forceinline__ bool gauss_fast_xy(const SignConst& c, const double2* zt, const U4& w, double& xc,
+                                              double& yc) {
+  const double2 t1 = zt[zig_j1(w.w2)], t2 = zt[zig_j2(w.w2)];
+  const double z1 = fma(zig_d(w.w0, zig_y1(w.w2)), t1.x, -t1.x);
+  const double z2 = fma(zig_d(w.w1, zig_y2(w.w2)), t2.x, -t2.x);
+  const bool ok = ((int)(fabs(z1) < t1.y) & (int)(fabs(z2) < t2.y)) != 0;
+  double x, y;
+  mvn_z(z1, z2, c.g.mu0, c.g.mu1, c.g.a00, c.g.a01, c.g.a10, c.g.a11, &x, &y);
+  xc = rclip_fin(x, c.L);
+  yc = rclip_fin(y, c.L);
+  return ok;
+}
+// A sample's slab record: the code pair of (clip(x), clip(y)) and the INT flip (u < flipT) in bit 31.
+__device__ __forceinline__ uint32_t sign_record(const SignConst& c, double xc, double yc, uint32_t u) {
+  const uint32_t ftm1 = (uint32_t)(c.flipT - 1u), fbit = c.flipT != 0 ? 0x80000000u : 0u;
+  return code_pair(xc, yc, c.cinv_xf, c.cinv_yf, c.cnb_xf, c.cnb_yf) | (u <= ftm1 ? fbit : 0u);
+}
+
+// Per-wave slow-normal queue (the wave-per-replicate pass 1): a group adds at most 256 entries per wave (about 1.6 % of a wave's
 // samples are queued).  With DCOR_DRAIN_AT = 0 the loop drains the whole queue above ZQ_CAP - 256,
 // so at the headline's n a wave usually drains once, at the end of its replicate; 768: the
 // workgroup's LDS (28.7 KB with the table) still fits five workgroups per CU.
@@ -401,44 +422,32 @@ __device__ __forceinline__ uint4 slab_ld4(const uint32_t* p) { return *reinterpr
 
 // WAVE = false: one 256-thread workgroup per replicate; WAVE = true: one wave per replicate (the
 // caller's workgroup has loaded the ziggurat table `zt` into LDS once for all its replicates).
-// zq / zqn: the calling wave's slow-normal queue and its counter (LDS).
-// CEIL (Gaussian only; a measurement kernel, never a result): the same hot loop with its memory
-// side removed -- no slab store, no slow-normal queue or drain; an empty asm consumes the records
-// and the pending mask, so the compiler keeps every instruction that computes them.  Its time is
+// Slow samples (Gaussian DGP): the workgroup form marks them in the replicate's bitmap `bm`
+// (sign_bm_words) for k_sign_drain, a kernel of its own at full occupancy; the wave form queues
+// them in its LDS queue zq / zqn and drains it itself.
+// CEIL (Gaussian workgroup form only; a measurement kernel, never a result): the same hot loop with
+// its memory side removed -- no slab store, no slow-sample bitmap; an empty asm consumes the records
+// and the pending masks, so the compiler keeps every instruction that computes them.  Its time is
 // the loop's own VALU-issue ceiling (dcor_diag_sign_pass, bench.py roofline.issue_frac).  CEIL = 2
-// keeps the slab stores only, CEIL = 3 the slow-normal queue and drain only (the cost of each).
+// keeps the slab stores only, CEIL = 3 the bitmap stores only (the cost of each).
 template <int DGP, bool WAVE, int CEIL = 0>
 __device__ __forceinline__ void sign_pass1_core(const SignConst& c, uint32_t rep,
                                                 uint32_t* __restrict__ slab,
                                                 double* __restrict__ sums_out, const double2* zt,
-                                                uint32_t* zq, uint32_t* zqn) {
+                                                uint32_t* zq, uint32_t* zqn, uint32_t* __restrict__ bm = nullptr) {
   constexpr int NT = WAVE ? 64 : DCOR_BLOCK;
   const int tid = WAVE ? (int)(threadIdx.x & 63) : (int)threadIdx.x;
   DD sx{0.0, 0.0}, sy{0.0, 0.0};
   const float cix = c.cinv_xf, ciy = c.cinv_yf, cbx = c.cnb_xf, cby = c.cnb_yf;
   // the INT flip from its 32-bit word: u < flipT (flipT <= 2^32) as a 32-bit compare
   const uint32_t ftm1 = (uint32_t)(c.flipT - 1u), fbit = c.flipT != 0 ? 0x80000000u : 0u;
-  auto record_w = [&](double xc, double yc, uint32_t u) {
-    return code_pair(xc, yc, cix, ciy, cbx, cby) | (u <= ftm1 ? fbit : 0u);
-  };
+  auto record_w = [&](double xc, double yc, uint32_t u) { return sign_record(c, xc, yc, u); };
   // each thread runs its groups in increasing order; the partial last group (n % 4) is the last
   // group of its thread
   const int64_t nfull = c.n / 4;
   if constexpr (DGP == DCOR_DGP_GAUSSIAN) {
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    // the fast path's clipped sample from its Philox block; false: a normal missed the fast path
-    // (the values are then a finite placeholder in [-L, L])
-    auto fast_xy = [&](const U4& w, double& xc, double& yc) -> bool {
-      const double2 t1 = zt[zig_j1(w.w2)], t2 = zt[zig_j2(w.w2)];
-      const double z1 = fma(zig_d(w.w0, zig_y1(w.w2)), t1.x, -t1.x);
-      const double z2 = fma(zig_d(w.w1, zig_y2(w.w2)), t2.x, -t2.x);
-      const bool ok = ((int)(fabs(z1) < t1.y) & (int)(fabs(z2) < t2.y)) != 0;
-      double x, y;
-      mvn_z(z1, z2, c.g.mu0, c.g.mu1, c.g.a00, c.g.a01, c.g.a10, c.g.a11, &x, &y);
-      xc = rclip_fin(x, c.L);
-      yc = rclip_fin(y, c.L);
-      return ok;
-    };
+    auto fast_xy = [&](const U4& w, double& xc, double& yc) -> bool { return gauss_fast_xy(c, zt, w, xc, yc); };
     // Every valid sample enters the group sums, a queued one with its placeholder: the drain
     // takes the placeholder out and adds the true values (both compensated), so the hot loop
     // selects nothing.  The group's plain sums are added into (hx, hy); the caller folds them
@@ -535,7 +544,45 @@ __device__ __forceinline__ void sign_pass1_core(const SignConst& c, uint32_t rep
     // two groups per step (wave groups b + lane and b + NT + lane), one compensated fold of their
     // plain 8-sample sums: half the TwoSum chains of a fold per group (the low bits of the sums
     // differ from per-group folds; the private centres they decide are unchanged in practice)
-    for (int64_t b = WAVE ? 0 : 64 * wv; b < nfull; b += 2 * NT) {  // trip count uniform per wave
+    if constexpr (!WAVE) {
+      // The step's two pend nibbles enter a per-lane byte shift register, stored every four steps
+      // (one coalesced u32 per lane, bitmap word [wv][step / 4][lane], step 4q + t in byte 3 - t);
+      // a partial last quad is stored left-aligned, its missing steps' bytes zero.
+      uint32_t acc = 0, s4 = 0;
+      uint32_t* bw = bm + (size_t)wv * (64 * sign_bm_quads(c.n)) + lane;
+      for (int64_t b = 64 * wv; b < nfull; b += 2 * NT) {  // trip count uniform per wave
+        double hx = 0.0, hy = 0.0;
+        uint32_t pa = 0, pb = 0;
+        if (b + lane < nfull) group(b + lane, std::true_type(), hx, hy, pa);
+        if (b + NT + lane < nfull) group(b + NT + lane, std::true_type(), hx, hy, pb);
+        ks_acc(sx, hx);
+        ks_acc(sy, hy);
+        acc = (acc << 8) | pa | (pb << 4);
+        if (++s4 == 4) {
+          if constexpr (CEIL == 0 || CEIL == 3) *bw = acc;
+          else asm volatile("" ::"v"(acc));
+          bw += 64;
+          acc = 0;
+          s4 = 0;
+        }
+      }
+      if (s4) {
+        if constexpr (CEIL == 0 || CEIL == 3) *bw = acc << (8 * (4 - s4));
+        else asm volatile("" ::"v"(acc));
+      }
+      // the partial last group (n % 4): its pend bits in the tail word
+      const bool last = (c.n & 3) && tid == (int)(nfull % NT);
+      uint32_t pt = 0;
+      if (last) {
+        double hx = 0.0, hy = 0.0;
+        group(nfull, std::false_type(), hx, hy, pt);
+        ks_acc(sx, hx);
+        ks_acc(sy, hy);
+      }
+      if constexpr (CEIL == 0 || CEIL == 3)
+        if ((c.n & 3) ? last : tid == 0) bm[4 * 64 * sign_bm_quads(c.n)] = pt;
+    } else {
+    for (int64_t b = 0; b < nfull; b += 2 * NT) {  // trip count uniform per wave
       double hx = 0.0, hy = 0.0;
       uint32_t pa = 0, pb = 0;
       if (b + lane < nfull) group(b + lane, std::true_type(), hx, hy, pa);
@@ -559,6 +606,7 @@ __device__ __forceinline__ void sign_pass1_core(const SignConst& c, uint32_t rep
       }
     }
     drain(false);
+    }
   } else {
     static_assert(CEIL == 0, "the ceiling kernel runs the Gaussian loop");
     // group g4 = samples 4 g4 .. 4 g4 + 3; FULL: all four exist (the hot loop has no guards)
@@ -611,20 +659,18 @@ __device__ __forceinline__ void sign_pass1_core(const SignConst& c, uint32_t rep
   }
 }
 
+// slab: the replicate's item (sign_item_words): its records, then (Gaussian) its slow-sample bitmap
 template <int DGP, int CEIL = 0>
 __device__ __forceinline__ void sign_pass1_body(const SignConst& c, uint32_t rep,
                                                 uint32_t* __restrict__ slab,
                                                 double* __restrict__ sums_out) {
   if constexpr (DGP == DCOR_DGP_GAUSSIAN) {
     __shared__ double2 zt[2 * DCOR_ZIG_N];
-    __shared__ uint32_t zq[DCOR_WAVES][ZQ_CAP];
-    __shared__ uint32_t zqn[DCOR_WAVES];
-    const int tid = threadIdx.x, wv = tid >> 6;
+    const int tid = threadIdx.x;
     for (int e = tid; e < 2 * DCOR_ZIG_N; e += DCOR_BLOCK)
       zt[e] = make_double2(dcor_zig_tab[e][0], dcor_zig_tab[e][1]);
-    if (tid < DCOR_WAVES) zqn[tid] = 0u;
     __syncthreads();
-    sign_pass1_core<DGP, false, CEIL>(c, rep, slab, sums_out, zt, zq[wv], &zqn[wv]);
+    sign_pass1_core<DGP, false, CEIL>(c, rep, slab, sums_out, zt, nullptr, nullptr, slab + sign_rec_words(c.n));
   } else {
     sign_pass1_core<DGP, false>(c, rep, slab, sums_out, nullptr, nullptr, nullptr);
   }
@@ -642,7 +688,7 @@ __global__ __launch_bounds__(DCOR_BLOCK, DCOR_P1_WPE) void k_sign_pass1(SignCons
                                                            uint32_t* __restrict__ scratch,
                                                            double* __restrict__ sums) {
   sign_pass1_body<DGP>(c, (uint32_t)(c.rep_begin + blockIdx.x),
-                       scratch + (size_t)blockIdx.x * (size_t)c.n, sums + SIGN_SUMS * (size_t)blockIdx.x);
+                       scratch + (size_t)blockIdx.x * sign_item_words(c.n, DGP), sums + SIGN_SUMS * (size_t)blockIdx.x);
 }
 // The pass-1 ceiling (CEIL above): same grid, registers and occupancy target as k_sign_pass1.
 template <int CM>
@@ -650,8 +696,74 @@ __global__ __launch_bounds__(DCOR_BLOCK, DCOR_P1_WPE) void k_sign_pass1_ceil(Sig
                                                                          uint32_t* __restrict__ scratch,
                                                                          double* __restrict__ sums) {
   sign_pass1_body<DCOR_DGP_GAUSSIAN, CM>(c, (uint32_t)(c.rep_begin + blockIdx.x),
-                                         scratch + (size_t)blockIdx.x * (size_t)c.n,
+                                         scratch + (size_t)blockIdx.x * sign_item_words(c.n, DCOR_DGP_GAUSSIAN),
                                          sums + SIGN_SUMS * (size_t)blockIdx.x);
+}
+
+// k_sign_drain: the slow samples pass 1 marked in a replicate's bitmap (workgroup Gaussian pass 1),
+// one workgroup per replicate at full occupancy.  Each is regenerated from its Philox block in full
+// (Dgp::from_block, the ziggurat's wedge and tail), its record rewritten, and its placeholder taken
+// out of / its true values put into compensated correction sums, which are block-reduced and added
+// to pass 1's sums of the replicate (double-double).  Only the summation order differs from adding
+// every sample in one loop (the low bits of the sums; the private centres they decide are unchanged
+// in practice).
+__device__ __forceinline__ void sign_drain_body(const SignConst& c, uint32_t rep, uint32_t* __restrict__ slab,
+                                                double* __restrict__ sums) {
+  __shared__ double2 zt[2 * DCOR_ZIG_N];
+  __shared__ double red[16 * DCOR_WAVES];
+  const int tid = threadIdx.x;
+  for (int e = tid; e < 2 * DCOR_ZIG_N; e += DCOR_BLOCK)
+    zt[e] = make_double2(dcor_zig_tab[e][0], dcor_zig_tab[e][1]);
+  __syncthreads();
+  const uint32_t* __restrict__ bm = slab + sign_rec_words(c.n);
+  const int64_t nfull = c.n / 4;
+  const uint32_t Q = (uint32_t)sign_bm_quads(c.n);
+  DD sx{0.0, 0.0}, sy{0.0, 0.0};
+  auto fix = [&](uint32_t i) {
+    const U4 w = draw(i, rep, DCOR_SITE_DGP_A, c.k0, c.k1);   // one block: placeholder and sample
+    double px, py;
+    gauss_fast_xy(c, zt, w, px, py);
+    ks_acc(sx, -px);
+    ks_acc(sy, -py);
+    double x, y;
+    Dgp<DCOR_DGP_GAUSSIAN>::from_block(c.g, i, rep, c.k0, c.k1, w, x, y, zt);
+    const double xc = rclip_fin(x, c.L), yc = rclip_fin(y, c.L);
+    ks_acc(sx, xc);
+    ks_acc(sy, yc);
+    slab[i] = sign_record(c, xc, yc, w.w3);
+  };
+  for (uint32_t t = (uint32_t)tid; t < 4u * 64u * Q; t += DCOR_BLOCK) {
+    const uint32_t wv = t / (64u * Q), q = (t / 64u) % Q, lane = t & 63u;
+    // steps of wave wv: groups 64 wv + 512 s + (0 | 256) + lane, s < its step count
+    const int64_t g0 = 64 * (int64_t)wv;
+    const uint32_t steps = g0 < nfull ? (uint32_t)((nfull - g0 + SIGN_P1_STEP - 1) / SIGN_P1_STEP) : 0u;
+    if (4u * q >= steps) continue;   // never written
+    uint32_t word = bm[t];
+    while (word) {
+      const uint32_t bit = (uint32_t)(__ffs(word) - 1);
+      word &= word - 1u;
+      const uint32_t s = 4u * q + 3u - (bit >> 3), j = bit & 7u;
+      const int64_t g = g0 + (int64_t)SIGN_P1_STEP * s + (j >= 4 ? DCOR_BLOCK : 0) + lane;
+      fix((uint32_t)(4 * g) + (j & 3u));
+    }
+  }
+  if (tid == 0 && (c.n & 3)) {
+    for (uint32_t word = bm[4u * 64u * Q]; word; word &= word - 1u)
+      fix((uint32_t)(4 * nfull) + (uint32_t)(__ffs(word) - 1));
+  }
+  DD d2[2] = {sx, sy};
+  block_sum_dd<2>(d2, red);
+  if (tid == 0) {
+    const DD ax = dd_add(DD{sums[0], sums[1]}, d2[0]), ay = dd_add(DD{sums[3], sums[4]}, d2[1]);
+    sums[0] = ax.hi; sums[1] = ax.lo;
+    sums[3] = ay.hi; sums[4] = ay.lo;
+  }
+}
+__global__ __launch_bounds__(DCOR_BLOCK) void k_sign_drain(SignConst c, uint32_t* __restrict__ scratch,
+                                                           double* __restrict__ sums) {
+  sign_drain_body(c, (uint32_t)(c.rep_begin + blockIdx.x),
+                  scratch + (size_t)blockIdx.x * sign_item_words(c.n, DCOR_DGP_GAUSSIAN),
+                  sums + SIGN_SUMS * (size_t)blockIdx.x);
 }
 
 // The private centres and scales from pass 1's sums (vert-cor.R:335-344): mean(xc) is the
@@ -1052,7 +1164,7 @@ __global__ __launch_bounds__(DCOR_BLOCK, DCOR_P2_WPE) void k_sign_pass2(SignCons
                                                            const double* __restrict__ sums,
                                                            SignPartial* __restrict__ part) {
   sign_pass2_body<DGP>(c, (uint32_t)(c.rep_begin + blockIdx.x),
-                       scratch + (size_t)blockIdx.x * (size_t)c.n,
+                       scratch + (size_t)blockIdx.x * sign_item_words(c.n, DGP),
                        sums + SIGN_SUMS * (size_t)blockIdx.x, part + blockIdx.x);
 }
 // The pass-2 ceiling (CEIL above, m = 8): same grid as k_sign_pass2, compiled for 4 waves per SIMD
@@ -1062,7 +1174,7 @@ __global__ __launch_bounds__(DCOR_BLOCK, 4) void k_sign_pass2_ceil(SignConst c,
                                                                          const double* __restrict__ sums,
                                                                          SignPartial* __restrict__ part) {
   sign_pass2_body<DCOR_DGP_GAUSSIAN, true>(c, (uint32_t)(c.rep_begin + blockIdx.x),
-                                           scratch + (size_t)blockIdx.x * (size_t)c.n,
+                                           scratch + (size_t)blockIdx.x * sign_item_words(c.n, DCOR_DGP_GAUSSIAN),
                                            sums + SIGN_SUMS * (size_t)blockIdx.x, part + blockIdx.x);
 }
 
@@ -1135,7 +1247,7 @@ __global__ __launch_bounds__(DCOR_BLOCK) void k_sign_pass1_w(SignConst c, int64_
   pass1_w_setup<DGP>(zt, zqn);
   const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   for (int64_t r = (int64_t)blockIdx.x * DCOR_WAVES + wv; r < nreps; r += (int64_t)gridDim.x * DCOR_WAVES)
-    sign_pass1_core<DGP, true>(c, (uint32_t)(c.rep_begin + r), scratch + (size_t)r * (size_t)c.n,
+    sign_pass1_core<DGP, true>(c, (uint32_t)(c.rep_begin + r), scratch + (size_t)r * sign_item_words(c.n, DGP),
                                sums + SIGN_SUMS * (size_t)r, zt, zq[wv], &zqn[wv]);
 }
 
@@ -1164,7 +1276,7 @@ __global__ __launch_bounds__(DCOR_BLOCK) void k_sign_pass2_w(SignConst c, int64_
   __syncthreads();
   const int64_t r = (int64_t)blockIdx.x * DCOR_WAVES + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   if (r >= nreps) return;
-  sign_pass2_wave_part<DGP>(c, (uint32_t)(c.rep_begin + r), scratch + (size_t)r * (size_t)c.n,
+  sign_pass2_wave_part<DGP>(c, (uint32_t)(c.rep_begin + r), scratch + (size_t)r * sign_item_words(c.n, DGP),
                             sums + SIGN_SUMS * (size_t)r, part + r, lt);
 }
 
@@ -1181,7 +1293,7 @@ __global__ __launch_bounds__(DCOR_BLOCK, DCOR_P2E_WPE) void k_sign_p2e_w(SignCon
   const int64_t r = (int64_t)blockIdx.x * DCOR_WAVES + __builtin_amdgcn_readfirstlane(wv);
   if (r >= nreps) return;  // whole waves only
   const uint32_t rep = (uint32_t)(c.rep_begin + r);
-  const P2Result p = sign_pass2_core<DGP, true>(c, rep, scratch + (size_t)r * (size_t)c.n,
+  const P2Result p = sign_pass2_core<DGP, true>(c, rep, scratch + (size_t)r * sign_item_words(c.n, DGP),
                                                 sums + SIGN_SUMS * (size_t)r, lt);
   sign_finish_wave<VPL>(c, rep, p, out + r, &wsel[wv]);
 }
@@ -1727,6 +1839,14 @@ __global__ __launch_bounds__(DCOR_BLOCK) void k_grid_sign_pass1(const SignConst*
   sign_pass1_body<DGP>(cells[it.cell], it.rep, scratch + it.scratch, sums + SIGN_SUMS * (size_t)blockIdx.x);
 }
 
+__global__ __launch_bounds__(DCOR_BLOCK) void k_grid_sign_drain(const SignConst* __restrict__ cells,
+                                                                const GridItem* __restrict__ items,
+                                                                uint32_t* __restrict__ scratch,
+                                                                double* __restrict__ sums) {
+  const GridItem it = items[blockIdx.x];
+  sign_drain_body(cells[it.cell], it.rep, scratch + it.scratch, sums + SIGN_SUMS * (size_t)blockIdx.x);
+}
+
 template <int DGP>
 __global__ __launch_bounds__(DCOR_BLOCK) void k_grid_sign_pass2(const SignConst* __restrict__ cells,
                                                                 const GridItem* __restrict__ items,
@@ -1893,6 +2013,9 @@ static void grid_codes_t(const SignConst* cells, const GridItem* items, int64_t 
                          uint32_t* scratch, double* sums, SignPartial* part, hipStream_t st) {
   hipLaunchKernelGGL(k_grid_sign_pass1<DGP>, dim3((unsigned)nitems), dim3(DCOR_BLOCK), 0, st, cells,
                      items, scratch, sums);
+  if (DGP == DCOR_DGP_GAUSSIAN)
+    hipLaunchKernelGGL(k_grid_sign_drain, dim3((unsigned)nitems), dim3(DCOR_BLOCK), 0, st, cells, items, scratch,
+                       sums);
   hipLaunchKernelGGL(k_grid_sign_pass2<DGP>, dim3((unsigned)nitems), dim3(DCOR_BLOCK), 0, st, cells,
                      items, scratch, sums, part);
 }
@@ -2096,6 +2219,8 @@ static int launch_codes_t(SignConst c, int64_t reps, int64_t chunk, const CodesB
     SignPartial* part = reinterpret_cast<SignPartial*>(bf.sums[b] + SIGN_SUMS * chunk);
     hipLaunchKernelGGL(k_sign_pass1<DGP>, dim3((unsigned)nr), dim3(DCOR_BLOCK), 0, st[b], c,
                        bf.slab[b], bf.sums[b]);
+    if (DGP == DCOR_DGP_GAUSSIAN)
+      hipLaunchKernelGGL(k_sign_drain, dim3((unsigned)nr), dim3(DCOR_BLOCK), 0, st[b], c, bf.slab[b], bf.sums[b]);
     hipLaunchKernelGGL(k_sign_pass2<DGP>, dim3((unsigned)nr), dim3(DCOR_BLOCK), 0, st[b], c,
                        bf.slab[b], bf.sums[b], part);
     if (int e = before_out(b)) return e;
@@ -2133,7 +2258,7 @@ static int occupancy_pad(const void* real, const void* ceil, size_t* pad) {
 }
 
 // One pass of the one-pass sign path over `reps` replicates as a single chunk on `stream`, for
-// timing (dcor_diag_sign_pass): 1 pass 1, 2 pass 2, 3 the epilogue; 11 / 12 the pass-1 / pass-2
+// timing (dcor_diag_sign_pass): 1 pass 1, 4 its slow-sample drain, 2 pass 2, 3 the epilogue; 11 / 12 the pass-1 / pass-2
 // ceilings (Gaussian DGP, m = 8) at the real passes' occupancy, 13 the pass-1 ceiling at its own.  slab / sums / part / out as launch_codes_t lays them out.
 int launch_sign_diag(const SignConst& c, int64_t reps, int which, uint32_t* slab, double* sums,
                      void* part_v, dcor_rep_out* out, void* stream) {
@@ -2157,6 +2282,9 @@ int launch_sign_diag(const SignConst& c, int64_t reps, int which, uint32_t* slab
       }
       break;
     case 3: launch_sign_epilogue(c, reps, part, out, st); break;
+    case 4:
+      if (c.g.dgp == DCOR_DGP_GAUSSIAN) hipLaunchKernelGGL(k_sign_drain, g, b, 0, st, c, slab, sums);
+      break;
     case 11: case 13: {
       // 11: at pass 1's occupancy (pass 1 holds more VGPRs and LDS than its ceiling); 13: its own
       size_t pad = 0;

@@ -50,9 +50,10 @@ size_t env_size(const char* name, size_t dflt, int shift) {
 bool codes_kind(int kind) { return kind == GK_SIGN_CODES || kind == GK_SIGN_CODES_W; }
 bool subg_kind(int kind) { return kind == GK_SUBG || kind == GK_SUBG_W; }
 
-uint64_t item_scratch(int kind, int64_t n) {
-  // code slabs start on 256-B boundaries (the kernels move records 16 B at a time)
-  if (codes_kind(kind)) return ((uint64_t)n + 63) & ~(uint64_t)63;   // u32 records
+uint64_t item_scratch(int kind, int dgp, int64_t n) {
+  // code slabs start on 256-B boundaries (the kernels move records 16 B at a time); the workgroup
+  // Gaussian pass 1 adds its slow-sample bitmap (sign_item_words)
+  if (codes_kind(kind)) return sign_item_words(n, dgp);   // u32 words
   if (kind == GK_SIGN_BERN) return (uint64_t)3 * 4 * ((n + 255) / 256);  // u64 plane words
   return 0;
 }
@@ -113,7 +114,7 @@ int exec_ranges(const dcor_cell* cells, const std::vector<CellPlan>& cp, const s
     if (r.count == 0 || p.nan_dgp) continue;
     Lim& l = lim[std::make_tuple(p.kind, p.dgp, p.vpl32)];
     l.items += (uint64_t)r.count;
-    l.scratch += (uint64_t)r.count * item_scratch(p.kind, cells[r.cell].n) * (p.kind == GK_SIGN_BERN ? 2 : 1);
+    l.scratch += (uint64_t)r.count * item_scratch(p.kind, p.dgp, cells[r.cell].n) * (p.kind == GK_SIGN_BERN ? 2 : 1);
   }
   for (auto& kv : lim) {
     Lim& l = kv.second;
@@ -150,7 +151,7 @@ int exec_ranges(const dcor_cell* cells, const std::vector<CellPlan>& cp, const s
       ci = it->second;
     }
     const int64_t n = cells[r.cell].n;
-    const uint64_t need = item_scratch(p.kind, n);
+    const uint64_t need = item_scratch(p.kind, p.dgp, n);
     const uint64_t unit = (p.kind == GK_SIGN_BERN) ? 2 : 1;
     const Lim& lm = lim[key];
     int64_t done = 0;

@@ -71,3 +71,29 @@ def test_launcher_parent_loads_no_gpu_library():
     p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
     assert p.returncode == 0, p.stderr[-2000:]
     assert "CLEAN" in p.stdout, p.stdout
+
+
+def _run_configs(args, env=None):
+    e = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    e.update(env or {})
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench_configs.py")] + args, capture_output=True,
+                          text=True, timeout=180, env=e)
+
+
+def test_configs_gpus_2_forms_two_ranks_for_c3_c4():
+    """bench_configs.py --gpus 2: two rank processes form one group and
+    split every C3 / C4 cell's replicates into contiguous shards (vert-cor.R:513,534-553)."""
+    p = _run_configs(["--gpus", "2", "--dry-run", "--only", "C3,C4"])
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [json.loads(ln) for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert [d["config"] for d in lines] == ["C3", "C4"]     # rank 0 only
+    c3, c4 = lines
+    assert c3["world_formed"] == 2 and c3["replicates"] == 24 * 100_000
+    assert c3["shards"] == [[[0, 50_000], [50_000, 50_000]]]
+    assert c4["world_formed"] == 2 and c4["shards"][1] == [[0, 50_000], [50_000, 50_000]]
+
+
+def test_configs_more_gpus_than_visible_is_refused():
+    p = _run_configs(["--gpus", "2", "--only", "C3"], env={"HIP_VISIBLE_DEVICES": ""})
+    assert p.returncode != 0
+    assert "visible" in p.stderr

@@ -134,3 +134,21 @@ def _assert_equals_world1(flat):
         for k in sa:
             x, y = sa[k], sr[k]
             assert (math.isnan(x) and math.isnan(y)) or abs(x - y) <= 1e-13 * max(abs(x), abs(y)) + 1e-300, (i, k, x, y)
+
+
+def test_bench_configs_c3_over_ranks_runs():
+    """bench_configs.py --gpus 1 takes the rank path C3 / C4 use on a node (one process per GPU,
+    RCCL all-gather of the accumulators) and prints a measured line with the world it formed; a
+    reduced C3 (64 replicates per cell of the eps = (1, 1) cells)."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    e = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    p = subprocess.run([sys.executable, os.path.join(root, "bench_configs.py"), "--gpus", "1", "--only", "C3",
+                        "--c3-reps", "64", "--c3-eps", "1x1"], capture_output=True, text=True, timeout=240, env=e)
+    assert p.returncode == 0, p.stderr[-3000:]
+    d = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
+    assert d["config"] == "C3" and d["world_formed"] == 1 and d["backend"] == "nccl"
+    assert d["replicates"] == 8 * 64 and d["cells_with_results"] == 8 and d["reps_per_s"] > 0

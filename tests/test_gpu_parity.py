@@ -262,3 +262,15 @@ def test_saturated_cells_vs_oracle(dc, orc, spec):
     got = simulate(cell, 6, rep_begin=2).cpu().numpy()
     ref = orc.sim_reps(cell.to_c(), 2, 8)
     assert_close(got, ref, what=f"saturated {spec}")
+
+
+# The workgroup Gaussian pass 1 marks slow samples in a per-replicate bitmap and k_sign_drain
+# regenerates them: n % 4 != 0 puts slow samples in the tail group's word, and n just above a
+# multiple of the 512-group loop step leaves waves with different step counts (partial quads).
+@pytest.mark.parametrize("n", [16_387, 100_003, 2_048 * 4 * 4 + 4 * 64 + 2, 131_071])
+def test_fused_vs_oracle_bitmap_geometry(dc, orc, n):
+    from dcor.sim import CellSpec, simulate
+    cell = CellSpec(n=n, rho=0.4, eps1=1.0, eps2=1.0, mu=(0.5, 0.5), sigma=(2.0, 2.0), seed=5_000_000 + n)
+    got = simulate(cell, 4, rep_begin=3).cpu().numpy()
+    ref = orc.sim_reps(cell.to_c(), 3, 7)
+    assert_close(got, ref, what=f"bitmap geometry n={n}")
