@@ -209,6 +209,7 @@ int make_sign(int64_t n, double eps1, double eps2, double alpha, int normalise, 
   if (md > 0x7fffffff) return fail(DCOR_EINVAL, "batch size m too large");
   c.n = n; c.m = (int32_t)md; c.k = kd >= 1 ? (int64_t)kd : 0;
   c.nd = nd; c.md = md; c.kd = kd;
+  c.pieces = sign_pieces(c.m);
   {
     int e = 0;
     c.md_pow2 = (std::frexp(md, &e) == 0.5) ? 1 : 0;  // md = 2^(e-1): count / md == count * 2^(1-e)

@@ -50,7 +50,16 @@ struct SignConst {
   double scale_Z, coefZ, q2, ratio, inv_sqrt_n, eps_r, w_laplace;
   double cbase_x, cinv_x, cbase_y, cinv_y;    // monotone code maps of clip(x), clip(y)
   float cinv_xf, cnb_xf, cinv_yf, cnb_yf;     // the same maps in fp32 / 65535: t = fma(v, inv, -base*inv)
+  int32_t pieces;                             // pass 2 by 8-record pieces: m / 8 for m % 8 == 0,
+                                              // 16 <= m <= 8 SIGN_PIECES_MAX; else 0
+  int32_t pad_pc;
 };
+// Pass 2's piece path (m % 8 == 0, 16 <= m <= 8 SIGN_PIECES_MAX): a wave's 64 lanes read 64
+// consecutive 8-record pieces (2 KB, coalesced), and each batch's P = m / 8 piece counts meet in
+// the wave's LDS buffer of 64 P words (dynamic shared memory: DCOR_WAVES x 64 x P_max x 4 B).
+#define SIGN_PIECES_MAX 31
+inline int32_t sign_pieces(int64_t m) { return (m % 8 == 0 && m >= 16 && m <= 8 * SIGN_PIECES_MAX) ? (int32_t)(m / 8) : 0; }
+inline size_t sign_piece_lds(int32_t pmax) { return (size_t)4 * 64 * (size_t)pmax * sizeof(uint32_t); }
 
 // Sub-G family: correlation_NI_subG + ci_INT_subG (ver-cor-subG.R:25-108).
 struct SubgConst {
@@ -200,12 +209,14 @@ __host__ __device__ inline uint64_t sign_item_words(int64_t n, int dgp) {
 #define SIGN_PARTIAL_BYTES 48
 // Pass 1 + pass 2 over `nitems` items (scratch: the items' code slabs; sums: SIGN_SUMS doubles per
 // item; part: per-item SignPartial), then the wave epilogue writing out[item.out].
+// pmax: the largest SignConst.pieces of the launch's cells (its pass-2 LDS, sign_piece_lds).
 int launch_grid_sign_codes(int dgp, const SignConst* cells, const GridItem* items, int64_t nitems,
-                           uint32_t* scratch, double* sums, SignPartial* part, int vpl32,
+                           uint32_t* scratch, double* sums, SignPartial* part, int vpl32, int pmax,
                            dcor_rep_out* out, void* stream);
 // Small cells: wave pass 1 + wave pass 2 / epilogue (sums: SIGN_SUMS doubles per item, no partials).
 int launch_grid_sign_codes_w(int dgp, const SignConst* cells, const GridItem* items, int64_t nitems,
-                             uint32_t* scratch, double* sums, int vpl32, dcor_rep_out* out, void* stream);
+                             uint32_t* scratch, double* sums, int vpl32, int pmax, dcor_rep_out* out,
+                             void* stream);
 int launch_grid_sign_regen(int dgp, const SignConst* cells, const GridItem* items, int64_t nitems,
                            dcor_rep_out* out, void* stream);
 int launch_grid_sign_bern(bool wave, const SignConst* cells, const GridItem* items, int64_t nitems,

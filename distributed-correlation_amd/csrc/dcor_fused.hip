@@ -817,11 +817,12 @@ __device__ __forceinline__ void scalar_laplace_wave(uint32_t rep, uint32_t k0, u
 // first two batches' records loaded once and then held in registers (an empty asm redefines them
 // every step, so nothing is hoisted), and no tie fix-up (1e-4 of samples): the loop's own
 // VALU-issue ceiling without the slab stream (dcor_diag_sign_pass, bench.py roofline.issue_frac).
+// pbuf: the calling wave's piece buffer (64 c.pieces words of LDS) when c.pieces > 0.
 template <int DGP, bool WAVE, bool CEIL = false>
 __device__ __forceinline__ P2Result sign_pass2_core(const SignConst& c, uint32_t rep,
                                                     const uint32_t* __restrict__ slab,
                                                     const double* __restrict__ sums_in,
-                                                    const double2* lt) {
+                                                    const double2* lt, uint32_t* pbuf = nullptr) {
   constexpr int NT = WAVE ? 64 : DCOR_BLOCK;   // threads sharing the replicate
   const int tid = WAVE ? (int)(threadIdx.x & 63) : (int)threadIdx.x;
   double lap[10];
@@ -997,6 +998,96 @@ __device__ __forceinline__ P2Result sign_pass2_core(const SignConst& c, uint32_t
       }
     }
   } else if constexpr (!CEIL) {
+    // m % 8 == 0, 16 <= m <= 248 (the grids' 32, C4's 200): 8-record pieces.  A replicate's
+    // batches go in rounds of 64 (waves take rounds wv, wv + 4, ...); in a round the wave's lanes
+    // read 64 consecutive pieces at a time (2 KB, coalesced -- lane-per-batch loads would touch 64
+    // cache lines per instruction at m = 32), decide their 8 records as the m = 8 loop does and
+    // store the piece's packed counts (x negatives, y negatives, INT bits, tie) to the wave's LDS
+    // buffer; then lane L adds batch L's P = m / 8 piece words and finishes the batch (fix-up on a
+    // tie, T).  Counts are the per-record decisions'; each lane adds its batches' T in round order.
+    if (c.pieces > 0) {
+      const uint32_t P = (uint32_t)c.pieces, m = (uint32_t)c.m;
+      const int lane = (int)(threadIdx.x & 63);
+      const int wv0 = WAVE ? 0 : (int)(threadIdx.x >> 6);
+      constexpr int NWV = WAVE ? 1 : DCOR_WAVES;
+      const int64_t rounds = (c.k + 63) / 64, npc = c.k * (int64_t)P;
+      auto ldp = [&](int64_t pc, uint4& lo, uint4& hi) {
+        const int64_t q = pc < npc ? pc : npc - 1;
+        lo = slab_ld4(slab + 8 * q);
+        hi = slab_ld4(slab + 8 * q + 4);
+      };
+      // one piece's packed counts: x negatives (byte 0), y negatives (byte 1), INT bits (byte 2),
+      // tie (byte 3); P <= 31 pieces sum without carries (8 P <= 248)
+      auto piece = [&](const uint4& lo, const uint4& hi) -> uint32_t {
+        const U4 w0{lo.x, lo.y, lo.z, lo.w}, w1{hi.x, hi.y, hi.z, hi.w};
+        uint32_t neg = 0, par = 0, mn = 0xffffffffu;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const uint32_t w = word(q < 4 ? w0 : w1, q & 3);
+          const uint32_t r = w & 0x7fff7fffu;
+          const uint32_t dN = pk_sub16(r, TN), dI = pk_sub16(r, TI);
+          mn = pk_min16(pk_min16(mn, dN), dI);
+          neg += pk_sign_bits(dN);
+          par = __builtin_amdgcn_alignbit(par, int_bit31(dI, w), 31u);
+        }
+        const uint32_t nb = __builtin_amdgcn_perm(neg, neg, 0x0c0c0400u);   // x | y << 8
+        return nb | ((uint32_t)__popc(par & 0xffu) << 16) | (has_zero16(mn) ? 0x01000000u : 0u);
+      };
+      // the wave's pieces as one stream of steps (its rounds wv0, wv0 + NWV, ..., P steps each),
+      // two register sets used in place and loaded two steps ahead across round ends
+      const int64_t my_rounds = rounds > wv0 ? (rounds - wv0 + NWV - 1) / NWV : 0;
+      const int64_t nsteps = my_rounds * (int64_t)P;
+      int64_t lt = 0;
+      uint32_t lit = 0;
+      auto load_next = [&](uint4& lo, uint4& hi) {
+        ldp((wv0 + NWV * lt) * 64 * (int64_t)P + (int64_t)lit * 64 + lane, lo, hi);
+        if (++lit == P) { lit = 0; ++lt; }
+      };
+      int64_t dt = 0;     // the decision cursor's round (of this wave) and piece
+      uint32_t dit = 0;
+      auto step = [&](const uint4& lo, const uint4& hi) {
+        pbuf[dit * 64 + (uint32_t)lane] = piece(lo, hi);
+        if (++dit < P) return;
+        // the round's pieces are in: lane L finishes batch 64 rd + L
+        __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
+        __builtin_amdgcn_wave_barrier();
+        uint32_t sum = 0;
+        for (uint32_t q = 0; q < P; ++q) sum += pbuf[(uint32_t)lane * P + q];
+        __builtin_amdgcn_s_waitcnt(0xC07F);   // read before the next round overwrites the buffer
+        __builtin_amdgcn_wave_barrier();
+        const int64_t j = (wv0 + NWV * dt) * 64 + lane;
+        if (j < c.k) {
+          const int64_t i0 = j * (int64_t)m;
+          int cx = (int)m - 2 * (int)(sum & 0xffu), cy = (int)m - 2 * (int)((sum >> 8) & 0xffu);
+          int cc = 2 * (int)((sum >> 16) & 0xffu) - (int)m;
+          if ((sum >> 24) != 0 || force_exact) {
+            ++ties;
+#pragma unroll 1
+            for (uint32_t r = 0; r < m; ++r) fix_fast(i0 + r, slab[i0 + r], cx, cy, cc);
+          }
+          core += cc;
+          batch_T(j, cx, cy, std::false_type());
+        }
+        dit = 0;
+        ++dt;
+      };
+      if (nsteps > 0) {
+        uint4 a0, a1, b0, b1;
+        load_next(a0, a1);
+        __builtin_amdgcn_sched_barrier(0);
+        load_next(b0, b1);
+        __builtin_amdgcn_sched_barrier(0);
+        // an odd step count runs one step past the end: it writes a buffer word no round reads
+        for (int64_t st = 0; st < nsteps; st += 2) {
+          step(a0, a1);
+          load_next(a0, a1);
+          __builtin_amdgcn_sched_barrier(0);
+          step(b0, b1);
+          load_next(b0, b1);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+    } else
     // any other m < 32768 (the reference grids' 11, 32, 200): the same packed decisions over a
     // stream of 16-B units.  A thread's batches j = tid, tid + NT, ... are U = ceil(m / 4) units
     // each, loaded 4-B aligned (one dwordx4 whatever m % 4; the last unit of a batch reads up to three
@@ -1138,6 +1229,13 @@ __device__ __forceinline__ P2Result sign_pass2_core(const SignConst& c, uint32_t
   return r;
 }
 
+// The calling wave's piece buffer in the launch's dynamic LDS (sign_piece_lds): 64 `stride` words
+// per wave of the workgroup.
+extern __shared__ uint32_t dcor_pbuf_dyn[];
+__device__ __forceinline__ uint32_t* wave_pbuf(int stride) {
+  return dcor_pbuf_dyn + (size_t)(threadIdx.x >> 6) * 64u * (uint32_t)stride;
+}
+
 template <int DGP, bool CEIL = false>
 __device__ __forceinline__ void sign_pass2_body(const SignConst& c, uint32_t rep,
                                                 const uint32_t* __restrict__ slab,
@@ -1146,7 +1244,7 @@ __device__ __forceinline__ void sign_pass2_body(const SignConst& c, uint32_t rep
   __shared__ double2 lt[256];
   log_tab_to_lds(lt, DCOR_BLOCK);
   __syncthreads();
-  const P2Result r = sign_pass2_core<DGP, false, CEIL>(c, rep, slab, sums_in, lt);
+  const P2Result r = sign_pass2_core<DGP, false, CEIL>(c, rep, slab, sums_in, lt, wave_pbuf(c.pieces));
   if (threadIdx.x == 0) {
     SignPartial p;
     p.sT[0] = r.sT.hi; p.sT[1] = r.sT.lo; p.sT2[0] = r.sT2.hi; p.sT2[1] = r.sT2.lo;
@@ -1255,8 +1353,8 @@ __global__ __launch_bounds__(DCOR_BLOCK) void k_sign_pass1_w(SignConst c, int64_
 template <int DGP>
 __device__ __forceinline__ void sign_pass2_wave_part(const SignConst& c, uint32_t rep, const uint32_t* slab,
                                                      const double* sums_in, SignPartial* part_out,
-                                                     const double2* lt) {
-  const P2Result r = sign_pass2_core<DGP, true>(c, rep, slab, sums_in, lt);
+                                                     const double2* lt, int pstride) {
+  const P2Result r = sign_pass2_core<DGP, true>(c, rep, slab, sums_in, lt, wave_pbuf(pstride));
   if ((threadIdx.x & 63) == 0) {
     SignPartial p;
     p.sT[0] = r.sT.hi; p.sT[1] = r.sT.lo; p.sT2[0] = r.sT2.hi; p.sT2[1] = r.sT2.lo;
@@ -1270,21 +1368,21 @@ template <int DGP>
 __global__ __launch_bounds__(DCOR_BLOCK) void k_sign_pass2_w(SignConst c, int64_t nreps,
                                                              const uint32_t* __restrict__ scratch,
                                                              const double* __restrict__ sums,
-                                                             SignPartial* __restrict__ part) {
+                                                             SignPartial* __restrict__ part, int pstride) {
   __shared__ double2 lt[256];
   log_tab_to_lds(lt, DCOR_BLOCK);
   __syncthreads();
   const int64_t r = (int64_t)blockIdx.x * DCOR_WAVES + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   if (r >= nreps) return;
   sign_pass2_wave_part<DGP>(c, (uint32_t)(c.rep_begin + r), scratch + (size_t)r * sign_item_words(c.n, DGP),
-                            sums + SIGN_SUMS * (size_t)r, part + r, lt);
+                            sums + SIGN_SUMS * (size_t)r, part + r, lt, pstride);
 }
 
 template <int DGP, int VPL>
 __global__ __launch_bounds__(DCOR_BLOCK, DCOR_P2E_WPE) void k_sign_p2e_w(SignConst c, int64_t nreps,
                                                            const uint32_t* __restrict__ scratch,
                                                            const double* __restrict__ sums,
-                                                           dcor_rep_out* out) {
+                                                           dcor_rep_out* out, int pstride) {
   __shared__ WaveMix<VPL> wsel[DCOR_WAVES];
   __shared__ double2 lt[256];
   log_tab_to_lds(lt, DCOR_BLOCK);
@@ -1294,7 +1392,7 @@ __global__ __launch_bounds__(DCOR_BLOCK, DCOR_P2E_WPE) void k_sign_p2e_w(SignCon
   if (r >= nreps) return;  // whole waves only
   const uint32_t rep = (uint32_t)(c.rep_begin + r);
   const P2Result p = sign_pass2_core<DGP, true>(c, rep, scratch + (size_t)r * sign_item_words(c.n, DGP),
-                                                sums + SIGN_SUMS * (size_t)r, lt);
+                                                sums + SIGN_SUMS * (size_t)r, lt, wave_pbuf(pstride));
   sign_finish_wave<VPL>(c, rep, p, out + r, &wsel[wv]);
 }
 
@@ -1902,7 +2000,7 @@ __global__ __launch_bounds__(DCOR_BLOCK) void k_grid_sign_pass2_w(const SignCons
                                                                   int64_t nitems,
                                                                   const uint32_t* __restrict__ scratch,
                                                                   const double* __restrict__ sums,
-                                                                  SignPartial* __restrict__ part) {
+                                                                  SignPartial* __restrict__ part, int pstride) {
   __shared__ double2 lt[256];
   log_tab_to_lds(lt, DCOR_BLOCK);
   __syncthreads();
@@ -1910,7 +2008,7 @@ __global__ __launch_bounds__(DCOR_BLOCK) void k_grid_sign_pass2_w(const SignCons
   if (r >= nitems) return;
   const GridItem it = items[r];
   sign_pass2_wave_part<DGP>(cells[it.cell], it.rep, scratch + it.scratch, sums + SIGN_SUMS * (size_t)r, part + r,
-                            lt);
+                            lt, pstride);
 }
 
 template <int DGP, int VPL>
@@ -1919,7 +2017,7 @@ __global__ __launch_bounds__(DCOR_BLOCK, DCOR_P2E_WPE) void k_grid_sign_p2e_w(co
                                                                 int64_t nitems,
                                                                 const uint32_t* __restrict__ scratch,
                                                                 const double* __restrict__ sums,
-                                                                dcor_rep_out* out) {
+                                                                dcor_rep_out* out, int pstride) {
   __shared__ WaveMix<VPL> wsel[DCOR_WAVES];
   __shared__ double2 lt[256];
   log_tab_to_lds(lt, DCOR_BLOCK);
@@ -1928,7 +2026,8 @@ __global__ __launch_bounds__(DCOR_BLOCK, DCOR_P2E_WPE) void k_grid_sign_p2e_w(co
   if (r >= nitems) return;  // whole waves only
   const GridItem it = items[r];
   const SignConst& c = cells[it.cell];
-  const P2Result p = sign_pass2_core<DGP, true>(c, it.rep, scratch + it.scratch, sums + SIGN_SUMS * (size_t)r, lt);
+  const P2Result p = sign_pass2_core<DGP, true>(c, it.rep, scratch + it.scratch, sums + SIGN_SUMS * (size_t)r, lt,
+                                                wave_pbuf(pstride));
   sign_finish_wave<VPL>(c, it.rep, p, out + it.out, &wsel[threadIdx.x >> 6]);
 }
 
@@ -2010,26 +2109,26 @@ static void launch_grid_epilogue(const SignConst* cells, const GridItem* items, 
 
 template <int DGP>
 static void grid_codes_t(const SignConst* cells, const GridItem* items, int64_t nitems,
-                         uint32_t* scratch, double* sums, SignPartial* part, hipStream_t st) {
+                         uint32_t* scratch, double* sums, SignPartial* part, int pmax, hipStream_t st) {
   hipLaunchKernelGGL(k_grid_sign_pass1<DGP>, dim3((unsigned)nitems), dim3(DCOR_BLOCK), 0, st, cells,
                      items, scratch, sums);
   if (DGP == DCOR_DGP_GAUSSIAN)
     hipLaunchKernelGGL(k_grid_sign_drain, dim3((unsigned)nitems), dim3(DCOR_BLOCK), 0, st, cells, items, scratch,
                        sums);
-  hipLaunchKernelGGL(k_grid_sign_pass2<DGP>, dim3((unsigned)nitems), dim3(DCOR_BLOCK), 0, st, cells,
-                     items, scratch, sums, part);
+  hipLaunchKernelGGL(k_grid_sign_pass2<DGP>, dim3((unsigned)nitems), dim3(DCOR_BLOCK), sign_piece_lds(pmax), st,
+                     cells, items, scratch, sums, part);
 }
 
 int launch_grid_sign_codes(int dgp, const SignConst* cells, const GridItem* items, int64_t nitems,
-                           uint32_t* scratch, double* sums, SignPartial* part, int vpl32,
+                           uint32_t* scratch, double* sums, SignPartial* part, int vpl32, int pmax,
                            dcor_rep_out* out, void* stream) {
   if (nitems <= 0) return 0;
   const hipStream_t st = (hipStream_t)stream;
   switch (dgp) {
-    case DCOR_DGP_GAUSSIAN: grid_codes_t<DCOR_DGP_GAUSSIAN>(cells, items, nitems, scratch, sums, part, st); break;
-    case DCOR_DGP_BERNOULLI: grid_codes_t<DCOR_DGP_BERNOULLI>(cells, items, nitems, scratch, sums, part, st); break;
-    case DCOR_DGP_MIX_GAUSSIAN: grid_codes_t<DCOR_DGP_MIX_GAUSSIAN>(cells, items, nitems, scratch, sums, part, st); break;
-    default: grid_codes_t<DCOR_DGP_BOUNDED_FACTOR>(cells, items, nitems, scratch, sums, part, st);
+    case DCOR_DGP_GAUSSIAN: grid_codes_t<DCOR_DGP_GAUSSIAN>(cells, items, nitems, scratch, sums, part, pmax, st); break;
+    case DCOR_DGP_BERNOULLI: grid_codes_t<DCOR_DGP_BERNOULLI>(cells, items, nitems, scratch, sums, part, pmax, st); break;
+    case DCOR_DGP_MIX_GAUSSIAN: grid_codes_t<DCOR_DGP_MIX_GAUSSIAN>(cells, items, nitems, scratch, sums, part, pmax, st); break;
+    default: grid_codes_t<DCOR_DGP_BOUNDED_FACTOR>(cells, items, nitems, scratch, sums, part, pmax, st);
   }
   launch_grid_epilogue(cells, items, nitems, part, vpl32, out, st);
   return last_err();
@@ -2054,33 +2153,35 @@ static bool p2e_fused() {
 
 template <int DGP>
 static void grid_codes_w_t(const SignConst* cells, const GridItem* items, int64_t nitems, uint32_t* scratch,
-                           double* sums, int vpl32, dcor_rep_out* out, hipStream_t st) {
+                           double* sums, int vpl32, int pmax, dcor_rep_out* out, hipStream_t st) {
   hipLaunchKernelGGL(k_grid_sign_pass1_w<DGP>, dim3(persistent_groups(nitems)), dim3(DCOR_BLOCK), 0, st, cells,
                      items, nitems, scratch, sums);
+  const size_t lds = sign_piece_lds(pmax);
   if (!p2e_fused()) {
     SignPartial* part = reinterpret_cast<SignPartial*>(sums + SIGN_SUMS * nitems);
-    hipLaunchKernelGGL(k_grid_sign_pass2_w<DGP>, dim3(wave_groups(nitems)), dim3(DCOR_BLOCK), 0, st, cells,
-                       items, nitems, scratch, sums, part);
+    hipLaunchKernelGGL(k_grid_sign_pass2_w<DGP>, dim3(wave_groups(nitems)), dim3(DCOR_BLOCK), lds, st, cells,
+                       items, nitems, scratch, sums, part, pmax);
     launch_grid_epilogue(cells, items, nitems, part, vpl32, out, st);
     return;
   }
   if (vpl32)
-    hipLaunchKernelGGL((k_grid_sign_p2e_w<DGP, 32>), dim3(wave_groups(nitems)), dim3(DCOR_BLOCK), 0, st, cells,
-                       items, nitems, scratch, sums, out);
+    hipLaunchKernelGGL((k_grid_sign_p2e_w<DGP, 32>), dim3(wave_groups(nitems)), dim3(DCOR_BLOCK), lds, st, cells,
+                       items, nitems, scratch, sums, out, pmax);
   else
-    hipLaunchKernelGGL((k_grid_sign_p2e_w<DGP, 16>), dim3(wave_groups(nitems)), dim3(DCOR_BLOCK), 0, st, cells,
-                       items, nitems, scratch, sums, out);
+    hipLaunchKernelGGL((k_grid_sign_p2e_w<DGP, 16>), dim3(wave_groups(nitems)), dim3(DCOR_BLOCK), lds, st, cells,
+                       items, nitems, scratch, sums, out, pmax);
 }
 
 int launch_grid_sign_codes_w(int dgp, const SignConst* cells, const GridItem* items, int64_t nitems,
-                             uint32_t* scratch, double* sums, int vpl32, dcor_rep_out* out, void* stream) {
+                             uint32_t* scratch, double* sums, int vpl32, int pmax, dcor_rep_out* out,
+                             void* stream) {
   if (nitems <= 0) return 0;
   const hipStream_t st = (hipStream_t)stream;
   switch (dgp) {
-    case DCOR_DGP_GAUSSIAN: grid_codes_w_t<DCOR_DGP_GAUSSIAN>(cells, items, nitems, scratch, sums, vpl32, out, st); break;
-    case DCOR_DGP_BERNOULLI: grid_codes_w_t<DCOR_DGP_BERNOULLI>(cells, items, nitems, scratch, sums, vpl32, out, st); break;
-    case DCOR_DGP_MIX_GAUSSIAN: grid_codes_w_t<DCOR_DGP_MIX_GAUSSIAN>(cells, items, nitems, scratch, sums, vpl32, out, st); break;
-    default: grid_codes_w_t<DCOR_DGP_BOUNDED_FACTOR>(cells, items, nitems, scratch, sums, vpl32, out, st);
+    case DCOR_DGP_GAUSSIAN: grid_codes_w_t<DCOR_DGP_GAUSSIAN>(cells, items, nitems, scratch, sums, vpl32, pmax, out, st); break;
+    case DCOR_DGP_BERNOULLI: grid_codes_w_t<DCOR_DGP_BERNOULLI>(cells, items, nitems, scratch, sums, vpl32, pmax, out, st); break;
+    case DCOR_DGP_MIX_GAUSSIAN: grid_codes_w_t<DCOR_DGP_MIX_GAUSSIAN>(cells, items, nitems, scratch, sums, vpl32, pmax, out, st); break;
+    default: grid_codes_w_t<DCOR_DGP_BOUNDED_FACTOR>(cells, items, nitems, scratch, sums, vpl32, pmax, out, st);
   }
   return last_err();
 }
@@ -2202,17 +2303,18 @@ static int launch_codes_t(SignConst c, int64_t reps, int64_t chunk, const CodesB
       hipLaunchKernelGGL(k_sign_pass1_w<DGP>, dim3(persistent_groups(nr)), dim3(DCOR_BLOCK), 0, st[b], c, nr,
                          bf.slab[b], bf.sums[b]);
       if (int e = before_out(b)) return e;
+      const size_t lds = sign_piece_lds(c.pieces);
       if (!p2e_fused()) {
         SignPartial* part = reinterpret_cast<SignPartial*>(bf.sums[b] + SIGN_SUMS * chunk);
-        hipLaunchKernelGGL(k_sign_pass2_w<DGP>, dim3(wave_groups(nr)), dim3(DCOR_BLOCK), 0, st[b], c, nr,
-                           bf.slab[b], bf.sums[b], part);
+        hipLaunchKernelGGL(k_sign_pass2_w<DGP>, dim3(wave_groups(nr)), dim3(DCOR_BLOCK), lds, st[b], c, nr,
+                           bf.slab[b], bf.sums[b], part, c.pieces);
         launch_sign_epilogue(c, nr, part, out + r, st[b]);
       } else if (c.mix.nsim > 1024)
-        hipLaunchKernelGGL((k_sign_p2e_w<DGP, 32>), dim3(wave_groups(nr)), dim3(DCOR_BLOCK), 0, st[b], c, nr,
-                           bf.slab[b], bf.sums[b], out + r);
+        hipLaunchKernelGGL((k_sign_p2e_w<DGP, 32>), dim3(wave_groups(nr)), dim3(DCOR_BLOCK), lds, st[b], c, nr,
+                           bf.slab[b], bf.sums[b], out + r, c.pieces);
       else
-        hipLaunchKernelGGL((k_sign_p2e_w<DGP, 16>), dim3(wave_groups(nr)), dim3(DCOR_BLOCK), 0, st[b], c, nr,
-                           bf.slab[b], bf.sums[b], out + r);
+        hipLaunchKernelGGL((k_sign_p2e_w<DGP, 16>), dim3(wave_groups(nr)), dim3(DCOR_BLOCK), lds, st[b], c, nr,
+                           bf.slab[b], bf.sums[b], out + r, c.pieces);
       if (int e = last_err()) return e;
       continue;
     }
@@ -2221,7 +2323,7 @@ static int launch_codes_t(SignConst c, int64_t reps, int64_t chunk, const CodesB
                        bf.slab[b], bf.sums[b]);
     if (DGP == DCOR_DGP_GAUSSIAN)
       hipLaunchKernelGGL(k_sign_drain, dim3((unsigned)nr), dim3(DCOR_BLOCK), 0, st[b], c, bf.slab[b], bf.sums[b]);
-    hipLaunchKernelGGL(k_sign_pass2<DGP>, dim3((unsigned)nr), dim3(DCOR_BLOCK), 0, st[b], c,
+    hipLaunchKernelGGL(k_sign_pass2<DGP>, dim3((unsigned)nr), dim3(DCOR_BLOCK), sign_piece_lds(c.pieces), st[b], c,
                        bf.slab[b], bf.sums[b], part);
     if (int e = before_out(b)) return e;
     launch_sign_epilogue(c, nr, part, out + r, st[b]);
@@ -2276,9 +2378,9 @@ int launch_sign_diag(const SignConst& c, int64_t reps, int which, uint32_t* slab
       break;
     case 2:
       switch (c.g.dgp) {
-        case DCOR_DGP_GAUSSIAN: hipLaunchKernelGGL(k_sign_pass2<DCOR_DGP_GAUSSIAN>, g, b, 0, st, c, slab, sums, part); break;
-        case DCOR_DGP_MIX_GAUSSIAN: hipLaunchKernelGGL(k_sign_pass2<DCOR_DGP_MIX_GAUSSIAN>, g, b, 0, st, c, slab, sums, part); break;
-        default: hipLaunchKernelGGL(k_sign_pass2<DCOR_DGP_BOUNDED_FACTOR>, g, b, 0, st, c, slab, sums, part);
+        case DCOR_DGP_GAUSSIAN: hipLaunchKernelGGL(k_sign_pass2<DCOR_DGP_GAUSSIAN>, g, b, sign_piece_lds(c.pieces), st, c, slab, sums, part); break;
+        case DCOR_DGP_MIX_GAUSSIAN: hipLaunchKernelGGL(k_sign_pass2<DCOR_DGP_MIX_GAUSSIAN>, g, b, sign_piece_lds(c.pieces), st, c, slab, sums, part); break;
+        default: hipLaunchKernelGGL(k_sign_pass2<DCOR_DGP_BOUNDED_FACTOR>, g, b, sign_piece_lds(c.pieces), st, c, slab, sums, part);
       }
       break;
     case 3: launch_sign_epilogue(c, reps, part, out, st); break;

@@ -68,6 +68,7 @@ struct Range {
 // and the pieces of its chunks.
 struct Group {
   int kind = 0, dgp = 0, vpl32 = 0;
+  int pmax = 0;                            // largest SignConst.pieces of the group's cells
   std::vector<SignConst> sign;
   std::vector<SubgConst> subg;
   std::map<int, uint32_t> slot;            // global cell -> constant table index
@@ -145,7 +146,12 @@ int exec_ranges(const dcor_cell* cells, const std::vector<CellPlan>& cp, const s
     uint32_t ci;
     if (it == g.slot.end()) {
       ci = (uint32_t)(subg_kind(p.kind) ? g.subg.size() : g.sign.size());
-      if (subg_kind(p.kind)) g.subg.push_back(p.subg); else g.sign.push_back(p.sign);
+      if (subg_kind(p.kind)) {
+        g.subg.push_back(p.subg);
+      } else {
+        g.sign.push_back(p.sign);
+        g.pmax = std::max<int>(g.pmax, p.sign.pieces);
+      }
       g.slot[r.cell] = ci;
     } else {
       ci = it->second;
@@ -271,11 +277,11 @@ int exec_ranges(const dcor_cell* cells, const std::vector<CellPlan>& cp, const s
       int rc = 0;
       if (g.kind == GK_SIGN_CODES_W) {
         rc = launch_grid_sign_codes_w(g.dgp, dsign, items, nit, (uint32_t*)((char*)scr + (size_t)b * slab_one),
-                                      (double*)sums, g.vpl32, d_out, sts[b]);
+                                      (double*)sums, g.vpl32, g.pmax, d_out, sts[b]);
       } else if (g.kind == GK_SIGN_CODES) {
         rc = launch_grid_sign_codes(g.dgp, dsign, items, nit, (uint32_t*)((char*)scr + (size_t)b * slab_one),
                                     (double*)sums, (SignPartial*)(sums + SIGN_SUMS * sizeof(double) * (size_t)nit),
-                                    g.vpl32, d_out, sts[b]);
+                                    g.vpl32, g.pmax, d_out, sts[b]);
       } else if (g.kind == GK_SIGN_REGEN) {
         rc = launch_grid_sign_regen(g.dgp, dsign, items, nit, d_out, st0);
       } else if (g.kind == GK_SIGN_BERN_W || g.kind == GK_SIGN_BERN) {
