@@ -1030,7 +1030,7 @@ __device__ __forceinline__ P2Result sign_pass2_core(const SignConst& c, uint32_t
           neg += pk_sign_bits(dN);
           par = __builtin_amdgcn_alignbit(par, int_bit31(dI, w), 31u);
         }
-        const uint32_t nb = __builtin_amdgcn_perm(neg, neg, 0x0c0c0400u);   // x | y << 8
+        const uint32_t nb = __builtin_amdgcn_perm(neg, neg, 0x0c0c0200u);   // x | y << 8 (bytes 0, 2 of neg)
         return nb | ((uint32_t)__popc(par & 0xffu) << 16) | (has_zero16(mn) ? 0x01000000u : 0u);
       };
       // the wave's pieces as one stream of steps (its rounds wv0, wv0 + NWV, ..., P steps each),
