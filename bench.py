@@ -149,8 +149,8 @@ def measure_passes(cell, reps: int = 2048, rep_begin: int = 0, iters: int = 5) -
     GPU, now (dcor_diag_sign_pass): each pass over `reps` replicates as one chunk on the current
     stream, alone on the device, median of `iters` launches timed with HIP events on that stream.
 
-      pass1 / drain / pass2 / epilogue   the real kernels (k_sign_pass1, k_sign_drain -- pass 1's slow
-                                 samples regenerated -- k_sign_pass2, k_sign_epilogue_w)
+      pass1 / pass2 / epilogue   the real kernels (k_sign_pass1, k_sign_pass2 -- whose first phase
+                                 regenerates pass 1's slow samples -- k_sign_epilogue_w)
       pass1_ceiling              k_sign_pass1's own hot loop -- Philox, ziggurat fast path, mvrnorm
                                  transform, clips, record codes, group sums -- with the slab store
                                  and the slow-normal queue removed, at pass 1's waves per SIMD
@@ -182,7 +182,7 @@ def measure_passes(cell, reps: int = 2048, rep_begin: int = 0, iters: int = 5) -
         torch.cuda.synchronize()
         return sorted(a.elapsed_time(b) for a, b in ev)[iters // 2]
 
-    out = {"pass1": timed(1), "drain": timed(4), "pass2": timed(2), "epilogue": timed(3),
+    out = {"pass1": timed(1), "pass2": timed(2), "epilogue": timed(3),
            "pass1_ceiling": timed(11), "pass1_ceiling_own_occ": timed(13), "pass2_ceiling": timed(12),
            "pass1_ceiling_plus_stores": timed(14), "pass1_ceiling_plus_queue": timed(15)}
     return {k: round(v, 5) for k, v in out.items()}
@@ -199,7 +199,7 @@ def sim_chunking(cell, reps: int):
     return ch.value, nc.value
 
 
-def serial_valu_time(names=("k_sign_pass1<0>", "k_sign_drain", "k_sign_pass2<0>", "k_sign_epilogue_w<16>")):
+def serial_valu_time(names=("k_sign_pass1<0>", "k_sign_pass2<0>", "k_sign_epilogue_w<16>")):
     """Hardware-anchored fraction per kernel from the committed serial profile (rocprofv3 PMC,
     scripts/summarize_prof.py): VALU time / SIMD-cycles, each VALU wave-instruction priced at its
     measured absolute issue cost -- the share of the SIMDs' cycles the kernel spends issuing VALU work
@@ -389,7 +389,7 @@ def main():
     if passes:
         ceil_call = nch * (passes["pass1_ceiling"] + passes["pass2_ceiling"] + passes["epilogue"])
         issue = {"call": ceil_call / kern_ms,
-                 "pass1": passes["pass1_ceiling"] / (passes["pass1"] + passes["drain"]),
+                 "pass1": passes["pass1_ceiling"] / passes["pass1"],
                  "pass2": passes["pass2_ceiling"] / passes["pass2"],
                  "pass1_occupancy_gain": passes["pass1_ceiling"] / passes["pass1_ceiling_own_occ"],
                  "chunk_reps": chunk, "chunks_per_call": nch, "ms": passes}
@@ -416,8 +416,9 @@ def main():
                                             "(chunks x (pass-1 ceiling + pass-2 ceiling + epilogue), "
                                             "dcor_diag_sign_pass 11/12/3: each pass's own instruction "
                                             "stream with its memory side removed, at its occupancy) "
-                                            "over the call's kernel time; issue.pass1 = the pass-1 "
-                                            "ceiling over pass 1 + its drain",
+                                            "over the call's kernel time (pass 2 includes the "
+                                            "regeneration of pass 1's slow samples, which its ceiling "
+                                            "does not)",
                          "issue": issue,
                          "valu_time": serial_valu_time(),
                          "valu_time_kind": "per kernel, from the serial rocprofv3 profile: VALU time at the "
@@ -428,7 +429,7 @@ def main():
                          "traffic_source_head": profile_stamp(_profile("headline"))[0] if _profile("headline") else None,
                          "traffic_source_fresh": profile_stamp(_profile("headline"))[1] if _profile("headline") else False,
                          "traffic_unit": "HBM B per simulate() call (rocprofv3 PMC, FETCH_SIZE x2 + WRITE_SIZE)",
-                         "kernel": "k_sign_pass1 + k_sign_drain + k_sign_pass2 + k_sign_epilogue_w (one simulate() call)",
+                         "kernel": "k_sign_pass1 + k_sign_pass2 + k_sign_epilogue_w (one simulate() call)",
                          "kernel_ms_avg": kern_ms,
                          "kernel_ms_kind": "HIP events: first call's start to last call's end over the timed calls, / K",
                          "work_units_per_rep": W},

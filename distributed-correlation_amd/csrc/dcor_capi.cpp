@@ -556,9 +556,10 @@ int prepare_cell(const dcor_cell& c, CellPlan& p) {
     } else {
       cx = cy = 0.0; rx = ry = 2.0;
     }
-    code_map(cx, rx, 32768.0, &k.cbase_x, &k.cinv_x);
-    code_map(cy, ry, 32768.0, &k.cbase_y, &k.cinv_y);
-    // code_pair's unorm16 maps t in [0, 1] to [0, 65535]: the fp32 map is the code map / 65535
+    // the window onto t in [0, 1], whose unorm16 (t 65535, rounded) >> 9 is the 7-bit record code
+    code_map(cx, rx, 65535.0, &k.cbase_x, &k.cinv_x);
+    code_map(cy, ry, 65535.0, &k.cbase_y, &k.cinv_y);
+    // code16_pair's unorm16 maps t in [0, 1] to [0, 65535]: the fp32 map is the code map / 65535
     k.cinv_xf = (float)(k.cinv_x / 65535.0); k.cnb_xf = (float)(-k.cbase_x * k.cinv_x / 65535.0);
     k.cinv_yf = (float)(k.cinv_y / 65535.0); k.cnb_yf = (float)(-k.cbase_y * k.cinv_y / 65535.0);
     if (c.dgp == DCOR_DGP_BERNOULLI && !force_regen)
@@ -797,8 +798,8 @@ int dcor_sim_chunking(const dcor_cell* cell, int64_t rep_count, int64_t* chunk, 
 int dcor_diag_sign_pass(const dcor_cell* cell, int64_t rep_begin, int64_t reps, int which, void* stream) {
   if (!cell || reps < 1 || reps > 65535 || rep_begin < 0 || rep_begin + reps > 0xffffffffLL)
     return fail(DCOR_EINVAL, "diag_sign_pass: bad arguments");
-  if ((which < 1 || which > 4) && (which < 11 || which > 15))
-    return fail(DCOR_EINVAL, "diag_sign_pass: which must be 1-4 or 11-15");
+  if ((which < 1 || which > 3) && (which < 11 || which > 15))
+    return fail(DCOR_EINVAL, "diag_sign_pass: which must be 1-3 or 11-15");
   if (int st = need_device()) return st;
   CellPlan cp;
   if (int st = prepare_cell(*cell, cp)) return st;
@@ -823,7 +824,6 @@ int dcor_diag_sign_pass(const dcor_cell* cell, int64_t rep_begin, int64_t reps, 
 int dcor_diag_sign_ties(const dcor_cell* cell, int64_t rep_begin, int64_t reps, int64_t* h_ties) {
   if (!h_ties) return fail(DCOR_EINVAL, "diag_sign_ties: null output");
   if (int st = dcor_diag_sign_pass(cell, rep_begin, reps, 1, nullptr)) return st;
-  if (int st = dcor_diag_sign_pass(cell, rep_begin, reps, 4, nullptr)) return st;
   if (int st = dcor_diag_sign_pass(cell, rep_begin, reps, 2, nullptr)) return st;
   void* scratch = nullptr;
   if (int st = arena_get(0, &scratch)) return st;   // the same arena dcor_diag_sign_pass used

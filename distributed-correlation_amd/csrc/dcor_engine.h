@@ -190,21 +190,10 @@ enum GridKind { GK_SIGN_CODES = 0, GK_SIGN_REGEN = 1, GK_SIGN_BERN_W = 2, GK_SIG
 #define GRID_BERN_W_NMAX 16384
 // doubles per replicate handed from the one-pass sign kernel's pass 1 to pass 2
 #define SIGN_SUMS 8
-// The one-pass sign path's per-replicate scratch ("item"): n u32 records padded to 64, then, for the
-// workgroup Gaussian pass 1 (n > SIGN_W_NMAX), the bitmap of its slow samples (a normal off the
-// ziggurat's fast path) that k_sign_drain regenerates.  Bitmap: per wave w of the 256-thread
-// workgroup and quad of loop steps q, one u32 per lane (4 steps x 8 bits: its two groups' pend
-// nibbles), [4][Q][64]; then 64 words, the first holding the n % 4 tail group's pend bits.
-#define SIGN_P1_STEP 512   // groups of 4 samples per pass-1 loop step of the workgroup (2 x 256)
-__host__ __device__ inline uint64_t sign_rec_words(int64_t n) { return ((uint64_t)n + 63) & ~(uint64_t)63; }
-__host__ __device__ inline uint64_t sign_bm_quads(int64_t n) {
-  const uint64_t steps = ((uint64_t)(n / 4) + SIGN_P1_STEP - 1) / SIGN_P1_STEP;
-  return (steps + 3) / 4;
-}
-__host__ __device__ inline uint64_t sign_bm_words(int64_t n) { return 4 * 64 * sign_bm_quads(n) + 64; }
-__host__ __device__ inline uint64_t sign_item_words(int64_t n, int dgp) {
-  return sign_rec_words(n) + (dgp == DCOR_DGP_GAUSSIAN && n > SIGN_W_NMAX ? sign_bm_words(n) : 0);
-}
+// The one-pass sign path's per-replicate scratch ("item", in u32 words): n u16 records, two per
+// word, padded to 64 words (256 B).
+__host__ __device__ inline uint64_t sign_rec_words(int64_t n) { return ((uint64_t)(n + 1) / 2 + 63) & ~(uint64_t)63; }
+__host__ __device__ inline uint64_t sign_item_words(int64_t n, int /*dgp*/) { return sign_rec_words(n); }
 // bytes of a SignPartial (pass 2 -> epilogue; dcor_fused.hip)
 #define SIGN_PARTIAL_BYTES 48
 // Pass 1 + pass 2 over `nitems` items (scratch: the items' code slabs; sums: SIGN_SUMS doubles per

@@ -34,6 +34,26 @@ template <> struct Dgp<DCOR_DGP_GAUSSIAN> {  // MASS::mvrnorm (vert-cor.R:389-39
     const double z2 = zig_draw(i, 1u, rep, k0, k1, w.w1, w.w2 >> 16, zt);
     mvn_z(z1, z2, g.mu0, g.mu1, g.a00, g.a01, g.a10, g.a11, &x, &y);
   }
+  // The same sample for the slow-sample drains, where (nearly) every lane has one normal off the
+  // fast path: the lanes run ONE divergent zig_slow loop between them -- each for its own slow
+  // normal, z1 or z2 -- instead of one loop for z1 and one for z2; a sample with both normals slow
+  // (about 1 in 4000) runs z2's after.  Same draws, same values as from_block.
+  static __device__ __forceinline__ void from_block_slow(const DgpConst& g, uint32_t i, uint32_t rep,
+                                                         uint32_t k0, uint32_t k1, const U4& w, double& x,
+                                                         double& y, const double2* zt) {
+    const uint32_t H1 = w.w2 & 0xffffu, H2 = w.w2 >> 16;
+    const double2 t1 = zig_entry(zt, H1 >> 6), t2 = zig_entry(zt, H2 >> 6);
+    double z1 = fma(zig_d(w.w0, zig_y_lo(H1)), t1.x, -t1.x);
+    double z2 = fma(zig_d(w.w1, zig_y_lo(H2)), t2.x, -t2.x);
+    const bool ok1 = fabs(z1) < t1.y, ok2 = fabs(z2) < t2.y;
+    if (!ok1 || !ok2) {
+      const uint32_t wh = ok1 ? 1u : 0u;
+      const double zs = zig_slow(i, wh, rep, k0, k1, ok1 ? w.w1 : w.w0, ok1 ? H2 : H1, zt);
+      if (ok1) z2 = zs; else z1 = zs;
+      if (!ok1 && !ok2) z2 = zig_slow(i, 1u, rep, k0, k1, w.w1, H2, zt);
+    }
+    mvn_z(z1, z2, g.mu0, g.mu1, g.a00, g.a01, g.a10, g.a11, &x, &y);
+  }
   static __device__ __forceinline__ void one_w3(const DgpConst& g, uint32_t i, uint32_t rep,
                                                 uint32_t k0, uint32_t k1, double& x, double& y,
                                                 uint32_t& w3) {
@@ -280,62 +300,43 @@ __device__ __forceinline__ void sign_finish(const SignConst& c, uint32_t rep, DD
 
 // ======================================== fused sign family, one pass (hot) ===
 // Pass 1 generates each sample once: the DP-mean sums of clip(x), clip(y) (vert-cor.R:
-// 328-340) and a 4-byte record per sample in a per-workgroup slab -- monotone 15-bit codes
-// of clip(x) (bits 0-14) and clip(y) (bits 16-30) and the INT flip bit (31); bit 15 is 0.  The
+// 328-340) and a 2-byte record per sample in a per-replicate slab -- monotone 7-bit codes of
+// clip(x) (bits 0-6) and clip(y) (bits 8-14) and the INT flip bit S (bit 7); bit 15 is 0.  The
 // code map q (below) is monotone non-decreasing, so q(xc) != q(mu) proves sign(xc - mu); pass 2
 // decides every sign from codes and regenerates only samples whose code ties a threshold's code.
 // Results equal the two-pass algorithm's exactly.  Each thread generates groups of 4 consecutive
-// samples (16-B slab stores).
-// Two launches per replicate chunk (pass 1, pass 2); scratch = chunk * n * 4 B.
-// The code pair of (x, y) is one record word: q(v) = min(unorm16(fma(float(v), inv, nb)), 32767)
-// per half, inv = levels / (2 R 65535), nb = -base inv.  Every step (round to float, fma with
-// inv > 0, v_cvt_pknorm_u16_f32's clamp to [0, 1] and round to nearest, the min) is monotone
-// non-decreasing, which is all the sign decision needs; the 2^15 code levels sit far above fp32
-// resolution.  Both codes come from one v_pk_fma_f32 and one v_cvt_pknorm_u16_f32 (a NaN codes
-// as 0; a NaN threshold is flagged), and bit 15 of each half is 0 (code_pair, below).
+// samples (8-B slab stores).
+// q(v) = unorm16(fma(float(v), inv, nb)) >> 9 per coordinate, inv = 1 / (2 R), nb = -base inv:
+// every step (round to float, fma with inv > 0, v_cvt_pknorm_u16_f32's clamp to [0, 1] and round
+// to nearest, the shift) is monotone non-decreasing, which is all the sign decision needs.  Both
+// 16-bit unorms come from one v_pk_fma_f32 and one v_cvt_pknorm_u16_f32 (a NaN codes as 0; a NaN
+// threshold is flagged); one v_perm_b32 takes two samples' high bytes, and a shift and mask make
+// the 7-bit codes of a record pair.  128 levels per coordinate over the window (prepare_cell) put
+// about 1e-3 of the headline's records on a threshold's code; pass 2 recomputes those batches
+// exactly, deferred (sign_pass2_core).  Round 4's 4-byte records with 15-bit codes took twice the
+// slab bytes and twice pass 2's decision work (packed 16-bit compares).
 __device__ __forceinline__ int sgnq(uint32_t q, uint32_t qm) { return (q > qm) - (q < qm); }
-// sign(q - qm) for 16-bit codes as one subtract + one v_med3_i32 (clamp to [-1, 1]); asm
-// keeps the compiler from expanding the clamp into compare/select pairs.
-__device__ __forceinline__ int sgnd(uint32_t q, uint32_t qm) {
-  const int d = (int)q - (int)qm;
-  int r;
-  asm("v_med3_i32 %0, %1, -1, 1" : "=v"(r) : "v"(d));
-  return r;
-}
-
-// Packed 16-bit halves of a record word (both codes are 15-bit): one v_pk_sub_u16 gives
-// (qx - tx, qy - ty) with the sign bits at 15 and 31, one v_pk_lshrrev_b16 moves them to 0 and 16.
 typedef unsigned short dcor_u16x2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ uint32_t pk_sub16(uint32_t a, uint32_t b) {
-  return __builtin_bit_cast(uint32_t, __builtin_bit_cast(dcor_u16x2, a) - __builtin_bit_cast(dcor_u16x2, b));
-}
-__device__ __forceinline__ uint32_t pk_sign_bits(uint32_t a) {
-  const dcor_u16x2 v = __builtin_bit_cast(dcor_u16x2, a);
-  return __builtin_bit_cast(uint32_t, (dcor_u16x2)(v >> (dcor_u16x2){15, 15}));
-}
-__device__ __forceinline__ uint32_t pk_min16(uint32_t a, uint32_t b) {
-  return __builtin_bit_cast(uint32_t, __builtin_elementwise_min(__builtin_bit_cast(dcor_u16x2, a),
-                                                                __builtin_bit_cast(dcor_u16x2, b)));
-}
-__device__ __forceinline__ bool has_zero16(uint32_t a) { return (a & 0xffffu) == 0u || (a >> 16) == 0u; }
-// bit 31: dI[31] ^ dI[15] ^ w[31] (one v_bitop3 after the shift)
-__device__ __forceinline__ uint32_t int_bit31(uint32_t dI, uint32_t w) {
-  return __builtin_amdgcn_bitop3_b32(dI, dI << 16, w, 0x96);
-}
 typedef float dcor_f32x2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ uint32_t code_pair(double x, double y, float ix, float iy, float bx,
-                                              float by) {
+// the 16-bit unorms of (x, y), x in the low half
+__device__ __forceinline__ uint32_t code16_pair(double x, double y, float ix, float iy, float bx, float by) {
   const dcor_f32x2 v = {(float)x, (float)y};
   const dcor_f32x2 t = __builtin_elementwise_fma(v, dcor_f32x2{ix, iy}, dcor_f32x2{bx, by});
-  const dcor_u16x2 q = __builtin_amdgcn_cvt_pknorm_u16(t.x, t.y);
-  return __builtin_bit_cast(uint32_t, __builtin_elementwise_min(q, (dcor_u16x2){32767, 32767}));
+  return __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pknorm_u16(t.x, t.y));
 }
-// the same codes from two scalar fmas (fma rounds exactly either way): the thresholds' form, which
-// keeps the kernel-argument fields out of a vector build
-__device__ __forceinline__ uint32_t code_pair_s(double x, double y, float ix, float iy, float bx,
-                                                float by) {
-  const dcor_u16x2 q = __builtin_amdgcn_cvt_pknorm_u16(fmaf((float)x, ix, bx), fmaf((float)y, iy, by));
-  return __builtin_bit_cast(uint32_t, __builtin_elementwise_min(q, (dcor_u16x2){32767, 32767}));
+// the same from two scalar fmas (fma rounds exactly either way): the thresholds' form, which keeps
+// the kernel-argument fields out of a vector build
+__device__ __forceinline__ uint32_t code16_pair_s(double x, double y, float ix, float iy, float bx, float by) {
+  return __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pknorm_u16(fmaf((float)x, ix, bx), fmaf((float)y, iy, by)));
+}
+// one record from a unorm pair and its flip (0 or 0x80)
+__device__ __forceinline__ uint32_t rec_of(uint32_t P, uint32_t fl) {
+  return ((P >> 9) & 0x7fu) | ((P >> 17) & 0x7f00u) | fl;
+}
+// two records in one word: sample a in the low half
+__device__ __forceinline__ uint32_t rec_pair(uint32_t Pa, uint32_t Pb, uint32_t fla, uint32_t flb) {
+  const uint32_t hb = __builtin_amdgcn_perm(Pb, Pa, 0x07050301u);   // high bytes: xa, ya, xb, yb
+  return ((hb >> 1) & 0x7f7f7f7fu) | fla | (flb << 16);
 }
 
 template <int DGP>
@@ -370,18 +371,25 @@ __device__ __forceinline__ void exact_signs(const SignConst& c, const SignStd& s
 // Pass 1 folds two sample groups' plain sums per compensated add (one TwoSum per 8 samples); pass 2
 // (m = 8) pair-groups the T sums of a thread's two batches in flight.  Measured (round 4): 11 and 4 us
 // per headline chunk against per-group / per-batch sums.
-// Slab layout: record i of a replicate at slab[i].  (Measured and dropped in round 4: a
-// wave-contiguous half-batch layout for m = 8, pass 2 181 vs 177 us; non-temporal slab stores and
-// loads, +-0.)
-typedef uint32_t dcor_u32x4 __attribute__((ext_vector_type(4)));
-// four records from any 4-B aligned position (global_load_dwordx4 takes dword alignment)
+// Slab layout: record i of a replicate is u16 i of its slab (two records per 32-bit word).
+// (Measured and dropped in round 4, with 4-B records: a wave-contiguous half-batch layout for
+// m = 8, pass 2 181 vs 177 us; non-temporal slab stores and loads, +-0.)
 typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
-__device__ __forceinline__ void slab_st4(uint32_t* p, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
-  *reinterpret_cast<uint4*>(p) = make_uint4(a, b, c, d);
+// a group of 4 records (i0 % 4 == 0): one 8-B store of two record pairs
+__device__ __forceinline__ void slab_st_group(uint32_t* slab, uint32_t i0, uint32_t r01, uint32_t r23) {
+  *reinterpret_cast<uint2*>(slab + (i0 >> 1)) = make_uint2(r01, r23);
+}
+__device__ __forceinline__ void slab_st1(uint32_t* slab, uint32_t i, uint32_t r) {
+  reinterpret_cast<uint16_t*>(slab)[i] = (uint16_t)r;
 }
 __device__ __forceinline__ uint4 slab_ld4(const uint32_t* p) { return *reinterpret_cast<const uint4*>(p); }
+// 16 B from a 4-B aligned word (global_load_dwordx4 takes dword alignment)
+__device__ __forceinline__ uint4 slab_ld4a(const uint32_t* p) {
+  const u32x4a4 v = *reinterpret_cast<const u32x4a4*>(p);
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
 
-// The Gaussian DGP's ziggurat fast path for one sample's Philox block (pass 1 and k_sign_drain
+// The Gaussian DGP's ziggurat fast path for one sample's Philox block (pass 1 and the drain
 // compute it alike): the clipped sample, true = both normals took the fast path (otherwise the
 // values are a finite placeholder in [-L, L] that pass 1 adds and the drain takes out again).
 __device__ __forceinline__ bool gauss_fast_xy(const SignConst& c, const double2* zt, const U4& w, double& xc,
@@ -396,10 +404,13 @@ __device__ __forceinline__ bool gauss_fast_xy(const SignConst& c, const double2*
   yc = rclip_fin(y, c.L);
   return ok;
 }
-// A sample's slab record: the code pair of (clip(x), clip(y)) and the INT flip (u < flipT) in bit 31.
+// The INT flip of a sample's 32-bit word, u < flipT (flipT <= 2^32), as the record's bit 7.
+__device__ __forceinline__ uint32_t sign_flip7(const SignConst& c, uint32_t u) {
+  return (c.flipT != 0 && u <= (uint32_t)(c.flipT - 1u)) ? 0x80u : 0u;
+}
+// A sample's slab record (u16): the codes of (clip(x), clip(y)) and its INT flip.
 __device__ __forceinline__ uint32_t sign_record(const SignConst& c, double xc, double yc, uint32_t u) {
-  const uint32_t ftm1 = (uint32_t)(c.flipT - 1u), fbit = c.flipT != 0 ? 0x80000000u : 0u;
-  return code_pair(xc, yc, c.cinv_xf, c.cinv_yf, c.cnb_xf, c.cnb_yf) | (u <= ftm1 ? fbit : 0u);
+  return rec_of(code16_pair(xc, yc, c.cinv_xf, c.cinv_yf, c.cnb_xf, c.cnb_yf), sign_flip7(c, u));
 }
 
 // Per-wave slow-normal queue (the wave-per-replicate pass 1): a group adds at most 256 entries per wave (about 1.6 % of a wave's
@@ -422,25 +433,25 @@ __device__ __forceinline__ uint32_t sign_record(const SignConst& c, double xc, d
 
 // WAVE = false: one 256-thread workgroup per replicate; WAVE = true: one wave per replicate (the
 // caller's workgroup has loaded the ziggurat table `zt` into LDS once for all its replicates).
-// Slow samples (Gaussian DGP): the workgroup form marks them in the replicate's bitmap `bm`
-// (sign_bm_words) for k_sign_drain, a kernel of its own at full occupancy; the wave form queues
-// them in its LDS queue zq / zqn and drains it itself.
+// Slow samples (Gaussian DGP): both forms regenerate them inside the kernel, 64 at a time, from a
+// per-wave LDS list zq: the workgroup form fills it from a register of pend bits every four loop
+// steps (ballot compaction, no atomics); the wave form through an LDS atomic counter zqn.
 // CEIL (Gaussian workgroup form only; a measurement kernel, never a result): the same hot loop with
-// its memory side removed -- no slab store, no slow-sample bitmap; an empty asm consumes the records
+// its memory side removed -- no slab store, no slow-sample list or regeneration; an empty asm consumes the records
 // and the pending masks, so the compiler keeps every instruction that computes them.  Its time is
 // the loop's own VALU-issue ceiling (dcor_diag_sign_pass, bench.py roofline.issue_frac).  CEIL = 2
-// keeps the slab stores only, CEIL = 3 the bitmap stores only (the cost of each).
+// keeps the slab stores only, CEIL = 3 the slow-sample list and its regenerations only (the cost of each).
 template <int DGP, bool WAVE, int CEIL = 0>
 __device__ __forceinline__ void sign_pass1_core(const SignConst& c, uint32_t rep,
                                                 uint32_t* __restrict__ slab,
                                                 double* __restrict__ sums_out, const double2* zt,
-                                                uint32_t* zq, uint32_t* zqn, uint32_t* __restrict__ bm = nullptr) {
+                                                uint32_t* zq, uint32_t* zqn) {
   constexpr int NT = WAVE ? 64 : DCOR_BLOCK;
   const int tid = WAVE ? (int)(threadIdx.x & 63) : (int)threadIdx.x;
   DD sx{0.0, 0.0}, sy{0.0, 0.0};
   const float cix = c.cinv_xf, ciy = c.cinv_yf, cbx = c.cnb_xf, cby = c.cnb_yf;
-  // the INT flip from its 32-bit word: u < flipT (flipT <= 2^32) as a 32-bit compare
-  const uint32_t ftm1 = (uint32_t)(c.flipT - 1u), fbit = c.flipT != 0 ? 0x80000000u : 0u;
+  // the INT flip from its 32-bit word: u < flipT (flipT <= 2^32) as a 32-bit compare, bit 7
+  const uint32_t ftm1 = (uint32_t)(c.flipT - 1u), fbit = c.flipT != 0 ? 0x80u : 0u;
   auto record_w = [&](double xc, double yc, uint32_t u) { return sign_record(c, xc, yc, u); };
   // each thread runs its groups in increasing order; the partial last group (n % 4) is the last
   // group of its thread
@@ -457,7 +468,7 @@ __device__ __forceinline__ void sign_pass1_core(const SignConst& c, uint32_t rep
     auto group = [&](int64_t g4, auto full_tag, double& hx, double& hy, uint32_t& pend) {
       constexpr bool FULL = decltype(full_tag)::value;
       const uint32_t i0 = (uint32_t)(4 * g4);
-      uint32_t rec[4];
+      uint32_t P[4], fl[4];
       pend = 0;
       double gx, gy;
 #pragma unroll
@@ -470,21 +481,23 @@ __device__ __forceinline__ void sign_pass1_core(const SignConst& c, uint32_t rep
         gx = q == 0 ? ax : gx + ax;
         gy = q == 0 ? ay : gy + ay;
         pend |= (valid && !ok) ? (1u << q) : 0u;
-        rec[q] = record_w(xc, yc, w.w3);
+        P[q] = code16_pair(xc, yc, cix, ciy, cbx, cby);
+        fl[q] = w.w3 <= ftm1 ? fbit : 0u;
       }
       hx += gx;
       hy += gy;
+      const uint32_t r01 = rec_pair(P[0], P[1], fl[0], fl[1]), r23 = rec_pair(P[2], P[3], fl[2], fl[3]);
       if constexpr (CEIL == 1 || CEIL == 3)
-        asm volatile("" ::"v"(rec[0]), "v"(rec[1]), "v"(rec[2]), "v"(rec[3]));
+        asm volatile("" ::"v"(r01), "v"(r23));
       if constexpr (CEIL == 1 || CEIL == 2) {
         asm volatile("" ::"v"(pend));
         if constexpr (CEIL == 1) return;
       }
       if constexpr (CEIL == 0 || CEIL == 2) {
         if (FULL) {
-          slab_st4(slab + i0, rec[0], rec[1], rec[2], rec[3]);
+          slab_st_group(slab, i0, r01, r23);
         } else {
-          for (int q = 0; q < 4; ++q) if ((int64_t)(i0 + q) < c.n) slab[i0 + q] = rec[q];
+          for (int q = 0; q < 4; ++q) if ((int64_t)(i0 + q) < c.n) slab_st1(slab, i0 + q, rec_of(P[q], fl[q]));
         }
       }
     };
@@ -526,7 +539,7 @@ __device__ __forceinline__ void sign_pass1_core(const SignConst& c, uint32_t rep
         const uint32_t w3 = w.w3;
         // the table from LDS in the workgroup kernel (the wave kernel keeps the global table: the
         // LDS pointer costs it six VGPRs and a wave per SIMD)
-        Dgp<DGP>::from_block(c.g, i, rep, c.k0, c.k1, w, x, y, WAVE ? nullptr : zt);
+        Dgp<DGP>::from_block_slow(c.g, i, rep, c.k0, c.k1, w, x, y, WAVE ? nullptr : zt);
         const double xc = rclip_fin(x, c.L), yc = rclip_fin(y, c.L);
         ks_acc(sx, xc);
         ks_acc(sy, yc);
@@ -534,7 +547,7 @@ __device__ __forceinline__ void sign_pass1_core(const SignConst& c, uint32_t rep
           const uint32_t r = record_w(xc, yc, w3);
           asm volatile("" ::"v"(r));
         } else {
-          slab[i] = record_w(xc, yc, w3);
+          slab_st1(slab, i, record_w(xc, yc, w3));
         }
       }
       wave_sync();
@@ -545,11 +558,60 @@ __device__ __forceinline__ void sign_pass1_core(const SignConst& c, uint32_t rep
     // plain 8-sample sums: half the TwoSum chains of a fold per group (the low bits of the sums
     // differ from per-group folds; the private centres they decide are unchanged in practice)
     if constexpr (!WAVE) {
-      // The step's two pend nibbles enter a per-lane byte shift register, stored every four steps
-      // (one coalesced u32 per lane, bitmap word [wv][step / 4][lane], step 4q + t in byte 3 - t);
-      // a partial last quad is stored left-aligned, its missing steps' bytes zero.
-      uint32_t acc = 0, s4 = 0;
-      uint32_t* bw = bm + (size_t)wv * (64 * sign_bm_quads(c.n)) + lane;
+      // Slow samples: the step's two pend nibbles enter a per-lane byte shift register; every four
+      // steps the wave compacts the register's set bits into its LDS list -- each lane hands over one
+      // bit per sub-round (ballot + mbcnt slots, the count wave-uniform) -- and regenerates 64 at a
+      // time, every lane busy, between its hot-loop steps (so the regenerations of a CU's waves
+      // interleave with the others' hot loops instead of coinciding at the replicates' ends).
+      // Each regeneration takes the placeholder out of and the true value into the lane's sums (one
+      // compensated add of their difference per coordinate) and rewrites the record.
+      uint32_t acc = 0, s4 = 0, q = 0, cnt = 0;
+      auto fix = [&](uint32_t i) {
+        const U4 w = draw(i, rep, DCOR_SITE_DGP_A, c.k0, c.k1);   // one block: placeholder and sample
+        double px, py, x, y;
+        fast_xy(w, px, py);
+        Dgp<DGP>::from_block_slow(c.g, i, rep, c.k0, c.k1, w, x, y, zt);
+        const double xc = rclip_fin(x, c.L), yc = rclip_fin(y, c.L);
+        ks_acc(sx, xc - px);
+        ks_acc(sy, yc - py);
+        const uint32_t r = record_w(xc, yc, w.w3);
+        if constexpr (CEIL == 3) asm volatile("" ::"v"(r));
+        else slab_st1(slab, i, r);
+      };
+      auto flush = [&](uint32_t upto) {   // regenerate the list's top `upto` entries
+        __builtin_amdgcn_s_waitcnt(0x0070);   // vmcnt(0), lgkmcnt(0): placeholders stored, list in LDS
+        __builtin_amdgcn_wave_barrier();
+        if ((uint32_t)lane < upto) fix(zq[cnt - upto + (uint32_t)lane]);
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        __builtin_amdgcn_wave_barrier();
+        cnt -= upto;
+      };
+      // bit (byte 3 - t, nibble h, bit j) of a quad word whose first step's groups start at g0: step
+      // t of the quad, group g0 + 2 NT t + h NT + lane; tail: the n % 4 group's bit j
+      auto take = [&](uint32_t word, int64_t g0, bool tail) {   // every lane, converged
+        while (__ballot(word != 0u)) {
+          const bool has = word != 0u;
+          uint32_t idx = 0;
+          if (has) {
+            const uint32_t bit = (uint32_t)(__ffs(word) - 1);
+            const int64_t g = g0 + (int64_t)(2 * NT) * (3 - (bit >> 3)) + ((bit & 4u) ? NT : 0) + lane;
+            idx = tail ? (uint32_t)(4 * nfull) + bit : (uint32_t)(4 * g) + (bit & 3u);
+            word &= word - 1u;
+          }
+          const uint64_t bal = __ballot(has);
+          if (has)
+            zq[cnt + __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u))] = idx;
+          cnt += (uint32_t)__popcll(bal);
+          if (cnt >= 64u) flush(64u);
+        }
+      };
+      auto quad_word = [&](uint32_t word) {
+        if constexpr (CEIL == 1 || CEIL == 2)
+          asm volatile("" ::"v"(word));
+        else
+          take(word, 64 * (int64_t)wv + (int64_t)(2 * NT) * (4 * (int64_t)q), false);
+        ++q;
+      };
       for (int64_t b = 64 * wv; b < nfull; b += 2 * NT) {  // trip count uniform per wave
         double hx = 0.0, hy = 0.0;
         uint32_t pa = 0, pb = 0;
@@ -559,18 +621,13 @@ __device__ __forceinline__ void sign_pass1_core(const SignConst& c, uint32_t rep
         ks_acc(sy, hy);
         acc = (acc << 8) | pa | (pb << 4);
         if (++s4 == 4) {
-          if constexpr (CEIL == 0 || CEIL == 3) *bw = acc;
-          else asm volatile("" ::"v"(acc));
-          bw += 64;
+          quad_word(acc);
           acc = 0;
           s4 = 0;
         }
       }
-      if (s4) {
-        if constexpr (CEIL == 0 || CEIL == 3) *bw = acc << (8 * (4 - s4));
-        else asm volatile("" ::"v"(acc));
-      }
-      // the partial last group (n % 4): its pend bits in the tail word
+      if (s4) quad_word(acc << (8 * (4 - s4)));   // the partial last quad, left-aligned
+      // the partial last group (n % 4)
       const bool last = (c.n & 3) && tid == (int)(nfull % NT);
       uint32_t pt = 0;
       if (last) {
@@ -579,8 +636,10 @@ __device__ __forceinline__ void sign_pass1_core(const SignConst& c, uint32_t rep
         ks_acc(sx, hx);
         ks_acc(sy, hy);
       }
-      if constexpr (CEIL == 0 || CEIL == 3)
-        if ((c.n & 3) ? last : tid == 0) bm[4 * 64 * sign_bm_quads(c.n)] = pt;
+      if constexpr (CEIL == 0 || CEIL == 3) {
+        take(pt, 0, true);
+        if (cnt) flush(cnt);
+      }
     } else {
     for (int64_t b = 0; b < nfull; b += 2 * NT) {  // trip count uniform per wave
       double hx = 0.0, hy = 0.0;
@@ -614,32 +673,32 @@ __device__ __forceinline__ void sign_pass1_core(const SignConst& c, uint32_t rep
       constexpr bool FULL = decltype(full_tag)::value;
       const uint32_t i0 = (uint32_t)(4 * g4);
       double x[4], y[4];
-      uint32_t fl[4];  // INT flip bits (vert-cor.R:175), in bit 31
+      uint32_t fl[4];  // INT flip bits (vert-cor.R:175), in bit 7
       if constexpr (Dgp<DGP>::flip_src == FLIP_SPARE24) {
         uint32_t u24[4];
         Dgp<DGP>::quad_u24(c.g, i0, rep, c.k0, c.k1, x, y, u24);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) fl[q] = u24[q] < c.flipT24 ? 0x80000000u : 0u;
+        for (int q = 0; q < 4; ++q) fl[q] = u24[q] < c.flipT24 ? 0x80u : 0u;
       } else {
         const U4 fw = draw((uint32_t)g4, rep, DCOR_SITE_FLIP, c.k0, c.k1);
         Dgp<DGP>::quad(c.g, i0, rep, c.k0, c.k1, x, y);
 #pragma unroll
         for (int q = 0; q < 4; ++q) fl[q] = word(fw, q) <= ftm1 ? fbit : 0u;
       }
-      uint32_t rec[4];
+      uint32_t P[4];
       double gx = 0.0, gy = 0.0;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const double xc = rclip_fin(x[q], c.L), yc = rclip_fin(y[q], c.L);
         if (FULL || (int64_t)(i0 + q) < c.n) { gx += xc; gy += yc; }
-        rec[q] = code_pair(xc, yc, cix, ciy, cbx, cby) | fl[q];
+        P[q] = code16_pair(xc, yc, cix, ciy, cbx, cby);
       }
       ks_acc(sx, gx);
       ks_acc(sy, gy);
       if (FULL) {
-        slab_st4(slab + i0, rec[0], rec[1], rec[2], rec[3]);
+        slab_st_group(slab, i0, rec_pair(P[0], P[1], fl[0], fl[1]), rec_pair(P[2], P[3], fl[2], fl[3]));
       } else {
-        for (int q = 0; q < 4; ++q) if ((int64_t)(i0 + q) < c.n) slab[i0 + q] = rec[q];
+        for (int q = 0; q < 4; ++q) if ((int64_t)(i0 + q) < c.n) slab_st1(slab, i0 + q, rec_of(P[q], fl[q]));
       }
     };
     for (int64_t g4 = tid; g4 < nfull; g4 += NT) group(g4, std::true_type());
@@ -659,18 +718,19 @@ __device__ __forceinline__ void sign_pass1_core(const SignConst& c, uint32_t rep
   }
 }
 
-// slab: the replicate's item (sign_item_words): its records, then (Gaussian) its slow-sample bitmap
+// slab: the replicate's records (sign_item_words)
 template <int DGP, int CEIL = 0>
 __device__ __forceinline__ void sign_pass1_body(const SignConst& c, uint32_t rep,
                                                 uint32_t* __restrict__ slab,
                                                 double* __restrict__ sums_out) {
   if constexpr (DGP == DCOR_DGP_GAUSSIAN) {
     __shared__ double2 zt[2 * DCOR_ZIG_N];
+    __shared__ uint32_t zl[DCOR_WAVES][128];   // each wave's slow-sample list
     const int tid = threadIdx.x;
     for (int e = tid; e < 2 * DCOR_ZIG_N; e += DCOR_BLOCK)
       zt[e] = make_double2(dcor_zig_tab[e][0], dcor_zig_tab[e][1]);
     __syncthreads();
-    sign_pass1_core<DGP, false, CEIL>(c, rep, slab, sums_out, zt, nullptr, nullptr, slab + sign_rec_words(c.n));
+    sign_pass1_core<DGP, false, CEIL>(c, rep, slab, sums_out, zt, zl[tid >> 6], nullptr);
   } else {
     sign_pass1_core<DGP, false>(c, rep, slab, sums_out, nullptr, nullptr, nullptr);
   }
@@ -681,7 +741,7 @@ __device__ __forceinline__ void sign_pass1_body(const SignConst& c, uint32_t rep
 #define DCOR_P1_WPE 1
 #endif
 #ifndef DCOR_P2_WPE
-#define DCOR_P2_WPE 1
+#define DCOR_P2_WPE 4
 #endif
 template <int DGP>
 __global__ __launch_bounds__(DCOR_BLOCK, DCOR_P1_WPE) void k_sign_pass1(SignConst c,
@@ -700,71 +760,6 @@ __global__ __launch_bounds__(DCOR_BLOCK, DCOR_P1_WPE) void k_sign_pass1_ceil(Sig
                                          sums + SIGN_SUMS * (size_t)blockIdx.x);
 }
 
-// k_sign_drain: the slow samples pass 1 marked in a replicate's bitmap (workgroup Gaussian pass 1),
-// one workgroup per replicate at full occupancy.  Each is regenerated from its Philox block in full
-// (Dgp::from_block, the ziggurat's wedge and tail), its record rewritten, and its placeholder taken
-// out of / its true values put into compensated correction sums, which are block-reduced and added
-// to pass 1's sums of the replicate (double-double).  Only the summation order differs from adding
-// every sample in one loop (the low bits of the sums; the private centres they decide are unchanged
-// in practice).
-__device__ __forceinline__ void sign_drain_body(const SignConst& c, uint32_t rep, uint32_t* __restrict__ slab,
-                                                double* __restrict__ sums) {
-  __shared__ double2 zt[2 * DCOR_ZIG_N];
-  __shared__ double red[16 * DCOR_WAVES];
-  const int tid = threadIdx.x;
-  for (int e = tid; e < 2 * DCOR_ZIG_N; e += DCOR_BLOCK)
-    zt[e] = make_double2(dcor_zig_tab[e][0], dcor_zig_tab[e][1]);
-  __syncthreads();
-  const uint32_t* __restrict__ bm = slab + sign_rec_words(c.n);
-  const int64_t nfull = c.n / 4;
-  const uint32_t Q = (uint32_t)sign_bm_quads(c.n);
-  DD sx{0.0, 0.0}, sy{0.0, 0.0};
-  auto fix = [&](uint32_t i) {
-    const U4 w = draw(i, rep, DCOR_SITE_DGP_A, c.k0, c.k1);   // one block: placeholder and sample
-    double px, py;
-    gauss_fast_xy(c, zt, w, px, py);
-    ks_acc(sx, -px);
-    ks_acc(sy, -py);
-    double x, y;
-    Dgp<DCOR_DGP_GAUSSIAN>::from_block(c.g, i, rep, c.k0, c.k1, w, x, y, zt);
-    const double xc = rclip_fin(x, c.L), yc = rclip_fin(y, c.L);
-    ks_acc(sx, xc);
-    ks_acc(sy, yc);
-    slab[i] = sign_record(c, xc, yc, w.w3);
-  };
-  for (uint32_t t = (uint32_t)tid; t < 4u * 64u * Q; t += DCOR_BLOCK) {
-    const uint32_t wv = t / (64u * Q), q = (t / 64u) % Q, lane = t & 63u;
-    // steps of wave wv: groups 64 wv + 512 s + (0 | 256) + lane, s < its step count
-    const int64_t g0 = 64 * (int64_t)wv;
-    const uint32_t steps = g0 < nfull ? (uint32_t)((nfull - g0 + SIGN_P1_STEP - 1) / SIGN_P1_STEP) : 0u;
-    if (4u * q >= steps) continue;   // never written
-    uint32_t word = bm[t];
-    while (word) {
-      const uint32_t bit = (uint32_t)(__ffs(word) - 1);
-      word &= word - 1u;
-      const uint32_t s = 4u * q + 3u - (bit >> 3), j = bit & 7u;
-      const int64_t g = g0 + (int64_t)SIGN_P1_STEP * s + (j >= 4 ? DCOR_BLOCK : 0) + lane;
-      fix((uint32_t)(4 * g) + (j & 3u));
-    }
-  }
-  if (tid == 0 && (c.n & 3)) {
-    for (uint32_t word = bm[4u * 64u * Q]; word; word &= word - 1u)
-      fix((uint32_t)(4 * nfull) + (uint32_t)(__ffs(word) - 1));
-  }
-  DD d2[2] = {sx, sy};
-  block_sum_dd<2>(d2, red);
-  if (tid == 0) {
-    const DD ax = dd_add(DD{sums[0], sums[1]}, d2[0]), ay = dd_add(DD{sums[3], sums[4]}, d2[1]);
-    sums[0] = ax.hi; sums[1] = ax.lo;
-    sums[3] = ay.hi; sums[4] = ay.lo;
-  }
-}
-__global__ __launch_bounds__(DCOR_BLOCK) void k_sign_drain(SignConst c, uint32_t* __restrict__ scratch,
-                                                           double* __restrict__ sums) {
-  sign_drain_body(c, (uint32_t)(c.rep_begin + blockIdx.x),
-                  scratch + (size_t)blockIdx.x * sign_item_words(c.n, DCOR_DGP_GAUSSIAN),
-                  sums + SIGN_SUMS * (size_t)blockIdx.x);
-}
 
 // The private centres and scales from pass 1's sums (vert-cor.R:335-344): mean(xc) is the
 // double-double sum divided by n, rounded once.
@@ -817,12 +812,14 @@ __device__ __forceinline__ void scalar_laplace_wave(uint32_t rep, uint32_t k0, u
 // first two batches' records loaded once and then held in registers (an empty asm redefines them
 // every step, so nothing is hoisted), and no tie fix-up (1e-4 of samples): the loop's own
 // VALU-issue ceiling without the slab stream (dcor_diag_sign_pass, bench.py roofline.issue_frac).
-// pbuf: the calling wave's piece buffer (64 c.pieces words of LDS) when c.pieces > 0.
+// pbuf: the calling wave's piece buffer (64 c.pieces words of LDS) when c.pieces > 0; tq: its
+// tie-deferral queue (TQ words of LDS).
+#define TQ 512
 template <int DGP, bool WAVE, bool CEIL = false>
 __device__ __forceinline__ P2Result sign_pass2_core(const SignConst& c, uint32_t rep,
                                                     const uint32_t* __restrict__ slab,
                                                     const double* __restrict__ sums_in,
-                                                    const double2* lt, uint32_t* pbuf = nullptr) {
+                                                    const double2* lt, uint32_t* pbuf, uint32_t* tq) {
   constexpr int NT = WAVE ? 64 : DCOR_BLOCK;   // threads sharing the replicate
   const int tid = WAVE ? (int)(threadIdx.x & 63) : (int)threadIdx.x;
   double lap[10];
@@ -848,35 +845,46 @@ __device__ __forceinline__ P2Result sign_pass2_core(const SignConst& c, uint32_t
   // sign(d/sd) == sign(d) needs sd < 2^900 (no underflow of the quotient); else exact path.
   const bool force_exact = !(s.sdNx < 0x1p900 && s.sdNy < 0x1p900 && s.sdIx < 0x1p900 &&
                              s.sdIy < 0x1p900);
-  const uint32_t TN = code_pair_s(s.muNx, s.muNy, c.cinv_xf, c.cinv_yf, c.cnb_xf, c.cnb_yf);
-  const uint32_t TI = code_pair_s(s.muIx, s.muIy, c.cinv_xf, c.cinv_yf, c.cnb_xf, c.cnb_yf);
-  const uint32_t qNx = TN & 0xffffu, qNy = TN >> 16, qIx = TI & 0xffffu, qIy = TI >> 16;
+  // threshold codes (the records' map), and as the four bytes (x, y, x, y) of a record pair
+  const uint32_t TN = code16_pair_s(s.muNx, s.muNy, c.cinv_xf, c.cinv_yf, c.cnb_xf, c.cnb_yf);
+  const uint32_t TI = code16_pair_s(s.muIx, s.muIy, c.cinv_xf, c.cinv_yf, c.cnb_xf, c.cnb_yf);
+  const uint32_t qNx = (TN & 0xffffu) >> 9, qNy = TN >> 25, qIx = (TI & 0xffffu) >> 9, qIy = TI >> 25;
+  const uint32_t TN4 = (qNx | (qNy << 8)) * 0x00010001u, TI4 = (qIx | (qIy << 8)) * 0x00010001u;
+  const uint32_t TN4p = TN4 + 0x01010101u, TI4p = TI4 + 0x01010101u;
+  const uint16_t* __restrict__ s16 = reinterpret_cast<const uint16_t*>(slab);
   bool bad_ni = thr_nan, bad_int = thr_nan;
   DD sT{0.0, 0.0}, sT2{0.0, 0.0};
   long long core = 0;
   int ties = 0;   // batches whose codes tie a threshold (diagnostic: dcor_diag_sign_ties)
-  // Fast path: signs from codes (branch-free).  A sample whose code ties a threshold's
-  // code is flagged and fixed up afterwards by exact regeneration (rolled loop, rare).
-  // sign(xc - mu) from codes: sgnd in {-1, 0, 1}; 0 is a tie (the code cannot decide).
-  // Bit 0 of a sign is set iff it is nonzero, so the AND of the four flags a tie.
-  auto fast = [&](uint32_t w, int& cx, int& cy, int& cc) -> bool {
-    const uint32_t qx = w & 0xffffu, qy = (w >> 16) & 0x7fffu;
-    const int sNx = sgnd(qx, qNx), sNy = sgnd(qy, qNy), sIx = sgnd(qx, qIx), sIy = sgnd(qy, qIy);
-    cx += sNx;
-    cy += sNy;
-    const int p = __mul24(sIx, sIy);
-    const int m = (int)(w >> 31) - 1;  // 0 for flip S = 1, -1 for S = 0: (2S - 1) p
-    cc += (p ^ m) - m;
-    return ((sNx & sNy & sIx & sIy) & 1) == 0;
-  };
-  auto fixup = [&](int64_t i, uint32_t w, int& cx, int& cy, int& cc, bool& bni) {
-    const uint32_t qx = w & 0xffffu, qy = (w >> 16) & 0x7fffu;
-    const int f = (w >> 31) ? 1 : -1;
+  // One record's exact signs: from the codes unless a code ties a threshold's (then the sample is
+  // regenerated, exact_signs).  Adds its NI signs to (cx, cy) and its INT term to cc.
+  auto exact_rec = [&](int64_t i, uint32_t w, int& cx, int& cy, int& cc, bool& bni) {
+    const uint32_t qx = w & 0x7fu, qy = (w >> 8) & 0x7fu;
+    const int f = (w & 0x80u) ? 1 : -1;
     int nx, ny, ix, iy;
-    exact_signs<DGP>(c, s, (uint32_t)i, rep, nx, ny, ix, iy, bni, bad_int);
-    cx += nx - sgnq(qx, qNx);
-    cy += ny - sgnq(qy, qNy);
-    cc += f * (ix * iy - sgnq(qx, qIx) * sgnq(qy, qIy));
+    if (force_exact || qx == qNx || qy == qNy || qx == qIx || qy == qIy) {
+      exact_signs<DGP>(c, s, (uint32_t)i, rep, nx, ny, ix, iy, bni, bad_int);
+    } else {
+      nx = qx < qNx ? -1 : 1;
+      ny = qy < qNy ? -1 : 1;
+      ix = qx < qIx ? -1 : 1;
+      iy = qy < qIy ? -1 : 1;
+    }
+    cx += nx;
+    cy += ny;
+    cc += f * ix * iy;
+  };
+  // Two records (one word) by SWAR: g = w | 0x80 per byte, g - T per byte has bit 7 = (q >= t) with
+  // no borrow between bytes (0x80 + q - t >= 1), and g - (T + 1) has it = (q > t): the two differ
+  // exactly on a tie.  neg counts (q < t) per byte (x0, y0, x1, y1); the INT bit of each record is
+  // px ^ py ^ S (bits 7, 23 of dI ^ dI >> 8 ^ w), +1 when set.  13 full-rate operations and one
+  // v_bcnt for two records.
+  auto word2 = [&](uint32_t w, uint32_t& neg, uint32_t& pc, uint32_t& tie) {
+    const uint32_t g = w | 0x80808080u;
+    const uint32_t dN = g - TN4, dN1 = g - TN4p, dI = g - TI4, dI1 = g - TI4p;
+    tie |= (dN ^ dN1) | (dI ^ dI1);
+    neg += (~dN >> 7) & 0x01010101u;
+    pc += (uint32_t)__popc((dI ^ (dI >> 8) ^ w) & 0x00800080u);
   };
   // mean of m signs = count / m (exact quotient for the configs' m); a power-of-two m divides by
   // an exact multiply.  M8: the headline geometry, m = 8 known at compile time.
@@ -904,149 +912,149 @@ __device__ __forceinline__ P2Result sign_pass2_core(const SignConst& c, uint32_t
     const double yt = (double)cy * 0.125 + c.by * unit_laplace_t(u53(w.w2, w.w3), lt);
     return 8.0 * xt * yt;                                                 // vert-cor.R:233
   };
-  auto fix_fast = [&](int64_t i, uint32_t w, int& cx, int& cy, int& cc) {
-    const uint32_t qx = w & 0x7fffu, qy = (w >> 16) & 0x7fffu;
-    if (!(force_exact || qx == qNx || qy == qNy || qx == qIx || qy == qIy)) return;
-    const int f = (w >> 31) ? 1 : -1;
-    const int fNx = qx < qNx ? -1 : 1, fNy = qy < qNy ? -1 : 1;
-    const int fIx = qx < qIx ? -1 : 1, fIy = qy < qIy ? -1 : 1;
-    int nx, ny, ix, iy;
-    exact_signs<DGP>(c, s, (uint32_t)i, rep, nx, ny, ix, iy, bad_ni, bad_int);
-    cx += nx - fNx;
-    cy += ny - fNy;
-    cc += f * (ix * iy - fIx * fIy);
+  // Tie deferral.  A batch whose codes tie a threshold (about 1e-3 of records at the headline's 128
+  // code levels) is not fixed up inside the loop, where every lane would wait for its regeneration:
+  // its index goes to the wave's LDS queue (ballot + mbcnt slots, the count wave-uniform) and the
+  // whole wave recomputes queued batches exactly, one per lane (exact_rec over its m records, then
+  // its T), once per loop trip when the queue holds more than TQ - 256 entries (a trip queues at most
+  // 256) and after the loop: one inlined copy of the recomputation per loop.  Callers defer at
+  // wave-uniform points.  Which batches tie depends on the replicate alone, so a replicate's bits
+  // do not depend on the launch; the code window moves only the order of the T sums.
+  const int lane = (int)(threadIdx.x & 63);
+  uint32_t tqn = 0;
+  auto drain_ties = [&]() {
+    if (tqn == 0) return;
+    __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): the queue's entries are in LDS
+    __builtin_amdgcn_wave_barrier();
+    for (uint32_t e = (uint32_t)lane; e < tqn; e += 64) {
+      const int64_t j = tq[e];
+      const int64_t i0 = j * c.m;
+      int cx = 0, cy = 0, cc = 0;
+#pragma unroll 1
+      for (int r = 0; r < c.m; ++r) exact_rec(i0 + r, s16[i0 + r], cx, cy, cc, bad_ni);
+      core += cc;
+      batch_T(j, cx, cy, std::false_type());
+      ++ties;
+    }
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_wave_barrier();
+    tqn = 0;
+  };
+  auto defer = [&](bool tie, int64_t j) -> bool {
+    const uint64_t bal = __ballot(tie);
+    if (bal) {
+      if (tie)
+        tq[tqn + __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u))] =
+            (uint32_t)j;
+      tqn += (uint32_t)__popcll(bal);
+    }
+    return tie;
+  };
+  auto drain_if_full = [&]() {
+    if (tqn > TQ - 256) drain_ties();
   };
   if (c.m == 8) {
-    // headline geometry: one thread = one batch = two 16-B loads.
-    // Signs by packed 16-bit subtraction of the threshold pairs T = (tx, ty) from the record with the
-    // flip bit masked: the sign bit of each half of d = rec - T is (q < t), and a half of d is zero
-    // exactly on a tie, so the running packed minimum of the d's has a zero half iff the batch holds
-    // a tie.  A tie is counted as +1 here and corrected by the fix-up.  Bit 31 of
-    // dI ^ (dI << 16) ^ rec is the sample's INT bit sbx ^ sby ^ S (the flip S is the record's bit
-    // 31) -- contribution (2S - 1) sx sy = +1 exactly when it is set.
-    // the count triple (cx, cy, cc) of batch j from its two 16-B record loads
-    auto decide = [&](int64_t j, const uint4& lo, const uint4& hi, int& cx, int& cy, int& cc) {
-      const U4 w0{lo.x, lo.y, lo.z, lo.w}, w1{hi.x, hi.y, hi.z, hi.w};
-      uint32_t neg = 0, par = 0, mn = 0xffffffffu;
-#pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        const uint32_t w = word(q < 4 ? w0 : w1, q & 3);
-        const uint32_t r = w & 0x7fff7fffu;
-        const uint32_t dN = pk_sub16(r, TN), dI = pk_sub16(r, TI);
-        mn = pk_min16(pk_min16(mn, dN), dI);                         // a zero half is a tie
-        neg += pk_sign_bits(dN);                                     // halves count to <= 8
-        par = __builtin_amdgcn_alignbit(par, int_bit31(dI, w), 31u); // (par << 1) | INT bit
-      }
-      cx = 8 - 2 * (int)(neg & 0xffffu);
-      cy = 8 - 2 * (int)(neg >> 16);
-      cc = 2 * __popc(par) - 8;
+    // headline geometry: one thread = one batch = one 16-B load (8 records), decided by word2.
+    auto decide = [&](const uint4& v, int& cx, int& cy, int& cc) -> bool {
+      uint32_t neg = 0, pc = 0, tie = 0;
+      word2(v.x, neg, pc, tie);
+      word2(v.y, neg, pc, tie);
+      word2(v.z, neg, pc, tie);
+      word2(v.w, neg, pc, tie);
+      const uint32_t t = neg + (neg >> 16);      // x0 + x1 in byte 0, y0 + y1 in byte 1
+      cx = 8 - 2 * (int)(t & 0xffu);
+      cy = 8 - 2 * (int)((t >> 8) & 0xffu);
+      cc = 2 * (int)pc - 8;
       if constexpr (CEIL) {
-        uint32_t tie = has_zero16(mn) || force_exact;
         asm volatile("" : "+v"(tie));
-        cc += (int)tie;
-        return;
+        cc += (int)(tie & 1u);
+        return false;
       }
-      if (has_zero16(mn) || force_exact) {
-        ++ties;
-#pragma unroll 1
-        for (int q = 0; q < 8; ++q)  // re-read the record (L2-hot): no dynamically indexed registers
-          fix_fast(8 * j + q, slab[8 * j + q], cx, cy, cc);
+      return (tie & 0x80808080u) != 0 || force_exact;
+    };
+    // Two batches in flight per thread in two register sets, used in place (a move of a register
+    // with a load pending waits for the load): batch j is decided while j + NT loads, j + 2 NT is
+    // issued into j's registers, then j + NT is decided.  The trip count is uniform per wave; loads
+    // past the last batch re-read it, and batches past it are dropped.
+    auto load = [&](int64_t jj, uint4& v) {
+      if constexpr (CEIL) {
+        asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w));
+      } else {
+        const int64_t jc = jj < c.k ? jj : c.k - 1;
+        v = slab_ld4(slab + 4 * jc);
       }
-    };
-    // Two batches' records in flight per thread in two register sets, used in place (a move of a
-    // register with a load pending waits for the load): batch j is decided while j + NT loads, j +
-    // 2 NT is issued into j's registers, then j + NT is decided.  Batch j + NT is computed even past
-    // the last batch (on the last batch's records) and dropped, so the body has no branch the
-    // compiler could merge the two copies across.  Loads past the end re-read the last batch.
-    auto load_mem = [&](int64_t jj, uint4& lo, uint4& hi) {
-      const int64_t jc = jj < c.k ? jj : c.k - 1;
-      lo = slab_ld4(slab + 8 * jc);
-      hi = slab_ld4(slab + 8 * jc + 4);
-    };
-    auto load = [&](int64_t jj, uint4& lo, uint4& hi) {
-      if constexpr (CEIL)
-        asm volatile("" : "+v"(lo.x), "+v"(lo.y), "+v"(lo.z), "+v"(lo.w), "+v"(hi.x), "+v"(hi.y),
-                     "+v"(hi.z), "+v"(hi.w));
-      else
-        load_mem(jj, lo, hi);
     };
     if (c.k > 0) {
-      uint4 a0, a1, b0, b1;
-      // issued in this order (a older than b), as in the loop, so the loop header's wait for
-      // a's records is vmcnt(2) on every incoming path
-      load_mem(tid, a0, a1);
-      __builtin_amdgcn_sched_barrier(0);
-      load_mem(tid + NT, b0, b1);
-      __builtin_amdgcn_sched_barrier(0);
-      for (int64_t j = tid; j < c.k; j += 2 * NT) {
-        const bool vb = j + NT < c.k;
-        const int64_t jb = vb ? j + NT : c.k - 1;
-        int cxa, cya, cca, cxb, cyb, ccb;
-        decide(j, a0, a1, cxa, cya, cca);
-        load(j + 2 * NT, a0, a1);
-        __builtin_amdgcn_sched_barrier(0);  // keep j + NT's decisions after j + 2 NT's loads
-        decide(jb, b0, b1, cxb, cyb, ccb);
-        load(j + 3 * NT, b0, b1);
+      const int64_t base = tid - lane;       // the wave's first batch
+      uint4 a, b;
+      {
+        const int64_t ja = tid < c.k ? tid : c.k - 1, jb = tid + NT < c.k ? tid + NT : c.k - 1;
+        a = slab_ld4(slab + 4 * ja);
         __builtin_amdgcn_sched_barrier(0);
-        core += cca + (vb ? ccb : 0);
+        b = slab_ld4(slab + 4 * jb);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      for (int64_t jw = base; jw < c.k; jw += 2 * NT) {   // uniform per wave
+        const int64_t j = jw + lane, jb = j + NT;
+        const bool va = j < c.k, vb = jb < c.k;
+        int cxa, cya, cca, cxb, cyb, ccb;
+        const bool ta = decide(a, cxa, cya, cca);
+        load(j + 2 * NT, a);
+        __builtin_amdgcn_sched_barrier(0);  // keep j + NT's decisions after j + 2 NT's loads
+        const bool tb = decide(b, cxb, cyb, ccb);
+        load(j + 3 * NT, b);
+        __builtin_amdgcn_sched_barrier(0);
+        // defer() is called by every lane (its ballot and the queue count are wave-wide)
+        const bool fa = defer(va && ta, j);
+        const bool fb = defer(vb && tb, jb);
+        const bool da = va && !fa, db = vb && !fb;
+        core += (da ? cca : 0) + (db ? ccb : 0);
         // the two batches' T and T^2 added plainly, the pair sums compensated: half the TwoSum
-        // chains (the low bits differ from per-batch sums, within the oracle's 1e-12)
-        const double Ta = batch_T_val(j, cxa, cya);
-        const double Tb = vb ? batch_T_val(jb, cxb, cyb) : 0.0;
+        // chains (the low bits differ from per-batch sums, within the oracle's 1e-12); a batch
+        // dropped here (past the end or deferred) adds 0
+        const double Ta = da ? batch_T_val(j, cxa, cya) : 0.0;
+        const double Tb = db ? batch_T_val(jb, cxb, cyb) : 0.0;
         ks_acc(sT, Ta + Tb);
         ks_acc(sT2, Ta * Ta + Tb * Tb);
+        drain_if_full();
       }
     }
   } else if constexpr (!CEIL) {
-    // m % 8 == 0, 16 <= m <= 248 (the grids' 32, C4's 200): 8-record pieces.  A replicate's
+    // m % 8 == 0, 16 <= m <= 248 (the grids' 32, C4's 200): 16-B pieces of 8 records.  A replicate's
     // batches go in rounds of 64 (waves take rounds wv, wv + 4, ...); in a round the wave's lanes
-    // read 64 consecutive pieces at a time (2 KB, coalesced -- lane-per-batch loads would touch 64
-    // cache lines per instruction at m = 32), decide their 8 records as the m = 8 loop does and
-    // store the piece's packed counts (x negatives, y negatives, INT bits, tie) to the wave's LDS
-    // buffer; then lane L adds batch L's P = m / 8 piece words and finishes the batch (fix-up on a
-    // tie, T).  Counts are the per-record decisions'; each lane adds its batches' T in round order.
+    // read 64 consecutive pieces at a time (1 KB, coalesced -- lane-per-batch loads would touch 64
+    // cache lines per instruction at m = 32), decide their 8 records by word2 and store the piece's
+    // packed counts (x negatives, y negatives, INT bits, tie) to the wave's LDS buffer; then lane L
+    // adds batch L's P = m / 8 piece words and finishes the batch (deferred on a tie, else T).
     if (c.pieces > 0) {
       const uint32_t P = (uint32_t)c.pieces, m = (uint32_t)c.m;
-      const int lane = (int)(threadIdx.x & 63);
       const int wv0 = WAVE ? 0 : (int)(threadIdx.x >> 6);
       constexpr int NWV = WAVE ? 1 : DCOR_WAVES;
       const int64_t rounds = (c.k + 63) / 64, npc = c.k * (int64_t)P;
-      auto ldp = [&](int64_t pc, uint4& lo, uint4& hi) {
-        const int64_t q = pc < npc ? pc : npc - 1;
-        lo = slab_ld4(slab + 8 * q);
-        hi = slab_ld4(slab + 8 * q + 4);
-      };
-      // one piece's packed counts: x negatives (byte 0), y negatives (byte 1), INT bits (byte 2),
-      // tie (byte 3); P <= 31 pieces sum without carries (8 P <= 248)
-      auto piece = [&](const uint4& lo, const uint4& hi) -> uint32_t {
-        const U4 w0{lo.x, lo.y, lo.z, lo.w}, w1{hi.x, hi.y, hi.z, hi.w};
-        uint32_t neg = 0, par = 0, mn = 0xffffffffu;
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-          const uint32_t w = word(q < 4 ? w0 : w1, q & 3);
-          const uint32_t r = w & 0x7fff7fffu;
-          const uint32_t dN = pk_sub16(r, TN), dI = pk_sub16(r, TI);
-          mn = pk_min16(pk_min16(mn, dN), dI);
-          neg += pk_sign_bits(dN);
-          par = __builtin_amdgcn_alignbit(par, int_bit31(dI, w), 31u);
-        }
-        const uint32_t nb = __builtin_amdgcn_perm(neg, neg, 0x0c0c0200u);   // x | y << 8 (bytes 0, 2 of neg)
-        return nb | ((uint32_t)__popc(par & 0xffu) << 16) | (has_zero16(mn) ? 0x01000000u : 0u);
+      auto piece = [&](const uint4& v) -> uint32_t {
+        uint32_t neg = 0, pc = 0, tie = 0;
+        word2(v.x, neg, pc, tie);
+        word2(v.y, neg, pc, tie);
+        word2(v.z, neg, pc, tie);
+        word2(v.w, neg, pc, tie);
+        const uint32_t t = neg + (neg >> 16);
+        return (t & 0xffffu) | (pc << 16) | ((tie & 0x80808080u) != 0 ? 0x01000000u : 0u);
       };
       // the wave's pieces as one stream of steps (its rounds wv0, wv0 + NWV, ..., P steps each),
       // two register sets used in place and loaded two steps ahead across round ends
       const int64_t my_rounds = rounds > wv0 ? (rounds - wv0 + NWV - 1) / NWV : 0;
       const int64_t nsteps = my_rounds * (int64_t)P;
-      int64_t lt = 0;
+      int64_t lt_ = 0;
       uint32_t lit = 0;
-      auto load_next = [&](uint4& lo, uint4& hi) {
-        ldp((wv0 + NWV * lt) * 64 * (int64_t)P + (int64_t)lit * 64 + lane, lo, hi);
-        if (++lit == P) { lit = 0; ++lt; }
+      auto load_next = [&](uint4& v) {
+        const int64_t pc = (wv0 + NWV * lt_) * 64 * (int64_t)P + (int64_t)lit * 64 + lane;
+        v = slab_ld4(slab + 4 * (pc < npc ? pc : npc - 1));
+        if (++lit == P) { lit = 0; ++lt_; }
       };
       int64_t dt = 0;     // the decision cursor's round (of this wave) and piece
       uint32_t dit = 0;
-      auto step = [&](const uint4& lo, const uint4& hi) {
-        pbuf[dit * 64 + (uint32_t)lane] = piece(lo, hi);
+      auto step = [&](const uint4& v) {
+        pbuf[dit * 64 + (uint32_t)lane] = piece(v);
         if (++dit < P) return;
         // the round's pieces are in: lane L finishes batch 64 rd + L
         __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
@@ -1056,98 +1064,80 @@ __device__ __forceinline__ P2Result sign_pass2_core(const SignConst& c, uint32_t
         __builtin_amdgcn_s_waitcnt(0xC07F);   // read before the next round overwrites the buffer
         __builtin_amdgcn_wave_barrier();
         const int64_t j = (wv0 + NWV * dt) * 64 + lane;
-        if (j < c.k) {
-          const int64_t i0 = j * (int64_t)m;
-          int cx = (int)m - 2 * (int)(sum & 0xffu), cy = (int)m - 2 * (int)((sum >> 8) & 0xffu);
-          int cc = 2 * (int)((sum >> 16) & 0xffu) - (int)m;
-          if ((sum >> 24) != 0 || force_exact) {
-            ++ties;
-#pragma unroll 1
-            for (uint32_t r = 0; r < m; ++r) fix_fast(i0 + r, slab[i0 + r], cx, cy, cc);
-          }
-          core += cc;
-          batch_T(j, cx, cy, std::false_type());
+        const bool ok = j < c.k;
+        if (!defer(ok && ((sum >> 24) != 0 || force_exact), j) && ok) {
+          core += 2 * (int)((sum >> 16) & 0xffu) - (int)m;
+          batch_T(j, (int)m - 2 * (int)(sum & 0xffu), (int)m - 2 * (int)((sum >> 8) & 0xffu), std::false_type());
         }
         dit = 0;
         ++dt;
       };
       if (nsteps > 0) {
-        uint4 a0, a1, b0, b1;
-        load_next(a0, a1);
+        uint4 a, b;
+        load_next(a);
         __builtin_amdgcn_sched_barrier(0);
-        load_next(b0, b1);
+        load_next(b);
         __builtin_amdgcn_sched_barrier(0);
         // an odd step count runs one step past the end: it writes a buffer word no round reads
         for (int64_t st = 0; st < nsteps; st += 2) {
-          step(a0, a1);
-          load_next(a0, a1);
+          step(a);
+          load_next(a);
           __builtin_amdgcn_sched_barrier(0);
-          step(b0, b1);
-          load_next(b0, b1);
+          step(b);
+          load_next(b);
           __builtin_amdgcn_sched_barrier(0);
+          drain_if_full();
         }
       }
-    } else
-    // any other m < 32768 (the reference grids' 11, 32, 200): the same packed decisions over a
-    // stream of 16-B units.  A thread's batches j = tid, tid + NT, ... are U = ceil(m / 4) units
-    // each, loaded 4-B aligned (one dwordx4 whatever m % 4; the last unit of a batch reads up to three
-    // records past it, which it replaces by PAD), four units in flight in four register sets used in
-    // place, as the m = 8 loop keeps two batches: the loop waits vmcnt(3), never for a unit it does
-    // not need yet.  PAD = (32767, 32767), flip 0, adds nothing to the counts (its halves are >= any
-    // threshold code, its INT bit 0) and ties only a threshold coded 32767, which the exact fix-up
-    // then settles.  The loop runs a multiple of four units; units past the thread's last batch
-    // re-read it and are dropped.  Counts and the per-batch T sums are the per-batch loop's, bit for
-    // bit (batch j's T is added after batch j - NT's).
-    if (c.m < 32768) {
-      const uint32_t m = (uint32_t)c.m, U = (m + 3u) >> 2, rem = m & 3u;
-      const int64_t rounds = (c.k + NT - 1) / NT;       // batches per thread (the last one partial)
-      const int64_t nu = ((rounds * (int64_t)U) + 3) & ~(int64_t)3;
-      constexpr uint32_t PAD = 0x7fff7fffu;
-      // load cursor: round rl, unit ul of this thread's batch tid + NT rl (clamped to the last batch)
+    } else if (c.m <= 252) {
+      // any other m <= 252 (the reference grids' 11): a stream of 16-B units.  Batch j's records
+      // [j m, j m + m) are read from the 4-B aligned record j m & ~1 on, U = ceil((m + (m & 1)) / 8)
+      // units, four units in flight in four register sets used in place (the loop waits vmcnt(3));
+      // a record outside the batch (a leading one when j m is odd, trailing ones in the last unit) is
+      // replaced by PAD = (127, 127), flip 0: no negatives, INT bit 0, and a tie only with a threshold
+      // coded 127, which the exact recomputation settles.  The loop runs a multiple of four units
+      // with a uniform trip count per wave; units past the thread's last batch are dropped.
+      const uint32_t m = (uint32_t)c.m, U = (m + (m & 1u) + 7u) >> 3;
+      const int64_t rounds = (c.k + NT - 1 - (tid - lane)) / NT;   // this wave's batch rounds (uniform)
+      const int64_t nu = rounds > 0 ? ((rounds * (int64_t)U) + 3) & ~(int64_t)3 : 0;
+      constexpr uint32_t PAD = 0x7f7f7f7fu;
       int64_t rl = 0;
       uint32_t ul = 0;
-      auto load_next = [&](u32x4a4& v) {
+      auto load_next = [&](uint4& v) {
         const int64_t jj = tid + NT * rl;
         const int64_t jc = jj < c.k ? jj : c.k - 1;
-        v = *reinterpret_cast<const u32x4a4*>(slab + jc * m + 4u * ul);
+        const int64_t s0 = (jc * (int64_t)m) & ~(int64_t)1;     // even record: 4-B aligned
+        v = slab_ld4a(slab + (s0 >> 1) + 4 * ul);
         if (++ul == U) { ul = 0; ++rl; }
       };
-      // decision cursor and the current batch's packed counts
       int64_t rd = 0;
-      uint32_t ud = 0, neg = 0, pc = 0, par = 0, mn = 0xffffffffu;
-      auto one = [&](uint32_t w) {
-        const uint32_t r = w & 0x7fff7fffu;
-        const uint32_t dN = pk_sub16(r, TN), dI = pk_sub16(r, TI);
-        mn = pk_min16(pk_min16(mn, dN), dI);
-        neg += pk_sign_bits(dN);                                     // halves count to <= m < 32768
-        par = __builtin_amdgcn_alignbit(par, int_bit31(dI, w), 31u); // (par << 1) | INT bit
-      };
-      auto step = [&](const u32x4a4& v) {
+      uint32_t ud = 0, neg = 0, pc = 0, tie = 0;
+      auto step = [&](const uint4& v) {
+        const int64_t j = tid + NT * rd;
+        const uint32_t lead = (uint32_t)((j * (int64_t)m) & 1);
+        uint32_t w[4] = {v.x, v.y, v.z, v.w};
+        if (ud == 0) w[0] = lead ? ((w[0] & 0xffff0000u) | (PAD & 0xffffu)) : w[0];
         const bool last = ud + 1u == U;
-        uint32_t w1 = v.y, w2 = v.z, w3 = v.w;
-        if (last && rem) {
-          w3 = PAD;
-          if (rem < 3u) w2 = PAD;
-          if (rem < 2u) w1 = PAD;
-        }
-        one(v.x); one(w1); one(w2); one(w3);
-        pc += __popc(par & 15u);
         if (last) {
-          const int64_t j = tid + NT * rd;
-          const int64_t i0 = j * (int64_t)m;
-          int cx = (int)m - 2 * (int)(neg & 0xffffu), cy = (int)m - 2 * (int)(neg >> 16);
-          int cc = 2 * (int)pc - (int)m;
-          if (j < c.k) {
-            if (has_zero16(mn) || force_exact) {
-              ++ties;
-#pragma unroll 1
-              for (uint32_t r = 0; r < m; ++r) fix_fast(i0 + r, slab[i0 + r], cx, cy, cc);
-            }
-            core += cc;
-            batch_T(j, cx, cy, std::false_type());
+          // records r >= nv of the unit are past the batch: PAD halves from bit 16 nv on
+          const uint32_t nv = m + lead - 8u * ud;       // 1 .. 8
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const int sh = 16 * (int)nv - 32 * k;       // invalid bits from `sh` on in word k
+            const uint32_t M = sh <= 0 ? 0xffffffffu : (sh >= 32 ? 0u : (0xffffffffu << sh));
+            w[k] = (w[k] & ~M) | (PAD & M);
           }
-          neg = pc = 0;
-          mn = 0xffffffffu;
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) word2(w[k], neg, pc, tie);
+        if (last) {
+          const bool ok = j < c.k;
+          const uint32_t t = neg + (neg >> 16);
+          if (!defer(ok && ((tie & 0x80808080u) != 0 || force_exact), j) && ok) {
+            core += 2 * (int)pc - (int)m;
+            batch_T(j, (int)m - 2 * (int)(t & 0xffu), (int)m - 2 * (int)((t >> 8) & 0xffu), std::false_type());
+          }
+          neg = pc = tie = 0;
           ud = 0;
           ++rd;
         } else {
@@ -1155,7 +1145,7 @@ __device__ __forceinline__ P2Result sign_pass2_core(const SignConst& c, uint32_t
         }
       };
       if (nu > 0) {
-        u32x4a4 u0, u1, u2, u3;
+        uint4 u0, u1, u2, u3;
         load_next(u0);
         __builtin_amdgcn_sched_barrier(0);
         load_next(u1);
@@ -1177,30 +1167,25 @@ __device__ __forceinline__ P2Result sign_pass2_core(const SignConst& c, uint32_t
           step(u3);
           load_next(u3);
           __builtin_amdgcn_sched_barrier(0);
+          drain_if_full();
         }
       }
-    } else for (int64_t j = tid; j < c.k; j += NT) {
-      int cx = 0, cy = 0, cc = 0;
-      const int64_t i0 = j * c.m;
-      bool any = false;
-      for (int r = 0; r < c.m; ++r) any |= fast(slab[i0 + r], cx, cy, cc);
-      any |= force_exact;
-      if (any) {
-        for (int r = 0; r < c.m; ++r) {
-          const uint32_t w = slab[i0 + r];
-          int dx = 0, dy = 0, dc = 0;
-          if (fast(w, dx, dy, dc) || force_exact) fixup(i0 + r, w, cx, cy, cc, bad_ni);
-        }
+    } else {
+      // m > 252 (byte counters would overflow): record by record, exactly
+      for (int64_t j = tid; j < c.k; j += NT) {
+        int cx = 0, cy = 0, cc = 0;
+        const int64_t i0 = j * c.m;
+        for (int r = 0; r < c.m; ++r) exact_rec(i0 + r, s16[i0 + r], cx, cy, cc, bad_ni);
+        core += cc;
+        batch_T(j, cx, cy, std::false_type());
       }
-      core += cc;
-      batch_T(j, cx, cy, std::false_type());
     }
   }
+  if constexpr (!CEIL) drain_ties();
   for (int64_t i = c.k * c.m + tid; !CEIL && i < c.n; i += NT) {  // tail: INT only
     int dx = 0, dy = 0, cc = 0;
     bool ignore = false;  // NI never reads the tail
-    const uint32_t w = slab[i];
-    if (fast(w, dx, dy, cc) || force_exact) fixup(i, w, dx, dy, cc, ignore);
+    exact_rec(i, s16[i], dx, dy, cc, ignore);
     core += cc;
   }
   P2Result r;
@@ -1242,9 +1227,11 @@ __device__ __forceinline__ void sign_pass2_body(const SignConst& c, uint32_t rep
                                                 const double* __restrict__ sums_in,
                                                 SignPartial* __restrict__ part_out) {
   __shared__ double2 lt[256];
+  __shared__ uint32_t tq[DCOR_WAVES][TQ];
   log_tab_to_lds(lt, DCOR_BLOCK);
   __syncthreads();
-  const P2Result r = sign_pass2_core<DGP, false, CEIL>(c, rep, slab, sums_in, lt, wave_pbuf(c.pieces));
+  const P2Result r = sign_pass2_core<DGP, false, CEIL>(c, rep, slab, sums_in, lt, wave_pbuf(c.pieces),
+                                                       tq[threadIdx.x >> 6]);
   if (threadIdx.x == 0) {
     SignPartial p;
     p.sT[0] = r.sT.hi; p.sT[1] = r.sT.lo; p.sT2[0] = r.sT2.hi; p.sT2[1] = r.sT2.lo;
@@ -1353,8 +1340,8 @@ __global__ __launch_bounds__(DCOR_BLOCK) void k_sign_pass1_w(SignConst c, int64_
 template <int DGP>
 __device__ __forceinline__ void sign_pass2_wave_part(const SignConst& c, uint32_t rep, const uint32_t* slab,
                                                      const double* sums_in, SignPartial* part_out,
-                                                     const double2* lt, int pstride) {
-  const P2Result r = sign_pass2_core<DGP, true>(c, rep, slab, sums_in, lt, wave_pbuf(pstride));
+                                                     const double2* lt, int pstride, uint32_t* tq) {
+  const P2Result r = sign_pass2_core<DGP, true>(c, rep, slab, sums_in, lt, wave_pbuf(pstride), tq);
   if ((threadIdx.x & 63) == 0) {
     SignPartial p;
     p.sT[0] = r.sT.hi; p.sT[1] = r.sT.lo; p.sT2[0] = r.sT2.hi; p.sT2[1] = r.sT2.lo;
@@ -1370,12 +1357,13 @@ __global__ __launch_bounds__(DCOR_BLOCK) void k_sign_pass2_w(SignConst c, int64_
                                                              const double* __restrict__ sums,
                                                              SignPartial* __restrict__ part, int pstride) {
   __shared__ double2 lt[256];
+  __shared__ uint32_t tq[DCOR_WAVES][TQ];
   log_tab_to_lds(lt, DCOR_BLOCK);
   __syncthreads();
   const int64_t r = (int64_t)blockIdx.x * DCOR_WAVES + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   if (r >= nreps) return;
   sign_pass2_wave_part<DGP>(c, (uint32_t)(c.rep_begin + r), scratch + (size_t)r * sign_item_words(c.n, DGP),
-                            sums + SIGN_SUMS * (size_t)r, part + r, lt, pstride);
+                            sums + SIGN_SUMS * (size_t)r, part + r, lt, pstride, tq[threadIdx.x >> 6]);
 }
 
 template <int DGP, int VPL>
@@ -1385,6 +1373,7 @@ __global__ __launch_bounds__(DCOR_BLOCK, DCOR_P2E_WPE) void k_sign_p2e_w(SignCon
                                                            dcor_rep_out* out, int pstride) {
   __shared__ WaveMix<VPL> wsel[DCOR_WAVES];
   __shared__ double2 lt[256];
+  __shared__ uint32_t tq[DCOR_WAVES][TQ];
   log_tab_to_lds(lt, DCOR_BLOCK);
   __syncthreads();
   const int wv = threadIdx.x >> 6;
@@ -1392,7 +1381,7 @@ __global__ __launch_bounds__(DCOR_BLOCK, DCOR_P2E_WPE) void k_sign_p2e_w(SignCon
   if (r >= nreps) return;  // whole waves only
   const uint32_t rep = (uint32_t)(c.rep_begin + r);
   const P2Result p = sign_pass2_core<DGP, true>(c, rep, scratch + (size_t)r * sign_item_words(c.n, DGP),
-                                                sums + SIGN_SUMS * (size_t)r, lt, wave_pbuf(pstride));
+                                                sums + SIGN_SUMS * (size_t)r, lt, wave_pbuf(pstride), tq[wv]);
   sign_finish_wave<VPL>(c, rep, p, out + r, &wsel[wv]);
 }
 
@@ -1937,16 +1926,8 @@ __global__ __launch_bounds__(DCOR_BLOCK) void k_grid_sign_pass1(const SignConst*
   sign_pass1_body<DGP>(cells[it.cell], it.rep, scratch + it.scratch, sums + SIGN_SUMS * (size_t)blockIdx.x);
 }
 
-__global__ __launch_bounds__(DCOR_BLOCK) void k_grid_sign_drain(const SignConst* __restrict__ cells,
-                                                                const GridItem* __restrict__ items,
-                                                                uint32_t* __restrict__ scratch,
-                                                                double* __restrict__ sums) {
-  const GridItem it = items[blockIdx.x];
-  sign_drain_body(cells[it.cell], it.rep, scratch + it.scratch, sums + SIGN_SUMS * (size_t)blockIdx.x);
-}
-
 template <int DGP>
-__global__ __launch_bounds__(DCOR_BLOCK) void k_grid_sign_pass2(const SignConst* __restrict__ cells,
+__global__ __launch_bounds__(DCOR_BLOCK, DCOR_P2_WPE) void k_grid_sign_pass2(const SignConst* __restrict__ cells,
                                                                 const GridItem* __restrict__ items,
                                                                 const uint32_t* __restrict__ scratch,
                                                                 const double* __restrict__ sums,
@@ -2002,13 +1983,14 @@ __global__ __launch_bounds__(DCOR_BLOCK) void k_grid_sign_pass2_w(const SignCons
                                                                   const double* __restrict__ sums,
                                                                   SignPartial* __restrict__ part, int pstride) {
   __shared__ double2 lt[256];
+  __shared__ uint32_t tq[DCOR_WAVES][TQ];
   log_tab_to_lds(lt, DCOR_BLOCK);
   __syncthreads();
   const int64_t r = wave_item();
   if (r >= nitems) return;
   const GridItem it = items[r];
   sign_pass2_wave_part<DGP>(cells[it.cell], it.rep, scratch + it.scratch, sums + SIGN_SUMS * (size_t)r, part + r,
-                            lt, pstride);
+                            lt, pstride, tq[threadIdx.x >> 6]);
 }
 
 template <int DGP, int VPL>
@@ -2020,6 +2002,7 @@ __global__ __launch_bounds__(DCOR_BLOCK, DCOR_P2E_WPE) void k_grid_sign_p2e_w(co
                                                                 dcor_rep_out* out, int pstride) {
   __shared__ WaveMix<VPL> wsel[DCOR_WAVES];
   __shared__ double2 lt[256];
+  __shared__ uint32_t tq[DCOR_WAVES][TQ];
   log_tab_to_lds(lt, DCOR_BLOCK);
   __syncthreads();
   const int64_t r = wave_item();
@@ -2027,7 +2010,7 @@ __global__ __launch_bounds__(DCOR_BLOCK, DCOR_P2E_WPE) void k_grid_sign_p2e_w(co
   const GridItem it = items[r];
   const SignConst& c = cells[it.cell];
   const P2Result p = sign_pass2_core<DGP, true>(c, it.rep, scratch + it.scratch, sums + SIGN_SUMS * (size_t)r, lt,
-                                                wave_pbuf(pstride));
+                                                wave_pbuf(pstride), tq[threadIdx.x >> 6]);
   sign_finish_wave<VPL>(c, it.rep, p, out + it.out, &wsel[threadIdx.x >> 6]);
 }
 
@@ -2112,9 +2095,6 @@ static void grid_codes_t(const SignConst* cells, const GridItem* items, int64_t 
                          uint32_t* scratch, double* sums, SignPartial* part, int pmax, hipStream_t st) {
   hipLaunchKernelGGL(k_grid_sign_pass1<DGP>, dim3((unsigned)nitems), dim3(DCOR_BLOCK), 0, st, cells,
                      items, scratch, sums);
-  if (DGP == DCOR_DGP_GAUSSIAN)
-    hipLaunchKernelGGL(k_grid_sign_drain, dim3((unsigned)nitems), dim3(DCOR_BLOCK), 0, st, cells, items, scratch,
-                       sums);
   hipLaunchKernelGGL(k_grid_sign_pass2<DGP>, dim3((unsigned)nitems), dim3(DCOR_BLOCK), sign_piece_lds(pmax), st,
                      cells, items, scratch, sums, part);
 }
@@ -2321,8 +2301,6 @@ static int launch_codes_t(SignConst c, int64_t reps, int64_t chunk, const CodesB
     SignPartial* part = reinterpret_cast<SignPartial*>(bf.sums[b] + SIGN_SUMS * chunk);
     hipLaunchKernelGGL(k_sign_pass1<DGP>, dim3((unsigned)nr), dim3(DCOR_BLOCK), 0, st[b], c,
                        bf.slab[b], bf.sums[b]);
-    if (DGP == DCOR_DGP_GAUSSIAN)
-      hipLaunchKernelGGL(k_sign_drain, dim3((unsigned)nr), dim3(DCOR_BLOCK), 0, st[b], c, bf.slab[b], bf.sums[b]);
     hipLaunchKernelGGL(k_sign_pass2<DGP>, dim3((unsigned)nr), dim3(DCOR_BLOCK), sign_piece_lds(c.pieces), st[b], c,
                        bf.slab[b], bf.sums[b], part);
     if (int e = before_out(b)) return e;
@@ -2360,7 +2338,7 @@ static int occupancy_pad(const void* real, const void* ceil, size_t* pad) {
 }
 
 // One pass of the one-pass sign path over `reps` replicates as a single chunk on `stream`, for
-// timing (dcor_diag_sign_pass): 1 pass 1, 4 its slow-sample drain, 2 pass 2, 3 the epilogue; 11 / 12 the pass-1 / pass-2
+// timing (dcor_diag_sign_pass): 1 pass 1, 2 pass 2 (with the slow-sample drain), 3 the epilogue; 11 / 12 the pass-1 / pass-2
 // ceilings (Gaussian DGP, m = 8) at the real passes' occupancy, 13 the pass-1 ceiling at its own.  slab / sums / part / out as launch_codes_t lays them out.
 int launch_sign_diag(const SignConst& c, int64_t reps, int which, uint32_t* slab, double* sums,
                      void* part_v, dcor_rep_out* out, void* stream) {
@@ -2384,9 +2362,6 @@ int launch_sign_diag(const SignConst& c, int64_t reps, int which, uint32_t* slab
       }
       break;
     case 3: launch_sign_epilogue(c, reps, part, out, st); break;
-    case 4:
-      if (c.g.dgp == DCOR_DGP_GAUSSIAN) hipLaunchKernelGGL(k_sign_drain, g, b, 0, st, c, slab, sums);
-      break;
     case 11: case 13: {
       // 11: at pass 1's occupancy (pass 1 holds more VGPRs and LDS than its ceiling); 13: its own
       size_t pad = 0;

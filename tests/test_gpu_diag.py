@@ -51,7 +51,7 @@ def test_ceilings_do_not_disturb_results(dc):
     cell = headline_cell()
     a = simulate(cell, 2048, 4096).cpu().numpy()
     c = cell.to_c()
-    for which in (1, 4, 2, 3, 11, 12, 13, 14, 15):
+    for which in (1, 2, 3, 11, 12, 13, 14, 15):
         _lib.check(_lib.lib.dcor_diag_sign_pass(C.byref(c), 4096, 256, which, None))
     b = simulate(cell, 2048, 4096).cpu().numpy()
     assert np.array_equal(a.view(np.int64), b.view(np.int64))

@@ -172,10 +172,11 @@ def test_sim_grid_sim_on_one_stream(dc):
 def test_headline_bench_step_every_replicate(dc, orc):
     """VERDICT r03 "next" #4: one whole bench step -- all 8,192 replicates of simulate(headline,
     8192, r0), launched after an overlapping warm-up call into the same buffer as bench.py does --
-    against the oracle fed the same Philox streams, every row at 1e-12.  The tie fix-up (the exact
-    regeneration of samples whose record code ties a private centre's code) is a rare-event path:
-    the same replicates' tie batches are counted (dcor_diag_sign_ties) and must be non-zero, so the
-    comparison covers it."""
+    against the oracle fed the same Philox streams, every row at 1e-12.  The tie path (a batch with a
+    record whose 7-bit code ties a private centre's code, deferred and recomputed exactly, with its
+    tied samples regenerated) is a rare-event path: the same replicates' tie batches are counted
+    (dcor_diag_sign_ties) and must be non-zero, so the comparison covers it, and a small share of
+    the 12,500 batches per replicate."""
     import ctypes as C
     import torch
     from dcor import _lib
@@ -195,14 +196,15 @@ def test_headline_bench_step_every_replicate(dc, orc):
     _lib.check(_lib.lib.dcor_diag_sign_ties(C.byref(c), r0, R, ties.ctypes.data_as(C.POINTER(C.c_int64))))
     print(f"tie batches in the step: {int(ties.sum())} over {int((ties > 0).sum())} replicates")
     assert ties.sum() > 0
-    assert (ties > 0).sum() < R        # rare: most replicates have none
+    assert ties.sum() < 0.03 * R * 12_500      # rare: about 1 % of batches at 128 code levels
 
 
 def test_headline_wide_code_window(dc, orc, monkeypatch):
     """The record codes' window only decides how many samples tie a private centre's code (each tie
-    is regenerated exactly), never a result: with round 3's wide window (DCOR_CODE_WINDOW=wide,
-    ~20x the ties of the default) 2048 headline replicates equal the default window's bit for bit
-    and the oracle at 1e-12, and tie more often."""
+    batch is recomputed exactly), never a count: with round 3's wide window (DCOR_CODE_WINDOW=wide,
+    many times the ties of the default) 2048 headline replicates give the default window's INT
+    results bit for bit (exact integer counts), NI results that differ at most in the order their
+    compensated T sums were added (1e-14), and the oracle's at 1e-12."""
     import ctypes as C
     from dcor import _lib
     from dcor.sim import headline_cell, simulate
@@ -218,7 +220,8 @@ def test_headline_wide_code_window(dc, orc, monkeypatch):
     narrow, t_narrow = simulate(cell, R, r0).cpu().numpy(), ties()
     monkeypatch.setenv("DCOR_CODE_WINDOW", "wide")
     wide, t_wide = simulate(cell, R, r0).cpu().numpy(), ties()
-    assert np.array_equal(narrow.view(np.int64), wide.view(np.int64))
+    assert np.array_equal(narrow[:, 3:].view(np.int64), wide[:, 3:].view(np.int64))
+    assert_close(wide[:, :3], narrow[:, :3], rtol=1e-14, what="NI, wide vs default window")
     assert_close(wide, orc.sim_reps(c, r0, r0 + R, threads=min(16, os.cpu_count() or 1)),
                  what="headline, wide code window")
     print(f"tie batches over {R} replicates: default window {t_narrow}, wide {t_wide}")
