@@ -530,11 +530,14 @@ int prepare_cell(const dcor_cell& c, CellPlan& p) {
     double cx = 0.0, cy = 0.0, rx = 1.0, ry = 1.0;
     if (c.dgp == DCOR_DGP_GAUSSIAN) {
       // The private centres are mean(clip(x)) + Laplace(s_mu) (vert-cor.R:335-336): within
-      // 12 sd(mean) + 40 noise scales of E[clip(x)] but with probability ~1e-17 per replicate.  A
-      // window that narrow spends the 2^15 code levels where the thresholds fall, so few samples
-      // tie one (each tie costs an exact regeneration in pass 2); samples outside it clamp to the
-      // end codes, still decided exactly while the thresholds lie inside.  DCOR_CODE_WINDOW=wide:
-      // the round-3 window, 2 sd of the sample around mu.
+      // 7 sd(mean) + 24 noise scales of E[clip(x)] but with probability below 1e-9 per replicate
+      // (sd(mean) <= sd(x) / sqrt(n)).  A window that narrow spends the 128 code levels where the
+      // thresholds fall, so few samples tie one (each tie batch is recomputed exactly in pass 2);
+      // samples outside it clamp to the end codes, still decided exactly while the thresholds lie
+      // inside -- and when one does not, its end code ties every clamped sample, and those batches
+      // are recomputed too: exact, only slower.  (Round 4 used 12 sd + 40 scales with 2^15 levels;
+      // at 128 levels the narrower window takes 40 % of the ties off.)  DCOR_CODE_WINDOW=wide: the
+      // round-3 window, 2 sd of the sample around mu.
       const double sx = std::sqrt(g.a00 * g.a00 + g.a01 * g.a01);
       const double sy = std::sqrt(g.a10 * g.a10 + g.a11 * g.a11);
       const char* wv = std::getenv("DCOR_CODE_WINDOW");
@@ -546,8 +549,8 @@ int prepare_cell(const dcor_cell& c, CellPlan& p) {
         const double rn = 1.0 / std::sqrt((double)c.n);
         cx = clipped_normal_mean(c.mu[0], sx, k.L);
         cy = clipped_normal_mean(c.mu[1], sy, k.L);
-        rx = r_min(2.0 * sx, 12.0 * sx * rn + 40.0 * k.s_mu_x);
-        ry = r_min(2.0 * sy, 12.0 * sy * rn + 40.0 * k.s_mu_y);
+        rx = r_min(2.0 * sx, 7.0 * sx * rn + 24.0 * k.s_mu_x);
+        ry = r_min(2.0 * sy, 7.0 * sy * rn + 24.0 * k.s_mu_y);
       }
     } else if (c.dgp == DCOR_DGP_BERNOULLI) {
       cx = cy = 0.5; rx = ry = 1.0;

@@ -814,7 +814,7 @@ __device__ __forceinline__ void scalar_laplace_wave(uint32_t rep, uint32_t k0, u
 // VALU-issue ceiling without the slab stream (dcor_diag_sign_pass, bench.py roofline.issue_frac).
 // pbuf: the calling wave's piece buffer (64 c.pieces words of LDS) when c.pieces > 0; tq: its
 // tie-deferral queue (TQ words of LDS).
-#define TQ 512
+#define TQ 256
 template <int DGP, bool WAVE, bool CEIL = false>
 __device__ __forceinline__ P2Result sign_pass2_core(const SignConst& c, uint32_t rep,
                                                     const uint32_t* __restrict__ slab,
@@ -916,9 +916,9 @@ __device__ __forceinline__ P2Result sign_pass2_core(const SignConst& c, uint32_t
   // code levels) is not fixed up inside the loop, where every lane would wait for its regeneration:
   // its index goes to the wave's LDS queue (ballot + mbcnt slots, the count wave-uniform) and the
   // whole wave recomputes queued batches exactly, one per lane (exact_rec over its m records, then
-  // its T), once per loop trip when the queue holds more than TQ - 256 entries (a trip queues at most
-  // 256) and after the loop: one inlined copy of the recomputation per loop.  Callers defer at
-  // wave-uniform points.  Which batches tie depends on the replicate alone, so a replicate's bits
+  // its T), once per loop trip when a next trip could overflow the queue (a trip of the m = 8 and
+  // piece loops queues at most 128 batches, of the unit loop 64 per batch end) and after the loop:
+  // one inlined copy of the recomputation per loop.  Callers defer at wave-uniform points.  Which batches tie depends on the replicate alone, so a replicate's bits
   // do not depend on the launch; the code window moves only the order of the T sums.
   const int lane = (int)(threadIdx.x & 63);
   uint32_t tqn = 0;
@@ -926,15 +926,39 @@ __device__ __forceinline__ P2Result sign_pass2_core(const SignConst& c, uint32_t
     if (tqn == 0) return;
     __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): the queue's entries are in LDS
     __builtin_amdgcn_wave_barrier();
-    for (uint32_t e = (uint32_t)lane; e < tqn; e += 64) {
-      const int64_t j = tq[e];
+    for (uint32_t e0 = 0; e0 < tqn; e0 += 64) {   // uniform trips
+      const uint32_t e = e0 + (uint32_t)lane;
+      const bool has = e < tqn;
+      const int64_t j = has ? (int64_t)tq[e] : 0;
       const int64_t i0 = j * c.m;
       int cx = 0, cy = 0, cc = 0;
+      // records decided by their codes first; the tied ones (m <= 64) are regenerated afterwards one
+      // per lane per round, every lane's regeneration in the same pass -- in record order, a round
+      // per record position, nearly every lane would wait for some other lane's regeneration
+      uint64_t tmask = 0;
+      if (has) {
 #pragma unroll 1
-      for (int r = 0; r < c.m; ++r) exact_rec(i0 + r, s16[i0 + r], cx, cy, cc, bad_ni);
-      core += cc;
-      batch_T(j, cx, cy, std::false_type());
-      ++ties;
+        for (int r = 0; r < c.m; ++r) {
+          const uint32_t w = s16[i0 + r];
+          const uint32_t qx = w & 0x7fu, qy = (w >> 8) & 0x7fu;
+          if (c.m <= 64 && (force_exact || qx == qNx || qy == qNy || qx == qIx || qy == qIy))
+            tmask |= 1ull << r;
+          else
+            exact_rec(i0 + r, w, cx, cy, cc, bad_ni);
+        }
+      }
+      while (__ballot(tmask != 0)) {
+        if (tmask) {
+          const int r = __ffsll((long long)tmask) - 1;
+          tmask &= tmask - 1;
+          exact_rec(i0 + r, s16[i0 + r], cx, cy, cc, bad_ni);
+        }
+      }
+      if (has) {
+        core += cc;
+        batch_T(j, cx, cy, std::false_type());
+        ++ties;
+      }
     }
     __builtin_amdgcn_s_waitcnt(0xC07F);
     __builtin_amdgcn_wave_barrier();
@@ -950,8 +974,8 @@ __device__ __forceinline__ P2Result sign_pass2_core(const SignConst& c, uint32_t
     }
     return tie;
   };
-  auto drain_if_full = [&]() {
-    if (tqn > TQ - 256) drain_ties();
+  auto drain_if_full = [&](uint32_t per_trip) {
+    if (tqn > TQ - per_trip) drain_ties();
   };
   if (c.m == 8) {
     // headline geometry: one thread = one batch = one 16-B load (8 records), decided by word2.
@@ -1016,7 +1040,7 @@ __device__ __forceinline__ P2Result sign_pass2_core(const SignConst& c, uint32_t
         const double Tb = db ? batch_T_val(jb, cxb, cyb) : 0.0;
         ks_acc(sT, Ta + Tb);
         ks_acc(sT2, Ta * Ta + Tb * Tb);
-        drain_if_full();
+        drain_if_full(128u);
       }
     }
   } else if constexpr (!CEIL) {
@@ -1086,7 +1110,7 @@ __device__ __forceinline__ P2Result sign_pass2_core(const SignConst& c, uint32_t
           step(b);
           load_next(b);
           __builtin_amdgcn_sched_barrier(0);
-          drain_if_full();
+          drain_if_full(128u);
         }
       }
     } else if (c.m <= 252) {
@@ -1098,6 +1122,7 @@ __device__ __forceinline__ P2Result sign_pass2_core(const SignConst& c, uint32_t
       // coded 127, which the exact recomputation settles.  The loop runs a multiple of four units
       // with a uniform trip count per wave; units past the thread's last batch are dropped.
       const uint32_t m = (uint32_t)c.m, U = (m + (m & 1u) + 7u) >> 3;
+      const uint32_t per_trip = 64u * (U >= 4u ? 1u : (U >= 2u ? 2u : 4u));   // batch ends per 4 units
       const int64_t rounds = (c.k + NT - 1 - (tid - lane)) / NT;   // this wave's batch rounds (uniform)
       const int64_t nu = rounds > 0 ? ((rounds * (int64_t)U) + 3) & ~(int64_t)3 : 0;
       constexpr uint32_t PAD = 0x7f7f7f7fu;
@@ -1167,7 +1192,7 @@ __device__ __forceinline__ P2Result sign_pass2_core(const SignConst& c, uint32_t
           step(u3);
           load_next(u3);
           __builtin_amdgcn_sched_barrier(0);
-          drain_if_full();
+          drain_if_full(per_trip);
         }
       }
     } else {
@@ -1370,7 +1395,7 @@ template <int DGP, int VPL>
 __global__ __launch_bounds__(DCOR_BLOCK, DCOR_P2E_WPE) void k_sign_p2e_w(SignConst c, int64_t nreps,
                                                            const uint32_t* __restrict__ scratch,
                                                            const double* __restrict__ sums,
-                                                           dcor_rep_out* out, int pstride) {
+                                                           dcor_rep_out* out) {
   __shared__ WaveMix<VPL> wsel[DCOR_WAVES];
   __shared__ double2 lt[256];
   __shared__ uint32_t tq[DCOR_WAVES][TQ];
@@ -1380,8 +1405,11 @@ __global__ __launch_bounds__(DCOR_BLOCK, DCOR_P2E_WPE) void k_sign_p2e_w(SignCon
   const int64_t r = (int64_t)blockIdx.x * DCOR_WAVES + __builtin_amdgcn_readfirstlane(wv);
   if (r >= nreps) return;  // whole waves only
   const uint32_t rep = (uint32_t)(c.rep_begin + r);
+  // the piece buffer lives in the wave's mixquant keys, which the epilogue fills only after pass 2
+  static_assert(sizeof(wsel[0].keys) >= 64 * SIGN_PIECES_MAX * sizeof(uint32_t), "piece buffer");
   const P2Result p = sign_pass2_core<DGP, true>(c, rep, scratch + (size_t)r * sign_item_words(c.n, DGP),
-                                                sums + SIGN_SUMS * (size_t)r, lt, wave_pbuf(pstride), tq[wv]);
+                                                sums + SIGN_SUMS * (size_t)r, lt,
+                                                reinterpret_cast<uint32_t*>(wsel[wv].keys), tq[wv]);
   sign_finish_wave<VPL>(c, rep, p, out + r, &wsel[wv]);
 }
 
@@ -1999,7 +2027,7 @@ __global__ __launch_bounds__(DCOR_BLOCK, DCOR_P2E_WPE) void k_grid_sign_p2e_w(co
                                                                 int64_t nitems,
                                                                 const uint32_t* __restrict__ scratch,
                                                                 const double* __restrict__ sums,
-                                                                dcor_rep_out* out, int pstride) {
+                                                                dcor_rep_out* out) {
   __shared__ WaveMix<VPL> wsel[DCOR_WAVES];
   __shared__ double2 lt[256];
   __shared__ uint32_t tq[DCOR_WAVES][TQ];
@@ -2009,8 +2037,10 @@ __global__ __launch_bounds__(DCOR_BLOCK, DCOR_P2E_WPE) void k_grid_sign_p2e_w(co
   if (r >= nitems) return;  // whole waves only
   const GridItem it = items[r];
   const SignConst& c = cells[it.cell];
+  // the piece buffer lives in the wave's mixquant keys, which the epilogue fills only after pass 2
   const P2Result p = sign_pass2_core<DGP, true>(c, it.rep, scratch + it.scratch, sums + SIGN_SUMS * (size_t)r, lt,
-                                                wave_pbuf(pstride), tq[threadIdx.x >> 6]);
+                                                reinterpret_cast<uint32_t*>(wsel[threadIdx.x >> 6].keys),
+                                                tq[threadIdx.x >> 6]);
   sign_finish_wave<VPL>(c, it.rep, p, out + it.out, &wsel[threadIdx.x >> 6]);
 }
 
@@ -2145,11 +2175,11 @@ static void grid_codes_w_t(const SignConst* cells, const GridItem* items, int64_
     return;
   }
   if (vpl32)
-    hipLaunchKernelGGL((k_grid_sign_p2e_w<DGP, 32>), dim3(wave_groups(nitems)), dim3(DCOR_BLOCK), lds, st, cells,
-                       items, nitems, scratch, sums, out, pmax);
+    hipLaunchKernelGGL((k_grid_sign_p2e_w<DGP, 32>), dim3(wave_groups(nitems)), dim3(DCOR_BLOCK), 0, st, cells,
+                       items, nitems, scratch, sums, out);
   else
-    hipLaunchKernelGGL((k_grid_sign_p2e_w<DGP, 16>), dim3(wave_groups(nitems)), dim3(DCOR_BLOCK), lds, st, cells,
-                       items, nitems, scratch, sums, out, pmax);
+    hipLaunchKernelGGL((k_grid_sign_p2e_w<DGP, 16>), dim3(wave_groups(nitems)), dim3(DCOR_BLOCK), 0, st, cells,
+                       items, nitems, scratch, sums, out);
 }
 
 int launch_grid_sign_codes_w(int dgp, const SignConst* cells, const GridItem* items, int64_t nitems,
@@ -2290,11 +2320,11 @@ static int launch_codes_t(SignConst c, int64_t reps, int64_t chunk, const CodesB
                            bf.slab[b], bf.sums[b], part, c.pieces);
         launch_sign_epilogue(c, nr, part, out + r, st[b]);
       } else if (c.mix.nsim > 1024)
-        hipLaunchKernelGGL((k_sign_p2e_w<DGP, 32>), dim3(wave_groups(nr)), dim3(DCOR_BLOCK), lds, st[b], c, nr,
-                           bf.slab[b], bf.sums[b], out + r, c.pieces);
+        hipLaunchKernelGGL((k_sign_p2e_w<DGP, 32>), dim3(wave_groups(nr)), dim3(DCOR_BLOCK), 0, st[b], c, nr,
+                           bf.slab[b], bf.sums[b], out + r);
       else
-        hipLaunchKernelGGL((k_sign_p2e_w<DGP, 16>), dim3(wave_groups(nr)), dim3(DCOR_BLOCK), lds, st[b], c, nr,
-                           bf.slab[b], bf.sums[b], out + r, c.pieces);
+        hipLaunchKernelGGL((k_sign_p2e_w<DGP, 16>), dim3(wave_groups(nr)), dim3(DCOR_BLOCK), 0, st[b], c, nr,
+                           bf.slab[b], bf.sums[b], out + r);
       if (int e = last_err()) return e;
       continue;
     }
