@@ -37,12 +37,12 @@ template <> struct Dgp<DCOR_DGP_GAUSSIAN> {  // MASS::mvrnorm (vert-cor.R:389-39
   // The same sample for the slow-sample drains, where (nearly) every lane has one normal off the
   // fast path: the lanes run ONE divergent zig_slow loop between them -- each for its own slow
   // normal, z1 or z2 -- instead of one loop for z1 and one for z2; a sample with both normals slow
-  // (about 1 in 4000) runs z2's after.  Same draws, same values as from_block.
+  // (about 1 in 55000) runs z2's after.  Same draws, same values as from_block.
   static __device__ __forceinline__ void from_block_slow(const DgpConst& g, uint32_t i, uint32_t rep,
                                                          uint32_t k0, uint32_t k1, const U4& w, double& x,
                                                          double& y, const double2* zt) {
     const uint32_t H1 = w.w2 & 0xffffu, H2 = w.w2 >> 16;
-    const double2 t1 = zig_entry(zt, H1 >> 6), t2 = zig_entry(zt, H2 >> 6);
+    const double2 t1 = zig_entry(zt, H1 >> 5), t2 = zig_entry(zt, H2 >> 5);
     double z1 = fma(zig_d(w.w0, zig_y_lo(H1)), t1.x, -t1.x);
     double z2 = fma(zig_d(w.w1, zig_y_lo(H2)), t2.x, -t2.x);
     const bool ok1 = fabs(z1) < t1.y, ok2 = fabs(z2) < t2.y;
@@ -364,7 +364,7 @@ __device__ __forceinline__ void exact_signs(const SignConst& c, const SignStd& s
 // terms overflow -- the same for every such value -- so the slot carries 0 and every sign, hence
 // every result, is unchanged.
 // Gaussian DGP in pass 1: the ziggurat's fast path inline; a sample with a normal that misses it
-// (1.6 % of samples) is queued in a per-wave LDS list and generated in full later by the whole
+// (0.85 % of samples) is queued in a per-wave LDS list and generated in full later by the whole
 // wave at once (zig_slow would otherwise run under divergence nearly every iteration).  The
 // queued sample's record is rewritten and its clipped values replace its placeholder's in the
 // sums at the drain.
@@ -413,12 +413,12 @@ __device__ __forceinline__ uint32_t sign_record(const SignConst& c, double xc, d
   return rec_of(code16_pair(xc, yc, c.cinv_xf, c.cinv_yf, c.cnb_xf, c.cnb_yf), sign_flip7(c, u));
 }
 
-// Per-wave slow-normal queue (the wave-per-replicate pass 1): a group adds at most 256 entries per wave (about 1.6 % of a wave's
-// samples are queued).  With DCOR_DRAIN_AT = 0 the loop drains the whole queue above ZQ_CAP - 256,
-// so at the headline's n a wave usually drains once, at the end of its replicate; 768: the
-// workgroup's LDS (28.7 KB with the table) still fits five workgroups per CU.
+// Per-wave slow-normal queue (the wave-per-replicate pass 1): a loop step adds at most 256 entries
+// per wave (about 0.85 % of a wave's samples are queued); it drains at DCOR_DRAIN_AT (or, with 0,
+// above ZQ_CAP - 256), so it never holds more than DCOR_DRAIN_AT - 1 + 256 entries.  384: the
+// workgroup's LDS (38.9 KB with the 32 KB layer table) fits four workgroups per CU.
 #ifndef DCOR_ZQ_CAP
-#define DCOR_ZQ_CAP 768
+#define DCOR_ZQ_CAP 384
 #endif
 #define ZQ_CAP DCOR_ZQ_CAP
 // DCOR_DRAIN_AT > 0: a wave drains whole 64-entry rounds of its queue as soon as it holds
@@ -430,6 +430,7 @@ __device__ __forceinline__ uint32_t sign_record(const SignConst& c, double xc, d
 #ifndef DCOR_DRAIN_AT
 #define DCOR_DRAIN_AT 64
 #endif
+static_assert(ZQ_CAP >= 256 && (DCOR_DRAIN_AT == 0 || DCOR_DRAIN_AT - 1 + 256 <= ZQ_CAP), "slow-sample queue bound");
 
 // WAVE = false: one 256-thread workgroup per replicate; WAVE = true: one wave per replicate (the
 // caller's workgroup has loaded the ziggurat table `zt` into LDS once for all its replicates).

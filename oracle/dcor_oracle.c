@@ -539,12 +539,12 @@ static void orc_normal_polar(const uint32_t w[4], double* r, double* s, double* 
 }
 
 /* The Gaussian DGP's ziggurat normal (dcor_device.h zig_d / zig_slow / zig_draw; Marsaglia &
- * Tsang, 512 layers, tables in dcor_tables.h).  Attempt 0 takes a 32-bit word A and a 16-bit
- * field H from the sample's DGP_A block: j = H >> 6 (layer j >> 1, sign j & 1), |u| = (2 x + 1)
- * 2^-39 with x = A : H[5:0], x_draw = round(|u| (-1)^s X[L]) = fma(1 + |u|, SX, -SX). */
+ * Tsang, 1024 layers, tables in dcor_tables.h).  Attempt 0 takes a 32-bit word A and a 16-bit
+ * field H from the sample's DGP_A block: j = H >> 5 (layer j >> 1, sign j & 1), |u| = (2 x + 1)
+ * 2^-38 with x = A : H[4:0], x_draw = round(|u| (-1)^s X[L]) = fma(1 + |u|, SX, -SX). */
 static double orc_zig_d(uint32_t A, uint32_t H) {
   const uint64_t hi = 0x3ff00000ull | (A >> 12);
-  const uint64_t lo = ((uint64_t)(A & 0xfffu) << 20) | ((uint64_t)(H & 0x3fu) << 14) | (1u << 13);
+  const uint64_t lo = ((uint64_t)(A & 0xfffu) << 20) | ((uint64_t)(H & 0x1fu) << 15) | (1u << 14);
   const uint64_t bits = (hi << 32) | lo;
   double d;
   memcpy(&d, &bits, 8);
@@ -562,7 +562,7 @@ double orc_zig(uint64_t seed, uint32_t i, uint32_t which, uint32_t rep, uint32_t
     uint32_t q[4];
     blk4(seed, i, rep, DCOR_SITE_ZIG, 2u * a + which, q);
     if (a > 0) { A = q[0]; H = q[1] & 0xffffu; }
-    const uint32_t j = H >> 6, L = j >> 1;
+    const uint32_t j = H >> 5, L = j >> 1;
     const double sx = dcor_zig_tab[j][0];
     const double x = fma(orc_zig_d(A, H), sx, -sx);
     if (fabs(x) < dcor_zig_tab[j][1]) return x;     /* fast test: inside the strip's rectangle */

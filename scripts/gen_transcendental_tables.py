@@ -12,9 +12,9 @@ sin(pi t) = S_j cos d + C_j sin d, cos(pi t) = C_j cos d - S_j sin d, with S_j, 
 sin, cos(pi j / 64) and degree-7 / degree-6 Taylor polynomials in d (truncation d^8/8! <
 3.3e-18).
 
-Ziggurat (the Gaussian DGP's normals, Marsaglia & Tsang 2000 with 512 layers): f(x) =
+Ziggurat (the Gaussian DGP's normals, Marsaglia & Tsang 2000 with 1024 layers): f(x) =
 exp(-x^2/2); r solves the layer recursion X[1] = r, X[i+1] = f^-1(v / X[i] + f(X[i])) with the
-top layer closing at f(0) = 1 (v = r f(r) + int_r^inf f, X[0] = v / f(r), X[512] = 0).
+top layer closing at f(0) = 1 (v = r f(r) + int_r^inf f, X[0] = v / f(r), X[1024] = 0).
 dcor_zig_tab[2L + s] = {(-1)^s X[L], X[L+1]} (the signed strip width and the fast-accept bound);
 dcor_zig_wedge[L] = {f(X[L]), f(X[L+1]) - f(X[L])}.  Computed with mpmath at 50 digits.
 
@@ -98,7 +98,7 @@ def log8_table():
     return rows
 
 
-ZIG_N = 512
+ZIG_N = 1024
 
 
 def zig_tables():

@@ -264,9 +264,10 @@ def test_saturated_cells_vs_oracle(dc, orc, spec):
     assert_close(got, ref, what=f"saturated {spec}")
 
 
-# The workgroup Gaussian pass 1 marks slow samples in a per-replicate bitmap and k_sign_drain
-# regenerates them: n % 4 != 0 puts slow samples in the tail group's word, and n just above a
-# multiple of the 512-group loop step leaves waves with different step counts (partial quads).
+# The workgroup Gaussian pass 1 compacts its slow samples into a per-wave list every four loop
+# steps and regenerates them in-kernel: n % 4 != 0 puts slow samples in the tail group, and n
+# just above a multiple of the 512-group loop step leaves waves with different step counts
+# (partial quads).
 @pytest.mark.parametrize("n", [16_387, 100_003, 2_048 * 4 * 4 + 4 * 64 + 2, 131_071])
 def test_fused_vs_oracle_bitmap_geometry(dc, orc, n):
     from dcor.sim import CellSpec, simulate
