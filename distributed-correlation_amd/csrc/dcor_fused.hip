@@ -2,7 +2,7 @@
 // reduce -> Laplace -> NI + INT estimate + CI, one 256-thread workgroup per replicate.
 //
 // Nothing of a replicate's input is materialised in HBM except, for the one-pass sign
-// kernel, a 4-byte code per sample (k_sign_fused_codes).  The DGP is a template parameter
+// kernel, a 2-byte record per sample (k_sign_pass1 / k_sign_pass2).  The DGP is a template parameter
 // so the sample loops are straight-line code.  fp64 throughout (R `double`).
 #include <hip/hip_runtime.h>
 

@@ -753,6 +753,13 @@ __global__ __launch_bounds__(DICT_NT, WPE) void k_premat_subg_dict(PrematSubgCon
 // batch pairs gathered per scheduling group; NA accumulator sets; WPE waves per SIMD.
 // INTK = false: the INT sums are left to k_premat_subg_int (s[6..9] of each partial); the kernel
 // then streams no INT bytes, writes s[0..5] only and needs 106 VGPRs instead of 128.
+// DCOR_TILED_EARLY_NZ: batch pairs (of NQ) whose NI noise is loaded before the tile sweeps
+// instead of after them (NI-only kernel).  Measured (C5-continuous, 8192 replicates, one box, two
+// runs each, round 5): 8.97e6 replicates/s with none, 9.80e6-9.84e6 with 1, 2 or 3, 9.64e6 with 4
+// (3 VGPRs spilled), 9.50e6 with all 5 (11 spilled).
+#ifndef DCOR_TILED_EARLY_NZ
+#define DCOR_TILED_EARLY_NZ 2
+#endif
 template <int NT, int NQ, int FU, int GB, int NA, int WPE, bool PG = false, bool INTK = true>
 __global__ __launch_bounds__(NT, WPE) void k_premat_subg_tiled(PrematSubgConst p,
                                                               const int* __restrict__ dict_ok,
@@ -852,6 +859,21 @@ __global__ __launch_bounds__(NT, WPE) void k_premat_subg_tiled(PrematSubgConst p
         const uint32_t q = qb + tid + (uint32_t)u * NT;
         pr[u] = ld_pr(q < nbp ? q : nbp - 1);
       }
+      // NI noise of every pair (past the last pair: the last pair's): that of the first
+      // DCOR_TILED_EARLY_NZ pairs issued here, so its HBM round trip overlaps the tile sweeps, the
+      // rest after them
+      dv2 nx[NQ], ny[NQ];
+      auto ld_noise = [&](int u0, int u1) {
+#pragma unroll
+        for (int u = 0; u < NQ; ++u) {
+          if (u < u0 || u >= u1) continue;
+          const uint32_t q = qb + tid + (uint32_t)u * NT, qc = q < nbp ? q : nbp - 1;
+          nx[u] = ld_nz(x_row, qc);
+          ny[u] = ld_nz(y_row, qc);
+        }
+      };
+      constexpr int NZE = INTK ? 0 : (DCOR_TILED_EARLY_NZ < NQ ? DCOR_TILED_EARLY_NZ : NQ);
+      ld_noise(0, NZE);
 #pragma unroll
       for (int u = 0; u < NQ; ++u) {
         const uint32_t q = qb + tid + (uint32_t)u * NT;
@@ -943,14 +965,8 @@ __global__ __launch_bounds__(NT, WPE) void k_premat_subg_tiled(PrematSubgConst p
         wave_put(4, merged(sU2));
       }
       // NI terms of this round's batch pairs, ascending q (real-data-sims.R:131-137); the noise
-      // of every pair loaded first (past the last pair: the last pair's), one round trip per round
-      dv2 nx[NQ], ny[NQ];
-#pragma unroll
-      for (int u = 0; u < NQ; ++u) {
-        const uint32_t q = qb + tid + (uint32_t)u * NT, qc = q < nbp ? q : nbp - 1;
-        nx[u] = ld_nz(x_row, qc);
-        ny[u] = ld_nz(y_row, qc);
-      }
+      // of every pair loaded first, one round trip per round
+      ld_noise(NZE, NQ);
 #pragma unroll
       for (int u = 0; u < NQ; ++u) {
         const uint32_t q = qb + tid + (uint32_t)u * NT;
