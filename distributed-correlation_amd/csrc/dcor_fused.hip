@@ -579,6 +579,11 @@ __device__ __forceinline__ void sign_pass1_core(const SignConst& c, uint32_t rep
         if constexpr (CEIL == 3) asm volatile("" ::"v"(r));
         else slab_st1(slab, i, r);
       };
+      // (Measured, round 5, headline, one box: the regenerations cost about 40 us of pass 1's ~494
+      // per chunk -- without them 454 -- at about 430 VALU instructions per 64-entry flush, 4.5 % of
+      // the kernel's VALU count.  Two entries per lane, their slow normals in one attempt loop so
+      // each lane runs two independent chains: 494-497 us, no gain, so the flush is VALU-bound, not
+      // latency-bound.  Dropping the vmcnt(0) below: no gain either.)
       auto flush = [&](uint32_t upto) {   // regenerate the list's top `upto` entries
         __builtin_amdgcn_s_waitcnt(0x0070);   // vmcnt(0), lgkmcnt(0): placeholders stored, list in LDS
         __builtin_amdgcn_wave_barrier();
