@@ -753,14 +753,16 @@ __global__ __launch_bounds__(DICT_NT, WPE) void k_premat_subg_dict(PrematSubgCon
 // batch pairs gathered per scheduling group; NA accumulator sets; WPE waves per SIMD.
 // INTK = false: the INT sums are left to k_premat_subg_int (s[6..9] of each partial); the kernel
 // then streams no INT bytes, writes s[0..5] only and needs 106 VGPRs instead of 128.
-// DCOR_TILED_EARLY_NZ: batch pairs (of NQ) whose NI noise is loaded before the tile sweeps
-// instead of after them (NI-only kernel).  Measured (C5-continuous, 8192 replicates, one box, two
-// runs each, round 5): 8.97e6 replicates/s with none, 9.80e6-9.84e6 with 1, 2 or 3, 9.64e6 with 4
-// (3 VGPRs spilled), 9.50e6 with all 5 (11 spilled).
-#ifndef DCOR_TILED_EARLY_NZ
-#define DCOR_TILED_EARLY_NZ 2
-#endif
-template <int NT, int NQ, int FU, int GB, int NA, int WPE, bool PG = false, bool INTK = true>
+// Measured and dropped (round 5, C5-continuous, one box): the NI noise of the first 1-5 batch pairs
+// loaded before the tile sweeps instead of after them -- 1.08e7-1.10e7 replicates/s with 0, 1 or 2
+// pairs (it had looked like +9 % while the loads still branched on alignment at run time), 4 and 5
+// pairs spill.
+// AL: the caller's perm / lap_ni_x / lap_ni_y are 16-B aligned (every row is then, k being even):
+// 16-B loads; otherwise element loads of the same values.  The launcher picks the instantiation, so
+// the arithmetic -- and every replicate's bits -- does not depend on the buffers' alignment, and the
+// aligned kernel carries no run-time branch around its loads (measured, round 5: the branch took
+// the tiled kernel from 496 to 551 us per 8192 C5-continuous replicates).
+template <int NT, int NQ, int FU, int GB, int NA, int WPE, bool PG = false, bool INTK = true, bool AL = true>
 __global__ __launch_bounds__(NT, WPE) void k_premat_subg_tiled(PrematSubgConst p,
                                                               const int* __restrict__ dict_ok,
                                                               int64_t reps, int64_t tile_pairs_,
@@ -783,16 +785,12 @@ __global__ __launch_bounds__(NT, WPE) void k_premat_subg_tiled(PrematSubgConst p
   for (int64_t it = blockIdx.x; it < reps; it += gridDim.x) {
     const int64_t rep = it;
     const double* __restrict__ ll = p.lap_local + rep * c.n;
-    // batch pair q's four indices and two noise pairs: 16-B loads when the caller's arrays are
-    // 16-B aligned (every row is then, k being even), element loads otherwise -- the same values,
-    // so the kernel (and every replicate's bits) does not depend on the buffers' alignment
+    // batch pair q's four indices and two noise pairs (AL above)
     const int* __restrict__ pr_row = p.perm + rep * (c.k * 2);
     const double* __restrict__ x_row = p.lap_ni_x + rep * c.k;
     const double* __restrict__ y_row = p.lap_ni_y + rep * c.k;
-    const bool al_ni = ((reinterpret_cast<uintptr_t>(p.perm) | reinterpret_cast<uintptr_t>(p.lap_ni_x) |
-                         reinterpret_cast<uintptr_t>(p.lap_ni_y)) & 15) == 0;
     auto ld_pr = [&](uint32_t q) -> iv4 {
-      if (al_ni) return __builtin_nontemporal_load(reinterpret_cast<const iv4*>(pr_row) + q);
+      if constexpr (AL) return __builtin_nontemporal_load(reinterpret_cast<const iv4*>(pr_row) + q);
       iv4 v;
       v.x = __builtin_nontemporal_load(pr_row + 4 * q);
       v.y = __builtin_nontemporal_load(pr_row + 4 * q + 1);
@@ -801,7 +799,7 @@ __global__ __launch_bounds__(NT, WPE) void k_premat_subg_tiled(PrematSubgConst p
       return v;
     };
     auto ld_nz = [&](const double* __restrict__ row, uint32_t q) -> dv2 {
-      if (al_ni) return __builtin_nontemporal_load(reinterpret_cast<const dv2*>(row) + q);
+      if constexpr (AL) return __builtin_nontemporal_load(reinterpret_cast<const dv2*>(row) + q);
       dv2 v;
       v.x = __builtin_nontemporal_load(row + 2 * q);
       v.y = __builtin_nontemporal_load(row + 2 * q + 1);
@@ -859,21 +857,6 @@ __global__ __launch_bounds__(NT, WPE) void k_premat_subg_tiled(PrematSubgConst p
         const uint32_t q = qb + tid + (uint32_t)u * NT;
         pr[u] = ld_pr(q < nbp ? q : nbp - 1);
       }
-      // NI noise of every pair (past the last pair: the last pair's): that of the first
-      // DCOR_TILED_EARLY_NZ pairs issued here, so its HBM round trip overlaps the tile sweeps, the
-      // rest after them
-      dv2 nx[NQ], ny[NQ];
-      auto ld_noise = [&](int u0, int u1) {
-#pragma unroll
-        for (int u = 0; u < NQ; ++u) {
-          if (u < u0 || u >= u1) continue;
-          const uint32_t q = qb + tid + (uint32_t)u * NT, qc = q < nbp ? q : nbp - 1;
-          nx[u] = ld_nz(x_row, qc);
-          ny[u] = ld_nz(y_row, qc);
-        }
-      };
-      constexpr int NZE = INTK ? 0 : (DCOR_TILED_EARLY_NZ < NQ ? DCOR_TILED_EARLY_NZ : NQ);
-      ld_noise(0, NZE);
 #pragma unroll
       for (int u = 0; u < NQ; ++u) {
         const uint32_t q = qb + tid + (uint32_t)u * NT;
@@ -965,8 +948,14 @@ __global__ __launch_bounds__(NT, WPE) void k_premat_subg_tiled(PrematSubgConst p
         wave_put(4, merged(sU2));
       }
       // NI terms of this round's batch pairs, ascending q (real-data-sims.R:131-137); the noise
-      // of every pair loaded first, one round trip per round
-      ld_noise(NZE, NQ);
+      // of every pair loaded first (past the last pair: the last pair's), one round trip per round
+      dv2 nx[NQ], ny[NQ];
+#pragma unroll
+      for (int u = 0; u < NQ; ++u) {
+        const uint32_t q = qb + tid + (uint32_t)u * NT, qc = q < nbp ? q : nbp - 1;
+        nx[u] = ld_nz(x_row, qc);
+        ny[u] = ld_nz(y_row, qc);
+      }
 #pragma unroll
       for (int u = 0; u < NQ; ++u) {
         const uint32_t q = qb + tid + (uint32_t)u * NT;
@@ -1047,27 +1036,31 @@ __global__ __launch_bounds__(256, DCOR_INT_WPE) void k_premat_subg_int(PrematSub
     return v;
   };
   DD sU[R][2] = {}, sU2[R][2] = {};      // [replicate][logical thread tid, tid + 256]
-  // Pair p belongs to logical thread p mod 512: a trip takes pair q (logical thread tid, set 0) and
-  // then pair q + 256 (logical thread tid + 256, set 1), so each set sums its pairs in ascending
-  // order, as the 512-thread kernels do.  The set is a compile-time index of each slot.
-  auto slot = [&](uint32_t qj, auto set_tag) {
+  // Pair p belongs to logical thread p mod 512, so the pairs q = tid (mod 512) go to set 0 and
+  // q = tid + 256 (mod 512) to set 1, each set in ascending order, as in the 512-thread kernels.
+  // One loop per set, one pair slot per trip (its loads first, then its terms; the set a
+  // compile-time index).  Measured (round 5, per 8192 C5-continuous replicates, one box): 245 us, as
+  // round 4's loop (which summed both sets into one); both slots of a 512-pair trip in one loop body
+  // took 269 us (the second slot's loads waited behind the first's terms and its branch), or 354 us
+  // with both slots' loads issued first.
+  auto sweep = [&](uint32_t q0, auto set_tag) {
     constexpr int SET = decltype(set_tag)::value;
-    const double2 v0 = so[2 * qj], v1 = so[2 * qj + 1];
-    dv2 l[R];
+    for (uint32_t q = q0; q < np; q += 512) {
+      const double2 v0 = so[2 * q], v1 = so[2 * q + 1];
+      dv2 l[R];
 #pragma unroll
-    for (int r = 0; r < R; ++r) l[r] = ldp(r, qj);
+      for (int r = 0; r < R; ++r) l[r] = ldp(r, q);
 #pragma unroll
-    for (int r = 0; r < R; ++r) {
-      const double U0 = rclip((v0.x + c.bs * l[r].x) * v0.y, c.lr);
-      const double U1 = rclip((v1.x + c.bs * l[r].y) * v1.y, c.lr);
-      ks_acc(sU[r][SET], U0 + U1);
-      ks_acc(sU2[r][SET], U0 * U0 + U1 * U1);
+      for (int r = 0; r < R; ++r) {
+        const double U0 = rclip((v0.x + c.bs * l[r].x) * v0.y, c.lr);
+        const double U1 = rclip((v1.x + c.bs * l[r].y) * v1.y, c.lr);
+        ks_acc(sU[r][SET], U0 + U1);
+        ks_acc(sU2[r][SET], U0 * U0 + U1 * U1);
+      }
     }
   };
-  for (uint32_t q = tid; q < np; q += 512) {
-    slot(q, std::integral_constant<int, 0>());
-    if (q + 256 < np) slot(q + 256, std::integral_constant<int, 1>());
-  }
+  sweep(tid, std::integral_constant<int, 0>());
+  sweep(tid + 256, std::integral_constant<int, 1>());
   if (tid == 255 && 2 * np < n) {        // logical thread 511: the odd tail sample
     const double2 v = so[n - 1];
 #pragma unroll
@@ -1963,18 +1956,22 @@ static int tiled_int_mode() {
 #ifndef DCOR_INT_R
 #define DCOR_INT_R 4
 #endif
-static TiledKernel tiled_kernel(bool intk) {
-  static const TiledKernel ks[2][2] = {
-      {{k_premat_subg_tiled<512, 5, 1, 1, 1, 4, true>, 512, 80 * 1024},
-       {k_premat_subg_tiled<512, 5, 1, 1, 1, 4, true, false>, 512, 80 * 1024}},
-      {{k_premat_subg_tiled<1024, 5, 1, 1, 1, 4, true>, 1024, 160 * 1024},
-       {k_premat_subg_tiled<1024, 5, 1, 1, 1, 4, true, false>, 1024, 160 * 1024}}};
+static TiledKernel tiled_kernel(bool intk, bool al) {
+  static const TiledKernel ks[2][2][2] = {
+      {{{k_premat_subg_tiled<512, 5, 1, 1, 1, 4, true, true, false>, 512, 80 * 1024},
+        {k_premat_subg_tiled<512, 5, 1, 1, 1, 4, true, true, true>, 512, 80 * 1024}},
+       {{k_premat_subg_tiled<512, 5, 1, 1, 1, 4, true, false, false>, 512, 80 * 1024},
+        {k_premat_subg_tiled<512, 5, 1, 1, 1, 4, true, false, true>, 512, 80 * 1024}}},
+      {{{k_premat_subg_tiled<1024, 5, 1, 1, 1, 4, true, true, false>, 1024, 160 * 1024},
+        {k_premat_subg_tiled<1024, 5, 1, 1, 1, 4, true, true, true>, 1024, 160 * 1024}},
+       {{k_premat_subg_tiled<1024, 5, 1, 1, 1, 4, true, false, false>, 1024, 160 * 1024},
+        {k_premat_subg_tiled<1024, 5, 1, 1, 1, 4, true, false, true>, 1024, 160 * 1024}}}};
   static const int v = [] {
     const char* e = std::getenv("DCOR_TILED_VARIANT");
     const int x = e ? std::atoi(e) : 1;
     return (x >= 0 && x < 2) ? x : 1;
   }();
-  return ks[v][intk ? 0 : 1];
+  return ks[v][intk ? 0 : 1][al ? 1 : 0];
 }
 static bool tiled_enabled() {
   static const bool on = [] {
@@ -2049,7 +2046,9 @@ int launch_premat_subg(const PrematSubgConst& c0, int64_t reps, void* part, dcor
       };
       if (conc && hipEventRecord((hipEvent_t)ev_fork, (hipStream_t)stream) != hipSuccess) return last_err();
       if (!intk && !conc) launch_int((hipStream_t)stream);
-      const TiledKernel tk = tiled_kernel(intk);
+      const bool al = ((reinterpret_cast<uintptr_t>(c.perm) | reinterpret_cast<uintptr_t>(c.lap_ni_x) |
+                        reinterpret_cast<uintptr_t>(c.lap_ni_y)) & 15) == 0;
+      const TiledKernel tk = tiled_kernel(intk, al);
       const int64_t np = c.s.n >> 1;  // INT pairs (at most; h = 1 rows have (n - 1) / 2)
       const size_t red_b = (size_t)(20 * (tk.nt / 64)) * sizeof(double);
       const int64_t tp_max = (int64_t)((tk.lds_budget - red_b) / 16 - 3) / 2;
