@@ -546,11 +546,17 @@ int prepare_cell(const dcor_cell& c, CellPlan& p) {
         rx = 2.0 * sx;
         ry = 2.0 * sy;
       } else {
+        // DCOR_CODE_WINDOW=<a>,<b> (A/B runs): a sd(mean) + b noise scales instead of 7, 24
+        double wa = 7.0, wb = 24.0;
+        if (wv) {
+          double a2 = 0, b2 = 0;
+          if (std::sscanf(wv, "%lf,%lf", &a2, &b2) == 2 && a2 > 0 && b2 > 0) { wa = a2; wb = b2; }
+        }
         const double rn = 1.0 / std::sqrt((double)c.n);
         cx = clipped_normal_mean(c.mu[0], sx, k.L);
         cy = clipped_normal_mean(c.mu[1], sy, k.L);
-        rx = r_min(2.0 * sx, 7.0 * sx * rn + 24.0 * k.s_mu_x);
-        ry = r_min(2.0 * sy, 7.0 * sy * rn + 24.0 * k.s_mu_y);
+        rx = r_min(2.0 * sx, wa * sx * rn + wb * k.s_mu_x);
+        ry = r_min(2.0 * sy, wa * sy * rn + wb * k.s_mu_y);
       }
     } else if (c.dgp == DCOR_DGP_BERNOULLI) {
       cx = cy = 0.5; rx = ry = 1.0;
@@ -806,7 +812,9 @@ int dcor_diag_sign_pass(const dcor_cell* cell, int64_t rep_begin, int64_t reps, 
   if (int st = need_device()) return st;
   CellPlan cp;
   if (int st = prepare_cell(*cell, cp)) return st;
-  if (cp.kind != GK_SIGN_CODES || cp.nan_dgp)
+  // a small cell (wave kernels) runs here in the workgroup kernels: the same records, ties and
+  // results per replicate (passes 1-3 only; the ceilings are the headline's)
+  if ((cp.kind != GK_SIGN_CODES && !(cp.kind == GK_SIGN_CODES_W && which <= 3)) || cp.nan_dgp)
     return fail(DCOR_EINVAL, "diag_sign_pass: the cell does not run the one-pass sign kernels");
   if (which > 10 && (cp.dgp != DCOR_DGP_GAUSSIAN || cp.sign.m != 8))
     return fail(DCOR_EINVAL, "diag_sign_pass: the ceilings run the Gaussian DGP at m = 8");

@@ -116,15 +116,16 @@ int64_t dcor_device_bytes(void);
  * family).  Planning only: no device work.  bench.py times its live pass ceilings at this chunk. */
 int dcor_sim_chunking(const dcor_cell* cell, int64_t rep_count, int64_t* chunk, int64_t* nchunks);
 /* Measurement only (bench.py's roofline, not part of the reference surface): one pass of the
- * one-pass sign path (the kernels dcor_sim_launch runs for cells with n > 16384 and
- * normalise = TRUE) over replicates rep_begin .. rep_begin + reps - 1 as ONE chunk, on `stream`, in
- * the calling thread's scratch arena.  which: 1 pass 1 (writes the slab, the clipped sums and, for
- * the Gaussian DGP, the bitmap of its slow samples), 2 pass 2 (regenerates those samples, then reads
- * the slab and sums), 3 the epilogue (reads pass 2's partials); 11 the pass-1 ceiling and 12 the
- * pass-2 ceiling (Gaussian DGP, m = 8): the same loops with their memory side removed, at the real
- * passes' waves per SIMD -- their time is the instruction stream's own issue-bound time on this
- * GPU; 13 the pass-1 ceiling at its own (higher) occupancy; 14 / 15 the pass-1 ceiling plus
- * only its slab stores / plus only its slow-sample bitmap (what each costs).  Run 1, 2, 3 in that order
+ * one-pass sign path (the workgroup kernels dcor_sim_launch runs for cells with n > 16384 and
+ * normalise = TRUE; a smaller cell runs passes 1-3 in them too, with the same per-replicate records
+ * and results as its wave kernels) over replicates rep_begin .. rep_begin + reps - 1 as ONE chunk,
+ * on `stream`, in the calling thread's scratch arena.  which: 1 pass 1 (writes the slab and the
+ * clipped sums; for the Gaussian DGP it also regenerates its slow samples), 2 pass 2 (reads the slab
+ * and sums), 3 the epilogue (reads pass 2's partials); 11 the pass-1 ceiling and 12 the pass-2
+ * ceiling (Gaussian DGP, m = 8): the same loops with their memory side removed, at the real passes'
+ * waves per SIMD -- their time is the instruction stream's own issue-bound time on this GPU; 13 the
+ * pass-1 ceiling at its own (higher) occupancy; 14 / 15 the pass-1 ceiling plus only its slab stores
+ * / plus only its slow-sample list and regenerations (what each costs).  Run 1, 2, 3 in that order
  * on the same cell and reps (12 after 1).  No result is returned; time them with events. */
 int dcor_diag_sign_pass(const dcor_cell* cell, int64_t rep_begin, int64_t reps, int which, void* stream);
 /* Measurement only: passes 1 and 2 (as dcor_diag_sign_pass 1, 2, on the null stream) and, per
