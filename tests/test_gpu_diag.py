@@ -35,8 +35,11 @@ def test_measure_passes_orders(dc):
 def test_diag_refuses_other_cells(dc):
     from dcor import _lib
     from dcor.sim import CellSpec, headline_cell
-    small = headline_cell(2000).to_c()        # wave kernels, not the one-pass workgroup pair
-    assert _lib.lib.dcor_diag_sign_pass(C.byref(small), 0, 8, 1, None) == _lib.DCOR_EINVAL
+    small = headline_cell(2000).to_c()        # wave kernels: passes 1-3 only, in the workgroup kernels
+    assert _lib.lib.dcor_diag_sign_pass(C.byref(small), 0, 8, 11, None) == _lib.DCOR_EINVAL
+    bern = CellSpec(n=100_000, rho=0.5, eps1=1.0, eps2=1.0, dgp="bernoulli", mu=(0.0, 0.0),
+                    sigma=(1.0, 1.0), seed=7).to_c()
+    assert _lib.lib.dcor_diag_sign_pass(C.byref(bern), 0, 8, 1, None) == _lib.DCOR_EINVAL
     m11 = CellSpec(n=100_000, rho=0.5, eps1=1.5, eps2=0.5, mu=(0.5, 0.5), sigma=(2.0, 2.0), seed=7).to_c()
     assert _lib.lib.dcor_diag_sign_pass(C.byref(m11), 0, 8, 11, None) == _lib.DCOR_EINVAL   # ceilings: m = 8
     h = headline_cell().to_c()
@@ -54,4 +57,21 @@ def test_ceilings_do_not_disturb_results(dc):
     for which in (1, 2, 3, 11, 12, 13, 14, 15):
         _lib.check(_lib.lib.dcor_diag_sign_pass(C.byref(c), 4096, 256, which, None))
     b = simulate(cell, 2048, 4096).cpu().numpy()
+    assert np.array_equal(a.view(np.int64), b.view(np.int64))
+
+
+def test_diag_ties_on_small_cells(dc):
+    """dcor_diag_sign_ties on a wave-kernel cell (n = 1000, m = 32: the reference grid's most
+    tie-prone cell) runs its replicates in the workgroup kernels and counts tie batches per
+    replicate: some, and at most every batch; its passes leave simulate()'s results untouched."""
+    from dcor import _lib
+    from dcor.sim import CellSpec, simulate
+    cell = CellSpec(n=1000, rho=0.5, eps1=0.5, eps2=0.5, mu=(0.5, 0.5), sigma=(2.0, 2.0), seed=1_000_003)
+    a = simulate(cell, 256, 0).cpu().numpy()
+    c = cell.to_c()
+    ties = np.zeros(256, dtype=np.int64)
+    _lib.check(_lib.lib.dcor_diag_sign_ties(C.byref(c), 0, 256, ties.ctypes.data_as(C.POINTER(C.c_int64))))
+    k = 1000 // 32
+    assert 0 < ties.sum() and ties.max() <= k, ties
+    b = simulate(cell, 256, 0).cpu().numpy()
     assert np.array_equal(a.view(np.int64), b.view(np.int64))
