@@ -149,8 +149,8 @@ def measure_passes(cell, reps: int = 2048, rep_begin: int = 0, iters: int = 5) -
     GPU, now (dcor_diag_sign_pass): each pass over `reps` replicates as one chunk on the current
     stream, alone on the device, median of `iters` launches timed with HIP events on that stream.
 
-      pass1 / pass2 / epilogue   the real kernels (k_sign_pass1, k_sign_pass2 -- whose first phase
-                                 regenerates pass 1's slow samples -- k_sign_epilogue_w)
+      pass1 / pass2 / epilogue   the real kernels (k_sign_pass1 -- which regenerates its own slow
+                                 samples -- k_sign_pass2, k_sign_epilogue_w)
       pass1_ceiling              k_sign_pass1's own hot loop -- Philox, ziggurat fast path, mvrnorm
                                  transform, clips, record codes, group sums -- with the slab store
                                  and the slow-normal queue removed, at pass 1's waves per SIMD
@@ -158,7 +158,7 @@ def measure_passes(cell, reps: int = 2048, rep_begin: int = 0, iters: int = 5) -
       pass2_ceiling              k_sign_pass2's decision loop with its records held in registers
                                  (no slab stream, no tie fix-up), at pass 2's occupancy
       pass1_ceiling_plus_stores  the pass-1 ceiling with its slab stores put back
-      pass1_ceiling_plus_queue   the pass-1 ceiling with its slow-sample bitmap put back
+      pass1_ceiling_plus_queue   the pass-1 ceiling with its slow-sample list and regenerations put back
 
     A ceiling is the time the pass's own instruction stream takes when nothing but issue limits
     it: pass / ceiling is how far memory, queueing and fix-ups keep the pass from it."""

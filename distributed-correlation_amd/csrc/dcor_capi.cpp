@@ -692,13 +692,15 @@ int dcor_batch_geometry(int64_t n, double eps1, double eps2, int family, int hrs
 }
 
 // The one-pass sign path's replicate chunks: two slabs (two-stream chunk pipeline), each within a
-// budget of >= 1 GiB and >= 2048 replicates' codes, <= 8 GiB; equal chunks (no small tail launch).
-// dcor_sim_launch and dcor_sim_chunking (bench.py's live ceilings) share it.
+// budget of >= 512 MiB and >= 2048 replicates' records, <= 4 GiB; equal chunks (no small tail
+// launch).  At the headline's n that is four chunks of 2048 per 8192 replicates (round 2: chunks of
+// 512-1024 measured 3-8 % slower, 4096 the same).  dcor_sim_launch and dcor_sim_chunking (bench.py's
+// live ceilings) share it.
 static void codes_chunking(int64_t n, int64_t rep_count, int64_t* chunk, int64_t* nchunks) {
-  const size_t per_rep = (size_t)n * sizeof(uint32_t);
-  size_t budget = (size_t)1 << 30;
+  const size_t per_rep = (size_t)sign_rec_words(n) * sizeof(uint32_t);
+  size_t budget = (size_t)512 << 20;
   if (budget < 2048 * per_rep) budget = 2048 * per_rep;
-  if (budget > ((size_t)8 << 30)) budget = (size_t)8 << 30;
+  if (budget > ((size_t)4 << 30)) budget = (size_t)4 << 30;
   int64_t maxchunk = (int64_t)(budget / per_rep);
   if (maxchunk < 1) maxchunk = 1;
   int64_t nch = (rep_count + maxchunk - 1) / maxchunk;
@@ -746,7 +748,7 @@ int dcor_sim_launch(const dcor_cell* cell, int64_t rep_begin, int64_t rep_count,
     } else if ((cp.kind != GK_SIGN_CODES && cp.kind != GK_SIGN_CODES_W) || rep_count == 0) {
       rc = launch_sign_fused(k, rep_count, d_out, stream);
     } else {
-      const size_t per_rep = (size_t)sign_item_words(c.n, c.dgp) * sizeof(uint32_t);   // records + bitmap
+      const size_t per_rep = (size_t)sign_item_words(c.n, c.dgp) * sizeof(uint32_t);   // u16 records
       int64_t chunk = 0, nch = 0;
       codes_chunking(c.n, rep_count, &chunk, &nch);
       const size_t slab_b = ((size_t)chunk * per_rep + 255) / 256 * 256 + 256;  // + pass 2's over-read

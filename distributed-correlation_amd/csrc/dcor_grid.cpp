@@ -51,8 +51,7 @@ bool codes_kind(int kind) { return kind == GK_SIGN_CODES || kind == GK_SIGN_CODE
 bool subg_kind(int kind) { return kind == GK_SUBG || kind == GK_SUBG_W; }
 
 uint64_t item_scratch(int kind, int dgp, int64_t n) {
-  // code slabs start on 256-B boundaries (the kernels move records 16 B at a time); the workgroup
-  // Gaussian pass 1 adds its slow-sample bitmap (sign_item_words)
+  // code slabs (u16 records) start on 256-B boundaries: the kernels move records 16 B at a time
   if (codes_kind(kind)) return sign_item_words(n, dgp);   // u32 words
   if (kind == GK_SIGN_BERN) return (uint64_t)3 * 4 * ((n + 255) / 256);  // u64 plane words
   return 0;
