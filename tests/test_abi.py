@@ -138,3 +138,26 @@ def test_accum_merge_and_finalize_host():
     assert abs(s["var"] - np.var(est, ddof=1)) < 1e-13
     assert s["coverage"] == np.mean((0.5 >= lo) & (0.5 <= hi))
     assert abs(s["ci_length"] - 0.4) < 1e-15
+
+
+def test_sim_chunking_plan_without_gpu():
+    """dcor_sim_chunking is planning only (no device): the one-pass sign path splits the headline's
+    8192 replicates into four chunks of 2048 (the shape bench.py times its live ceilings at), always
+    at least two chunks from 512 replicates, equal chunks covering every replicate; other kernel
+    families take one launch."""
+    from dcor import _lib
+    from dcor.sim import CellSpec, headline_cell
+
+    def plan(cell, reps):
+        ch, nc = C.c_int64(), C.c_int64()
+        _lib.check(_lib.lib.dcor_sim_chunking(C.byref(cell.to_c()), reps, C.byref(ch), C.byref(nc)))
+        return ch.value, nc.value
+
+    assert plan(headline_cell(), 8192) == (2048, 4)
+    assert plan(headline_cell(), 512) == (256, 2)
+    for n, reps in ((100_000, 10_001), (1_000_000, 100_000), (20_000, 3)):
+        ch, nc = plan(headline_cell(n), reps)
+        assert nc >= 1 and ch * nc >= reps and ch * (nc - 1) < reps
+    bern = CellSpec(n=100_000, rho=0.5, eps1=1.0, eps2=1.0, dgp="bernoulli", mu=(0.0, 0.0), sigma=(1.0, 1.0))
+    assert plan(bern, 8192) == (8192, 1)
+    assert plan(headline_cell(), 0) == (0, 0)

@@ -97,3 +97,22 @@ def test_configs_more_gpus_than_visible_is_refused():
     p = _run_configs(["--gpus", "2", "--only", "C3"], env={"HIP_VISIBLE_DEVICES": ""})
     assert p.returncode != 0
     assert "visible" in p.stderr
+
+
+def test_config_lines_physical_fractions_from_timed_kernels():
+    """bench_configs.measured(): each config line names its committed profile, whether that profile
+    was taken on this tree's engine sources, and per-kernel physical fractions; VG and SG, whose
+    profiles also hold the per-cell comparison loop, report the timed grid call's kernels only."""
+    import importlib
+    import sys
+    sys.path.insert(0, ROOT)
+    bc = importlib.import_module("bench_configs")
+    for name in ("VG", "SG", "C3", "C5-continuous"):
+        m = bc.measured(name)
+        assert m and m["profile"].startswith("profiles/") and isinstance(m["profile_fresh"], bool)
+        assert m["physical"], name
+        for k, v in m["physical"].items():
+            assert v["pct_time"] >= 5.0
+            if name in bc.TIMED_KERNELS:
+                assert k.startswith(bc.TIMED_KERNELS[name]), (name, k)
+    assert bc.measured("C1") == {}
