@@ -277,6 +277,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-ceilings", action="store_true", help="skip the live pass ceilings (roofline.issue_frac)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--variant", action="append", default=[], metavar="NAME=VALUE",
+                    help="engine implementation switch for A/B runs (dcor_set_variant; repeatable)")
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher check on CPU: form the process group over gloo, exchange accumulators, "
                          "print the world size formed; no GPU, no timing")
@@ -323,6 +325,7 @@ def main():
         formed = 1
 
     import dcor
+    dcor._lib.apply_variant_args(args.variant)
     from dcor.dist import gather_accums, merge_ranked
     from dcor.sim import accum_from_bytes, accumulate, finalize, headline_cell, simulate
 
@@ -404,7 +407,8 @@ def main():
                                    "rho=.5, eps=(1,1), NI+INT CIs (mixquant)",
                        "n": cell.n, "m": m, "k": k, "replicates_per_gpu_per_step": R,
                        "parallelism": f"replicate-shard x{formed}",
-                       "world_formed": formed, "backend": "nccl (RCCL)" if world > 1 else "single process"},
+                       "world_formed": formed, "backend": "nccl (RCCL)" if world > 1 else "single process",
+                       **({"variants": args.variant} if args.variant else {})},
             "roofline": {"bound": "valu_fp64", "achieved": achieved, "peak": FP64_PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": achieved / FP64_PEAK_TFLOPS,
                          "frac_kind": "pinned convention: SURVEY §8d work weights (fp64-FMA units) per "

@@ -252,7 +252,7 @@ def ref_grid(name, cells, B=250):
               "host copy of every cell's accumulators), best of 5 x 4 back-to-back calls")
 
 
-def c5(R, panel="coded"):
+def c5(R, panel="coded", rep_begin=0, emit=True):
     """panel 'coded': generic stand-in of the HRS kind (whole-year ages, one-decimal BMIs,
     dcor.hrs.standin_panel, DP-standardised as real-data-sims.R:273-287): the dictionary-coded
     LDS kernel.  panel 'continuous': every value distinct: the L2-gather kernel."""
@@ -284,13 +284,14 @@ def c5(R, panel="coded"):
     ml = torch.empty((R, nsim), dtype=torch.float64, device="cuda")
     seed = 231
     P = lambda t: C.c_void_p(t.data_ptr())
-    _lib.check(_lib.lib.dcor_perm_launch(seed, _lib.SITE_PERM, 0, R, n, k * m, P(perm), None))
-    _lib.check(_lib.lib.dcor_draws_launch(0, seed, 11, 0, R, k, P(lx), None))
-    _lib.check(_lib.lib.dcor_draws_launch(0, seed, 12, 0, R, k, P(ly), None))
-    _lib.check(_lib.lib.dcor_draws_launch(0, seed, 13, 0, R, n, P(ll), None))
+    rb = rep_begin
+    _lib.check(_lib.lib.dcor_perm_launch(seed, _lib.SITE_PERM, rb, R, n, k * m, P(perm), None))
+    _lib.check(_lib.lib.dcor_draws_launch(0, seed, 11, rb, R, k, P(lx), None))
+    _lib.check(_lib.lib.dcor_draws_launch(0, seed, 12, rb, R, k, P(ly), None))
+    _lib.check(_lib.lib.dcor_draws_launch(0, seed, 13, rb, R, n, P(ll), None))
     _lib.check(_lib.lib.dcor_draws_launch(0, seed, 14, 0, 1, R, P(lc), None))
-    _lib.check(_lib.lib.dcor_draws_launch(1, seed, 15, 0, R, nsim, P(mz), None))
-    _lib.check(_lib.lib.dcor_draws_launch(0, seed, 16, 0, R, nsim, P(ml), None))
+    _lib.check(_lib.lib.dcor_draws_launch(1, seed, 15, rb, R, nsim, P(mz), None))
+    _lib.check(_lib.lib.dcor_draws_launch(0, seed, 16, rb, R, nsim, P(ml), None))
     out = torch.empty((R, 6), dtype=torch.float64, device="cuda")
     d = _lib.PrematSubg(n=n, reps=R, eps1=eps, eps2=eps, eta1=1.0, eta2=1.0, alpha=0.05, hrs=1,
                         lam_x=lam[0], lam_y=lam[1], lam_s=lam[0], lam_o=lam[1], lam_r=math.nan,
@@ -304,6 +305,9 @@ def c5(R, panel="coded"):
               reps=5, inner=8)
     per_rep = 8 * n + 4 * k * m + 16 * k + 8 * nsim    # SURVEY §8d pinned: 404,648 B
     read_rep = 8 * n + 4 * k * m + 16 * k + 8 + 16 * nsim  # bytes the ABI actually reads (z, l apart)
+    if not emit:
+        _lib.check(_lib.lib.dcor_panel_destroy(pn))
+        return t, per_rep
     cpu = c5_cpu(age, bmi, lam, eps, nsim, perm, lx, ly, ll, lc, mz, ml) if panel == "coded" else {}
     ok = C.c_int(-1)
     _lib.check(_lib.lib.dcor_panel_coded(pn, C.byref(ok)))
@@ -388,6 +392,25 @@ def c5_fused(R, panel="coded"):
          kernel="k_hrs_fused (LDS codes)" if panel == "coded" else "k_hrs_fused_l2 (clipped panel in L2)",
          note="HRS replicates with in-kernel Philox noise (+ epilogue), the D2H copy of all replicate "
               "records included")
+
+
+def hrs_sweep(R):
+    """a19: the HRS eps sweep of real-data-sims.R:345-448 (23 eps x R runs, Philox per-eps keys,
+    premat pipeline) on one GPU, summaries built on the host."""
+    import numpy as np
+    import torch
+    from dcor import hrs
+    args = hrs_panel("coded")
+    hrs.eps_sweep(*args, reps=R)    # warm-up
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    res = hrs.eps_sweep(*args, reps=R)
+    torch.cuda.synchronize()
+    t = time.perf_counter() - t0
+    total = len(hrs.EPS_GRID) * R
+    line("HS", replicates=total, seconds=t, reps_per_s=total / t, finite=bool(np.isfinite(res["runs"]).all()),
+         note="23 eps x R NI + INT runs on the coded stand-in panel, one hrs_replicates call per eps, "
+              "summaries (means, type-7 quantiles) on the host")
 
 
 def subg():
@@ -506,8 +529,96 @@ def dist_grid(name, groups, world, rank, dry_run=False, **extra):
                   "sequence per group, accumulators all-gathered (RCCL); time = max over ranks", **extra)
 
 
+def hrs_panel(panel="coded"):
+    """C5's panel: the coded stand-in (DP-standardised as real-data-sims.R:273-287) or a continuous
+    one (every value distinct), and its lambdas."""
+    import numpy as np
+    from dcor import hrs
+    if panel == "coded":
+        age_raw, bmi_raw = hrs.standin_panel(19433, -0.3)
+        z = hrs.standardize_panel(age_raw, bmi_raw, lap=np.zeros(4))
+        return (z["age_z"], z["bmi_z"], z["lambda_age_z"], z["lambda_bmi_z"])
+    g = np.random.default_rng(2)
+    age = np.clip(g.normal(0.0, 1.0, 19433), -2.22, 2.22)
+    bmi = -0.19 * age + math.sqrt(1 - 0.19 ** 2) * g.normal(0.0, 1.0, 19433)
+    return (age, bmi, 2.22, 2.60)
+
+
+def dist_hrs(name, world, rank, dry_run, R, mode, panel="coded", sweep=False):
+    """The HRS workload over the ranks (real-data-sims.R:411-436): C5-e2e / C5-fused give each rank
+    a contiguous range of C5's R replicates (dcor.dist.run_hrs_distributed), the sweep (a19) a
+    contiguous range of the flattened (eps, run) space (dcor.dist.eps_sweep_distributed); the records
+    are all-gathered in rank order (RCCL).  Strong scaling; time = max over ranks."""
+    import torch.distributed as dist
+    from dcor.dist import shard, sweep_shard
+    if sweep:
+        from dcor.hrs import EPS_GRID
+        total = len(EPS_GRID) * R
+        plan = [sweep_shard(len(EPS_GRID), R, r, world) for r in range(world)]
+    else:
+        total = R
+        plan = [shard(R, r, world) for r in range(world)]
+    if dry_run:
+        if rank == 0:
+            print(json.dumps({"config": name, "dry_run": True, "world_formed": dist.get_world_size(),
+                              "replicates": total, "shards": plan}), flush=True)
+        return
+    import numpy as np
+    import torch
+    from dcor.dist import eps_sweep_distributed, run_hrs_distributed
+    args = hrs_panel(panel)
+    if sweep:
+        def run():
+            return eps_sweep_distributed(*args, reps=R)["runs"].reshape(-1, 6)
+    else:
+        def run():
+            return run_hrs_distributed(*args, 2.0, R, mode=mode, chunk=65536 if mode == "fused" else 8192)
+    run()                                   # warm-up (panel, arenas, RCCL communicator)
+    torch.cuda.synchronize()
+    dist.barrier()
+    t0 = time.perf_counter()
+    res = run()
+    torch.cuda.synchronize()
+    dist.barrier()
+    el = time.perf_counter() - t0
+    t = torch.tensor([el], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    el = float(t.item())
+    if rank == 0:
+        line(name, world_formed=dist.get_world_size(), backend=dist.get_backend(), scaling="strong",
+             replicates=total, seconds=el, reps_per_s=total / el, shards=plan, panel=panel, mode=mode,
+             finite=bool(np.isfinite(res).all()), rows_gathered=int(res.shape[0]),
+             note="one process per GPU: each rank's contiguous replicate range, records all-gathered in rank "
+                  "order (RCCL), D2H of every record included; time = max over ranks")
+
+
+def dist_c5(world, rank, dry_run, R):
+    """C5 over the ranks, weak scaling: each rank streams R replicates of its own contiguous range
+    (rep_begin = rank R) through the pre-materialised kernel with its noise resident in HBM (c5()'s
+    timed launch); value = world R / the max over ranks of the per-launch time."""
+    import torch.distributed as dist
+    if dry_run:
+        if rank == 0:
+            print(json.dumps({"config": "C5", "dry_run": True, "world_formed": dist.get_world_size(),
+                              "replicates": world * R, "shards": [[r * R, R] for r in range(world)]}), flush=True)
+        return
+    import torch
+    dist.barrier()
+    t, per_rep = c5(R, rep_begin=rank * R, emit=False)
+    tt = torch.tensor([t], dtype=torch.float64, device="cuda")
+    dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    t = float(tt.item())
+    if rank == 0:
+        line("C5", world_formed=dist.get_world_size(), backend=dist.get_backend(), scaling="weak",
+             replicates=world * R, seconds=t, reps_per_s=world * R / t, hbm_frac_per_gpu=per_rep * R / t / HBM_PEAK,
+             shards=[[r * R, R] for r in range(world)],
+             note="one process per GPU, noise resident per rank; time = max over ranks of one "
+                  "dcor_premat_subg_panel_launch (best of 5 x 8)")
+
+
 def main_dist(a, world, rank, local):
-    """bench_configs.py under N ranks: C3 and C4 (the configs defined as multi-GPU)."""
+    """bench_configs.py under N ranks: C3, C4 and the HRS workload (C5 weak; C5-e2e, C5-fused,
+    C5-fused-continuous and the eps sweep HS strong) -- every config that shards."""
     import torch.distributed as dist
     which = a.only.split(",")
     if a.dry_run:
@@ -523,17 +634,30 @@ def main_dist(a, world, rank, local):
     formed = dist.get_world_size()
     if formed != world:
         sys.exit(f"bench_configs.py: process group formed {formed} ranks, expected {world}")
+    if not a.dry_run:
+        import dcor
+        dcor._lib.apply_variant_args(a.variant)
     if "C3" in which:
         eps = [tuple(float(v) for v in e.split("x")) for e in a.c3_eps.split(",")] if a.c3_eps else None
         cells = c3_cells(eps)
         dist_grid("C3", [(cells, a.c3_reps)], world, rank, a.dry_run, cells=len(cells), reps_per_cell=a.c3_reps,
                   eps_pairs=eps or C3_EPS)
+    if "C5" in which:
+        dist_c5(world, rank, a.dry_run, a.c5_R)
+    if "C5e" in which:
+        dist_hrs("C5-e2e", world, rank, a.dry_run, a.c5e_R, "premat")
+    if "C5f" in which:
+        dist_hrs("C5-fused", world, rank, a.dry_run, a.c5e_R, "fused")
+    if "C5fc" in which:
+        dist_hrs("C5-fused-continuous", world, rank, a.dry_run, a.c5e_R, "fused", panel="continuous")
+    if "HS" in which:
+        dist_hrs("HS", world, rank, a.dry_run, a.hs_R, "premat", sweep=True)
     if "C4" in which:
         ok, small, big, nskip = c4_cells()
         dist_grid("C4", [(small, a.c4_B), (big, a.c4_B_big)], world, rank, a.dry_run, cells=len(ok),
                   cells_skipped_k_lt_1=nskip, reps_per_cell=a.c4_B, reps_per_cell_n1e6=a.c4_B_big,
                   cells_n1e6=len(big))
-    others = [w for w in which if w not in ("C3", "C4")]
+    others = [w for w in which if w not in ("C3", "C4", "C5", "C5e", "C5f", "C5fc", "HS")]
     if others and rank == 0:
         print(json.dumps({"skipped": others, "reason": "single-GPU configs: run without --gpus"}), flush=True)
     dist.destroy_process_group()
@@ -541,16 +665,19 @@ def main_dist(a, world, rank, local):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--only", default="C1,C2,C3,C4,VG,SG,C5,C5c,C5e,C5f,C5fc,S,R1,RG,RH")
+    ap.add_argument("--only", default="C1,C2,C3,C4,VG,SG,C5,C5c,C5e,C5f,C5fc,HS,S,R1,RG,RH")
     ap.add_argument("--c3-reps", type=int, default=100_000)
     ap.add_argument("--c3-eps", default=None, help="subset of C3's eps pairs, e.g. 0.5x0.5,1.5x0.5")
     ap.add_argument("--c4-B", type=int, default=1000)
     ap.add_argument("--c4-B-big", type=int, default=100_000)
     ap.add_argument("--c5-R", type=int, default=8192)
     ap.add_argument("--c5e-R", type=int, default=1_000_000)
+    ap.add_argument("--hs-R", type=int, default=200, help="runs per eps of the HRS sweep (real-data-sims.R: R = 200)")
     ap.add_argument("--gpus", type=int, default=None,
-                    help="C3 / C4 over N ranks (one per GPU); without a launcher's WORLD_SIZE, N rank processes "
+                    help="C3, C4, C5, C5e, C5f, C5fc, HS over N ranks (one per GPU); without a launcher's WORLD_SIZE, N rank processes "
                          "are started")
+    ap.add_argument("--variant", action="append", default=[], metavar="NAME=VALUE",
+                    help="engine implementation switch for A/B runs (dcor_set_variant; repeatable)")
     ap.add_argument("--dry-run", action="store_true",
                     help="with --gpus: form the group over gloo on the CPU and print the shard plan, no GPU")
     a = ap.parse_args()
@@ -566,6 +693,8 @@ def main():
         return main_dist(a, int(env_world), int(os.environ.get("RANK", "0")), int(os.environ.get("LOCAL_RANK", "0")))
     import torch
     torch.cuda.set_device(0)
+    import dcor
+    dcor._lib.apply_variant_args(a.variant)
     which = a.only.split(",")
     if "C1" in which: c1()
     if "C2" in which: c2()
@@ -583,6 +712,7 @@ def main():
     if "C5e" in which: c5_e2e(a.c5e_R)
     if "C5f" in which: c5_fused(a.c5e_R)
     if "C5fc" in which: c5_fused(a.c5e_R, panel="continuous")
+    if "HS" in which: hrs_sweep(a.hs_R)
     if "S" in which: subg()
     if "R1" in which: rstream_c1()
     if "RG" in which: rstream_grid()

@@ -16,6 +16,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <string>
 #include <utility>
 #include <vector>
 
@@ -519,7 +520,7 @@ int prepare_cell(const dcor_cell& c, CellPlan& p) {
   if (int st = make_dgp(c, g)) return st;
   p.dgp = c.dgp;
   p.nan_dgp = g.nan_dgp != 0;
-  const char* var = std::getenv("DCOR_SIGN_KERNEL");
+  const char* var = dcor::variant("DCOR_SIGN_KERNEL");
   const bool force_regen = var && std::strcmp(var, "regen") == 0;
   if (c.family == DCOR_FAMILY_SIGN) {
     SignConst& k = p.sign;
@@ -540,7 +541,7 @@ int prepare_cell(const dcor_cell& c, CellPlan& p) {
       // round-3 window, 2 sd of the sample around mu.
       const double sx = std::sqrt(g.a00 * g.a00 + g.a01 * g.a01);
       const double sy = std::sqrt(g.a10 * g.a10 + g.a11 * g.a11);
-      const char* wv = std::getenv("DCOR_CODE_WINDOW");
+      const char* wv = dcor::variant("DCOR_CODE_WINDOW");
       if (wv && std::strcmp(wv, "wide") == 0) {
         cx = r_min(r_max(c.mu[0], -k.L), k.L); cy = r_min(r_max(c.mu[1], -k.L), k.L);
         rx = 2.0 * sx;
@@ -593,6 +594,57 @@ int prepare_cell(const dcor_cell& c, CellPlan& p) {
 }
 
 }  // namespace host
+
+// ------------------------------------------------------------------ implementation switches
+// The A/B and test switches of the kernels and launchers, set only through dcor_set_variant.
+// Each one selects a kernel variant, a launch plan or a test hook; none is read from the
+// environment, so a stray variable in a user's shell cannot move a replicate's bits.
+namespace {
+const char* const kVariantNames[] = {
+    "DCOR_SIGN_KERNEL",      // "regen": the regenerate-everything sign kernel
+    "DCOR_CODE_WINDOW",      // "wide" or "a,b": the sign records' code window
+    "DCOR_SIGN_PIPELINE",    // "0": sign chunks on one stream
+    "DCOR_SIGN_XCALL",       // "0": no overlap of back-to-back sign calls
+    "DCOR_SIGN_P2E",         // "0": small cells' pass 2 and epilogue as two kernels
+    "DCOR_EPILOGUE",         // "block" (sign) / "wave" (premat): epilogue kernel form
+    "DCOR_HRS_FUSED_L2",     // "1": a coded panel through the uncoded fused HRS kernel
+    "DCOR_HRS_WPE",          // "4": fused HRS kernel at 4 waves per SIMD
+    "DCOR_PREMAT_PIPELINE",  // "1": two-stream premat halves
+    "DCOR_DICT_VARIANT",     // 0-3: coded-panel kernel shape
+    "DCOR_L2_VARIANT",       // 0-3: L2-gather kernel shape
+    "DCOR_TILED",            // "0": no tiled kernel (L2 gathers)
+    "DCOR_TILED_VARIANT",    // 0/1: 512- or 1024-thread tiled kernel
+    "DCOR_TILED_INT",        // 0/1/2: where the tiled path's INT sums run
+    "DCOR_GRID_CHUNK_ITEMS", // grid planner caps (memory-bound tests)
+    "DCOR_GRID_SLAB_MB",
+    "DCOR_GRID_MIN_CHUNKS",
+    "DCOR_GRID_REC_MB",
+    "DCOR_RS_JUMP",          // R-stream: 0 never / 1 always the jump path
+    "DCOR_RS_BUDGET_MB",
+    "DCOR_RS_MAX_CHUNK",     // test hook: short R-stream chunks
+    "DCOR_RSJ_TIGHT",        // test hook: a jump budget every mixquant chunk overruns
+};
+constexpr int kNVariants = (int)(sizeof(kVariantNames) / sizeof(kVariantNames[0]));
+std::mutex g_var_mu;
+std::string g_var_val[kNVariants];
+bool g_var_set[kNVariants] = {};
+
+int variant_index(const char* name) {
+  for (int i = 0; i < kNVariants; ++i)
+    if (std::strcmp(name, kVariantNames[i]) == 0) return i;
+  return -1;
+}
+}  // namespace
+
+const char* variant(const char* name) {
+  const int i = variant_index(name);
+  if (i < 0) return nullptr;
+  thread_local std::string copy[kNVariants];
+  std::lock_guard<std::mutex> lk(g_var_mu);
+  if (!g_var_set[i]) return nullptr;
+  copy[i] = g_var_val[i];
+  return copy[i].c_str();
+}
 }  // namespace dcor
 
 using namespace dcor::host;
@@ -601,6 +653,32 @@ using namespace dcor::host;
 extern "C" {
 
 const char* dcor_version(void) { return "dcor-mi355x 0.1.0 (gfx950)"; }
+
+int dcor_set_variant(const char* name, const char* value) {
+  std::lock_guard<std::mutex> lk(dcor::g_var_mu);
+  if (name == nullptr) {
+    for (int i = 0; i < dcor::kNVariants; ++i) { dcor::g_var_set[i] = false; dcor::g_var_val[i].clear(); }
+    return DCOR_OK;
+  }
+  const int i = dcor::variant_index(name);
+  if (i < 0) return fail(DCOR_EINVAL, "unknown implementation switch %s", name);
+  dcor::g_var_set[i] = value != nullptr;
+  dcor::g_var_val[i] = value ? value : "";
+  return DCOR_OK;
+}
+
+int dcor_get_variant(const char* name, char* buf, size_t len) {
+  if (name == nullptr || dcor::variant_index(name) < 0) {
+    fail(DCOR_EINVAL, "unknown implementation switch %s", name ? name : "(null)");
+    return -1;
+  }
+  const char* v = dcor::variant(name);
+  if (buf && len) {
+    std::strncpy(buf, v ? v : "", len - 1);
+    buf[len - 1] = 0;
+  }
+  return v != nullptr;
+}
 
 int dcor_last_error(char* buf, size_t len) {
   if (buf && len) {
@@ -769,7 +847,7 @@ int dcor_sim_launch(const dcor_cell* cell, int64_t rep_begin, int64_t rep_count,
       }
       bf.lib[0] = bf.lib[1] = bf.ev_entry = bf.ev_end[0] = bf.ev_end[1] = nullptr;
       bf.cross = false;
-      const char* pv = std::getenv("DCOR_SIGN_PIPELINE");
+      const char* pv = dcor::variant("DCOR_SIGN_PIPELINE");
       Pipe* pp = nullptr;
       if (int st = pipe_get(&pp)) return st;
       if (nbuf == 2 && !(pv && std::strcmp(pv, "0") == 0)) {
@@ -780,7 +858,7 @@ int dcor_sim_launch(const dcor_cell* cell, int64_t rep_begin, int64_t rep_count,
         // caller's stream)
         const uint64_t sig = ((uint64_t)(uintptr_t)scratch * 1000003u) ^ ((uint64_t)slab_b * 31u) ^
                              ((uint64_t)sums_b << 1) ^ 1u;
-        const char* xv = std::getenv("DCOR_SIGN_XCALL");
+        const char* xv = dcor::variant("DCOR_SIGN_XCALL");
         bf.cross = sig == prev_sig && !(xv && std::strcmp(xv, "0") == 0);
         pp->sig = sig;
       } else {
@@ -1086,8 +1164,8 @@ int dcor_hrs_fused_launch(const dcor_premat_subg* d, const dcor_panel* panel, ui
   if (int st = premat_subg_const(d, p)) return st;
   // DCOR_HRS_FUSED_L2=1 runs a coded panel through the uncoded kernel (A/B and the tests'
   // bit-identity check of the two kernels)
-  static const bool force_l2 = [] {
-    const char* e = std::getenv("DCOR_HRS_FUSED_L2");
+  const bool force_l2 = [] {
+    const char* e = dcor::variant("DCOR_HRS_FUSED_L2");
     return e && std::strcmp(e, "1") == 0;
   }();
   const bool coded = panel->coded && !force_l2;
@@ -1170,7 +1248,7 @@ static int premat_subg_run(const dcor_premat_subg* d, const dcor_panel* panel, d
     p.dict_built = 2;  // built and known coded: no L2-gather launch
   }
   int rc = 0;
-  const char* pv = std::getenv("DCOR_PREMAT_PIPELINE");
+  const char* pv = dcor::variant("DCOR_PREMAT_PIPELINE");
   if (panel != nullptr && panel->coded && p.perm && d->reps >= 4096 && pv && std::strcmp(pv, "1") == 0) {
     // DCOR_PREMAT_PIPELINE=1: two replicate halves, the first half's mixquant epilogue on the
     // auxiliary stream beside the second half's streaming kernel.  Off by default: the
@@ -1198,7 +1276,7 @@ static int premat_subg_run(const dcor_premat_subg* d, const dcor_panel* panel, d
   } else {
     // the tiled path's INT kernel may run on the auxiliary stream (DCOR_TILED_INT=2)
     Pipe* pp = nullptr;
-    const char* iv = std::getenv("DCOR_TILED_INT");
+    const char* iv = dcor::variant("DCOR_TILED_INT");
     if (iv && std::strcmp(iv, "2") == 0 && pipe_get(&pp) != 0) pp = nullptr;
     rc = launch_premat_subg(p, d->reps, part, d_out, stream, nullptr, nullptr, pp ? pp->s : nullptr,
                             pp ? pp->fork : nullptr, pp ? pp->join : nullptr);
@@ -1643,7 +1721,7 @@ int rs_plan(const dcor_cell& cell, RsPlan& p) {
   p.rep_max = pre + shuffle_words + (c.has_mix ? 18 * c.nsim : 0);
   c.jpost = c.has_mix ? c.nsim : 0;
   p.jrep = pre + (c.has_mix ? c.nsim + 2 * c.nsim + 64 + 8 * (int64_t)std::ceil(std::sqrt((double)c.nsim)) : 0);
-  if (std::getenv("DCOR_RSJ_TIGHT"))   // test hook: a budget every mixquant chunk overruns
+  if (dcor::variant("DCOR_RSJ_TIGHT"))   // test hook: a budget every mixquant chunk overruns
     p.jrep = pre + (c.has_mix ? c.nsim + c.nsim : 0);
   p.rep_max = std::max(p.rep_max, p.jrep);
   const int64_t fw = (n + 31) / 32;
@@ -1739,13 +1817,13 @@ size_t rsj_cell_bytes(const RsPlan& p) {
 bool rsj_use(const std::vector<RsPlan>& plan, int i0, int nb) {
   for (int i = 0; i < nb; ++i)
     if (plan[(size_t)(i0 + i)].c.shuffle) return false;
-  const char* e = std::getenv("DCOR_RS_JUMP");
+  const char* e = dcor::variant("DCOR_RS_JUMP");
   if (e && *e) return std::atoi(e) != 0;
   return nb <= 64;
 }
 
 size_t rs_budget() {
-  const char* e = std::getenv("DCOR_RS_BUDGET_MB");
+  const char* e = dcor::variant("DCOR_RS_BUDGET_MB");
   const long mb = e ? std::atol(e) : 4096;
   return (size_t)(mb > 16 ? mb : 16) << 20;
 }
@@ -1776,7 +1854,7 @@ int dcor_rstream_grid_run(const dcor_cell* cells, int ncells, int64_t B, dcor_ac
     }
     int64_t rc = (int64_t)(budget / std::max<size_t>(sum, 1));
     rc = std::max<int64_t>(1, std::min<int64_t>({rc, B, (int64_t)(0x7fffffff / nb)}));
-    if (const char* e = std::getenv("DCOR_RS_MAX_CHUNK"))   // test hook: force short chunks
+    if (const char* e = dcor::variant("DCOR_RS_MAX_CHUNK"))   // test hook: force short chunks
       rc = std::max<int64_t>(1, std::min<int64_t>(rc, std::atol(e)));
     bool jump = rsj_use(plan, i0, nb);
     size_t bytes = 0, jbytes = 0;

@@ -11,6 +11,10 @@
 
 namespace dcor {
 
+// The current value of an implementation switch set by dcor_set_variant (dcor_capi.cpp), or
+// nullptr when it is at its default.  Never the environment: see include/dcor.h.
+const char* variant(const char* name);
+
 struct DgpConst {
   int32_t dgp;
   int32_t nan_dgp;                      // gen_bounded_factor with rho outside [0, 1]: sqrt(3 rho)

@@ -1446,8 +1446,8 @@ __global__ __launch_bounds__(DCOR_BLOCK) void k_sign_epilogue(SignConst c,
 
 static inline void launch_sign_epilogue(const SignConst& c, int64_t nr, const SignPartial* part,
                                         dcor_rep_out* out, hipStream_t st) {
-  static const int block_epi = [] {
-    const char* v = std::getenv("DCOR_EPILOGUE");
+  const int block_epi = [] {
+    const char* v = dcor::variant("DCOR_EPILOGUE");
     return v && std::strcmp(v, "block") == 0;
   }();
   const unsigned gw = (unsigned)((nr + DCOR_WAVES - 1) / DCOR_WAVES);
@@ -2160,8 +2160,8 @@ static inline unsigned persistent_groups(int64_t nitems) {
 // replicates/s with the two kernels, r03c), or DCOR_SIGN_P2E=0 for the pass-2 wave kernel + the
 // wave epilogue kernel.
 static bool p2e_fused() {
-  static const bool v = [] {
-    const char* e = std::getenv("DCOR_SIGN_P2E");
+  const bool v = [] {
+    const char* e = dcor::variant("DCOR_SIGN_P2E");
     return !(e && std::strcmp(e, "0") == 0);
   }();
   return v;

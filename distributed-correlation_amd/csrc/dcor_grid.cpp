@@ -42,7 +42,7 @@ namespace {
 size_t al256(size_t b) { return (b + 255) & ~(size_t)255; }
 
 size_t env_size(const char* name, size_t dflt, int shift) {
-  const char* e = std::getenv(name);
+  const char* e = dcor::variant(name);
   const long long v = e ? std::atoll(e) : 0;
   return v > 0 ? (size_t)v << shift : dflt;
 }
@@ -221,8 +221,8 @@ int exec_ranges(const dcor_cell* cells, const std::vector<CellPlan>& cp, const s
   const size_t extra_off = tb;
   tb += al256(extra_b);
   tb = std::max<size_t>(tb, 256);
-  const bool two = ncodes_chunks > 1 && !(std::getenv("DCOR_SIGN_PIPELINE") &&
-                                         std::strcmp(std::getenv("DCOR_SIGN_PIPELINE"), "0") == 0);
+  const bool two = ncodes_chunks > 1 && !(dcor::variant("DCOR_SIGN_PIPELINE") &&
+                                         std::strcmp(dcor::variant("DCOR_SIGN_PIPELINE"), "0") == 0);
   const int nslot = two ? 2 : 1;
   const size_t sums_one = al256(std::max<size_t>(max_sums_b, 8));
   const size_t items_off = al256(tb), sums_off = items_off + al256(std::max<uint64_t>(tot_items, 1) * sizeof(GridItem));

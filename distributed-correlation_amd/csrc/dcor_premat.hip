@@ -1821,8 +1821,8 @@ int launch_hrs_fused(const PrematSubgConst& c, uint64_t seed_ni, uint64_t seed_i
   int bits = 1;
   while ((1ll << bits) < c.s.n) ++bits;
   hk.pa = bits / 2; hk.pc = bits - hk.pa;
-  static const int wsel = [] {
-    const char* e = std::getenv("DCOR_HRS_WPE");
+  const int wsel = [] {
+    const char* e = dcor::variant("DCOR_HRS_WPE");
     return (e && std::atoi(e) == 4) ? 4 : 6;
   }();
   const bool l2 = c.xyc != nullptr;  // uncoded panel: packed clips in HBM, indices in LDS
@@ -1898,8 +1898,8 @@ typedef void (*DictKernel)(PrematSubgConst, const uint16_t*, const double*, cons
 static DictKernel dict_kernel() {
   static const DictKernel ks[4] = {k_premat_subg_dict<4, 4, false>, k_premat_subg_dict<4, 6, false>,
                                    k_premat_subg_dict<8, 4, false>, k_premat_subg_dict<6, 6, false>};
-  static const int v = [] {
-    const char* e = std::getenv("DCOR_DICT_VARIANT");
+  const int v = [] {
+    const char* e = dcor::variant("DCOR_DICT_VARIANT");
     const int x = e ? std::atoi(e) : 0;
     return (x >= 0 && x < 4) ? x : 0;
   }();
@@ -1911,8 +1911,8 @@ static DictKernel dict_kernel() {
 static DictKernel l2_kernel() {
   static const DictKernel ks[4] = {k_premat_subg_dict<4, 8, true>, k_premat_subg_dict<4, 4, true>,
                                    k_premat_subg_dict<8, 8, true>, k_premat_subg_dict<8, 4, true>};
-  static const int v = [] {
-    const char* e = std::getenv("DCOR_L2_VARIANT");
+  const int v = [] {
+    const char* e = dcor::variant("DCOR_L2_VARIANT");
     const int x = e ? std::atoi(e) : 0;
     return (x >= 0 && x < 4) ? x : 0;
   }();
@@ -1946,8 +1946,8 @@ struct TiledKernel {
 // tile fills; 1 (default) in k_premat_subg_int before it on the same stream; 2 in
 // k_premat_subg_int on the library's auxiliary stream beside it.
 static int tiled_int_mode() {
-  static const int m = [] {
-    const char* e = std::getenv("DCOR_TILED_INT");
+  const int m = [] {
+    const char* e = dcor::variant("DCOR_TILED_INT");
     const int x = e ? std::atoi(e) : 1;
     return (x >= 0 && x <= 2) ? x : 1;
   }();
@@ -1966,16 +1966,16 @@ static TiledKernel tiled_kernel(bool intk, bool al) {
         {k_premat_subg_tiled<1024, 5, 1, 1, 1, 4, true, true, true>, 1024, 160 * 1024}},
        {{k_premat_subg_tiled<1024, 5, 1, 1, 1, 4, true, false, false>, 1024, 160 * 1024},
         {k_premat_subg_tiled<1024, 5, 1, 1, 1, 4, true, false, true>, 1024, 160 * 1024}}}};
-  static const int v = [] {
-    const char* e = std::getenv("DCOR_TILED_VARIANT");
+  const int v = [] {
+    const char* e = dcor::variant("DCOR_TILED_VARIANT");
     const int x = e ? std::atoi(e) : 1;
     return (x >= 0 && x < 2) ? x : 1;
   }();
   return ks[v][intk ? 0 : 1][al ? 1 : 0];
 }
 static bool tiled_enabled() {
-  static const bool on = [] {
-    const char* e = std::getenv("DCOR_TILED");
+  const bool on = [] {
+    const char* e = dcor::variant("DCOR_TILED");
     return !(e && std::strcmp(e, "0") == 0);
   }();
   return on;
@@ -2095,8 +2095,8 @@ int launch_premat_subg(const PrematSubgConst& c0, int64_t reps, void* part, dcor
   }
   // workgroup-per-replicate epilogue: measured faster here than the wave-per-replicate form
   // (k_premat_subg_epilogue_w: 2000 loaded keys per wave cost 200+ VGPRs, one wave per SIMD)
-  static const int wave_epi = [] {
-    const char* v = std::getenv("DCOR_EPILOGUE");
+  const int wave_epi = [] {
+    const char* v = dcor::variant("DCOR_EPILOGUE");
     return v && std::strcmp(v, "wave") == 0;
   }();
   const unsigned gw = (unsigned)((reps + DCOR_WAVES - 1) / DCOR_WAVES);

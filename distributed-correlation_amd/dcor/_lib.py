@@ -103,9 +103,12 @@ class RsDraws(C.Structure):
 # by tests/test_abi.py).
 SIGNATURES = {
     "dcor_version": (C.c_char_p, []),
+    "dcor_source_hash": (C.c_char_p, []),
     "dcor_last_error": (C.c_int, [C.c_char_p, C.c_size_t]),
     "dcor_device_count": (C.c_int, []),
     "dcor_shutdown": (C.c_int, []),
+    "dcor_set_variant": (C.c_int, [C.c_char_p, C.c_char_p]),
+    "dcor_get_variant": (C.c_int, [C.c_char_p, C.c_char_p, C.c_size_t]),
     "dcor_alloc_count": (C.c_int64, []),
     "dcor_device_bytes": (C.c_int64, []),
     "dcor_sim_chunking": (C.c_int, [C.POINTER(Cell), C.c_int64, _I64, _I64]),
@@ -225,3 +228,44 @@ def mode_code(mode) -> int:
 
 def nan_if_none(x) -> float:
     return math.nan if x is None else float(x)
+
+
+def set_variant(name, value) -> None:
+    """An implementation switch (dcor_set_variant): A/B scripts and tests only.  value None
+    restores the default; name None restores every default."""
+    check(lib.dcor_set_variant(None if name is None else name.encode(),
+                               None if value is None else str(value).encode()))
+
+
+def get_variant(name: str):
+    buf = C.create_string_buffer(256)
+    r = lib.dcor_get_variant(name.encode(), buf, 256)
+    if r < 0:
+        raise DcorError(DCOR_EINVAL, last_error())
+    return buf.value.decode() if r == 1 else None
+
+
+class variants:
+    """with dcor.variants(DCOR_TILED="0", ...): switches set for the block, restored after."""
+
+    def __init__(self, **kv):
+        self.kv = kv
+        self.old = {}
+
+    def __enter__(self):
+        for k, v in self.kv.items():
+            self.old[k] = get_variant(k)
+            set_variant(k, v)
+        return self
+
+    def __exit__(self, *exc):
+        for k, v in self.old.items():
+            set_variant(k, v)
+        return False
+
+
+def apply_variant_args(items) -> None:
+    """bench scripts' --variant NAME=VALUE arguments."""
+    for it in items or ():
+        k, _, v = it.partition("=")
+        set_variant(k, v)

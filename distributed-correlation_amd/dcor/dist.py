@@ -124,3 +124,80 @@ def run_grid_rstream_distributed(cells, B: int, group=None):
             local[2 * i], local[2 * i + 1] = r["accum"]
     merged = merge_ranked(gather_accums(local, group))
     return [(merged[2 * i], merged[2 * i + 1]) for i in range(len(cells))]
+
+
+# ------------------------------------------------- HRS replicates and eps sweep (a19 / C5)
+def gather_rows(local: np.ndarray, counts: List[int], group=None) -> np.ndarray:
+    """All-gather every rank's [count_r, w] float64 rows -> the [sum(counts), w] array in rank
+    order, identical on all ranks.  Shards differ in size by at most one row, so each rank pads
+    to the largest (one all_gather of equal tensors; RCCL from device memory under 'nccl')."""
+    import torch
+    import torch.distributed as dist
+
+    rank, world = dist.get_rank(group), dist.get_world_size(group)
+    w = local.shape[1] if local.ndim == 2 else 6
+    mx = max(counts) if counts else 0
+    buf = np.zeros((mx, w), dtype=np.float64)
+    buf[:counts[rank]] = local.reshape(counts[rank], w)
+    t = torch.from_numpy(buf)
+    if dist.get_backend(group) == "nccl":
+        t = t.cuda()
+    outs = [torch.empty_like(t) for _ in range(world)]
+    dist.all_gather(outs, t, group=group)
+    return np.concatenate([o.cpu().numpy()[:c] for o, c in zip(outs, counts)]) if counts else buf
+
+
+def run_hrs_distributed(age_z, bmi_z, lam_age, lam_bmi, eps, reps, group=None, rep_begin=0, **kw):
+    """The HRS replicates of one eps (real-data-sims.R:411-436; BASELINE C5's 1e6 replicates) over
+    G ranks: rank g runs the contiguous replicate range shard(reps, g, G) with dcor.hrs.hrs_replicates
+    (any rng / mode), and the records are all-gathered in rank order.  A replicate's numbers depend
+    only on (seeds, replicate index) -- Philox counters, or the reference's per-run set.seed in
+    rng='R' -- so the [reps, 6] result, identical on all ranks, equals one process's
+    hrs_replicates(..., reps, rep_begin) byte for byte."""
+    import torch.distributed as dist
+
+    from .hrs import hrs_replicates
+    rank, world = dist.get_rank(group), dist.get_world_size(group)
+    b0, nb = shard(reps, rank, world)
+    local = (hrs_replicates(age_z, bmi_z, lam_age, lam_bmi, eps, nb, rep_begin=rep_begin + b0, **kw)
+             if nb > 0 else np.zeros((0, 6)))
+    return gather_rows(local, [shard(reps, r, world)[1] for r in range(world)], group)
+
+
+def sweep_shard(n_eps: int, reps: int, rank: int, world: int):
+    """Rank `rank`'s part of an eps sweep of n_eps x reps runs: the contiguous range of the flattened
+    (eps index, run) space, as (eps index 0-based, first run, count) segments.  At the reference's
+    23 x 200 runs each rank gets whole launches of several hundred runs instead of reps / G per eps."""
+    b0, nb = shard(n_eps * reps, rank, world)
+    segs, i = [], b0
+    while i < b0 + nb:
+        e, r = divmod(i, reps)
+        c = min(reps - r, b0 + nb - i)
+        segs.append((e, r, c))
+        i += c
+    return segs
+
+
+def eps_sweep_distributed(age_z, bmi_z, lam_age, lam_bmi, eps_grid=None, reps=None, nsim=2000, rng="philox",
+                          group=None):
+    """dcor.hrs.eps_sweep (real-data-sims.R:345-448) over G ranks: the flattened (eps, run) space
+    is split into contiguous per-rank ranges (sweep_shard); each segment is one hrs_replicates call
+    with the sweep's per-eps keys (Philox 10 + 1000 idx / 20 + 1000 idx, or the reference's per-run
+    set.seed in rng='R'); the records are all-gathered in rank order and the per-eps summaries built
+    from them on every rank.  Equal to the single-process eps_sweep: runs byte for byte, summaries
+    identical."""
+    import torch.distributed as dist
+
+    from . import hrs
+    eps_grid = hrs.EPS_GRID if eps_grid is None else eps_grid
+    reps = hrs.R_PER_EPS if reps is None else reps
+    rank, world = dist.get_rank(group), dist.get_world_size(group)
+    parts = []
+    for e, r0, c in sweep_shard(len(eps_grid), reps, rank, world):
+        idx = e + 1
+        parts.append(hrs.hrs_replicates(age_z, bmi_z, lam_age, lam_bmi, eps_grid[e], c, seed_ni=10 + 1000 * idx,
+                                        seed_int=20 + 1000 * idx, nsim=nsim, rng=rng, eps_idx=idx, rep_begin=r0))
+    local = np.concatenate(parts) if parts else np.zeros((0, 6))
+    counts = [shard(len(eps_grid) * reps, r, world)[1] for r in range(world)]
+    runs = gather_rows(local, counts, group).reshape(len(eps_grid), reps, 6)
+    return hrs.sweep_summaries(eps_grid, runs)

@@ -198,11 +198,15 @@ def eps_sweep(age_z, bmi_z, lam_age, lam_bmi, eps_grid=EPS_GRID, reps=R_PER_EPS,
     `reps` NI and INT runs (Philox keys 10 + 1000 idx and 20 + 1000 idx, idx 1-based as
     which(eps_grid == eps); rng='R': the reference's own per-run set.seed streams) and the
     per-eps summaries ni_mean / int_mean."""
-    runs, ni_mean, int_mean = [], [], []
-    for idx, eps in enumerate(eps_grid, start=1):
-        res = hrs_replicates(age_z, bmi_z, lam_age, lam_bmi, eps, reps, seed_ni=10 + 1000 * idx,
-                             seed_int=20 + 1000 * idx, nsim=nsim, rng=rng, eps_idx=idx)
-        runs.append(res)
-        ni_mean.append(_summ("NI", eps, res[:, 0], res[:, 1], res[:, 2]))
-        int_mean.append(_summ("INT", eps, res[:, 3], res[:, 4], res[:, 5]))
-    return {"eps": list(eps_grid), "runs": np.stack(runs), "ni_mean": ni_mean, "int_mean": int_mean}
+    runs = [hrs_replicates(age_z, bmi_z, lam_age, lam_bmi, eps, reps, seed_ni=10 + 1000 * idx,
+                           seed_int=20 + 1000 * idx, nsim=nsim, rng=rng, eps_idx=idx)
+            for idx, eps in enumerate(eps_grid, start=1)]
+    return sweep_summaries(eps_grid, np.stack(runs))
+
+
+def sweep_summaries(eps_grid, runs) -> dict:
+    """The sweep's per-eps summaries from its runs [n_eps, reps, 6] (real-data-sims.R:408-437);
+    dcor.dist.eps_sweep_distributed builds the same from the ranks' gathered runs."""
+    ni_mean = [_summ("NI", eps, r[:, 0], r[:, 1], r[:, 2]) for eps, r in zip(eps_grid, runs)]
+    int_mean = [_summ("INT", eps, r[:, 3], r[:, 4], r[:, 5]) for eps, r in zip(eps_grid, runs)]
+    return {"eps": list(eps_grid), "runs": runs, "ni_mean": ni_mean, "int_mean": int_mean}

@@ -95,6 +95,9 @@ typedef struct dcor_summary {
 
 /* ------------------------------------------------------------------------ */
 const char* dcor_version(void);
+/* sha256 (hex) of the engine sources this library was built from (csrc/ + include/dcor.h), stamped
+ * by the build (__graft_entry__.build_engine), which rebuilds whenever it differs from the tree's. */
+const char* dcor_source_hash(void);
 int dcor_last_error(char* buf, size_t len);
 /* Number of visible HIP devices (0 on a host without GPU; never fails). */
 int dcor_device_count(void);
@@ -105,6 +108,16 @@ int dcor_device_count(void);
  * caller.  Call when no work is in flight.  In a process forked after its parent used the engine
  * it makes no HIP call and returns DCOR_EFORK. */
 int dcor_shutdown(void);
+/* Implementation switches for A/B runs and tests (no reference counterpart).  The library reads
+ * no environment variable: a replicate's bits are a function of (cell, seed, replicate) alone
+ * (vert-cor.R:364's per-cell set.seed contract), and the defaults of every switch are a function of
+ * the cell geometry.  `name` is one of the switches DESIGN.md lists ("DCOR_TILED",
+ * "DCOR_CODE_WINDOW", ...); value NULL restores its default; name NULL restores every default.
+ * Returns DCOR_EINVAL for an unknown name.  Process-wide; set it when no work is in flight.
+ * dcor_get_variant copies the current value (empty when unset) into buf and returns 1 if set, 0 if
+ * not, -1 for an unknown name. */
+int dcor_set_variant(const char* name, const char* value);
+int dcor_get_variant(const char* name, char* buf, size_t len);
 /* Device and pinned-host allocations the library has made so far (its scratch arenas, staging
  * buffers, panels and the host-pointer entries' transfer buffers): a repeated call of the same
  * shape on warm contexts adds none. */

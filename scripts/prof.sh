@@ -2,7 +2,7 @@
 # guide prescribes), then profiles/<tag>_summary.{json,md} + <tag>_kernel_stats.csv.
 #   bash scripts/prof.sh <tag> <passes> -- <python args...>
 # passes: comma list of trace, fetch, write, sq, mix, tcp, lds (default trace,fetch,write,sq,mix)
-# env: SERIAL=1 runs the sign path's chunks on one stream (DCOR_SIGN_PIPELINE=0: clean per-kernel
+# env: SERIAL=1 runs the sign path's chunks on one stream (--variant DCOR_SIGN_PIPELINE=0: clean per-kernel
 #      counters); PROF_HEAD=<git head> is stamped into the summary (the GPU box has no .git).
 # Example: bash scripts/prof.sh r04_serial trace,sq,mix -- bench.py --steps 5 --warmup 1 --no-cpu-baseline
 set -o pipefail
@@ -11,16 +11,17 @@ TAG=$1; PASSES=${2:-trace,fetch,write,sq,mix}; shift 2
 [ "$1" = "--" ] && shift
 O=gpurun_out/prof_$TAG
 rm -rf $O; mkdir -p $O
-[ "${SERIAL:-0}" = 1 ] && export DCOR_SIGN_PIPELINE=0
+EXTRA=()
+[ "${SERIAL:-0}" = 1 ] && EXTRA=(--variant DCOR_SIGN_PIPELINE=0)
 export PROF_CMD="SERIAL=${SERIAL:-0} bash scripts/prof.sh $TAG $PASSES -- $*"
 pmc() {  # one PMC pass: name, counters...
   local n=$1; shift
   timeout -s KILL 240 rocprofv3 --pmc "$@" --output-format csv -d $O/prof_$n -o run -- python3 "${ARGS[@]}" > $O/prof_$n.log 2>&1
 }
-ARGS=("$@")
+ARGS=("$@" "${EXTRA[@]}")
 for p in ${PASSES//,/ }; do
   case $p in
-    trace) timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_trace -o run -- python3 "$@" > $O/prof_trace.log 2>&1 ;;
+    trace) timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_trace -o run -- python3 "${ARGS[@]}" > $O/prof_trace.log 2>&1 ;;
     fetch) pmc fetch FETCH_SIZE ;;
     write) pmc write WRITE_SIZE ;;
     sq) pmc sq SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY SQ_WAIT_ANY GRBM_GUI_ACTIVE ;;

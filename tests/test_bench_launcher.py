@@ -93,6 +93,23 @@ def test_configs_gpus_2_forms_two_ranks_for_c3_c4():
     assert c4["world_formed"] == 2 and c4["shards"][1] == [[0, 50_000], [50_000, 50_000]]
 
 
+def test_configs_gpus_2_forms_two_ranks_for_hrs():
+    """The HRS workload shards too: C5 weak (each rank its own 8192-replicate
+    range), C5-e2e / C5-fused over contiguous ranges of 1e6 replicates, the eps sweep over the
+    flattened (eps, run) space (real-data-sims.R:411-436)."""
+    p = _run_configs(["--gpus", "2", "--dry-run", "--only", "C5,C5e,C5f,C5fc,HS"])
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = {d["config"]: d for d in (json.loads(ln) for ln in p.stdout.splitlines() if ln.startswith("{"))}
+    assert set(lines) == {"C5", "C5-e2e", "C5-fused", "C5-fused-continuous", "HS"}
+    assert all(d["world_formed"] == 2 for d in lines.values())
+    assert lines["C5"]["shards"] == [[0, 8192], [8192, 8192]]
+    assert lines["C5-e2e"]["shards"] == [[0, 500_000], [500_000, 500_000]]
+    hs = lines["HS"]
+    assert hs["replicates"] == 23 * 200
+    assert sum(c for segs in hs["shards"] for _, _, c in segs) == 4600
+    assert hs["shards"][1][0] == [11, 100, 100]
+
+
 def test_configs_more_gpus_than_visible_is_refused():
     p = _run_configs(["--gpus", "2", "--only", "C3"], env={"HIP_VISIBLE_DEVICES": ""})
     assert p.returncode != 0

@@ -130,3 +130,48 @@ def test_rstream_cell_shard_gather_two_ranks():
     for i in range(5):
         for m in range(2):
             assert res[0][2 * i + m] == (100 + 10 * i + m, 0.125 * (i + 1) + m, 1e-20 * (i + 1))
+
+
+def test_sweep_shard_covers_flattened_space():
+    from dcor.dist import shard, sweep_shard
+    for n_eps, reps in ((23, 200), (3, 7), (1, 1), (5, 1)):
+        for world in (1, 2, 3, 8, 13):
+            seen = []
+            for r in range(world):
+                segs = sweep_shard(n_eps, reps, r, world)
+                assert sum(c for _, _, c in segs) == shard(n_eps * reps, r, world)[1]
+                for e, r0, c in segs:
+                    assert 0 <= e < n_eps and 0 <= r0 and c >= 1 and r0 + c <= reps
+                    seen.extend(e * reps + r0 + i for i in range(c))
+            assert seen == list(range(n_eps * reps))   # rank order = flattened order
+
+
+def _rows_worker(rank, world, port, q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from dcor.dist import gather_rows, shard
+    total = 11
+    counts = [shard(total, r, world)[1] for r in range(world)]
+    b0, nb = shard(total, rank, world)
+    local = np.arange(b0 * 6, (b0 + nb) * 6, dtype=np.float64).reshape(nb, 6) + 0.5
+    q.put((rank, gather_rows(local, counts).tobytes()))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gather_rows_ranks_in_order(world):
+    """dcor.dist.gather_rows (the HRS records' all-gather): uneven shards padded to the largest and
+    trimmed, concatenated in rank order, identical on every rank."""
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_rows_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    want = (np.arange(11 * 6, dtype=np.float64).reshape(11, 6) + 0.5).tobytes()
+    assert all(v == want for v in res.values())

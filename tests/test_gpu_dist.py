@@ -152,3 +152,96 @@ def test_bench_configs_c3_over_ranks_runs():
     d = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
     assert d["config"] == "C3" and d["world_formed"] == 1 and d["backend"] == "nccl"
     assert d["replicates"] == 8 * 64 and d["cells_with_results"] == 8 and d["reps_per_s"] > 0
+
+
+# ------------------------------------------------ the HRS workload over ranks (a19 / C5)
+HRS_R = 41          # odd: uneven shards
+SWEEP = (0.55, 1.35, 2.05)
+
+
+def _hrs_args():
+    import numpy as np
+    from dcor import hrs
+    age, bmi = hrs.standin_panel(3001, -0.3, seed=5)
+    z = hrs.standardize_panel(age, bmi, lap=np.array([0.3, -0.2, 0.1, 0.4]))
+    return (z["age_z"], z["bmi_z"], z["lambda_age_z"], z["lambda_bmi_z"])
+
+
+def _hrs_runs():
+    """[premat, fused, R-stream] records of HRS_R replicates, and the sweep's runs + summaries."""
+    from dcor.dist import eps_sweep_distributed, run_hrs_distributed
+    a = _hrs_args()
+    recs = [run_hrs_distributed(*a, 2.0, HRS_R, rep_begin=3),
+            run_hrs_distributed(*a, 2.0, HRS_R, rep_begin=3, mode="fused"),
+            run_hrs_distributed(*a, 0.75, 9, rng="R", eps_idx=6)]
+    sw = eps_sweep_distributed(*a, eps_grid=SWEEP, reps=7)
+    return [r.tobytes() for r in recs], sw["runs"].tobytes(), sw["ni_mean"], sw["int_mean"]
+
+
+def _hrs_expected():
+    from dcor import hrs
+    a = _hrs_args()
+    recs = [hrs.hrs_replicates(*a, 2.0, HRS_R, rep_begin=3),
+            hrs.hrs_replicates(*a, 2.0, HRS_R, rep_begin=3, mode="fused"),
+            hrs.hrs_replicates(*a, 0.75, 9, rng="R", eps_idx=6)]
+    sw = hrs.eps_sweep(*a, eps_grid=SWEEP, reps=7)
+    return [r.tobytes() for r in recs], sw["runs"].tobytes(), sw["ni_mean"], sw["int_mean"]
+
+
+def test_hrs_distributed_rccl_world1():
+    """dcor.dist.run_hrs_distributed / eps_sweep_distributed at world 1 over RCCL: the records
+    equal one process's hrs_replicates byte for byte, the sweep equals eps_sweep."""
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        got = _hrs_runs()
+    finally:
+        dist.destroy_process_group()
+    assert got == _hrs_expected()
+
+
+def _hrs_worker(rank, world, port, q):
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    q.put((rank, _hrs_runs()))
+    dist.destroy_process_group()
+
+
+def test_hrs_distributed_two_ranks_on_gpu():
+    """Two gloo ranks sharing cuda:0: each runs its contiguous replicate range (and its part of the
+    flattened sweep); the gathered records are the single-process run's byte for byte on both."""
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_hrs_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=200) for _ in range(world))
+    for p in procs:
+        p.join(timeout=30)
+        assert p.exitcode == 0
+    want = _hrs_expected()
+    assert got[0] == want and got[1] == want
+
+
+def test_bench_configs_hrs_over_ranks_runs():
+    """bench_configs.py --gpus 1 --only C5e,HS takes the HRS rank path and prints lines with the
+    world it formed (reduced sizes)."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    e = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    p = subprocess.run([sys.executable, os.path.join(root, "bench_configs.py"), "--gpus", "1", "--only",
+                        "C5,C5e,HS", "--c5-R", "512", "--c5e-R", "3000", "--hs-R", "20"], capture_output=True,
+                       text=True, timeout=240, env=e)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = {d["config"]: d for d in (json.loads(ln) for ln in p.stdout.splitlines() if ln.startswith("{"))}
+    assert lines["C5-e2e"]["world_formed"] == 1 and lines["C5-e2e"]["rows_gathered"] == 3000
+    assert lines["HS"]["rows_gathered"] == 23 * 20 and lines["HS"]["finite"]
+    assert lines["C5"]["replicates"] == 512 and lines["C5"]["reps_per_s"] > 0

@@ -73,9 +73,9 @@ def test_grid_launch_equals_per_cell_launches(dc):
     _check_launch(cells, begins, counts)
 
 
-def test_grid_launch_chunks_and_streams(dc, monkeypatch):
+def test_grid_launch_chunks_and_streams(dc, variant):
     """A 1 MiB slab budget splits the code items into many chunks over the two streams."""
-    monkeypatch.setenv("DCOR_GRID_SLAB_MB", "1")
+    variant("DCOR_GRID_SLAB_MB", "1")
     from dcor.sim import CellSpec
     cells = [CellSpec(n=n, rho=0.5, eps1=1.0, eps2=1.0, seed=2_000_000 + n) for n in (3000, 700, 12_345)]
     _check_launch(cells, [0, 5, 11], [300, 129, 260])
@@ -171,15 +171,15 @@ def test_grid_run_multi_persistent_workers_allocate_once(dc):
             assert [bytes(x) for x in a["accum"]] == [bytes(x) for x in b["accum"]]
 
 
-def test_grid_memory_bounded_in_B(dc, monkeypatch):
+def test_grid_memory_bounded_in_B(dc, variant):
     """Device memory does not grow with B: with a 1 MiB record buffer the replicates
     run in many passes of whole accumulate blocks; the accumulators are still byte-identical to
     one dcor_accumulate_launch over each cell's records, the detail records to the per-cell
     launches, and a 4x larger B holds the same device bytes."""
     from dcor import _lib
     from dcor.sim import CellSpec, run_grid
-    monkeypatch.setenv("DCOR_GRID_REC_MB", "1")            # 21,845 records per pass
-    monkeypatch.setenv("DCOR_GRID_CHUNK_ITEMS", "4096")    # and many chunks per pass
+    variant("DCOR_GRID_REC_MB", "1")            # 21,845 records per pass
+    variant("DCOR_GRID_CHUNK_ITEMS", "4096")    # and many chunks per pass
     cells = [CellSpec(n=1000, rho=0.3, eps1=1.0, eps2=1.0, family="subG", dgp="bounded_factor", seed=1_000_031),
              CellSpec(n=1200, rho=0.5, eps1=1.0, eps2=1.0, mu=(0.5, 0.5), sigma=(2.0, 2.0), seed=1_000_032),
              CellSpec(n=900, rho=0.65, eps1=0.5, eps2=0.5, dgp="bernoulli", seed=1_000_033)]

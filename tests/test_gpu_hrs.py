@@ -145,11 +145,9 @@ def test_panel_pipelined_halves_bitexact(panel):
     z = panel
     args = (z["age_z"], z["bmi_z"], z["lambda_age_z"], z["lambda_bmi_z"], 2.0, 4100)
     serial = hrs.hrs_replicates(*args, chunk=4100)
-    os.environ["DCOR_PREMAT_PIPELINE"] = "1"
-    try:
+    from dcor import _lib
+    with _lib.variants(DCOR_PREMAT_PIPELINE="1"):
         piped = hrs.hrs_replicates(*args, chunk=4100)
-    finally:
-        del os.environ["DCOR_PREMAT_PIPELINE"]
     np.testing.assert_array_equal(piped.view(np.int64), serial.view(np.int64))
     assert np.isfinite(piped).all()
 
@@ -284,27 +282,12 @@ def test_hrs_fused_continuous_panel_matches_oracle(n, eps, reps, rb):
 def test_hrs_fused_l2_kernel_equals_coded_kernel(panel):
     """On a codable panel the uncoded kernel (DCOR_HRS_FUSED_L2=1) gathers the same clipped values
     the coded kernel reads from its dictionaries, in the same order: identical bits."""
-    import os
-    import subprocess
-    import sys
+    from dcor import _lib, hrs
     z = panel
     args = (z["age_z"], z["bmi_z"], z["lambda_age_z"], z["lambda_bmi_z"], 2.0, 23)
-    from dcor import hrs
     coded = hrs.hrs_replicates(*args, rep_begin=5, mode="fused")
-    # the override is read once per process: run the uncoded kernel in a child
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    paths = [root, os.path.join(root, "distributed-correlation_amd")]
-    code = ("import sys, numpy as np; sys.path[:0] = %r; from dcor import hrs; "
-            "z = np.load(sys.argv[1]); "
-            "r = hrs.hrs_replicates(z['a'], z['b'], float(z['la']), float(z['lb']), 2.0, 23, rep_begin=5, "
-            "mode='fused'); np.save(sys.argv[2], r)") % (paths,)
-    import tempfile
-    with tempfile.TemporaryDirectory() as d:
-        np.savez(os.path.join(d, "p.npz"), a=z["age_z"], b=z["bmi_z"], la=z["lambda_age_z"], lb=z["lambda_bmi_z"])
-        env = dict(os.environ, DCOR_HRS_FUSED_L2="1")
-        subprocess.run([sys.executable, "-c", code, os.path.join(d, "p.npz"), os.path.join(d, "o.npy")],
-                       check=True, env=env, timeout=120)
-        l2 = np.load(os.path.join(d, "o.npy"))
+    with _lib.variants(DCOR_HRS_FUSED_L2="1"):
+        l2 = hrs.hrs_replicates(*args, rep_begin=5, mode="fused")
     np.testing.assert_array_equal(l2.view(np.int64), coded.view(np.int64))
 
 
@@ -342,26 +325,15 @@ def test_premat_tiled_kernel_matches_l2_kernel():
     two (1024); 30,001 takes two rounds of batch pairs in both variants, 19,433 in the 512-thread
     one; odd n puts every other replicate's noise row off a 16-B boundary (the head-sample path).
     The estimators against the oracle on this path: test_gpu_more.py::test_premat_subg_hrs_shared_panel."""
-    import os
-    import subprocess
-    import sys
-    import tempfile
+    from dcor import _lib
     got = _premat_continuous_runs()
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    paths = [root, os.path.join(root, "distributed-correlation_amd"), os.path.join(root, "tests")]
-    code = ("import sys, numpy as np; sys.path[:0] = %r; import test_gpu_hrs as t; "
-            "np.savez(sys.argv[1], **t._premat_continuous_runs())") % (paths,)
     runs = {}
     variants = (("l2", {"DCOR_TILED": "0"}), ("v0", {"DCOR_TILED_VARIANT": "0"}),
                 ("v0_aux", {"DCOR_TILED_VARIANT": "0", "DCOR_TILED_INT": "2"}),
                 ("v0_in", {"DCOR_TILED_VARIANT": "0", "DCOR_TILED_INT": "0"}))
-    for name, env_over in variants:
-        with tempfile.TemporaryDirectory() as d:
-            env = dict(os.environ, **env_over)
-            subprocess.run([sys.executable, "-c", code, os.path.join(d, "o.npz")], check=True, env=env,
-                           timeout=120)
-            o = np.load(os.path.join(d, "o.npz"))
-            runs[name] = {key: o[key] for key in o.files}
+    for name, over in variants:
+        with _lib.variants(**over):
+            runs[name] = _premat_continuous_runs()
     for key, v in got.items():
         assert np.isfinite(v).all()
         for name in ("v0", "v0_aux", "v0_in"):
@@ -378,10 +350,6 @@ def test_premat_tiled_workgroup_runs_many_replicates():
     per workgroup with a short last group.  Sampled rows equal the same replicates run one per
     launch (a fresh workgroup, every tile filled), bit for bit, and the oracle-checked 512-thread
     variant's rows within the estimator tolerance."""
-    import os
-    import subprocess
-    import sys
-    import tempfile
     from dcor import hrs
     z = _continuous(3001, seed=11)
     args = (z["age_z"], z["bmi_z"], z["lambda_age_z"], z["lambda_bmi_z"], 2.0)
@@ -391,15 +359,9 @@ def test_premat_tiled_workgroup_runs_many_replicates():
     for r in (0, 1, 255, 256, 257, 511, 767, 1023, 1200, 1201, 1202):
         one = hrs.hrs_replicates(*args, 1, rep_begin=5 + r, chunk=1)
         np.testing.assert_array_equal(whole[r:r + 1].view(np.int64), one.view(np.int64), err_msg=f"row {r}")
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    paths = [root, os.path.join(root, "distributed-correlation_amd"), os.path.join(root, "tests")]
-    code = ("import sys, numpy as np; sys.path[:0] = %r; import test_gpu_hrs as t; from dcor import hrs; "
-            "z = t._continuous(3001, seed=11); np.save(sys.argv[1], hrs.hrs_replicates(z['age_z'], z['bmi_z'], "
-            "z['lambda_age_z'], z['lambda_bmi_z'], 2.0, %d, rep_begin=5, chunk=%d))") % (paths, R, R)
-    with tempfile.TemporaryDirectory() as d:
-        env = dict(os.environ, DCOR_TILED_VARIANT="0")
-        subprocess.run([sys.executable, "-c", code, os.path.join(d, "o.npy")], check=True, env=env, timeout=120)
-        v0 = np.load(os.path.join(d, "o.npy"))
+    from dcor import _lib
+    with _lib.variants(DCOR_TILED_VARIANT="0"):
+        v0 = hrs.hrs_replicates(*args, R, rep_begin=5, chunk=R)
     for r in range(0, R, 97):
         assert_close(whole[r], v0[r], what=f"row {r}: default vs 512-thread tiled kernel")
 

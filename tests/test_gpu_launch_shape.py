@@ -199,7 +199,7 @@ def test_headline_bench_step_every_replicate(dc, orc):
     assert ties.sum() < 0.03 * R * 12_500      # rare: about 1 % of batches at 128 code levels
 
 
-def test_headline_wide_code_window(dc, orc, monkeypatch):
+def test_headline_wide_code_window(dc, orc, variant):
     """The record codes' window only decides how many samples tie a private centre's code (each tie
     batch is recomputed exactly), never a count: with round 3's wide window (DCOR_CODE_WINDOW=wide,
     many times the ties of the default) 2048 headline replicates give the default window's INT
@@ -218,7 +218,7 @@ def test_headline_wide_code_window(dc, orc, monkeypatch):
         return int(t.sum())
 
     narrow, t_narrow = simulate(cell, R, r0).cpu().numpy(), ties()
-    monkeypatch.setenv("DCOR_CODE_WINDOW", "wide")
+    variant("DCOR_CODE_WINDOW", "wide")
     wide, t_wide = simulate(cell, R, r0).cpu().numpy(), ties()
     assert np.array_equal(narrow[:, 3:].view(np.int64), wide[:, 3:].view(np.int64))
     assert_close(wide[:, :3], narrow[:, :3], rtol=1e-14, what="NI, wide vs default window")

@@ -186,14 +186,14 @@ def test_bernoulli_planes_vs_oracle(dc, orc, spec):
 
 
 @pytest.mark.parametrize("eps", [(1.0, 1.0), (1.5, 0.5), (0.5, 0.5)])
-def test_bernoulli_planes_vs_regen(dc, eps, monkeypatch):
+def test_bernoulli_planes_vs_regen(dc, eps, variant):
     """Bit-plane kernel == per-sample regenerate kernel, bit for bit (clip(1) = 1 makes
     the DP-mean sums integers in both)."""
     from dcor.sim import CellSpec, simulate
     cell = CellSpec(n=30_011, rho=0.5, eps1=eps[0], eps2=eps[1], family="sign", dgp="bernoulli",
                     seed=77)
     a = simulate(cell, 64).cpu().numpy()
-    monkeypatch.setenv("DCOR_SIGN_KERNEL", "regen")
+    variant("DCOR_SIGN_KERNEL", "regen")
     b = simulate(cell, 64).cpu().numpy()
     assert np.array_equal(a, b, equal_nan=True)
 

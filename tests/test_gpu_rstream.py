@@ -104,11 +104,8 @@ def test_chunked_streams_are_continuous(dc, orc, max_chunk):
                    sigma=(1, 1), eps1=2.0, eps2=2.0, seed=77)]
     B = 60
     full = dc.rstream.run_grid(specs, B)
-    os.environ["DCOR_RS_MAX_CHUNK"] = str(max_chunk)
-    try:
+    with dc.variants(DCOR_RS_MAX_CHUNK=str(max_chunk)):
         small = dc.rstream.run_grid(specs, B)
-    finally:
-        del os.environ["DCOR_RS_MAX_CHUNK"]
     for spec, a, b in zip(specs, full, small):
         np.testing.assert_array_equal(a["records"], b["records"])
     assert_close(small[2]["records"], orc.rs_sim(specs[2].to_c(), B))
@@ -176,16 +173,10 @@ JUMP_CELLS = ["sign-gauss", "sign-gauss-neg", "sign-bern", "sign-nonorm-laplace"
 
 
 def _with_env(env, fn):
-    old = {k: os.environ.get(k) for k in env}
-    os.environ.update(env)
-    try:
+    """fn() with the engine switches `env` set (dcor_set_variant), restored afterwards."""
+    from dcor import _lib
+    with _lib.variants(**env):
         return fn()
-    finally:
-        for k, v in old.items():
-            if v is None:
-                os.environ.pop(k, None)
-            else:
-                os.environ[k] = v
 
 
 def _jump_specs(dc):
