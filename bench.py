@@ -123,7 +123,7 @@ def profile_stamp(path):
 
 
 def _profile(name):
-    for tag in ("r05", "r04", "r03", "r02", "r01"):
+    for tag in ("r06", "r05", "r04", "r03", "r02", "r01"):
         p = os.path.join(ROOT, "profiles", f"{tag}_{name}_summary.json")
         if os.path.exists(p):
             return p

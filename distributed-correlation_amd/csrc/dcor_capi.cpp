@@ -892,15 +892,16 @@ int dcor_diag_sign_pass(const dcor_cell* cell, int64_t rep_begin, int64_t reps, 
   if (int st = need_device()) return st;
   CellPlan cp;
   if (int st = prepare_cell(*cell, cp)) return st;
-  // a small cell (wave kernels) runs here in the workgroup kernels: the same records, ties and
-  // results per replicate (passes 1-3 only; the ceilings are the headline's)
+  // a small cell (wave kernels) runs here in the workgroup kernels: the same records and tie
+  // batches per replicate, results equal to the wave kernels' up to the order of the compensated
+  // sums (passes 1-3 only; the ceilings are the headline's)
   if ((cp.kind != GK_SIGN_CODES && !(cp.kind == GK_SIGN_CODES_W && which <= 3)) || cp.nan_dgp)
     return fail(DCOR_EINVAL, "diag_sign_pass: the cell does not run the one-pass sign kernels");
   if (which > 10 && (cp.dgp != DCOR_DGP_GAUSSIAN || cp.sign.m != 8))
     return fail(DCOR_EINVAL, "diag_sign_pass: the ceilings run the Gaussian DGP at m = 8");
   SignConst k = cp.sign;
   k.rep_begin = rep_begin;
-  const size_t slab_b = ((size_t)reps * sign_item_words(cell->n, cell->dgp) * sizeof(uint32_t) + 255) / 256 * 256;
+  const size_t slab_b = ((size_t)reps * sign_item_words(cell->n, cell->dgp) * sizeof(uint32_t) + 255) / 256 * 256 + 256;  // + pass 2's over-read
   const size_t sums_b = ((size_t)reps * SIGN_SUMS * sizeof(double) + 255) / 256 * 256;
   const size_t part_b = ((size_t)reps * SIGN_PARTIAL_BYTES + 255) / 256 * 256;
   void* scratch = nullptr;
@@ -918,7 +919,7 @@ int dcor_diag_sign_ties(const dcor_cell* cell, int64_t rep_begin, int64_t reps, 
   if (int st = dcor_diag_sign_pass(cell, rep_begin, reps, 2, nullptr)) return st;
   void* scratch = nullptr;
   if (int st = arena_get(0, &scratch)) return st;   // the same arena dcor_diag_sign_pass used
-  const size_t slab_b = ((size_t)reps * sign_item_words(cell->n, cell->dgp) * sizeof(uint32_t) + 255) / 256 * 256;
+  const size_t slab_b = ((size_t)reps * sign_item_words(cell->n, cell->dgp) * sizeof(uint32_t) + 255) / 256 * 256 + 256;  // + pass 2's over-read
   const size_t sums_b = ((size_t)reps * SIGN_SUMS * sizeof(double) + 255) / 256 * 256;
   std::vector<long long> part((size_t)reps * SIGN_PARTIAL_BYTES / sizeof(long long));
   HIPCHK(hipDeviceSynchronize());
@@ -1277,7 +1278,7 @@ static int premat_subg_run(const dcor_premat_subg* d, const dcor_panel* panel, d
     // the tiled path's INT kernel may run on the auxiliary stream (DCOR_TILED_INT=2)
     Pipe* pp = nullptr;
     const char* iv = dcor::variant("DCOR_TILED_INT");
-    if (iv && std::strcmp(iv, "2") == 0 && pipe_get(&pp) != 0) pp = nullptr;
+    if (iv && (std::strcmp(iv, "2") == 0 || std::strcmp(iv, "3") == 0) && pipe_get(&pp) != 0) pp = nullptr;
     rc = launch_premat_subg(p, d->reps, part, d_out, stream, nullptr, nullptr, pp ? pp->s : nullptr,
                             pp ? pp->fork : nullptr, pp ? pp->join : nullptr);
   }

@@ -330,13 +330,17 @@ __device__ __forceinline__ long long wave_sum_i(long long v) {
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
 }
+// Butterfly all-reduce.  dd_add is symmetric for finite operands (two_sum's error term is exact,
+// so two_sum(a, b) == two_sum(b, a) bit for bit, and every later step sees the same values), so each
+// lane adds its partner's sum on the right: lane 0 computes exactly what the lower-lane-left order
+// gave (every value reaching it came from a lane that was the lower one of its pairs), and the
+// lanes agree bit for bit unless a sum overflows.  Selecting between dd_add(v, w) and dd_add(w, v)
+// per lane made the compiler evaluate both: 52 fp64 adds per step instead of 26.
 __device__ __forceinline__ DD wave_sum_dd(DD v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
     DD w{__shfl_xor(v.hi, o, 64), __shfl_xor(v.lo, o, 64)};
-    // combine in a lane-order independent way: lower lane is left operand
-    const bool low = ((threadIdx.x & o) == 0);
-    v = low ? dd_add(v, w) : dd_add(w, v);
+    v = dd_add(v, w);
   }
   return v;
 }

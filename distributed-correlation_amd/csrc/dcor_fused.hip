@@ -821,7 +821,7 @@ __device__ __forceinline__ void scalar_laplace_wave(uint32_t rep, uint32_t k0, u
 // pbuf: the calling wave's piece buffer (64 c.pieces words of LDS) when c.pieces > 0; tq: its
 // tie-deferral queue (TQ words of LDS).
 #define TQ 256
-template <int DGP, bool WAVE, bool CEIL = false>
+template <int DGP, bool WAVE, bool CEIL = false, bool ONLY8 = false>
 __device__ __forceinline__ P2Result sign_pass2_core(const SignConst& c, uint32_t rep,
                                                     const uint32_t* __restrict__ slab,
                                                     const double* __restrict__ sums_in,
@@ -983,7 +983,7 @@ __device__ __forceinline__ P2Result sign_pass2_core(const SignConst& c, uint32_t
   auto drain_if_full = [&](uint32_t per_trip) {
     if (tqn > TQ - per_trip) drain_ties();
   };
-  if (c.m == 8) {
+  if (ONLY8 || c.m == 8) {
     // headline geometry: one thread = one batch = one 16-B load (8 records), decided by word2.
     auto decide = [&](const uint4& v, int& cx, int& cy, int& cc) -> bool {
       uint32_t neg = 0, pc = 0, tie = 0;
@@ -1049,7 +1049,7 @@ __device__ __forceinline__ P2Result sign_pass2_core(const SignConst& c, uint32_t
         drain_if_full(128u);
       }
     }
-  } else if constexpr (!CEIL) {
+  } else if constexpr (!CEIL && !ONLY8) {
     // m % 8 == 0, 16 <= m <= 248 (the grids' 32, C4's 200): 16-B pieces of 8 records.  A replicate's
     // batches go in rounds of 64 (waves take rounds wv, wv + 4, ...); in a round the wave's lanes
     // read 64 consecutive pieces at a time (1 KB, coalesced -- lane-per-batch loads would touch 64
@@ -1252,7 +1252,7 @@ __device__ __forceinline__ uint32_t* wave_pbuf(int stride) {
   return dcor_pbuf_dyn + (size_t)(threadIdx.x >> 6) * 64u * (uint32_t)stride;
 }
 
-template <int DGP, bool CEIL = false>
+template <int DGP, bool CEIL = false, bool M8 = false>
 __device__ __forceinline__ void sign_pass2_body(const SignConst& c, uint32_t rep,
                                                 const uint32_t* __restrict__ slab,
                                                 const double* __restrict__ sums_in,
@@ -1261,7 +1261,7 @@ __device__ __forceinline__ void sign_pass2_body(const SignConst& c, uint32_t rep
   __shared__ uint32_t tq[DCOR_WAVES][TQ];
   log_tab_to_lds(lt, DCOR_BLOCK);
   __syncthreads();
-  const P2Result r = sign_pass2_core<DGP, false, CEIL>(c, rep, slab, sums_in, lt, wave_pbuf(c.pieces),
+  const P2Result r = sign_pass2_core<DGP, false, CEIL, M8>(c, rep, slab, sums_in, lt, wave_pbuf(c.pieces),
                                                        tq[threadIdx.x >> 6]);
   if (threadIdx.x == 0) {
     SignPartial p;
@@ -1274,12 +1274,15 @@ __device__ __forceinline__ void sign_pass2_body(const SignConst& c, uint32_t rep
 
 
 
-template <int DGP>
+// M8: a cell with m = 8 (the headline geometry) gets an instantiation holding the m = 8 decision
+// loop only, so the other batch-size loops' registers do not weigh on its allocation (the generic
+// instantiation spilled 8 VGPRs at 4 waves per SIMD); the m = 8 code path is the same either way.
+template <int DGP, bool M8 = false>
 __global__ __launch_bounds__(DCOR_BLOCK, DCOR_P2_WPE) void k_sign_pass2(SignConst c,
                                                            const uint32_t* __restrict__ scratch,
                                                            const double* __restrict__ sums,
                                                            SignPartial* __restrict__ part) {
-  sign_pass2_body<DGP>(c, (uint32_t)(c.rep_begin + blockIdx.x),
+  sign_pass2_body<DGP, false, M8>(c, (uint32_t)(c.rep_begin + blockIdx.x),
                        scratch + (size_t)blockIdx.x * sign_item_words(c.n, DGP),
                        sums + SIGN_SUMS * (size_t)blockIdx.x, part + blockIdx.x);
 }
@@ -2337,8 +2340,12 @@ static int launch_codes_t(SignConst c, int64_t reps, int64_t chunk, const CodesB
     SignPartial* part = reinterpret_cast<SignPartial*>(bf.sums[b] + SIGN_SUMS * chunk);
     hipLaunchKernelGGL(k_sign_pass1<DGP>, dim3((unsigned)nr), dim3(DCOR_BLOCK), 0, st[b], c,
                        bf.slab[b], bf.sums[b]);
-    hipLaunchKernelGGL(k_sign_pass2<DGP>, dim3((unsigned)nr), dim3(DCOR_BLOCK), sign_piece_lds(c.pieces), st[b], c,
-                       bf.slab[b], bf.sums[b], part);
+    if (c.m == 8)
+      hipLaunchKernelGGL((k_sign_pass2<DGP, true>), dim3((unsigned)nr), dim3(DCOR_BLOCK), 0, st[b], c,
+                         bf.slab[b], bf.sums[b], part);
+    else
+      hipLaunchKernelGGL(k_sign_pass2<DGP>, dim3((unsigned)nr), dim3(DCOR_BLOCK), sign_piece_lds(c.pieces), st[b], c,
+                         bf.slab[b], bf.sums[b], part);
     if (int e = before_out(b)) return e;
     launch_sign_epilogue(c, nr, part, out + r, st[b]);
     if (int e = last_err()) return e;
@@ -2392,7 +2399,10 @@ int launch_sign_diag(const SignConst& c, int64_t reps, int which, uint32_t* slab
       break;
     case 2:
       switch (c.g.dgp) {
-        case DCOR_DGP_GAUSSIAN: hipLaunchKernelGGL(k_sign_pass2<DCOR_DGP_GAUSSIAN>, g, b, sign_piece_lds(c.pieces), st, c, slab, sums, part); break;
+        case DCOR_DGP_GAUSSIAN:
+          if (c.m == 8) hipLaunchKernelGGL((k_sign_pass2<DCOR_DGP_GAUSSIAN, true>), g, b, 0, st, c, slab, sums, part);
+          else hipLaunchKernelGGL(k_sign_pass2<DCOR_DGP_GAUSSIAN>, g, b, sign_piece_lds(c.pieces), st, c, slab, sums, part);
+          break;
         case DCOR_DGP_MIX_GAUSSIAN: hipLaunchKernelGGL(k_sign_pass2<DCOR_DGP_MIX_GAUSSIAN>, g, b, sign_piece_lds(c.pieces), st, c, slab, sums, part); break;
         default: hipLaunchKernelGGL(k_sign_pass2<DCOR_DGP_BOUNDED_FACTOR>, g, b, sign_piece_lds(c.pieces), st, c, slab, sums, part);
       }
@@ -2419,7 +2429,7 @@ int launch_sign_diag(const SignConst& c, int64_t reps, int which, uint32_t* slab
     }
     case 12: {
       size_t pad = 0;
-      const int e = occupancy_pad((const void*)k_sign_pass2<DCOR_DGP_GAUSSIAN>, (const void*)k_sign_pass2_ceil, &pad);
+      const int e = occupancy_pad((const void*)k_sign_pass2<DCOR_DGP_GAUSSIAN, true>, (const void*)k_sign_pass2_ceil, &pad);
       if (e) return e;
       hipLaunchKernelGGL(k_sign_pass2_ceil, g, b, pad, st, c, slab, sums, part);
       break;

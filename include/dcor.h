@@ -131,7 +131,8 @@ int dcor_sim_chunking(const dcor_cell* cell, int64_t rep_count, int64_t* chunk, 
 /* Measurement only (bench.py's roofline, not part of the reference surface): one pass of the
  * one-pass sign path (the workgroup kernels dcor_sim_launch runs for cells with n > 16384 and
  * normalise = TRUE; a smaller cell runs passes 1-3 in them too, with the same per-replicate records
- * and results as its wave kernels) over replicates rep_begin .. rep_begin + reps - 1 as ONE chunk,
+ * and tie batches as its wave kernels -- its results may differ from theirs in the low bits, since
+ * the workgroup and wave reductions add the compensated sums in different orders) over replicates rep_begin .. rep_begin + reps - 1 as ONE chunk,
  * on `stream`, in the calling thread's scratch arena.  which: 1 pass 1 (writes the slab and the
  * clipped sums; for the Gaussian DGP it also regenerates its slow samples), 2 pass 2 (reads the slab
  * and sums), 3 the epilogue (reads pass 2's partials); 11 the pass-1 ceiling and 12 the pass-2

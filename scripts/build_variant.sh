@@ -13,4 +13,5 @@ F="--offload-arch=gfx950 -O3 -fPIC -std=c++17 -ffp-contract=off"
 /opt/rocm/bin/hipcc $F $2 -c -o $V/dcor_premat.hip.o $C/dcor_premat.hip &
 wait
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $R/distributed-correlation_amd/dcor/libdcor_$1.so \
-  $V/dcor_fused.hip.o $V/dcor_premat.hip.o $O/dcor_rstream.hip.o $O/dcor_capi.cpp.o $O/dcor_grid.cpp.o $O/dcor_mtjump.cpp.o
+  $V/dcor_fused.hip.o $V/dcor_premat.hip.o $O/dcor_rstream.hip.o $O/dcor_capi.cpp.o $O/dcor_grid.cpp.o $O/dcor_mtjump.cpp.o \
+  $O/dcor_stamp.cpp.o

@@ -276,3 +276,24 @@ def test_fused_vs_oracle_bitmap_geometry(dc, orc, n):
     got = simulate(cell, 4, rep_begin=3).cpu().numpy()
     ref = orc.sim_reps(cell.to_c(), 3, 7)
     assert_close(got, ref, what=f"bitmap geometry n={n}")
+
+
+# Batch sizes above 252 take pass 2's record-by-record exact path (dcor_fused.hip, m > 252), in the
+# wave kernels (n <= 16384) and in the workgroup kernels: eps 0.1 x 0.1 gives m = 800,
+# eps 0.16 x 0.16 m = 313; through dcor_sim_launch and through the batched grid.
+M_BIG_CELLS = [dict(n=12_000, eps1=0.1, eps2=0.1), dict(n=20_000, eps1=0.1, eps2=0.1),
+               dict(n=9_391, eps1=0.16, eps2=0.16), dict(n=40_001, eps1=0.16, eps2=0.16, dgp="bernoulli")]
+
+
+@pytest.mark.parametrize("spec", M_BIG_CELLS)
+def test_fused_vs_oracle_m_over_252(dc, orc, spec):
+    from dcor.sim import CellSpec, run_grid, simulate
+    cell = CellSpec(rho=0.5, mu=(0.5, 0.5), sigma=(2.0, 2.0), seed=6_000_000 + spec["n"],
+                    **{"dgp": "gaussian", **spec})
+    k, m = dc.api.batch_geometry(cell.n, cell.eps1, cell.eps2, "sign")
+    assert m > 252 and k >= 10
+    got = simulate(cell, 8, rep_begin=5).cpu().numpy()
+    ref = orc.sim_reps(cell.to_c(), 5, 13)
+    assert_close(got, ref, what=f"m={m} {spec}")
+    grid = run_grid([cell], 13, detail=True, devices=[0])[0]["records"]
+    np.testing.assert_array_equal(grid[5:13].view(np.int64), got.view(np.int64))

@@ -52,11 +52,24 @@ def test_results_independent_of_environment():
 
 
 def test_switches_still_act_through_set_variant():
+    """The same switches set through dcor_set_variant do act: the wide code window multiplies the
+    headline's tie batches (dcor_diag_sign_ties) and the L2-gather kernel serves C5-continuous
+    (estimates within tolerance of the tiled kernel's; their compensated sums often round alike)."""
+    import ctypes as C
     from dcor import _lib
-    default = _runs()
-    with _lib.variants(DCOR_TILED="0"):
-        l2 = _runs()
-    np.testing.assert_array_equal(l2["headline"].view(np.int64), default["headline"].view(np.int64))
-    np.testing.assert_array_equal(l2["c5"].view(np.int64), default["c5"].view(np.int64))
-    assert not np.array_equal(l2["c5c"].view(np.int64), default["c5c"].view(np.int64))
-    assert_close(l2["c5c"], default["c5c"], what="C5-continuous, L2-gather vs tiled kernel")
+    from dcor.sim import headline_cell
+
+    def ties():
+        c = headline_cell().to_c()
+        t = np.zeros(512, dtype=np.int64)
+        _lib.check(_lib.lib.dcor_diag_sign_ties(C.byref(c), 8192 + 17, 512, t.ctypes.data_as(C.POINTER(C.c_int64))))
+        return int(t.sum())
+
+    default, t0 = _runs(), ties()
+    with _lib.variants(DCOR_TILED="0", DCOR_CODE_WINDOW="wide"):
+        alt, t1 = _runs(), ties()
+    assert t1 > 4 * max(t0, 1), (t0, t1)
+    np.testing.assert_array_equal(alt["c5"].view(np.int64), default["c5"].view(np.int64))
+    np.testing.assert_array_equal(alt["headline"][:, 3:].view(np.int64), default["headline"][:, 3:].view(np.int64))
+    assert_close(alt["headline"], default["headline"], rtol=1e-14, what="headline, wide vs default window")
+    assert_close(alt["c5c"], default["c5c"], what="C5-continuous, L2-gather vs tiled kernel")
