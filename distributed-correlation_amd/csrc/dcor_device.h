@@ -330,19 +330,30 @@ __device__ __forceinline__ long long wave_sum_i(long long v) {
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
 }
-// Butterfly all-reduce.  dd_add is symmetric for finite operands (two_sum's error term is exact,
-// so two_sum(a, b) == two_sum(b, a) bit for bit, and every later step sees the same values), so each
-// lane adds its partner's sum on the right: lane 0 computes exactly what the lower-lane-left order
-// gave (every value reaching it came from a lane that was the lower one of its pairs), and the
-// lanes agree bit for bit unless a sum overflows.  Selecting between dd_add(v, w) and dd_add(w, v)
-// per lane made the compiler evaluate both: 52 fp64 adds per step instead of 26.
+// Butterfly all-reduce of a double-double.  Each step keeps the pair unnormalised: two_sum of the
+// high parts (exact: s + e = a + b) and the low parts plus e added plainly; one two_sum renormalises
+// after the last step.  8 fp64 adds per step instead of dd_add's 26 -- in the premat and HRS kernels
+// the reductions were about two thirds of all fp64 adds (profiles/r06w_c5c) -- with an error of
+// order 2^-100 of the sum's magnitude.  Every step is symmetric in the two operands (two_sum's
+// error term is exact, the plain adds commute), so all lanes hold the same bits unless a sum
+// overflows.
+__device__ __forceinline__ DD dd_fold_step(DD a, DD b) {   // unnormalised: renormalise at the end
+  const DD s = two_sum(a.hi, b.hi);
+  return DD{s.hi, (a.lo + b.lo) + s.lo};
+}
 __device__ __forceinline__ DD wave_sum_dd(DD v) {
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    DD w{__shfl_xor(v.hi, o, 64), __shfl_xor(v.lo, o, 64)};
-    v = dd_add(v, w);
-  }
-  return v;
+  for (int o = 32; o > 0; o >>= 1) v = dd_fold_step(v, DD{__shfl_xor(v.hi, o, 64), __shfl_xor(v.lo, o, 64)});
+  return two_sum(v.hi, v.lo);
+}
+// The per-wave partials of one sum (hi at h[0..nw), lo at l[0..nw)) folded in wave order with the
+// same step: the workgroup kernels' last reduction stage, one thread per sum.
+template <int NW>
+__device__ __forceinline__ DD fold_waves_dd(const double* h, const double* l) {
+  DD a{h[0], l[0]};
+#pragma unroll
+  for (int w = 1; w < NW; ++w) a = dd_fold_step(a, DD{h[w], l[w]});
+  return two_sum(a.hi, a.lo);
 }
 
 // Workgroup sums of NV doubles; result broadcast to every thread. Scratch: NV*DCOR_WAVES.
@@ -381,11 +392,7 @@ __device__ __forceinline__ void block_sum_dd(DD (&v)[NV], double* scratch) {
   __syncthreads();
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
-    DD s{scratch[(2 * i) * NW], scratch[(2 * i + 1) * NW]};
-#pragma unroll
-    for (int w = 1; w < NW; ++w)
-      s = dd_add(s, DD{scratch[(2 * i) * NW + w], scratch[(2 * i + 1) * NW + w]});
-    v[i] = s;
+    v[i] = fold_waves_dd<NW>(scratch + (2 * i) * NW, scratch + (2 * i + 1) * NW);
   }
   __syncthreads();
 }

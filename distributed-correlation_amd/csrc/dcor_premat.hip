@@ -719,10 +719,7 @@ __global__ __launch_bounds__(DICT_NT, WPE) void k_premat_subg_dict(PrematSubgCon
     wave_put(2, sT2);
     __syncthreads();
     if (tid < 5) {
-      DD a{rb[(2 * tid) * DICT_NW], rb[(2 * tid + 1) * DICT_NW]};
-#pragma unroll
-      for (int w = 1; w < DICT_NW; ++w)
-        a = dd_add(a, DD{rb[(2 * tid) * DICT_NW + w], rb[(2 * tid + 1) * DICT_NW + w]});
+      const DD a = fold_waves_dd<DICT_NW>(rb + (2 * tid) * DICT_NW, rb + (2 * tid + 1) * DICT_NW);
       part[it].s[2 * tid] = a.hi;
       part[it].s[2 * tid + 1] = a.lo;
     }
@@ -1025,10 +1022,7 @@ __global__ __launch_bounds__(NT, WPE) void k_premat_subg_tiled(PrematSubgConst p
     wave_put(2, merged(sT2));
     __syncthreads();
     if (tid < (INTK ? 5u : 3u)) {
-      DD a{rb[(2 * tid) * NW], rb[(2 * tid + 1) * NW]};
-#pragma unroll
-      for (int w = 1; w < NW; ++w)
-        a = dd_add(a, DD{rb[(2 * tid) * NW + w], rb[(2 * tid + 1) * NW + w]});
+      const DD a = fold_waves_dd<NW>(rb + (2 * tid) * NW, rb + (2 * tid + 1) * NW);
       part[it].s[2 * tid] = a.hi;
       part[it].s[2 * tid + 1] = a.lo;
     }
@@ -1125,9 +1119,7 @@ __global__ __launch_bounds__(256, WPE) void k_premat_subg_int(PrematSubgConst p,
   __syncthreads();
   if (tid < 2 * R) {
     const int r = (int)tid >> 1, v = (int)tid & 1;
-    DD a{red[r][2 * v][0], red[r][2 * v + 1][0]};
-#pragma unroll
-    for (int w = 1; w < LNW; ++w) a = dd_add(a, DD{red[r][2 * v][w], red[r][2 * v + 1][w]});
+    const DD a = fold_waves_dd<LNW>(red[r][2 * v], red[r][2 * v + 1]);
     if (r0 + r < reps) {
       part[r0 + r].s[6 + 2 * v] = a.hi;
       part[r0 + r].s[7 + 2 * v] = a.lo;
@@ -1653,10 +1645,7 @@ __global__ __launch_bounds__(DICT_NT, WPE) void k_hrs_fused(PrematSubgConst p, H
     wave_put(2, sT2);
     __syncthreads();
     if (tid < 5) {
-      DD a{rb[(2 * tid) * DICT_NW], rb[(2 * tid + 1) * DICT_NW]};
-#pragma unroll
-      for (int w = 1; w < DICT_NW; ++w)
-        a = dd_add(a, DD{rb[(2 * tid) * DICT_NW + w], rb[(2 * tid + 1) * DICT_NW + w]});
+      const DD a = fold_waves_dd<DICT_NW>(rb + (2 * tid) * DICT_NW, rb + (2 * tid + 1) * DICT_NW);
       part[it].s[2 * tid] = a.hi;
       part[it].s[2 * tid + 1] = a.lo;
     }
@@ -1785,10 +1774,7 @@ __global__ __launch_bounds__(DICT_NT, WPE) void k_hrs_fused_l2(PrematSubgConst p
     wave_put(2, sT2);
     __syncthreads();
     if (tid < 5) {
-      DD a{rb[(2 * tid) * DICT_NW], rb[(2 * tid + 1) * DICT_NW]};
-#pragma unroll
-      for (int w = 1; w < DICT_NW; ++w)
-        a = dd_add(a, DD{rb[(2 * tid) * DICT_NW + w], rb[(2 * tid + 1) * DICT_NW + w]});
+      const DD a = fold_waves_dd<DICT_NW>(rb + (2 * tid) * DICT_NW, rb + (2 * tid + 1) * DICT_NW);
       part[it].s[2 * tid] = a.hi;
       part[it].s[2 * tid + 1] = a.lo;
     }
