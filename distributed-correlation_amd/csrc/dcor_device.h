@@ -320,15 +320,67 @@ __device__ __forceinline__ double dd_var(DD s1, DD s2, double n) {
 }
 
 // ------------------------------------------------------------ reductions
+// Lane exchanges for the wave all-reduces, without the LDS crossbar (__shfl_xor compiles to
+// ds_bpermute_b32 plus index arithmetic): DPP within rows of 16 lanes, the gfx950 permlane swaps
+// across rows.  lane_dpp<CTRL>: the value of lane quad_perm / mirror partner; lane_swap<32 | 16>:
+// the value pair {own, partner} for partner = lane ^ 32 (permlane32_swap) or lane ^ 16
+// (permlane16_swap), in an order that depends on the lane -- callers combine the pair with a
+// commutative operation.
+template <int CTRL>
+__device__ __forceinline__ uint32_t lane_dpp_u32(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, false);
+}
+template <int CTRL>
+__device__ __forceinline__ uint64_t lane_dpp_u64(uint64_t v) {
+  return ((uint64_t)lane_dpp_u32<CTRL>((uint32_t)(v >> 32)) << 32) | lane_dpp_u32<CTRL>((uint32_t)v);
+}
+template <int W>
+__device__ __forceinline__ void lane_swap_u32(uint32_t v, uint32_t& a, uint32_t& b) {
+  if constexpr (W == 32) {
+    const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+    a = r[0]; b = r[1];
+  } else {
+    static_assert(W == 16, "permlane16_swap or permlane32_swap");
+    const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+    a = r[0]; b = r[1];
+  }
+}
+template <int W>
+__device__ __forceinline__ void lane_swap_u64(uint64_t v, uint64_t& a, uint64_t& b) {
+  uint32_t al, bl, ah, bh;
+  lane_swap_u32<W>((uint32_t)v, al, bl);
+  lane_swap_u32<W>((uint32_t)(v >> 32), ah, bh);
+  a = ((uint64_t)ah << 32) | al;
+  b = ((uint64_t)bh << 32) | bl;
+}
+// The butterfly of the all-reduces: lanes i^1, i^2 (quad_perm), 7-i within 8 (row_half_mirror),
+// 15-i within 16 (row_mirror), rows 0<->1 and 2<->3 (permlane16_swap), halves (permlane32_swap).
+// Each step pairs two lanes that hold partials over disjoint lane sets, so every lane ends with the
+// op over all 64; with a commutative op both lanes of a pair compute the same bits, so all lanes
+// agree.  Take / put convert the reduced type to and from 64-bit words.
+template <class T, class Get, class Put, class Op>
+__device__ __forceinline__ T wave_allreduce(T v, Get get, Put put, Op op) {
+  v = op(v, put(lane_dpp_u64<0xB1>(get(v))));
+  v = op(v, put(lane_dpp_u64<0x4E>(get(v))));
+  v = op(v, put(lane_dpp_u64<0x141>(get(v))));
+  v = op(v, put(lane_dpp_u64<0x140>(get(v))));
+  uint64_t a, b;
+  lane_swap_u64<16>(get(v), a, b);
+  v = op(put(a), put(b));
+  lane_swap_u64<32>(get(v), a, b);
+  return op(put(a), put(b));
+}
+__device__ __forceinline__ uint64_t d_bits(double v) { return (uint64_t)__double_as_longlong(v); }
+__device__ __forceinline__ double d_from(uint64_t b) { return __longlong_as_double((long long)b); }
+
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
 }
 __device__ __forceinline__ long long wave_sum_i(long long v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+  return wave_allreduce(v, [](long long x) { return (uint64_t)x; }, [](uint64_t b) { return (long long)b; },
+                        [](long long x, long long y) { return x + y; });
 }
 // Butterfly all-reduce of a double-double.  Each step keeps the pair unnormalised: two_sum of the
 // high parts (exact: s + e = a + b) and the low parts plus e added plainly; one two_sum renormalises
@@ -342,9 +394,25 @@ __device__ __forceinline__ DD dd_fold_step(DD a, DD b) {   // unnormalised: reno
   return DD{s.hi, (a.lo + b.lo) + s.lo};
 }
 __device__ __forceinline__ DD wave_sum_dd(DD v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = dd_fold_step(v, DD{__shfl_xor(v.hi, o, 64), __shfl_xor(v.lo, o, 64)});
+  // a DD is two words: the exchanges move hi and lo alike
+  v = dd_fold_step(v, DD{d_from(lane_dpp_u64<0xB1>(d_bits(v.hi))), d_from(lane_dpp_u64<0xB1>(d_bits(v.lo)))});
+  v = dd_fold_step(v, DD{d_from(lane_dpp_u64<0x4E>(d_bits(v.hi))), d_from(lane_dpp_u64<0x4E>(d_bits(v.lo)))});
+  v = dd_fold_step(v, DD{d_from(lane_dpp_u64<0x141>(d_bits(v.hi))), d_from(lane_dpp_u64<0x141>(d_bits(v.lo)))});
+  v = dd_fold_step(v, DD{d_from(lane_dpp_u64<0x140>(d_bits(v.hi))), d_from(lane_dpp_u64<0x140>(d_bits(v.lo)))});
+  uint64_t ah, bh, al, bl;
+  lane_swap_u64<16>(d_bits(v.hi), ah, bh);
+  lane_swap_u64<16>(d_bits(v.lo), al, bl);
+  v = dd_fold_step(DD{d_from(ah), d_from(al)}, DD{d_from(bh), d_from(bl)});
+  lane_swap_u64<32>(d_bits(v.hi), ah, bh);
+  lane_swap_u64<32>(d_bits(v.lo), al, bl);
+  v = dd_fold_step(DD{d_from(ah), d_from(al)}, DD{d_from(bh), d_from(bl)});
   return two_sum(v.hi, v.lo);
+}
+__device__ __forceinline__ double wave_min(double v) {
+  return wave_allreduce(v, d_bits, d_from, [](double x, double y) { return fmin(x, y); });
+}
+__device__ __forceinline__ double wave_max(double v) {
+  return wave_allreduce(v, d_bits, d_from, [](double x, double y) { return fmax(x, y); });
 }
 // The per-wave partials of one sum (hi at h[0..nw), lo at l[0..nw)) folded in wave order with the
 // same step: the workgroup kernels' last reduction stage, one thread per sum.
@@ -500,11 +568,8 @@ __device__ __forceinline__ double value_select(const double (&v)[SEL_VPT], int p
 #pragma unroll
   for (int s = 0; s < SEL_VPT; ++s)
     if (v[s] == v[s]) { lo = fmin(lo, v[s]); hi = fmax(hi, v[s]); }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    lo = fmin(lo, __shfl_xor(lo, o, 64));
-    hi = fmax(hi, __shfl_xor(hi, o, 64));
-  }
+  lo = wave_min(lo);
+  hi = wave_max(hi);
   if (lane == 0) { sc->mm[wv] = lo; sc->mm[DCOR_WAVES + wv] = hi; }
   sc->hist[tid] = 0;
   if (tid == 0) sc->ncand = 0;
@@ -599,20 +664,16 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   __builtin_amdgcn_wave_barrier();
 }
-__device__ __forceinline__ double wave_min(double v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o, 64));
-  return v;
-}
-__device__ __forceinline__ double wave_max(double v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
-  return v;
-}
 __device__ __forceinline__ int wave_sum_int(int v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+  v += (int)lane_dpp_u32<0xB1>((uint32_t)v);
+  v += (int)lane_dpp_u32<0x4E>((uint32_t)v);
+  v += (int)lane_dpp_u32<0x141>((uint32_t)v);
+  v += (int)lane_dpp_u32<0x140>((uint32_t)v);
+  uint32_t a, b;
+  lane_swap_u32<16>((uint32_t)v, a, b);
+  v = (int)(a + b);
+  lane_swap_u32<32>((uint32_t)v, a, b);
+  return (int)(a + b);
 }
 
 // Monotone bin of v in [0, 255] for the active range [lo, hi]: by value when the range is
