@@ -1278,7 +1278,7 @@ static int premat_subg_run(const dcor_premat_subg* d, const dcor_panel* panel, d
     // the tiled path's INT kernel may run on the auxiliary stream (DCOR_TILED_INT=2)
     Pipe* pp = nullptr;
     const char* iv = dcor::variant("DCOR_TILED_INT");
-    if (iv && (std::strcmp(iv, "2") == 0 || std::strcmp(iv, "3") == 0) && pipe_get(&pp) != 0) pp = nullptr;
+    if (iv && std::strcmp(iv, "2") == 0 && pipe_get(&pp) != 0) pp = nullptr;
     rc = launch_premat_subg(p, d->reps, part, d_out, stream, nullptr, nullptr, pp ? pp->s : nullptr,
                             pp ? pp->fork : nullptr, pp ? pp->join : nullptr);
   }

@@ -730,10 +730,11 @@ __device__ __forceinline__ void sign_pass1_body(const SignConst& c, uint32_t rep
                                                 uint32_t* __restrict__ slab,
                                                 double* __restrict__ sums_out) {
   if constexpr (DGP == DCOR_DGP_GAUSSIAN) {
-    __shared__ double2 zt[2 * DCOR_ZIG_N];
+    constexpr int ZTN = 2 * DCOR_ZIG_N;
+    __shared__ double2 zt[ZTN];
     __shared__ uint32_t zl[DCOR_WAVES][128];   // each wave's slow-sample list
     const int tid = threadIdx.x;
-    for (int e = tid; e < 2 * DCOR_ZIG_N; e += DCOR_BLOCK)
+    for (int e = tid; e < ZTN; e += DCOR_BLOCK)
       zt[e] = make_double2(dcor_zig_tab[e][0], dcor_zig_tab[e][1]);
     __syncthreads();
     sign_pass1_core<DGP, false, CEIL>(c, rep, slab, sums_out, zt, zl[tid >> 6], nullptr);

@@ -759,11 +759,10 @@ __global__ __launch_bounds__(DICT_NT, WPE) void k_premat_subg_dict(PrematSubgCon
 // the arithmetic -- and every replicate's bits -- does not depend on the buffers' alignment, and the
 // aligned kernel carries no run-time branch around its loads (measured, round 5: the branch took
 // the tiled kernel from 496 to 551 us per 8192 C5-continuous replicates).
-// DMA (NI-only kernels): a tile is filled by LDS-direct loads (global_load_lds_dwordx4, 1 KB per
+// NI-only kernels (INTK = false) fill a tile by LDS-direct loads (global_load_lds_dwordx4, 1 KB per
 // wave-instruction, no VGPR staging), every wave's share issued at once and waited for once, instead
-// of a register-staged copy loop that waited one L2 round trip per trip.
-template <int NT, int NQ, int FU, int GB, int NA, int WPE, bool PG = false, bool INTK = true, bool AL = true,
-          bool DMA = !INTK>
+// of the register-staged copy loop the INT-sum form needs (round 6: the same time, 2 fewer VGPRs).
+template <int NT, int NQ, int FU, int GB, int NA, int WPE, bool PG = false, bool INTK = true, bool AL = true>
 __global__ __launch_bounds__(NT, WPE) void k_premat_subg_tiled(PrematSubgConst p,
                                                               const int* __restrict__ dict_ok,
                                                               int64_t reps, int64_t tile_pairs_,
@@ -856,12 +855,7 @@ __global__ __launch_bounds__(NT, WPE) void k_premat_subg_tiled(PrematSubgConst p
 #pragma unroll
       for (int u = 0; u < NQ; ++u) {
         const uint32_t q = qb + tid + (uint32_t)u * NT;
-#if defined(DCOR_TILED_ABL) && (DCOR_TILED_ABL & 1)
-        const uint32_t hq = (q * 2654435761u) ^ (uint32_t)it;
-        pr[u] = iv4{(int)(hq & 0x3fff), (int)((hq >> 7) & 0x3fff), (int)((hq >> 3) & 0x3fff), (int)((hq >> 11) & 0x3fff)};
-#else
         pr[u] = ld_pr(q < nbp ? q : nbp - 1);
-#endif
       }
 #pragma unroll
       for (int u = 0; u < NQ; ++u) {
@@ -882,13 +876,9 @@ __global__ __launch_bounds__(NT, WPE) void k_premat_subg_tiled(PrematSubgConst p
         const uint32_t lo = tp == 0 ? 0u : h + 2 * pa;
         const uint32_t hi = tp == ntiles - 1 ? n : h + 2 * pb;
         const uint32_t tn = hi - lo;
-#if defined(DCOR_TILED_ABL) && (DCOR_TILED_ABL & 8)
-        if (false) {
-#else
         if (INTK || tp != held) {
-#endif
           __syncthreads();  // the previous tile's readers are done
-          if constexpr (DMA && !INTK) {
+          if constexpr (!INTK) {
             // xy[lo, hi) -> tile[0, tn): chunk cc of 64 entries by wave cc mod NW, lane-linear
             const uint32_t wv = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63u;
             for (uint32_t cc = wv; cc * 64u < tn; cc += (uint32_t)NW) {
@@ -903,7 +893,7 @@ __global__ __launch_bounds__(NT, WPE) void k_premat_subg_tiled(PrematSubgConst p
             held = tp;
           }
         }
-        if (!(DMA && !INTK) && (INTK || tp != held)) {   // (the barrier above has run)
+        if (INTK) {   // (the barrier above has run)
           // fill: this thread's INT pairs q = tid (mod NT) in [pa, pb), FU per loop trip
           uint32_t q = pa + ((tid + NT - pa % NT) % NT);
           for (; q + (FU - 1) * NT < pb; q += FU * NT) {
@@ -956,13 +946,8 @@ __global__ __launch_bounds__(NT, WPE) void k_premat_subg_tiled(PrematSubgConst p
 #pragma unroll
         for (int u = 0; u < NQ; ++u) {
           const uint32_t i0 = sa[u] & 0xFFFFu, i1 = sa[u] >> 16, i2 = sb[u] & 0xFFFFu, i3 = sb[u] >> 16;
-#if defined(DCOR_TILED_ABL) && (DCOR_TILED_ABL & 4)
-          const double2 t0 = make_double2((double)i0, (double)i1), t1 = make_double2((double)i2, (double)i3);
-          const double2 t2 = t1, t3 = t0;
-#else
           const double2 t0 = tile[min(i0 - lo, tn)], t1 = tile[min(i1 - lo, tn)];
           const double2 t2 = tile[min(i2 - lo, tn)], t3 = tile[min(i3 - lo, tn)];
-#endif
           ax[u][0] = (ax[u][0] + t0.x) + t1.x;
           ay[u][0] = (ay[u][0] + t0.y) + t1.y;
           ax[u][1] = (ax[u][1] + t2.x) + t3.x;
@@ -984,12 +969,8 @@ __global__ __launch_bounds__(NT, WPE) void k_premat_subg_tiled(PrematSubgConst p
 #pragma unroll
       for (int u = 0; u < NQ; ++u) {
         const uint32_t q = qb + tid + (uint32_t)u * NT, qc = q < nbp ? q : nbp - 1;
-#if defined(DCOR_TILED_ABL) && (DCOR_TILED_ABL & 2)
-        nx[u] = dv2{(double)qc, 0.5}; ny[u] = dv2{0.25, (double)qc};
-#else
         nx[u] = ld_nz(x_row, qc);
         ny[u] = ld_nz(y_row, qc);
-#endif
       }
 #pragma unroll
       for (int u = 0; u < NQ; ++u) {
@@ -1042,11 +1023,8 @@ __global__ __launch_bounds__(NT, WPE) void k_premat_subg_tiled(PrematSubgConst p
 // C5-continuous (round 4) against 0.53-0.54 for 2, 2, 1 and 2, 1, 1, 0.52 for 2, 1, 8 (spills) and
 // 0.47 for 2, 2, 6 (spills).
 #define DCOR_INT_WPE 4
-// WPE: minimum waves per SIMD the kernel is compiled for (its VGPR cap); the co-resident form beside
-// the 768-thread tiled kernel (one INT wave per SIMD in the registers three tiled waves leave) is
-// R = 1 at a 64-VGPR cap.
-template <int R, int WPE = DCOR_INT_WPE>
-__global__ __launch_bounds__(256, WPE) void k_premat_subg_int(PrematSubgConst p, int64_t reps,
+template <int R>
+__global__ __launch_bounds__(256, DCOR_INT_WPE) void k_premat_subg_int(PrematSubgConst p, int64_t reps,
                                                          SubgPartial* __restrict__ part) {
   constexpr int LNW = 8;                 // logical waves (512 logical threads)
   __shared__ double red[R][4][LNW];      // [replicate][sU.hi, sU.lo, sU2.hi, sU2.lo][logical wave]
@@ -1976,7 +1954,7 @@ static int tiled_int_mode() {
   const int m = [] {
     const char* e = dcor::variant("DCOR_TILED_INT");
     const int x = e ? std::atoi(e) : 1;
-    return (x >= 0 && x <= 3) ? x : 1;
+    return (x >= 0 && x <= 2) ? x : 1;
   }();
   return m;
 }
@@ -1984,7 +1962,7 @@ static int tiled_int_mode() {
 #define DCOR_INT_R 4
 #endif
 static TiledKernel tiled_kernel(bool intk, bool al) {
-  static const TiledKernel ks[4][2][2] = {
+  static const TiledKernel ks[2][2][2] = {
       {{{k_premat_subg_tiled<512, 5, 1, 1, 1, 4, true, true, false>, 512, 80 * 1024},
         {k_premat_subg_tiled<512, 5, 1, 1, 1, 4, true, true, true>, 512, 80 * 1024}},
        {{k_premat_subg_tiled<512, 5, 1, 1, 1, 4, true, false, false>, 512, 80 * 1024},
@@ -1992,19 +1970,11 @@ static TiledKernel tiled_kernel(bool intk, bool al) {
       {{{k_premat_subg_tiled<1024, 5, 1, 1, 1, 4, true, true, false>, 1024, 160 * 1024},
         {k_premat_subg_tiled<1024, 5, 1, 1, 1, 4, true, true, true>, 1024, 160 * 1024}},
        {{k_premat_subg_tiled<1024, 5, 1, 1, 1, 4, true, false, false>, 1024, 160 * 1024},
-        {k_premat_subg_tiled<1024, 5, 1, 1, 1, 4, true, false, true>, 1024, 160 * 1024}}},
-      {{{k_premat_subg_tiled<768, 7, 1, 1, 1, 3, true, true, false>, 768, 159 * 1024},
-        {k_premat_subg_tiled<768, 7, 1, 1, 1, 3, true, true, true>, 768, 159 * 1024}},
-       {{k_premat_subg_tiled<768, 7, 1, 1, 1, 3, true, false, false>, 768, 159 * 1024},
-        {k_premat_subg_tiled<768, 7, 1, 1, 1, 3, true, false, true>, 768, 159 * 1024}}},
-      {{{k_premat_subg_tiled<1024, 5, 1, 1, 1, 4, true, true, false>, 1024, 160 * 1024},
-        {k_premat_subg_tiled<1024, 5, 1, 1, 1, 4, true, true, true>, 1024, 160 * 1024}},
-       {{k_premat_subg_tiled<1024, 5, 1, 1, 1, 4, true, false, false, false>, 1024, 160 * 1024},
-        {k_premat_subg_tiled<1024, 5, 1, 1, 1, 4, true, false, true, false>, 1024, 160 * 1024}}}};
+        {k_premat_subg_tiled<1024, 5, 1, 1, 1, 4, true, false, true>, 1024, 160 * 1024}}}};
   const int v = [] {
     const char* e = dcor::variant("DCOR_TILED_VARIANT");
     const int x = e ? std::atoi(e) : 1;
-    return (x >= 0 && x < 4) ? x : 1;
+    return (x >= 0 && x < 2) ? x : 1;
   }();
   return ks[v][intk ? 0 : 1][al ? 1 : 0];
 }
@@ -2071,17 +2041,13 @@ int launch_premat_subg(const PrematSubgConst& c0, int64_t reps, void* part, dcor
     if (tiled) {
       // the INT sums in k_premat_subg_int: on the auxiliary stream when the caller gave one
       const int im = tiled_int_mode();
-      const bool conc = im >= 2 && int_stream != nullptr && ev_fork != nullptr && ev_join != nullptr;
-      const bool intk = im == 0 || (im >= 2 && !conc);
+      const bool conc = im == 2 && int_stream != nullptr && ev_fork != nullptr && ev_join != nullptr;
+      const bool intk = im == 0 || (im == 2 && !conc);
       // serial: before the tiled kernel; concurrent: submitted after it, so the tiled kernel's
       // persistent workgroups are resident first and the INT workgroups fill what they leave
       auto launch_int = [&](hipStream_t is) {
-        if (im == 3)
-          hipLaunchKernelGGL((k_premat_subg_int<1, 8>), dim3((unsigned)reps), dim3(256), 0, is, c, reps,
-                             (SubgPartial*)part);
-        else
-          hipLaunchKernelGGL(k_premat_subg_int<DCOR_INT_R>, dim3((unsigned)((reps + DCOR_INT_R - 1) / DCOR_INT_R)),
-                             dim3(256), 0, is, c, reps, (SubgPartial*)part);
+        hipLaunchKernelGGL(k_premat_subg_int<DCOR_INT_R>, dim3((unsigned)((reps + DCOR_INT_R - 1) / DCOR_INT_R)),
+                           dim3(256), 0, is, c, reps, (SubgPartial*)part);
       };
       if (conc && hipEventRecord((hipEvent_t)ev_fork, (hipStream_t)stream) != hipSuccess) return last_err();
       if (!intk && !conc) launch_int((hipStream_t)stream);
