@@ -437,6 +437,9 @@ def main():
                          "kernel_ms_avg": kern_ms,
                          "kernel_ms_kind": "HIP events: first call's start to last call's end over the timed calls, / K",
                          "work_units_per_rep": W},
+            "engine": {"library_source_sha16": dcor.lib.dcor_source_hash().decode()[:16],
+                       "tree_source_sha16": src_sha16(),
+                       "fresh": dcor.lib.dcor_source_hash().decode()[:16] == src_sha16()},
             "summary": {"coverage_NI": summ["NI"]["coverage"], "coverage_INT": summ["INT"]["coverage"],
                         "ci_len_NI": summ["NI"]["ci_length"], "ci_len_INT": summ["INT"]["ci_length"]},
         }
