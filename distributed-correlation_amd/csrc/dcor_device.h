@@ -370,6 +370,17 @@ __device__ __forceinline__ T wave_allreduce(T v, Get get, Put put, Op op) {
   lane_swap_u64<32>(get(v), a, b);
   return op(put(a), put(b));
 }
+// Inclusive prefix sum over the wave's 64 lanes by DPP (row shifts, then the row broadcasts of lane
+// 15 and 31): exact, no LDS crossbar.
+__device__ __forceinline__ uint32_t wave_incl_scan_u32(uint32_t v) {
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false);   // row_shr:1
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false);   // row_shr:2
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false);   // row_shr:4
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false);   // row_shr:8
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);   // row_bcast:15
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false);   // row_bcast:31
+  return v;
+}
 __device__ __forceinline__ uint64_t d_bits(double v) { return (uint64_t)__double_as_longlong(v); }
 __device__ __forceinline__ double d_from(uint64_t b) { return __longlong_as_double((long long)b); }
 
@@ -521,12 +532,7 @@ __device__ __forceinline__ double reg_select(const unsigned long long (&key)[SEL
       if ((key[s] & mask) == prefix) atomicAdd(&sc->hist[(key[s] >> shift) & 255], 1u);
     __syncthreads();
     const uint32_t h = sc->hist[tid];
-    uint32_t inc = h;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t t = __shfl_up(inc, o, 64);
-      if (lane >= o) inc += t;
-    }
+    const uint32_t inc = wave_incl_scan_u32(h);
     if (lane == 63) sc->wtot[wv] = inc;
     __syncthreads();
     uint32_t base = 0;
@@ -601,12 +607,7 @@ __device__ __forceinline__ double value_select(const double (&v)[SEL_VPT], int p
   }
   __syncthreads();
   const uint32_t h = sc->hist[tid];
-  uint32_t inc = h;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const uint32_t t = __shfl_up(inc, o, 64);
-    if (lane >= o) inc += t;
-  }
+  const uint32_t inc = wave_incl_scan_u32(h);
   if (lane == 63) sc->wtot[wv] = inc;
   __syncthreads();
   uint32_t base = 0;
@@ -769,12 +770,7 @@ __device__ __forceinline__ double wave_select(const double (&v)[VPL], int pos, W
     uint32_t hb[4], s4 = 0;
 #pragma unroll
     for (int q = 0; q < 4; ++q) { hb[q] = ws->hist[4 * lane + q]; s4 += hb[q]; }
-    uint32_t inc = s4;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t t = __shfl_up(inc, o, 64);
-      if (lane >= o) inc += t;
-    }
+    const uint32_t inc = wave_incl_scan_u32(s4);
     const uint32_t ex = inc - s4;
     int B = -1;
     uint32_t cnt = 0, kk = 0;
@@ -786,10 +782,10 @@ __device__ __forceinline__ double wave_select(const double (&v)[VPL], int pos, W
         base += hb[q];
       }
     }
-    const int owner = __ffsll((long long)__ballot(B >= 0)) - 1;
-    B = __shfl(B, owner, 64);
-    cnt = __shfl(cnt, owner, 64);
-    kk = __shfl(kk, owner, 64);
+    const int owner = __builtin_amdgcn_readfirstlane(__ffsll((long long)__ballot(B >= 0)) - 1);
+    B = __builtin_amdgcn_readlane(B, owner);
+    cnt = __builtin_amdgcn_readlane(cnt, owner);
+    kk = __builtin_amdgcn_readlane(kk, owner);
     if (cnt <= 64) {  // rank the bin's keys directly
 #pragma unroll
       for (int s = 0; s < VPL; ++s)
@@ -904,12 +900,7 @@ __device__ __forceinline__ double wave_select_lds(const double* kv, int pos, Wav
     uint32_t hb[4], s4 = 0;
 #pragma unroll
     for (int q = 0; q < 4; ++q) { hb[q] = ws->hist[4 * lane + q]; s4 += hb[q]; }
-    uint32_t inc = s4;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t t = __shfl_up(inc, o, 64);
-      if (lane >= o) inc += t;
-    }
+    const uint32_t inc = wave_incl_scan_u32(s4);
     const uint32_t ex = inc - s4;
     int B = -1;
     uint32_t cnt = 0, kk = 0;
@@ -921,10 +912,10 @@ __device__ __forceinline__ double wave_select_lds(const double* kv, int pos, Wav
         base += hb[q];
       }
     }
-    const int owner = __ffsll((long long)__ballot(B >= 0)) - 1;
-    B = __shfl(B, owner, 64);
-    cnt = __shfl(cnt, owner, 64);
-    kk = __shfl(kk, owner, 64);
+    const int owner = __builtin_amdgcn_readfirstlane(__ffsll((long long)__ballot(B >= 0)) - 1);
+    B = __builtin_amdgcn_readlane(B, owner);
+    cnt = __builtin_amdgcn_readlane(cnt, owner);
+    kk = __builtin_amdgcn_readlane(kk, owner);
     if (cnt <= 64) {  // rank the bin's keys directly
 #pragma unroll
       for (int s = 0; s < VPL; ++s)

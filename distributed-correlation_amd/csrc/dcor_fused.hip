@@ -1338,8 +1338,16 @@ __device__ __forceinline__ void sign_epilogue_wave(const SignConst& c, uint32_t 
 }
 
 // ---- small cells (n <= SIGN_W_NMAX): one wave per replicate for both passes ------------------
+// The pass 2 + epilogue wave kernels: the tie queue (TQ words) lives in the wave's select histogram,
+// which the epilogue fills only after pass 2 has drained the queue, and the NI Laplace log table is
+// read from global memory (L1/L2) instead of a 4-KB LDS copy: 39 KB of LDS per 4-wave workgroup, four
+// workgroups per CU instead of three.  Measured (round 6, one box): VG 3.98e7 against 3.80e7 with the
+// LDS copy, C1 1.59e7 against 1.45e7.
+static_assert(TQ == 256, "the tie queue aliases WaveSelL::hist");
+#define P2E_LOG_TABLE(lt) const double2* lt = reinterpret_cast<const double2*>(dcor_log8_tab)
 #ifndef DCOR_P2E_WPE
-#define DCOR_P2E_WPE 4  // waves per SIMD the pass 2 + epilogue wave kernel is compiled for
+#define DCOR_P2E_WPE 4  // waves per SIMD the pass 2 + epilogue wave kernel is compiled for (the
+                        // mixture DGP's: 3, its sampler needs more than 128 VGPRs)
 #endif
 // At the reference grids' n (1000-12000) a 256-thread workgroup per replicate spends much of
 // its time in per-replicate fixed work -- the ziggurat table load, the scalar draws, the
@@ -1402,15 +1410,12 @@ __global__ __launch_bounds__(DCOR_BLOCK) void k_sign_pass2_w(SignConst c, int64_
 }
 
 template <int DGP, int VPL>
-__global__ __launch_bounds__(DCOR_BLOCK, DCOR_P2E_WPE) void k_sign_p2e_w(SignConst c, int64_t nreps,
+__global__ __launch_bounds__(DCOR_BLOCK, DGP == DCOR_DGP_MIX_GAUSSIAN ? 3 : DCOR_P2E_WPE) void k_sign_p2e_w(SignConst c, int64_t nreps,
                                                            const uint32_t* __restrict__ scratch,
                                                            const double* __restrict__ sums,
                                                            dcor_rep_out* out) {
   __shared__ WaveMix<VPL> wsel[DCOR_WAVES];
-  __shared__ double2 lt[256];
-  __shared__ uint32_t tq[DCOR_WAVES][TQ];
-  log_tab_to_lds(lt, DCOR_BLOCK);
-  __syncthreads();
+  P2E_LOG_TABLE(lt);
   const int wv = threadIdx.x >> 6;
   const int64_t r = (int64_t)blockIdx.x * DCOR_WAVES + __builtin_amdgcn_readfirstlane(wv);
   if (r >= nreps) return;  // whole waves only
@@ -1419,7 +1424,7 @@ __global__ __launch_bounds__(DCOR_BLOCK, DCOR_P2E_WPE) void k_sign_p2e_w(SignCon
   static_assert(sizeof(wsel[0].keys) >= 64 * SIGN_PIECES_MAX * sizeof(uint32_t), "piece buffer");
   const P2Result p = sign_pass2_core<DGP, true>(c, rep, scratch + (size_t)r * sign_item_words(c.n, DGP),
                                                 sums + SIGN_SUMS * (size_t)r, lt,
-                                                reinterpret_cast<uint32_t*>(wsel[wv].keys), tq[wv]);
+                                                reinterpret_cast<uint32_t*>(wsel[wv].keys), wsel[wv].sel.hist);
   sign_finish_wave<VPL>(c, rep, p, out + r, &wsel[wv]);
 }
 
@@ -2032,17 +2037,14 @@ __global__ __launch_bounds__(DCOR_BLOCK) void k_grid_sign_pass2_w(const SignCons
 }
 
 template <int DGP, int VPL>
-__global__ __launch_bounds__(DCOR_BLOCK, DCOR_P2E_WPE) void k_grid_sign_p2e_w(const SignConst* __restrict__ cells,
+__global__ __launch_bounds__(DCOR_BLOCK, DGP == DCOR_DGP_MIX_GAUSSIAN ? 3 : DCOR_P2E_WPE) void k_grid_sign_p2e_w(const SignConst* __restrict__ cells,
                                                                 const GridItem* __restrict__ items,
                                                                 int64_t nitems,
                                                                 const uint32_t* __restrict__ scratch,
                                                                 const double* __restrict__ sums,
                                                                 dcor_rep_out* out) {
   __shared__ WaveMix<VPL> wsel[DCOR_WAVES];
-  __shared__ double2 lt[256];
-  __shared__ uint32_t tq[DCOR_WAVES][TQ];
-  log_tab_to_lds(lt, DCOR_BLOCK);
-  __syncthreads();
+  P2E_LOG_TABLE(lt);
   const int64_t r = wave_item();
   if (r >= nitems) return;  // whole waves only
   const GridItem it = items[r];
@@ -2050,7 +2052,7 @@ __global__ __launch_bounds__(DCOR_BLOCK, DCOR_P2E_WPE) void k_grid_sign_p2e_w(co
   // the piece buffer lives in the wave's mixquant keys, which the epilogue fills only after pass 2
   const P2Result p = sign_pass2_core<DGP, true>(c, it.rep, scratch + it.scratch, sums + SIGN_SUMS * (size_t)r, lt,
                                                 reinterpret_cast<uint32_t*>(wsel[threadIdx.x >> 6].keys),
-                                                tq[threadIdx.x >> 6]);
+                                                wsel[threadIdx.x >> 6].sel.hist);
   sign_finish_wave<VPL>(c, it.rep, p, out + it.out, &wsel[threadIdx.x >> 6]);
 }
 
