@@ -762,7 +762,14 @@ __global__ __launch_bounds__(DICT_NT, WPE) void k_premat_subg_dict(PrematSubgCon
 // NI-only kernels (INTK = false) fill a tile by LDS-direct loads (global_load_lds_dwordx4, 1 KB per
 // wave-instruction, no VGPR staging), every wave's share issued at once and waited for once, instead
 // of the register-staged copy loop the INT-sum form needs (round 6: the same time, 2 fewer VGPRs).
-template <int NT, int NQ, int FU, int GB, int NA, int WPE, bool PG = false, bool INTK = true, bool AL = true>
+// ENQ: the NI noise of the first ENQ batch pairs is loaded when the round's last tile has been filled,
+// before its gathers, so those loads' HBM latency runs under the gathers (the rest after them); the
+// loads move, the arithmetic does not.  C5-continuous (round 6, two boxes): ENQ 3 1.29e7-1.30e7
+// replicates/s against 1.26e7-1.27e7 for ENQ 0 (4 VGPRs spill at the 128 cap); ENQ 2 1.28e7-1.29e7;
+// ENQ 4 and 5 spill 12 and 25 VGPRs, 1.21e7-1.23e7 and 1.01e7; ENQ 3 with the NI sums created after
+// the sweeps (no spill) 1.28e7.
+template <int NT, int NQ, int FU, int GB, int NA, int WPE, bool PG = false, bool INTK = true, bool AL = true,
+          int ENQ = 0>
 __global__ __launch_bounds__(NT, WPE) void k_premat_subg_tiled(PrematSubgConst p,
                                                               const int* __restrict__ dict_ok,
                                                               int64_t reps, int64_t tile_pairs_,
@@ -867,6 +874,14 @@ __global__ __launch_bounds__(NT, WPE) void k_premat_subg_tiled(PrematSubgConst p
         }
         ax[u][0] = ax[u][1] = ay[u][0] = ay[u][1] = -0.0;
       }
+      // NI noise of this round's batch pairs (past the last pair: the last pair's), every load issued
+      // before any is used: one round trip per round
+      dv2 nx[NQ], ny[NQ];
+      auto load_noise = [&](int u) {
+        const uint32_t q = qb + tid + (uint32_t)u * NT, qc = q < nbp ? q : nbp - 1;
+        nx[u] = ld_nz(x_row, qc);
+        ny[u] = ld_nz(y_row, qc);
+      };
       for (uint32_t ti = 0; ti < ntiles; ++ti) {
         // NI-only kernel: every other round sweeps the tiles in reverse, so it starts on the tile
         // the previous round (of this replicate or the last) ended on, still in LDS
@@ -942,6 +957,10 @@ __global__ __launch_bounds__(NT, WPE) void k_premat_subg_tiled(PrematSubgConst p
           __syncthreads();
           held = tp;
         }
+        if (ENQ > 0 && ti + 1 == ntiles) {
+#pragma unroll
+          for (int u = 0; u < ENQ; ++u) load_noise(u);
+        }
         // gather: every index of this thread's batch pairs against the tile
 #pragma unroll
         for (int u = 0; u < NQ; ++u) {
@@ -963,15 +982,9 @@ __global__ __launch_bounds__(NT, WPE) void k_premat_subg_tiled(PrematSubgConst p
         wave_put(3, merged(sU));
         wave_put(4, merged(sU2));
       }
-      // NI terms of this round's batch pairs, ascending q (real-data-sims.R:131-137); the noise
-      // of every pair loaded first (past the last pair: the last pair's), one round trip per round
-      dv2 nx[NQ], ny[NQ];
+      // NI terms of this round's batch pairs, ascending q (real-data-sims.R:131-137)
 #pragma unroll
-      for (int u = 0; u < NQ; ++u) {
-        const uint32_t q = qb + tid + (uint32_t)u * NT, qc = q < nbp ? q : nbp - 1;
-        nx[u] = ld_nz(x_row, qc);
-        ny[u] = ld_nz(y_row, qc);
-      }
+      for (int u = ENQ; u < NQ; ++u) load_noise(u);
 #pragma unroll
       for (int u = 0; u < NQ; ++u) {
         const uint32_t q = qb + tid + (uint32_t)u * NT;
@@ -1969,8 +1982,8 @@ static TiledKernel tiled_kernel(bool intk, bool al) {
         {k_premat_subg_tiled<512, 5, 1, 1, 1, 4, true, false, true>, 512, 80 * 1024}}},
       {{{k_premat_subg_tiled<1024, 5, 1, 1, 1, 4, true, true, false>, 1024, 160 * 1024},
         {k_premat_subg_tiled<1024, 5, 1, 1, 1, 4, true, true, true>, 1024, 160 * 1024}},
-       {{k_premat_subg_tiled<1024, 5, 1, 1, 1, 4, true, false, false>, 1024, 160 * 1024},
-        {k_premat_subg_tiled<1024, 5, 1, 1, 1, 4, true, false, true>, 1024, 160 * 1024}}}};
+       {{k_premat_subg_tiled<1024, 5, 1, 1, 1, 4, true, false, false, 3>, 1024, 160 * 1024},
+        {k_premat_subg_tiled<1024, 5, 1, 1, 1, 4, true, false, true, 3>, 1024, 160 * 1024}}}};
   const int v = [] {
     const char* e = dcor::variant("DCOR_TILED_VARIANT");
     const int x = e ? std::atoi(e) : 1;
