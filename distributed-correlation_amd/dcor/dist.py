@@ -181,10 +181,10 @@ def sweep_shard(n_eps: int, reps: int, rank: int, world: int):
 def eps_sweep_distributed(age_z, bmi_z, lam_age, lam_bmi, eps_grid=None, reps=None, nsim=2000, rng="philox",
                           group=None):
     """dcor.hrs.eps_sweep (real-data-sims.R:345-448) over G ranks: the flattened (eps, run) space
-    is split into contiguous per-rank ranges (sweep_shard); each segment is one hrs_replicates call
-    with the sweep's per-eps keys (Philox 10 + 1000 idx / 20 + 1000 idx, or the reference's per-run
-    set.seed in rng='R'); the records are all-gathered in rank order and the per-eps summaries built
-    from them on every rank.  Equal to the single-process eps_sweep: runs byte for byte, summaries
+    is split into contiguous per-rank ranges (sweep_shard); a rank runs its segments with the sweep's
+    per-eps keys (Philox 10 + 1000 idx / 20 + 1000 idx: hrs.sweep_segments over HIP streams; rng='R':
+    the reference's per-run set.seed, one hrs_replicates call per segment); the records are
+    all-gathered in rank order and the per-eps summaries built from them on every rank.  Equal to the single-process eps_sweep: runs byte for byte, summaries
     identical."""
     import torch.distributed as dist
 
@@ -192,12 +192,14 @@ def eps_sweep_distributed(age_z, bmi_z, lam_age, lam_bmi, eps_grid=None, reps=No
     eps_grid = hrs.EPS_GRID if eps_grid is None else eps_grid
     reps = hrs.R_PER_EPS if reps is None else reps
     rank, world = dist.get_rank(group), dist.get_world_size(group)
-    parts = []
-    for e, r0, c in sweep_shard(len(eps_grid), reps, rank, world):
-        idx = e + 1
-        parts.append(hrs.hrs_replicates(age_z, bmi_z, lam_age, lam_bmi, eps_grid[e], c, seed_ni=10 + 1000 * idx,
-                                        seed_int=20 + 1000 * idx, nsim=nsim, rng=rng, eps_idx=idx, rep_begin=r0))
-    local = np.concatenate(parts) if parts else np.zeros((0, 6))
+    segs = sweep_shard(len(eps_grid), reps, rank, world)
+    if rng == "philox" and segs:
+        local = hrs.sweep_segments(age_z, bmi_z, lam_age, lam_bmi, eps_grid, segs, nsim=nsim)
+    else:
+        parts = [hrs.hrs_replicates(age_z, bmi_z, lam_age, lam_bmi, eps_grid[e], c, seed_ni=10 + 1000 * (e + 1),
+                                    seed_int=20 + 1000 * (e + 1), nsim=nsim, rng=rng, eps_idx=e + 1, rep_begin=r0)
+                 for e, r0, c in segs]
+        local = np.concatenate(parts) if parts else np.zeros((0, 6))
     counts = [shard(len(eps_grid) * reps, r, world)[1] for r in range(world)]
     runs = gather_rows(local, counts, group).reshape(len(eps_grid), reps, 6)
     return hrs.sweep_summaries(eps_grid, runs)

@@ -77,6 +77,40 @@ def r_seeds(idx: int, reps, rep_begin: int = 0):
     return ((10 + 37 * rep + 1000 * idx).astype(np.int32), (20 + 41 * rep + 1000 * idx).astype(np.int32))
 
 
+def _philox_draws(seed_ni, seed_int, rb, nr, n, k, m, nsim, bufs, sp):
+    """The Philox unit-noise arrays of runs rb .. rb+nr-1 into bufs (perm, lap_x, lap_y,
+    lap_local, lap_central, mix_z, mix_l), enqueued on stream sp."""
+    import ctypes as C
+
+    from . import _lib
+    P = lambda t: C.c_void_p(t.data_ptr())
+    perm, lx, ly, ll, lc, mz, ml = bufs
+    chk = _lib.check
+    chk(_lib.lib.dcor_perm_launch(seed_ni, _lib.SITE_PERM, rb, nr, n, k * m, P(perm), sp))
+    chk(_lib.lib.dcor_draws_launch(DRAW_LAPLACE, seed_ni, SITE_NI_LAP_X, rb, nr, k, P(lx), sp))
+    chk(_lib.lib.dcor_draws_launch(DRAW_LAPLACE, seed_ni, SITE_NI_LAP_Y, rb, nr, k, P(ly), sp))
+    chk(_lib.lib.dcor_draws_launch(DRAW_LAPLACE, seed_int, SITE_INT_LOCAL, rb, nr, n, P(ll), sp))
+    chk(_lib.lib.dcor_draws_launch(DRAW_LAPLACE, seed_int, SITE_INT_CENTRAL, rb, nr, 1, P(lc), sp))
+    chk(_lib.lib.dcor_draws_launch(DRAW_NORMAL, seed_int, SITE_MIX_Z, rb, nr, nsim, P(mz), sp))
+    chk(_lib.lib.dcor_draws_launch(DRAW_LAPLACE, seed_int, SITE_MIX_L, rb, nr, nsim, P(ml), sp))
+
+
+def _premat_launch(X, Y, pn, n, nr, eps, lam_age, lam_bmi, lam_r, delta, nsim, alpha, bufs, out, sp):
+    """One pre-materialised HRS launch over the panel pn: nr runs from the noise in bufs into
+    out[:nr] (dcor_premat_subg_panel_launch), enqueued on stream sp."""
+    import ctypes as C
+
+    from . import _lib
+    perm, lx, ly, ll, lc, mz, ml = bufs
+    d = _lib.PrematSubg(n=n, reps=nr, eps1=eps, eps2=eps, eta1=1.0, eta2=1.0, alpha=alpha, hrs=1,
+                        lam_x=lam_age, lam_y=lam_bmi, lam_s=lam_age, lam_o=lam_bmi, lam_r=lam_r,
+                        delta=delta, nsim=nsim, X=X.data_ptr(), Y=Y.data_ptr(), xy_stride=0,
+                        perm=perm.data_ptr(), lap_ni_x=lx.data_ptr(), lap_ni_y=ly.data_ptr(),
+                        lap_local=ll.data_ptr(), lap_central=lc.data_ptr(), mix_z=mz.data_ptr(),
+                        mix_l=ml.data_ptr())
+    _lib.check(_lib.lib.dcor_premat_subg_panel_launch(C.byref(d), pn, C.c_void_p(out.data_ptr()), sp))
+
+
 def hrs_replicates(age_z, bmi_z, lam_age, lam_bmi, eps, reps, seed_ni=NI_SEED, seed_int=INT_SEED,
                    nsim=2000, rep_begin=0, chunk=8192, alpha=0.05, keep_noise=False, rng="philox",
                    eps_idx=None, mode="premat"):
@@ -156,20 +190,9 @@ def hrs_replicates(age_z, bmi_z, lam_age, lam_bmi, eps, reps, seed_ni=NI_SEED, s
                                                     si.ctypes.data_as(I32), P(perm), P(lx), P(ly),
                                                     P(ll), P(lc), P(mz), P(ml), sp))
             else:
-                chk(_lib.lib.dcor_perm_launch(seed_ni, _lib.SITE_PERM, rb, nr, n, k * m, P(perm), sp))
-                chk(_lib.lib.dcor_draws_launch(DRAW_LAPLACE, seed_ni, SITE_NI_LAP_X, rb, nr, k, P(lx), sp))
-                chk(_lib.lib.dcor_draws_launch(DRAW_LAPLACE, seed_ni, SITE_NI_LAP_Y, rb, nr, k, P(ly), sp))
-                chk(_lib.lib.dcor_draws_launch(DRAW_LAPLACE, seed_int, SITE_INT_LOCAL, rb, nr, n, P(ll), sp))
-                chk(_lib.lib.dcor_draws_launch(DRAW_LAPLACE, seed_int, SITE_INT_CENTRAL, rb, nr, 1, P(lc), sp))
-                chk(_lib.lib.dcor_draws_launch(DRAW_NORMAL, seed_int, SITE_MIX_Z, rb, nr, nsim, P(mz), sp))
-                chk(_lib.lib.dcor_draws_launch(DRAW_LAPLACE, seed_int, SITE_MIX_L, rb, nr, nsim, P(ml), sp))
-            d = _lib.PrematSubg(n=n, reps=nr, eps1=eps, eps2=eps, eta1=1.0, eta2=1.0, alpha=alpha, hrs=1,
-                                lam_x=lam_age, lam_y=lam_bmi, lam_s=lam_age, lam_o=lam_bmi, lam_r=lam_r,
-                                delta=delta, nsim=nsim, X=X.data_ptr(), Y=Y.data_ptr(), xy_stride=0,
-                                perm=perm.data_ptr(), lap_ni_x=lx.data_ptr(), lap_ni_y=ly.data_ptr(),
-                                lap_local=ll.data_ptr(), lap_central=lc.data_ptr(), mix_z=mz.data_ptr(),
-                                mix_l=ml.data_ptr())
-            chk(_lib.lib.dcor_premat_subg_panel_launch(C.byref(d), pn, P(out[r0:]), sp))
+                _philox_draws(seed_ni, seed_int, rb, nr, n, k, m, nsim, (perm, lx, ly, ll, lc, mz, ml), sp)
+            _premat_launch(X, Y, pn, n, nr, eps, lam_age, lam_bmi, lam_r, delta, nsim, alpha,
+                           (perm, lx, ly, ll, lc, mz, ml), out[r0:], sp)
             if keep_noise:
                 for key, t in (("perm", perm), ("lap_x", lx), ("lap_y", ly), ("lap_local", ll),
                                ("lap_central", lc), ("mix_z", mz), ("mix_l", ml)):
@@ -192,12 +215,73 @@ def _summ(method, eps, hat, lo, hi) -> dict:
             "ci_low_q10": q(lo, 0.10), "ci_high_q90": q(hi, 0.90)}
 
 
+def sweep_segments(age_z, bmi_z, lam_age, lam_bmi, eps_grid, segs, nsim=2000, alpha=0.05, streams=4):
+    """Philox pre-materialised runs of several (eps index 0-based, first run, count) segments of
+    an eps sweep on one shared panel -> [sum(count), 6] float64 in segment order.  Each segment's
+    runs equal hrs_replicates(eps_grid[e], count, seed_ni=10 + 1000 idx, seed_int=20 + 1000 idx,
+    rep_begin=first) byte for byte (idx = e + 1; same launches on the same inputs), but the panel
+    is uploaded and encoded once, the segments' launch chains are spread over `streams` HIP
+    streams so a sweep's small launches (200 runs per eps at BASELINE's R) overlap on the chip,
+    and the host waits once at the end instead of once per eps."""
+    import ctypes as C
+
+    import torch
+
+    from . import _lib, api
+    X = torch.as_tensor(np.ascontiguousarray(age_z, dtype=np.float64), device="cuda")
+    Y = torch.as_tensor(np.ascontiguousarray(bmi_z, dtype=np.float64), device="cuda")
+    n = int(X.shape[0])
+    total = sum(c for _, _, c in segs)
+    main = torch.cuda.current_stream()
+    pn = C.c_void_p()
+    _lib.check(_lib.lib.dcor_panel_create(C.c_void_p(X.data_ptr()), C.c_void_p(Y.data_ptr()), n,
+                                          C.c_void_p(main.cuda_stream), C.byref(pn)))
+    out = torch.empty((max(total, 1), 6), dtype=torch.float64, device="cuda")
+    side = [torch.cuda.Stream() for _ in range(max(1, streams))] if streams > 1 else [main]
+    f64 = dict(dtype=torch.float64, device="cuda")
+    try:
+        for s in side:
+            s.wait_stream(main)                  # X, Y, the panel and out exist before any launch
+        row = 0
+        for j, (e, r0, c) in enumerate(segs):
+            eps, idx = eps_grid[e], e + 1
+            k, m = api.batch_geometry(n, eps, eps, "subG", hrs=True)
+            delta = 1.0 / n
+            lam_r = api.lambda_receiver_from_noise(lam_age, lam_bmi, eps, delta)
+            s = side[j % len(side)]
+            sp = C.c_void_p(s.cuda_stream)
+            with torch.cuda.stream(s):           # the noise buffers belong to s: reuse is s-ordered
+                for q0 in range(0, c, 8192):
+                    nr = min(8192, c - q0)
+                    bufs = (torch.empty((nr, k * m), dtype=torch.int32, device="cuda"),
+                            torch.empty((nr, k), **f64), torch.empty((nr, k), **f64),
+                            torch.empty((nr, n), **f64), torch.empty((nr,), **f64),
+                            torch.empty((nr, nsim), **f64), torch.empty((nr, nsim), **f64))
+                    _philox_draws(10 + 1000 * idx, 20 + 1000 * idx, r0 + q0, nr, n, k, m, nsim, bufs, sp)
+                    _premat_launch(X, Y, pn, n, nr, eps, lam_age, lam_bmi, lam_r, delta, nsim, alpha,
+                                   bufs, out[row + q0:], sp)
+            row += c
+        for s in side:
+            main.wait_stream(s)
+        res = out[:total].cpu().numpy()
+    finally:
+        for s in side:
+            s.synchronize()
+        _lib.lib.dcor_panel_destroy(pn)
+    return res
+
+
 def eps_sweep(age_z, bmi_z, lam_age, lam_bmi, eps_grid=EPS_GRID, reps=R_PER_EPS, nsim=2000,
-              rng="philox"):
+              rng="philox", streams=4):
     """The replicate sweep of real-data-sims.R:345-448: for every eps in seq(.25, 2.5, .1),
     `reps` NI and INT runs (Philox keys 10 + 1000 idx and 20 + 1000 idx, idx 1-based as
     which(eps_grid == eps); rng='R': the reference's own per-run set.seed streams) and the
-    per-eps summaries ni_mean / int_mean."""
+    per-eps summaries ni_mean / int_mean.  rng='philox' runs every eps on one encoded panel
+    over `streams` HIP streams (sweep_segments); the runs equal one hrs_replicates call per eps."""
+    if rng == "philox":
+        segs = [(e, 0, reps) for e in range(len(eps_grid))]
+        runs = sweep_segments(age_z, bmi_z, lam_age, lam_bmi, eps_grid, segs, nsim=nsim, streams=streams)
+        return sweep_summaries(eps_grid, runs.reshape(len(eps_grid), reps, 6))
     runs = [hrs_replicates(age_z, bmi_z, lam_age, lam_bmi, eps, reps, seed_ni=10 + 1000 * idx,
                            seed_int=20 + 1000 * idx, nsim=nsim, rng=rng, eps_idx=idx)
             for idx, eps in enumerate(eps_grid, start=1)]
@@ -206,7 +290,22 @@ def eps_sweep(age_z, bmi_z, lam_age, lam_bmi, eps_grid=EPS_GRID, reps=R_PER_EPS,
 
 def sweep_summaries(eps_grid, runs) -> dict:
     """The sweep's per-eps summaries from its runs [n_eps, reps, 6] (real-data-sims.R:408-437);
-    dcor.dist.eps_sweep_distributed builds the same from the ranks' gathered runs."""
-    ni_mean = [_summ("NI", eps, r[:, 0], r[:, 1], r[:, 2]) for eps, r in zip(eps_grid, runs)]
-    int_mean = [_summ("INT", eps, r[:, 3], r[:, 4], r[:, 5]) for eps, r in zip(eps_grid, runs)]
+    dcor.dist.eps_sweep_distributed builds the same from the ranks' gathered runs.  Vectorised over
+    eps; every value equals _summ's per-eps one (same reductions along contiguous rows)."""
+    runs = np.asarray(runs, dtype=np.float64)
+    cols = [np.ascontiguousarray(runs[:, :, j]) for j in range(6)]     # [n_eps, reps] each
+    mean = [c.mean(axis=1) for c in cols]
+
+    def q(c, p):                                                       # type 7; a NaN row -> NaN
+        v = np.quantile(c, p, axis=1) if c.shape[1] else np.full(c.shape[0], np.nan)
+        return np.where(np.isnan(c).any(axis=1), np.nan, v)
+    lo_q = {1: q(cols[1], 0.10), 4: q(cols[4], 0.10)}
+    hi_q = {2: q(cols[2], 0.90), 5: q(cols[5], 0.90)}
+
+    def summ(method, j, i, eps):
+        return {"method": method, "eps_corr": eps, "rho_hat_mean": float(mean[j][i]),
+                "ci_low_mean": float(mean[j + 1][i]), "ci_high_mean": float(mean[j + 2][i]),
+                "ci_low_q10": float(lo_q[j + 1][i]), "ci_high_q90": float(hi_q[j + 2][i])}
+    ni_mean = [summ("NI", 0, i, eps) for i, eps in enumerate(eps_grid)]
+    int_mean = [summ("INT", 3, i, eps) for i, eps in enumerate(eps_grid)]
     return {"eps": list(eps_grid), "runs": runs, "ni_mean": ni_mean, "int_mean": int_mean}

@@ -137,6 +137,38 @@ def test_eps_sweep_summaries(panel):
     assert [round(e, 2) for e in hrs.EPS_GRID][:3] == [0.25, 0.35, 0.45] and len(hrs.EPS_GRID) == 23
 
 
+@pytest.mark.parametrize("kind", ["coded", "continuous"])
+def test_sweep_segments_equal_per_eps_calls(panel, kind):
+    """hrs.sweep_segments (one encoded panel, launch chains spread over HIP streams, one wait)
+    equals one hrs_replicates call per segment with the sweep's keys, byte for byte, whatever the
+    number of streams; segments start mid-eps (rep_begin > 0) as a rank's shard does."""
+    from dcor import hrs
+    z = panel if kind == "coded" else _continuous(2501, seed=9)
+    args = (z["age_z"], z["bmi_z"], z["lambda_age_z"], z["lambda_bmi_z"])
+    grid = (0.25, 1.05, 2.45)
+    segs = [(0, 3, 5), (1, 0, 7), (2, 2, 1), (0, 8, 2), (1, 7, 3)]
+    want = np.concatenate([hrs.hrs_replicates(*args, grid[e], c, seed_ni=10 + 1000 * (e + 1),
+                                              seed_int=20 + 1000 * (e + 1), rep_begin=r0)
+                           for e, r0, c in segs])
+    for streams in (1, 4):
+        got = hrs.sweep_segments(*args, grid, segs, streams=streams)
+        np.testing.assert_array_equal(got.view(np.int64), want.view(np.int64), err_msg=f"streams={streams}")
+    sw = hrs.eps_sweep(*args, eps_grid=grid, reps=4)
+    one = np.stack([hrs.hrs_replicates(*args, e, 4, seed_ni=10 + 1000 * i, seed_int=20 + 1000 * i)
+                    for i, e in enumerate(grid, start=1)])
+    np.testing.assert_array_equal(sw["runs"].view(np.int64), one.view(np.int64))
+
+
+def test_sweep_segments_past_one_launch(panel):
+    """A segment longer than one launch (8192 runs) splits like hrs_replicates' chunks."""
+    from dcor import hrs
+    z = panel
+    args = (z["age_z"], z["bmi_z"], z["lambda_age_z"], z["lambda_bmi_z"])
+    got = hrs.sweep_segments(*args, (2.0,), [(0, 5, 8195)], streams=2)
+    want = hrs.hrs_replicates(*args, 2.0, 8195, seed_ni=1010, seed_int=1020, rep_begin=5)
+    np.testing.assert_array_equal(got.view(np.int64), want.view(np.int64))
+
+
 def test_panel_pipelined_halves_bitexact(panel):
     """Large coded-panel launches split into two stream-pipelined halves; the result must
     equal the single-stream launch bit for bit."""

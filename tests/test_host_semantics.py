@@ -42,6 +42,25 @@ def test_eps_grid_is_r_seq_arithmetic():
     assert hrs.EPS_GRID[6] == 0.8500000000000001
 
 
+@pytest.mark.parametrize("R", [200, 7, 1])
+def test_sweep_summaries_equal_per_eps_summaries(R):
+    """The vectorised sweep summaries equal the per-eps means and type-7 quantiles of
+    real-data-sims.R:408-437 (hrs._summ) exactly, NaN rows included."""
+    from dcor import hrs
+    g = np.random.default_rng(R)
+    runs = g.standard_normal((23, R, 6)) * 3
+    runs[4, min(3, R - 1), 1] = np.nan
+    runs[9, 0, 5] = np.nan
+    runs[11, 0, 0] = np.nan
+    out = hrs.sweep_summaries(hrs.EPS_GRID, runs)
+    for i, (e, r) in enumerate(zip(hrs.EPS_GRID, runs)):
+        for want, got in ((hrs._summ("NI", e, r[:, 0], r[:, 1], r[:, 2]), out["ni_mean"][i]),
+                          (hrs._summ("INT", e, r[:, 3], r[:, 4], r[:, 5]), out["int_mean"][i])):
+            assert want.keys() == got.keys()
+            for k, v in want.items():
+                assert v == got[k] or (isinstance(v, float) and math.isnan(v) and math.isnan(got[k])), (i, k)
+
+
 @pytest.mark.parametrize("kw", [dict(rng="R", mode="fused", eps_idx=1),
                                 dict(mode="fused", keep_noise=True),
                                 dict(rng="mt"), dict(mode="stream"), dict(rng="R")])
