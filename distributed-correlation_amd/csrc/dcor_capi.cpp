@@ -1033,23 +1033,73 @@ struct dcor_panel {
 static int premat_subg_run(const dcor_premat_subg* d, const dcor_panel* panel, dcor_rep_out* d_out,
                            void* stream);
 
+// The Philox noise of HRS replicates materialised in HBM (the dcor_perm_launch /
+// dcor_draws_launch sites of the fused kernel's contract), then the pre-materialised panel
+// kernels: the pipeline of dcor.hrs.hrs_replicates(rng='philox', mode='premat'), natively.
+// hrs_noise_per: bytes of one replicate's noise; hrs_premat_chunks runs d->reps replicates in
+// chunks of cr over the caller's stream-ordered buffer of per * cr bytes.
+static size_t hrs_al(size_t b) { return (b + 255) & ~(size_t)255; }
+
+static int hrs_noise_geometry(const dcor_premat_subg* d, int64_t* k, int64_t* m, size_t* per) {
+  int64_t km[2];
+  if (int st = dcor_batch_geometry(d->n, d->eps1, d->eps2, DCOR_FAMILY_SUBG, 1, km)) return st;
+  *k = km[0]; *m = km[1];
+  *per = hrs_al((size_t)km[0] * km[1] * 4) + 2 * hrs_al((size_t)km[0] * 8) +
+         hrs_al((size_t)d->n * 8) + 256 + 2 * hrs_al((size_t)d->nsim * 8);
+  return DCOR_OK;
+}
+
+static int hrs_premat_chunks(const dcor_premat_subg* d, const dcor_panel* panel, uint64_t seed_ni,
+                             uint64_t seed_int, int64_t rep_begin, dcor_rep_out* d_out, char* buf,
+                             int64_t cr, int64_t k, int64_t m, void* stream) {
+  const int64_t n = d->n, ns = d->nsim;
+  int32_t* perm = (int32_t*)buf;
+  double* lx = (double*)(buf + hrs_al((size_t)cr * k * m * 4));
+  double* ly = lx + (hrs_al((size_t)cr * k * 8) / 8);
+  double* ll = ly + (hrs_al((size_t)cr * k * 8) / 8);
+  double* lc = ll + (hrs_al((size_t)cr * n * 8) / 8);
+  double* mz = lc + (hrs_al((size_t)cr * 8) / 8);
+  double* ml = mz + (hrs_al((size_t)cr * ns * 8) / 8);
+  const uint32_t n0 = (uint32_t)seed_ni, n1 = (uint32_t)(seed_ni >> 32);
+  const uint32_t i0 = (uint32_t)seed_int, i1 = (uint32_t)(seed_int >> 32);
+  for (int64_t r0 = 0; r0 < d->reps; r0 += cr) {
+    const int64_t nr = d->reps - r0 < cr ? d->reps - r0 : cr, rb = rep_begin + r0;
+    int rc = launch_perm(n0, n1, DCOR_SITE_PERM, rb, nr, n, k * m, perm, stream);
+    if (!rc) rc = launch_draws(0, n0, n1, 11, rb, nr, k, lx, stream);
+    if (!rc) rc = launch_draws(0, n0, n1, 12, rb, nr, k, ly, stream);
+    if (!rc) rc = launch_draws(0, i0, i1, 13, rb, nr, n, ll, stream);
+    if (!rc) rc = launch_draws(0, i0, i1, 14, rb, nr, 1, lc, stream);
+    if (!rc) rc = launch_draws(1, i0, i1, 15, rb, nr, ns, mz, stream);
+    if (!rc) rc = launch_draws(0, i0, i1, 16, rb, nr, ns, ml, stream);
+    if (rc) return hip_fail((hipError_t)rc, "hrs noise launch");
+    dcor_premat_subg q = *d;
+    q.reps = nr;
+    q.perm = perm; q.lap_ni_x = lx; q.lap_ni_y = ly; q.lap_local = ll; q.lap_central = lc;
+    q.mix_z = mz; q.mix_l = ml;
+    if (int e = premat_subg_run(&q, panel, d_out + r0, stream)) return e;
+  }
+  return DCOR_OK;
+}
+
+// chunk of replicates whose noise fits `budget` bytes, capped at `cap`
+static int64_t hrs_chunk(size_t per, int64_t reps, size_t budget, int64_t cap) {
+  int64_t cr = (int64_t)(budget / per);
+  if (cr < 1) cr = 1;
+  if (cr > cap) cr = cap;
+  return cr > reps ? reps : cr;
+}
+
 // dcor_hrs_fused_launch on an uncoded panel too large for the LDS index row (n > 65536): the
-// same Philox streams materialised per chunk (dcor_perm_launch / dcor_draws_launch sites), then
-// the pre-materialised panel kernels -- replicate r equals the fused kernel's replicate r within
-// the compensated sums' rounding, as for any panel.
+// same Philox streams materialised per chunk, then the pre-materialised panel kernels --
+// replicate r equals the fused kernel's replicate r within the compensated sums' rounding, as
+// for any panel.
 static int hrs_fused_materialised(const dcor_premat_subg* d, const dcor_panel* panel,
                                   uint64_t seed_ni, uint64_t seed_int, int64_t rep_begin,
                                   dcor_rep_out* d_out, void* stream) {
-  int64_t km[2];
-  if (int st = dcor_batch_geometry(d->n, d->eps1, d->eps2, DCOR_FAMILY_SUBG, 1, km)) return st;
-  const int64_t k = km[0], m = km[1], n = d->n, ns = d->nsim;
-  auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
-  const size_t per = al((size_t)k * m * 4) + 2 * al((size_t)k * 8) + al((size_t)n * 8) + 256 +
-                     2 * al((size_t)ns * 8);
-  int64_t cr = (int64_t)(((size_t)1 << 30) / per);
-  if (cr < 1) cr = 1;
-  if (cr > 65535) cr = 65535;
-  if (cr > d->reps) cr = d->reps;
+  int64_t k, m;
+  size_t per;
+  if (int st = hrs_noise_geometry(d, &k, &m, &per)) return st;
+  const int64_t cr = hrs_chunk(per, d->reps, (size_t)1 << 30, 65535);
   if (cr == 0) return DCOR_OK;
   char* buf = nullptr;
   const hipStream_t st = (hipStream_t)stream;
@@ -1058,38 +1108,9 @@ static int hrs_fused_materialised(const dcor_premat_subg* d, const dcor_panel* p
     return fail(DCOR_ENOMEM, "hrs_fused: cannot allocate %zu noise bytes", per * (size_t)cr);
   }
   count_alloc();
-  int32_t* perm = (int32_t*)buf;
-  double* lx = (double*)(buf + al((size_t)cr * k * m * 4));
-  double* ly = lx + (al((size_t)cr * k * 8) / 8);
-  double* ll = ly + (al((size_t)cr * k * 8) / 8);
-  double* lc = ll + (al((size_t)cr * n * 8) / 8);
-  double* mz = lc + (al((size_t)cr * 8) / 8);
-  double* ml = mz + (al((size_t)cr * ns * 8) / 8);
-  const uint32_t n0 = (uint32_t)seed_ni, n1 = (uint32_t)(seed_ni >> 32);
-  const uint32_t i0 = (uint32_t)seed_int, i1 = (uint32_t)(seed_int >> 32);
-  int rc = 0;
-  for (int64_t r0 = 0; r0 < d->reps && !rc; r0 += cr) {
-    const int64_t nr = d->reps - r0 < cr ? d->reps - r0 : cr, rb = rep_begin + r0;
-    rc = launch_perm(n0, n1, DCOR_SITE_PERM, rb, nr, n, k * m, perm, stream);
-    if (!rc) rc = launch_draws(0, n0, n1, 11, rb, nr, k, lx, stream);
-    if (!rc) rc = launch_draws(0, n0, n1, 12, rb, nr, k, ly, stream);
-    if (!rc) rc = launch_draws(0, i0, i1, 13, rb, nr, n, ll, stream);
-    if (!rc) rc = launch_draws(0, i0, i1, 14, rb, nr, 1, lc, stream);
-    if (!rc) rc = launch_draws(1, i0, i1, 15, rb, nr, ns, mz, stream);
-    if (!rc) rc = launch_draws(0, i0, i1, 16, rb, nr, ns, ml, stream);
-    if (rc) break;
-    dcor_premat_subg q = *d;
-    q.reps = nr;
-    q.perm = perm; q.lap_ni_x = lx; q.lap_ni_y = ly; q.lap_local = ll; q.lap_central = lc;
-    q.mix_z = mz; q.mix_l = ml;
-    if (int e = premat_subg_run(&q, panel, d_out + r0, stream)) {
-      (void)hipFreeAsync(buf, st);
-      return e;
-    }
-  }
+  const int e = hrs_premat_chunks(d, panel, seed_ni, seed_int, rep_begin, d_out, buf, cr, k, m, stream);
   (void)hipFreeAsync(buf, st);
-  if (rc) return hip_fail((hipError_t)rc, "hrs_fused noise launch");
-  return DCOR_OK;
+  return e;
 }
 
 extern "C" {
@@ -1198,6 +1219,62 @@ int dcor_hrs_fused_launch(const dcor_premat_subg* d, const dcor_panel* panel, ui
   (void)hipFreeAsync(part, (hipStream_t)stream);
   if (rc) return hip_fail((hipError_t)rc, "hrs_fused launch");
   return DCOR_OK;
+}
+
+int dcor_hrs_sweep_launch(const dcor_premat_subg* base, const dcor_panel* panel,
+                          const dcor_hrs_segment* segs, int64_t nseg, dcor_rep_out* d_out,
+                          void* stream) {
+  if (!base || !panel || nseg < 0 || (nseg > 0 && (!segs || !d_out)))
+    return fail(DCOR_EINVAL, "hrs_sweep: null argument");
+  if (base->X != panel->X || base->Y != panel->Y || base->xy_stride != 0 || base->n != panel->n)
+    return fail(DCOR_EINVAL, "hrs_sweep: X, Y, n must be the panel's and xy_stride 0");
+  if (!base->hrs) return fail(DCOR_EINVAL, "hrs_sweep: the HRS variant only (hrs = 1)");
+  if (!(base->delta > 0.0)) return fail(DCOR_EINVAL, "hrs_sweep: delta must be positive");
+  // every segment's geometry first: nothing is enqueued for an invalid sweep
+  std::vector<dcor_premat_subg> qs((size_t)nseg);
+  std::vector<int64_t> ks((size_t)nseg), ms((size_t)nseg);
+  size_t need = 0;
+  int64_t cap = 0;
+  const size_t budget = (size_t)1 << 30;
+  for (int64_t i = 0; i < nseg; ++i) {
+    const dcor_hrs_segment& g = segs[i];
+    if (g.reps < 0 || g.rep_begin < 0 || g.out_row < 0 || !(g.eps > 0.0))
+      return fail(DCOR_EINVAL, "hrs_sweep: segment %lld: need eps > 0, reps, rep_begin, out_row >= 0",
+                  (long long)i);
+    dcor_premat_subg& q = qs[(size_t)i];
+    q = *base;
+    q.reps = g.reps;
+    q.eps1 = q.eps2 = g.eps;
+    q.eta1 = q.eta2 = 1.0;
+    q.lam_r = dcor_lambda_receiver_from_noise(base->lam_s, base->lam_o, g.eps, base->delta);
+    size_t per;
+    if (int st = hrs_noise_geometry(&q, &ks[(size_t)i], &ms[(size_t)i], &per)) return st;
+    const int64_t cr = hrs_chunk(per, g.reps, budget, 65535);
+    need = std::max(need, per * (size_t)cr);
+    cap = std::max(cap, cr);
+  }
+  if (need == 0) return DCOR_OK;
+  if (int st = need_device()) return st;
+  char* buf = nullptr;
+  const hipStream_t st = (hipStream_t)stream;
+  if (hipMallocAsync((void**)&buf, need, st) != hipSuccess) {
+    (void)hipGetLastError();
+    return fail(DCOR_ENOMEM, "hrs_sweep: cannot allocate %zu noise bytes", need);
+  }
+  count_alloc();
+  int e = DCOR_OK;
+  for (int64_t i = 0; i < nseg && !e; ++i) {
+    const dcor_hrs_segment& g = segs[i];
+    if (g.reps == 0) continue;
+    size_t per;
+    int64_t k, m;
+    if ((e = hrs_noise_geometry(&qs[(size_t)i], &k, &m, &per))) break;
+    const int64_t cr = hrs_chunk(per, g.reps, budget, 65535);
+    e = hrs_premat_chunks(&qs[(size_t)i], panel, g.seed_ni, g.seed_int, g.rep_begin,
+                          d_out + g.out_row, buf, cr, k, m, stream);
+  }
+  (void)hipFreeAsync(buf, st);
+  return e;
 }
 
 }  // extern "C" (reopened below)

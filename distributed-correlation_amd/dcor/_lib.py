@@ -89,6 +89,12 @@ class PrematSubg(C.Structure):
     ]
 
 
+class HrsSegment(C.Structure):
+    """dcor_hrs_segment (include/dcor.h): one (eps, keys, replicate range, output row) of a sweep."""
+    _fields_ = [("eps", C.c_double), ("seed_ni", C.c_uint64), ("seed_int", C.c_uint64),
+                ("rep_begin", C.c_int64), ("reps", C.c_int64), ("out_row", C.c_int64)]
+
+
 _D = C.POINTER(C.c_double)
 _I64 = C.POINTER(C.c_int64)
 
@@ -144,6 +150,8 @@ SIGNATURES = {
     "dcor_premat_subg_panel_launch": (C.c_int, [C.POINTER(PrematSubg), _P, _P, _P]),
     "dcor_hrs_fused_launch": (C.c_int, [C.POINTER(PrematSubg), _P, C.c_uint64, C.c_uint64,
                                         C.c_int64, _P, _P]),
+    "dcor_hrs_sweep_launch": (C.c_int, [C.POINTER(PrematSubg), _P, C.POINTER(HrsSegment), C.c_int64,
+                                        _P, _P]),
     "dcor_batch_geometry": (C.c_int, [C.c_int64, C.c_double, C.c_double, C.c_int, C.c_int, _I64]),
     "dcor_ci_ni_signbatch": (C.c_int, [_D, _D, C.c_int64, C.c_double, C.c_double, C.c_double,
                                        C.c_int, _D, _D, _D, _D]),

@@ -215,54 +215,50 @@ def _summ(method, eps, hat, lo, hi) -> dict:
             "ci_low_q10": q(lo, 0.10), "ci_high_q90": q(hi, 0.90)}
 
 
-def sweep_segments(age_z, bmi_z, lam_age, lam_bmi, eps_grid, segs, nsim=2000, alpha=0.05, streams=4):
+def sweep_segments(age_z, bmi_z, lam_age, lam_bmi, eps_grid, segs, nsim=2000, alpha=0.05, streams=1):
     """Philox pre-materialised runs of several (eps index 0-based, first run, count) segments of
     an eps sweep on one shared panel -> [sum(count), 6] float64 in segment order.  Each segment's
     runs equal hrs_replicates(eps_grid[e], count, seed_ni=10 + 1000 idx, seed_int=20 + 1000 idx,
-    rep_begin=first) byte for byte (idx = e + 1; same launches on the same inputs), but the panel
-    is uploaded and encoded once, the segments' launch chains are spread over `streams` HIP
-    streams so a sweep's small launches (200 runs per eps at BASELINE's R) overlap on the chip,
-    and the host waits once at the end instead of once per eps."""
+    rep_begin=first) byte for byte (idx = e + 1; the same draws and kernels), but the panel is
+    uploaded and encoded once and the per-eps launch chains run from one native call
+    (dcor_hrs_sweep_launch) instead of eight launches from Python per eps; with streams > 1 the
+    segments are dealt round-robin over that many HIP streams, one native call each.  The host
+    waits once, at the end."""
     import ctypes as C
 
     import torch
 
-    from . import _lib, api
+    from . import _lib
     X = torch.as_tensor(np.ascontiguousarray(age_z, dtype=np.float64), device="cuda")
     Y = torch.as_tensor(np.ascontiguousarray(bmi_z, dtype=np.float64), device="cuda")
     n = int(X.shape[0])
-    total = sum(c for _, _, c in segs)
+    rows = np.cumsum([0] + [c for _, _, c in segs])
+    total = int(rows[-1])
     main = torch.cuda.current_stream()
     pn = C.c_void_p()
     _lib.check(_lib.lib.dcor_panel_create(C.c_void_p(X.data_ptr()), C.c_void_p(Y.data_ptr()), n,
                                           C.c_void_p(main.cuda_stream), C.byref(pn)))
     out = torch.empty((max(total, 1), 6), dtype=torch.float64, device="cuda")
-    side = [torch.cuda.Stream() for _ in range(max(1, streams))] if streams > 1 else [main]
-    f64 = dict(dtype=torch.float64, device="cuda")
+    base = _lib.PrematSubg(n=n, reps=0, eps1=1.0, eps2=1.0, eta1=1.0, eta2=1.0, alpha=alpha, hrs=1,
+                           lam_x=lam_age, lam_y=lam_bmi, lam_s=lam_age, lam_o=lam_bmi, lam_r=float("nan"),
+                           delta=1.0 / n, nsim=nsim, X=X.data_ptr(), Y=Y.data_ptr(), xy_stride=0)
+    arr = (_lib.HrsSegment * max(1, len(segs)))()
+    for j, (e, r0, c) in enumerate(segs):
+        arr[j] = _lib.HrsSegment(eps=eps_grid[e], seed_ni=10 + 1000 * (e + 1), seed_int=20 + 1000 * (e + 1),
+                                 rep_begin=r0, reps=c, out_row=int(rows[j]))
+    ns = max(1, min(streams, len(segs)))
+    side = [torch.cuda.Stream() for _ in range(ns)] if ns > 1 else [main]
     try:
+        for j, s in enumerate(side):
+            if s is not main:
+                s.wait_stream(main)              # X, Y, the panel and out exist before any launch
+            mine = list(range(j, len(segs), ns))
+            part = (_lib.HrsSegment * max(1, len(mine)))(*[arr[i] for i in mine])
+            _lib.check(_lib.lib.dcor_hrs_sweep_launch(C.byref(base), pn, part, len(mine),
+                                                      C.c_void_p(out.data_ptr()), C.c_void_p(s.cuda_stream)))
         for s in side:
-            s.wait_stream(main)                  # X, Y, the panel and out exist before any launch
-        row = 0
-        for j, (e, r0, c) in enumerate(segs):
-            eps, idx = eps_grid[e], e + 1
-            k, m = api.batch_geometry(n, eps, eps, "subG", hrs=True)
-            delta = 1.0 / n
-            lam_r = api.lambda_receiver_from_noise(lam_age, lam_bmi, eps, delta)
-            s = side[j % len(side)]
-            sp = C.c_void_p(s.cuda_stream)
-            with torch.cuda.stream(s):           # the noise buffers belong to s: reuse is s-ordered
-                for q0 in range(0, c, 8192):
-                    nr = min(8192, c - q0)
-                    bufs = (torch.empty((nr, k * m), dtype=torch.int32, device="cuda"),
-                            torch.empty((nr, k), **f64), torch.empty((nr, k), **f64),
-                            torch.empty((nr, n), **f64), torch.empty((nr,), **f64),
-                            torch.empty((nr, nsim), **f64), torch.empty((nr, nsim), **f64))
-                    _philox_draws(10 + 1000 * idx, 20 + 1000 * idx, r0 + q0, nr, n, k, m, nsim, bufs, sp)
-                    _premat_launch(X, Y, pn, n, nr, eps, lam_age, lam_bmi, lam_r, delta, nsim, alpha,
-                                   bufs, out[row + q0:], sp)
-            row += c
-        for s in side:
-            main.wait_stream(s)
+            if s is not main:
+                main.wait_stream(s)
         res = out[:total].cpu().numpy()
     finally:
         for s in side:
@@ -272,12 +268,12 @@ def sweep_segments(age_z, bmi_z, lam_age, lam_bmi, eps_grid, segs, nsim=2000, al
 
 
 def eps_sweep(age_z, bmi_z, lam_age, lam_bmi, eps_grid=EPS_GRID, reps=R_PER_EPS, nsim=2000,
-              rng="philox", streams=4):
+              rng="philox", streams=1):
     """The replicate sweep of real-data-sims.R:345-448: for every eps in seq(.25, 2.5, .1),
     `reps` NI and INT runs (Philox keys 10 + 1000 idx and 20 + 1000 idx, idx 1-based as
     which(eps_grid == eps); rng='R': the reference's own per-run set.seed streams) and the
-    per-eps summaries ni_mean / int_mean.  rng='philox' runs every eps on one encoded panel
-    over `streams` HIP streams (sweep_segments); the runs equal one hrs_replicates call per eps."""
+    per-eps summaries ni_mean / int_mean.  rng='philox' runs every eps on one encoded panel from
+    one native call per HIP stream (sweep_segments); the runs equal one hrs_replicates call per eps."""
     if rng == "philox":
         segs = [(e, 0, reps) for e in range(len(eps_grid))]
         runs = sweep_segments(age_z, bmi_z, lam_age, lam_bmi, eps_grid, segs, nsim=nsim, streams=streams)

@@ -335,6 +335,27 @@ int dcor_premat_subg_panel_launch(const dcor_premat_subg* d, const dcor_panel* p
 int dcor_hrs_fused_launch(const dcor_premat_subg* d, const dcor_panel* panel, uint64_t seed_ni,
                           uint64_t seed_int, int64_t rep_begin, dcor_rep_out* d_out, void* stream);
 
+/* Segments of the HRS eps sweep (real-data-sims.R:345-448: for each eps, R NI runs under
+ * set.seed(10 + 37 rep + 1000 idx) and R INT runs under set.seed(20 + 41 rep + 1000 idx),
+ * :402-437) on one prepared panel, pre-materialised: for every segment, replicates rep_begin ..
+ * rep_begin + reps - 1 at eps1 = eps2 = eps with Philox keys seed_ni / seed_int, their noise
+ * drawn into a stream-ordered buffer (the dcor_perm_launch / dcor_draws_launch sites listed for
+ * dcor_hrs_fused_launch) and run by dcor_premat_subg_panel_launch, records to d_out[out_row ..].
+ * Each record equals the same replicate of dcor_premat_subg_panel_launch on those draws bit for
+ * bit (the host loop of dcor.hrs.hrs_replicates, run natively; one host call per sweep instead
+ * of eight launches from the host per eps).  base supplies n, X, Y (the panel's), alpha, nsim,
+ * hrs = 1, lam_x / lam_y (NI) and lam_s / lam_o (INT) and delta > 0; per segment eta = 1 and
+ * lam_r = dcor_lambda_receiver_from_noise(lam_s, lam_o, eps, delta).  Every segment is
+ * checked before anything is enqueued. */
+typedef struct dcor_hrs_segment {
+  double eps;
+  uint64_t seed_ni, seed_int;
+  int64_t rep_begin, reps, out_row;
+} dcor_hrs_segment;
+int dcor_hrs_sweep_launch(const dcor_premat_subg* base, const dcor_panel* panel,
+                          const dcor_hrs_segment* segs, int64_t nseg, dcor_rep_out* d_out,
+                          void* stream);
+
 int dcor_premat_sign_launch(const dcor_premat_sign* d, dcor_rep_out* d_out, void* stream);
 int dcor_premat_subg_launch(const dcor_premat_subg* d, dcor_rep_out* d_out, void* stream);
 

@@ -44,7 +44,8 @@ def test_struct_layout_matches_header():
     from dcor import _lib
     structs = {"dcor_cell": _lib.Cell, "dcor_rep_out": _lib.RepOut, "dcor_accum": _lib.Accum,
                "dcor_summary": _lib.Summary, "dcor_premat_sign": _lib.PrematSign,
-               "dcor_premat_subg": _lib.PrematSubg, "dcor_rs_draws": _lib.RsDraws}
+               "dcor_premat_subg": _lib.PrematSubg, "dcor_rs_draws": _lib.RsDraws,
+               "dcor_hrs_segment": _lib.HrsSegment}
     lines = ['#include <stdio.h>', '#include <stddef.h>', f'#include "{HEADER}"', "int main(void){"]
     for cname, py in structs.items():
         lines.append(f'printf("{cname} %zu\\n", sizeof({cname}));')
@@ -113,6 +114,15 @@ def test_argument_validation_without_gpu():
         dcor.ci_INT_signflip(np.ones(3), np.ones(4), 1.0, 1.0)
     with pytest.raises(dcor.DcorError):
         dcor.ci_INT_signflip(np.ones(3), np.ones(3), 0.0, 1.0)
+
+
+def test_hrs_sweep_argument_checks_without_gpu():
+    """dcor_hrs_sweep_launch rejects null arguments before any device access."""
+    from dcor import _lib
+    base = _lib.PrematSubg(n=10, hrs=1, delta=0.1, nsim=10)
+    seg = (_lib.HrsSegment * 1)(_lib.HrsSegment(eps=1.0, reps=1))
+    assert _lib.lib.dcor_hrs_sweep_launch(None, None, seg, 1, C.c_void_p(8), None) == _lib.DCOR_EINVAL
+    assert _lib.lib.dcor_hrs_sweep_launch(C.byref(base), None, seg, 1, C.c_void_p(8), None) == _lib.DCOR_EINVAL
 
 
 def test_accum_merge_and_finalize_host():
