@@ -396,7 +396,7 @@ def c5_fused(R, panel="coded"):
 
 def hrs_sweep(R):
     """a19: the HRS eps sweep of real-data-sims.R:345-448 (23 eps x R runs, Philox per-eps keys,
-    premat pipeline, the eps over HIP streams) on one GPU, summaries built on the host."""
+    premat pipeline, one native launch chain) on one GPU, summaries built on the host."""
     import numpy as np
     import torch
     from dcor import hrs
@@ -410,7 +410,7 @@ def hrs_sweep(R):
     total = len(hrs.EPS_GRID) * R
     line("HS", replicates=total, seconds=t, reps_per_s=total / t, finite=bool(np.isfinite(res["runs"]).all()),
          note="23 eps x R NI + INT runs on the coded stand-in panel, encoded once, the eps' launch chains "
-              "over 4 HIP streams (hrs.sweep_segments), summaries (means, type-7 quantiles) on the host")
+              "from one native call (hrs.sweep_segments), summaries (means, type-7 quantiles) on the host")
 
 
 def subg():

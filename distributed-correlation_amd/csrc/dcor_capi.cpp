@@ -1031,11 +1031,11 @@ struct dcor_panel {
 };
 
 static int premat_subg_run(const dcor_premat_subg* d, const dcor_panel* panel, dcor_rep_out* d_out,
-                           void* stream);
+                           void* stream, void* scratch = nullptr, size_t scratch_b = 0);
 
 // The Philox noise of HRS replicates materialised in HBM (the dcor_perm_launch /
-// dcor_draws_launch sites of the fused kernel's contract), then the pre-materialised panel
-// kernels: the pipeline of dcor.hrs.hrs_replicates(rng='philox', mode='premat'), natively.
+// dcor_draws_launch sites of the fused kernel's contract, all seven arrays from one
+// launch_hrs_noise), then the pre-materialised panel kernels: the pipeline of dcor.hrs.hrs_replicates(rng='philox', mode='premat'), natively.
 // hrs_noise_per: bytes of one replicate's noise; hrs_premat_chunks runs d->reps replicates in
 // chunks of cr over the caller's stream-ordered buffer of per * cr bytes.
 static size_t hrs_al(size_t b) { return (b + 255) & ~(size_t)255; }
@@ -1051,7 +1051,8 @@ static int hrs_noise_geometry(const dcor_premat_subg* d, int64_t* k, int64_t* m,
 
 static int hrs_premat_chunks(const dcor_premat_subg* d, const dcor_panel* panel, uint64_t seed_ni,
                              uint64_t seed_int, int64_t rep_begin, dcor_rep_out* d_out, char* buf,
-                             int64_t cr, int64_t k, int64_t m, void* stream) {
+                             int64_t cr, int64_t k, int64_t m, void* stream,
+                             void* scratch = nullptr, size_t scratch_b = 0) {
   const int64_t n = d->n, ns = d->nsim;
   int32_t* perm = (int32_t*)buf;
   double* lx = (double*)(buf + hrs_al((size_t)cr * k * m * 4));
@@ -1060,23 +1061,15 @@ static int hrs_premat_chunks(const dcor_premat_subg* d, const dcor_panel* panel,
   double* lc = ll + (hrs_al((size_t)cr * n * 8) / 8);
   double* mz = lc + (hrs_al((size_t)cr * 8) / 8);
   double* ml = mz + (hrs_al((size_t)cr * ns * 8) / 8);
-  const uint32_t n0 = (uint32_t)seed_ni, n1 = (uint32_t)(seed_ni >> 32);
-  const uint32_t i0 = (uint32_t)seed_int, i1 = (uint32_t)(seed_int >> 32);
   for (int64_t r0 = 0; r0 < d->reps; r0 += cr) {
-    const int64_t nr = d->reps - r0 < cr ? d->reps - r0 : cr, rb = rep_begin + r0;
-    int rc = launch_perm(n0, n1, DCOR_SITE_PERM, rb, nr, n, k * m, perm, stream);
-    if (!rc) rc = launch_draws(0, n0, n1, 11, rb, nr, k, lx, stream);
-    if (!rc) rc = launch_draws(0, n0, n1, 12, rb, nr, k, ly, stream);
-    if (!rc) rc = launch_draws(0, i0, i1, 13, rb, nr, n, ll, stream);
-    if (!rc) rc = launch_draws(0, i0, i1, 14, rb, nr, 1, lc, stream);
-    if (!rc) rc = launch_draws(1, i0, i1, 15, rb, nr, ns, mz, stream);
-    if (!rc) rc = launch_draws(0, i0, i1, 16, rb, nr, ns, ml, stream);
-    if (rc) return hip_fail((hipError_t)rc, "hrs noise launch");
+    const int64_t nr = d->reps - r0 < cr ? d->reps - r0 : cr;
+    const HrsNoise j{seed_ni, seed_int, rep_begin + r0, n, k, k * m, ns, perm, lx, ly, ll, lc, mz, ml};
+    if (int rc = launch_hrs_noise(j, nr, stream)) return hip_fail((hipError_t)rc, "hrs noise launch");
     dcor_premat_subg q = *d;
     q.reps = nr;
     q.perm = perm; q.lap_ni_x = lx; q.lap_ni_y = ly; q.lap_local = ll; q.lap_central = lc;
     q.mix_z = mz; q.mix_l = ml;
-    if (int e = premat_subg_run(&q, panel, d_out + r0, stream)) return e;
+    if (int e = premat_subg_run(&q, panel, d_out + r0, stream, scratch, scratch_b)) return e;
   }
   return DCOR_OK;
 }
@@ -1235,7 +1228,8 @@ int dcor_hrs_sweep_launch(const dcor_premat_subg* base, const dcor_panel* panel,
   std::vector<int64_t> ks((size_t)nseg), ms((size_t)nseg);
   size_t need = 0;
   int64_t cap = 0;
-  const size_t budget = (size_t)1 << 30;
+  // noise of up to 8192 replicates per launch chain (C5's 8192 x 420 KB: 3.4 GB), at most 4 GB
+  const size_t budget = (size_t)4 << 30;
   for (int64_t i = 0; i < nseg; ++i) {
     const dcor_hrs_segment& g = segs[i];
     if (g.reps < 0 || g.rep_begin < 0 || g.out_row < 0 || !(g.eps > 0.0))
@@ -1249,17 +1243,21 @@ int dcor_hrs_sweep_launch(const dcor_premat_subg* base, const dcor_panel* panel,
     q.lam_r = dcor_lambda_receiver_from_noise(base->lam_s, base->lam_o, g.eps, base->delta);
     size_t per;
     if (int st = hrs_noise_geometry(&q, &ks[(size_t)i], &ms[(size_t)i], &per)) return st;
-    const int64_t cr = hrs_chunk(per, g.reps, budget, 65535);
+    const int64_t cr = hrs_chunk(per, g.reps, budget, 8192);
     need = std::max(need, per * (size_t)cr);
     cap = std::max(cap, cr);
   }
   if (need == 0) return DCOR_OK;
   if (int st = need_device()) return st;
+  // the premat launches' partials (80 B per replicate slice) and packed panel (uncoded: 32 B
+  // per sample) follow the noise: one allocation per call, reused launch after launch in
+  // stream order
+  const size_t scr_b = hrs_al((size_t)cap * 80 * DCOR_DICT_SLICES) + hrs_al((size_t)base->n * 32);
   char* buf = nullptr;
   const hipStream_t st = (hipStream_t)stream;
-  if (hipMallocAsync((void**)&buf, need, st) != hipSuccess) {
+  if (hipMallocAsync((void**)&buf, need + scr_b, st) != hipSuccess) {
     (void)hipGetLastError();
-    return fail(DCOR_ENOMEM, "hrs_sweep: cannot allocate %zu noise bytes", need);
+    return fail(DCOR_ENOMEM, "hrs_sweep: cannot allocate %zu noise bytes", need + scr_b);
   }
   count_alloc();
   int e = DCOR_OK;
@@ -1269,9 +1267,9 @@ int dcor_hrs_sweep_launch(const dcor_premat_subg* base, const dcor_panel* panel,
     size_t per;
     int64_t k, m;
     if ((e = hrs_noise_geometry(&qs[(size_t)i], &k, &m, &per))) break;
-    const int64_t cr = hrs_chunk(per, g.reps, budget, 65535);
+    const int64_t cr = hrs_chunk(per, g.reps, budget, 8192);
     e = hrs_premat_chunks(&qs[(size_t)i], panel, g.seed_ni, g.seed_int, g.rep_begin,
-                          d_out + g.out_row, buf, cr, k, m, stream);
+                          d_out + g.out_row, buf, cr, k, m, stream, buf + need, scr_b);
   }
   (void)hipFreeAsync(buf, st);
   return e;
@@ -1280,7 +1278,7 @@ int dcor_hrs_sweep_launch(const dcor_premat_subg* base, const dcor_panel* panel,
 }  // extern "C" (reopened below)
 
 static int premat_subg_run(const dcor_premat_subg* d, const dcor_panel* panel, dcor_rep_out* d_out,
-                           void* stream) {
+                           void* stream, void* scratch, size_t scratch_b) {
   if (!d || !d_out || d->reps < 0) return fail(DCOR_EINVAL, "null argument");
   if (!d->X || !d->Y || !d->lap_ni_x || !d->lap_ni_y || !d->lap_local || !d->lap_central ||
       !d->mix_z || !d->mix_l)
@@ -1304,12 +1302,17 @@ static int premat_subg_run(const dcor_premat_subg* d, const dcor_panel* panel, d
   const size_t codes_b = dict ? (((size_t)p.s.n * 2 + 255) & ~(size_t)255) : 0;
   const size_t dict_b = dict ? 2 * 256 * sizeof(double) + 256 : 0;
   const size_t bytes = part_b + pack_b + codes_b + dict_b;
-  void* part = nullptr;
-  if (hipMallocAsync(&part, bytes, (hipStream_t)stream) != hipSuccess) {
-    (void)hipGetLastError();
-    return fail(DCOR_ENOMEM, "premat sub-G: cannot allocate %zu scratch bytes", bytes);
+  // a caller's stream-ordered scratch (the sweep's) when it is large enough: no per-launch
+  // pool allocation, whose cross-stream reuse would order one stream's launches after another's
+  const bool own = !(scratch != nullptr && scratch_b >= bytes);
+  void* part = own ? nullptr : scratch;
+  if (own) {
+    if (hipMallocAsync(&part, bytes, (hipStream_t)stream) != hipSuccess) {
+      (void)hipGetLastError();
+      return fail(DCOR_ENOMEM, "premat sub-G: cannot allocate %zu scratch bytes", bytes);
+    }
+    count_alloc();
   }
-  count_alloc();
   if (pack) {
     p.xyc = (const double2*)((char*)part + part_b);
     p.soc = p.xyc + p.s.n;
@@ -1333,7 +1336,10 @@ static int premat_subg_run(const dcor_premat_subg* d, const dcor_panel* panel, d
     // streaming kernel already reads at ~5.8 TB/s, and the epilogue's workgroups beside it
     // cost more than they hide (r01 A/B: 12.5e6 piped vs 13.0e6 serial replicates/s).
     Pipe* pp = nullptr;
-    if (int st = pipe_get(&pp)) { (void)hipFreeAsync(part, (hipStream_t)stream); return st; }
+    if (int st = pipe_get(&pp)) {
+      if (own) (void)hipFreeAsync(part, (hipStream_t)stream);
+      return st;
+    }
     const int64_t half = d->reps / 2;
     for (int h = 0; h < 2 && !rc; ++h) {
       const int64_t r0 = h ? half : 0, nr = h ? d->reps - half : half;
@@ -1359,7 +1365,7 @@ static int premat_subg_run(const dcor_premat_subg* d, const dcor_panel* panel, d
     rc = launch_premat_subg(p, d->reps, part, d_out, stream, nullptr, nullptr, pp ? pp->s : nullptr,
                             pp ? pp->fork : nullptr, pp ? pp->join : nullptr);
   }
-  (void)hipFreeAsync(part, (hipStream_t)stream);
+  if (own) (void)hipFreeAsync(part, (hipStream_t)stream);
   if (rc) return hip_fail((hipError_t)rc, "premat_subg launch");
   return DCOR_OK;
 }

@@ -264,6 +264,16 @@ int launch_draws(int kind, uint32_t k0, uint32_t k1, uint32_t site, int64_t rep_
                  int64_t reps, int64_t count, double* out, void* stream);
 int launch_perm(uint32_t k0, uint32_t k1, uint32_t site, int64_t rep_begin, int64_t reps,
                 int64_t n, int64_t count, int32_t* out, void* stream);
+// Every Philox noise array of `reps` HRS replicates in one launch: element for element the
+// launch_perm (seed_ni, DCOR_SITE_PERM) and launch_draws (Laplace seed_ni 11 / 12, Laplace
+// seed_int 13 / 14, normal 15, Laplace 16) outputs, rows [reps][count] as theirs.
+struct HrsNoise {
+  uint64_t seed_ni, seed_int;
+  int64_t rep_begin, n, k, km, nsim;
+  int32_t* perm;
+  double *lap_x, *lap_y, *lap_local, *lap_central, *mix_z, *mix_l;
+};
+int launch_hrs_noise(const HrsNoise& j, int64_t reps, void* stream);
 int launch_dp_sd(const double* x, int64_t n, double lo, double hi, double s_mu, double s_m2,
                  const double* lap2, double* out2, void* stream);
 // R-surface transforms (dcor_premat.hip): the arithmetic half of the R wrappers' DGPs and DP

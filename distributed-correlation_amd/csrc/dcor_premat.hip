@@ -1394,14 +1394,13 @@ __global__ __launch_bounds__(DCOR_BLOCK) void k_mvrnorm_apply(const double* z0, 
 }
 
 // ============================================================== draws ===
-__global__ __launch_bounds__(DCOR_BLOCK) void k_draws(int kind, uint32_t k0, uint32_t k1,
-                                                      uint32_t site, int64_t rep_begin,
-                                                      int64_t count, double* out) {
-  const int64_t r = blockIdx.y;
-  const uint32_t rep = (uint32_t)(rep_begin + r);
+// Pairs b = b0, b0 + bstride, ... of one replicate row: element 2b and 2b + 1 from Philox block
+// (b, rep, site).  The row's values do not depend on how the pairs are dealt to lanes.
+__device__ __forceinline__ void draws_span(int kind, uint32_t k0, uint32_t k1, uint32_t site,
+                                           uint32_t rep, int64_t count, double* __restrict__ o,
+                                           int64_t b0, int64_t bstride) {
   const int64_t npair = (count + 1) / 2;
-  for (int64_t b = (int64_t)blockIdx.x * DCOR_BLOCK + threadIdx.x; b < npair;
-       b += (int64_t)gridDim.x * DCOR_BLOCK) {
+  for (int64_t b = b0; b < npair; b += bstride) {
     const U4 w = draw((uint32_t)b, rep, site, k0, k1);
     double a, c;
     if (kind == 1) {
@@ -1413,10 +1412,17 @@ __global__ __launch_bounds__(DCOR_BLOCK) void k_draws(int kind, uint32_t k0, uin
       a = u53(w.w0, w.w1);
       c = u53(w.w2, w.w3);
     }
-    double* o = out + r * count;
     o[2 * b] = a;
     if (2 * b + 1 < count) o[2 * b + 1] = c;
   }
+}
+
+__global__ __launch_bounds__(DCOR_BLOCK) void k_draws(int kind, uint32_t k0, uint32_t k1,
+                                                      uint32_t site, int64_t rep_begin,
+                                                      int64_t count, double* out) {
+  const int64_t r = blockIdx.y;
+  draws_span(kind, k0, k1, site, (uint32_t)(rep_begin + r), count, out + r * count,
+             (int64_t)blockIdx.x * DCOR_BLOCK + threadIdx.x, (int64_t)gridDim.x * DCOR_BLOCK);
 }
 
 // ========================================================== permutation ===
@@ -1452,14 +1458,11 @@ __device__ __forceinline__ uint32_t feistel_pass(uint32_t x, int a, int c, const
 // as the current one lands: lanes stay busy while their walks differ in length (a loop per t
 // would run every lane of a wave to the longest of its 64 walks, ~3.4x the mean for n just
 // above a power of two).  The launcher gives every lane about 16 values of t.
-__global__ __launch_bounds__(DCOR_BLOCK) void k_perm(uint32_t k0, uint32_t k1, uint32_t site,
-                                                     int64_t rep_begin, uint32_t n, int a, int c,
-                                                     int64_t count, int32_t* out) {
-  const int64_t r = blockIdx.y;
-  const U4 kk = draw(0u, (uint32_t)(rep_begin + r), site, k0, k1);
-  int32_t* __restrict__ o = out + r * count;
-  const uint32_t stride = gridDim.x * DCOR_BLOCK, cnt = (uint32_t)count;  // count <= n < 2^31
-  uint32_t t = blockIdx.x * DCOR_BLOCK + threadIdx.x;
+__device__ __forceinline__ void perm_span(uint32_t k0, uint32_t k1, uint32_t site, uint32_t rep,
+                                          uint32_t n, int a, int c, int64_t count,
+                                          int32_t* __restrict__ o, uint32_t t, uint32_t stride) {
+  const U4 kk = draw(0u, rep, site, k0, k1);
+  const uint32_t cnt = (uint32_t)count;  // count <= n < 2^31
   uint32_t x = t;
   while (t < cnt) {
     x = feistel_pass(x, a, c, kk);
@@ -1468,6 +1471,48 @@ __global__ __launch_bounds__(DCOR_BLOCK) void k_perm(uint32_t k0, uint32_t k1, u
       t += stride;
       x = t;
     }
+  }
+}
+
+__global__ __launch_bounds__(DCOR_BLOCK) void k_perm(uint32_t k0, uint32_t k1, uint32_t site,
+                                                     int64_t rep_begin, uint32_t n, int a, int c,
+                                                     int64_t count, int32_t* out) {
+  const int64_t r = blockIdx.y;
+  perm_span(k0, k1, site, (uint32_t)(rep_begin + r), n, a, c, count, out + r * count,
+            blockIdx.x * DCOR_BLOCK + threadIdx.x, gridDim.x * DCOR_BLOCK);
+}
+
+// All seven noise arrays of an HRS launch (HrsNoise) in one grid: blockIdx.y is the replicate,
+// blockIdx.x ranges [g[i], g[i+1]) are the permutation row (i = 0) and the six draw rows, each
+// dealt exactly as its own launch would deal it (perm_span / draws_span), so every element equals
+// the separate launches' bit for bit.  One launch instead of seven: the HRS sweep's small
+// per-eps launches are launch-latency bound.
+struct HrsNoiseArgs {
+  HrsNoise j;
+  uint32_t g[8];
+  int pa, pc;
+};
+__global__ __launch_bounds__(DCOR_BLOCK) void k_hrs_noise(HrsNoiseArgs q) {
+  const int64_t r = blockIdx.y;
+  const uint32_t rep = (uint32_t)(q.j.rep_begin + r);
+  const uint32_t bx = blockIdx.x, tid = threadIdx.x;
+  const uint32_t n0 = (uint32_t)q.j.seed_ni, n1 = (uint32_t)(q.j.seed_ni >> 32);
+  const uint32_t i0 = (uint32_t)q.j.seed_int, i1 = (uint32_t)(q.j.seed_int >> 32);
+  int part = 0;
+#pragma unroll
+  for (int i = 1; i < 7; ++i) part += bx >= q.g[i] ? 1 : 0;
+  const uint32_t lo = q.g[part], span = q.g[part + 1] - lo;
+  const int64_t b0 = (int64_t)(bx - lo) * DCOR_BLOCK + tid, bs = (int64_t)span * DCOR_BLOCK;
+  const int64_t k = q.j.k, n = q.j.n, ns = q.j.nsim;
+  switch (part) {
+    case 0: perm_span(n0, n1, DCOR_SITE_PERM, rep, (uint32_t)n, q.pa, q.pc, q.j.km,
+                      q.j.perm + r * q.j.km, (uint32_t)b0, (uint32_t)bs); break;
+    case 1: draws_span(0, n0, n1, 11u, rep, k, q.j.lap_x + r * k, b0, bs); break;
+    case 2: draws_span(0, n0, n1, 12u, rep, k, q.j.lap_y + r * k, b0, bs); break;
+    case 3: draws_span(0, i0, i1, 13u, rep, n, q.j.lap_local + r * n, b0, bs); break;
+    case 4: draws_span(0, i0, i1, 14u, rep, 1, q.j.lap_central + r, b0, bs); break;
+    case 5: draws_span(1, i0, i1, 15u, rep, ns, q.j.mix_z + r * ns, b0, bs); break;
+    default: draws_span(0, i0, i1, 16u, rep, ns, q.j.mix_l + r * ns, b0, bs); break;
   }
 }
 
@@ -2189,26 +2234,53 @@ int launch_priv_standardize(const double* v, int64_t n, double L, double s_mu, d
                      n, L, s_mu, s_m2, lap2, out);
   return last_err();
 }
+static int64_t draws_gx(int64_t count) {
+  const int64_t npair = (count + 1) / 2;
+  const int64_t gx = (npair + DCOR_BLOCK - 1) / DCOR_BLOCK;
+  return gx > 4096 ? 4096 : gx;
+}
+// Values of t per lane: ~16 when the launch fills the chip many times over (C5-e2e's 8192
+// replicates: 8: 479 us, 32: 491 us, 16: 445-452 us), fewer for small launches (a sweep's 200
+// replicates), whose walks are latency bound at a few waves per SIMD.  Results never depend on it.
+static int64_t perm_gx(int64_t reps, int64_t count) {
+  int64_t v = (count * reps + 4096 * DCOR_BLOCK - 1) / (4096 * DCOR_BLOCK);
+  v = v < 2 ? 2 : (v > 16 ? 16 : v);
+  const int64_t gx = (count + v * DCOR_BLOCK - 1) / (v * DCOR_BLOCK);
+  return gx > 4096 ? 4096 : gx;
+}
+static void perm_split(int64_t n, int* a, int* c) {
+  int bits = 1;
+  while ((1ll << bits) < n) ++bits;
+  *a = bits / 2;
+  *c = bits - *a;
+}
 int launch_draws(int kind, uint32_t k0, uint32_t k1, uint32_t site, int64_t rep_begin,
                  int64_t reps, int64_t count, double* out, void* stream) {
   if (reps <= 0 || count <= 0) return 0;
-  const int64_t npair = (count + 1) / 2;
-  int64_t gx = (npair + DCOR_BLOCK - 1) / DCOR_BLOCK;
-  if (gx > 4096) gx = 4096;
-  hipLaunchKernelGGL(k_draws, dim3((unsigned)gx, (unsigned)reps), dim3(DCOR_BLOCK), 0,
+  hipLaunchKernelGGL(k_draws, dim3((unsigned)draws_gx(count), (unsigned)reps), dim3(DCOR_BLOCK), 0,
                      (hipStream_t)stream, kind, k0, k1, site, rep_begin, count, out);
   return last_err();
 }
 int launch_perm(uint32_t k0, uint32_t k1, uint32_t site, int64_t rep_begin, int64_t reps,
                 int64_t n, int64_t count, int32_t* out, void* stream) {
   if (reps <= 0 || count <= 0) return 0;
-  int bits = 1;
-  while ((1ll << bits) < n) ++bits;
-  const int a = bits / 2, c = bits - a;
-  int64_t gx = (count + 16 * DCOR_BLOCK - 1) / (16 * DCOR_BLOCK);  // ~16 values of t per lane (8: 479 us, 32: 491 us, 16: 445-452 us)
-  if (gx > 4096) gx = 4096;
-  hipLaunchKernelGGL(k_perm, dim3((unsigned)gx, (unsigned)reps), dim3(DCOR_BLOCK), 0,
-                     (hipStream_t)stream, k0, k1, site, rep_begin, (uint32_t)n, a, c, count, out);
+  int a, c;
+  perm_split(n, &a, &c);
+  hipLaunchKernelGGL(k_perm, dim3((unsigned)perm_gx(reps, count), (unsigned)reps), dim3(DCOR_BLOCK),
+                     0, (hipStream_t)stream, k0, k1, site, rep_begin, (uint32_t)n, a, c, count, out);
+  return last_err();
+}
+int launch_hrs_noise(const HrsNoise& j, int64_t reps, void* stream) {
+  if (reps <= 0) return 0;
+  HrsNoiseArgs q;
+  q.j = j;
+  perm_split(j.n, &q.pa, &q.pc);
+  const int64_t gx[7] = {j.km > 0 ? perm_gx(reps, j.km) : 0, draws_gx(j.k), draws_gx(j.k),
+                         draws_gx(j.n), draws_gx(1), draws_gx(j.nsim), draws_gx(j.nsim)};
+  q.g[0] = 0;
+  for (int i = 0; i < 7; ++i) q.g[i + 1] = q.g[i] + (uint32_t)gx[i];
+  hipLaunchKernelGGL(k_hrs_noise, dim3(q.g[7], (unsigned)reps), dim3(DCOR_BLOCK), 0,
+                     (hipStream_t)stream, q);
   return last_err();
 }
 int launch_dp_sd(const double* x, int64_t n, double lo, double hi, double s_mu, double s_m2,

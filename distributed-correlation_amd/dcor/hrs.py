@@ -172,6 +172,16 @@ def hrs_replicates(age_z, bmi_z, lam_age, lam_bmi, eps, reps, seed_ni=NI_SEED, s
             return out.cpu().numpy()
         finally:
             _lib.lib.dcor_panel_destroy(pn)
+    if rng == "philox" and not keep_noise:
+        # the launch chain natively (dcor_hrs_sweep_launch), one segment per chunk of cr runs
+        out = torch.empty((max(reps, 1), 6), **f64)
+        try:
+            _native_segments(X, Y, pn, lam_age, lam_bmi, nsim, alpha,
+                             [(eps, seed_ni, seed_int, rep_begin + r0, min(cr, reps - r0), r0)
+                              for r0 in range(0, reps, cr)], out, stream)
+            return out[:reps].cpu().numpy()
+        finally:
+            _lib.lib.dcor_panel_destroy(pn)
     perm = torch.empty((cr, k * m), dtype=torch.int32, device="cuda")
     lx, ly = torch.empty((cr, k), **f64), torch.empty((cr, k), **f64)
     ll, lc = torch.empty((cr, n), **f64), torch.empty((cr,), **f64)
@@ -215,6 +225,40 @@ def _summ(method, eps, hat, lo, hi) -> dict:
             "ci_low_q10": q(lo, 0.10), "ci_high_q90": q(hi, 0.90)}
 
 
+def _native_segments(X, Y, pn, lam_age, lam_bmi, nsim, alpha, rowsegs, out, stream):
+    """Enqueue (eps, seed_ni, seed_int, first run, count, output row) segments on `stream` with one
+    dcor_hrs_sweep_launch: per segment the seven Philox noise arrays in one launch, then the
+    pre-materialised panel kernels, records to out[row ..]."""
+    import ctypes as C
+
+    from . import _lib
+    if not rowsegs:
+        return
+    n = int(X.shape[0])
+    base = _lib.PrematSubg(n=n, reps=0, eps1=1.0, eps2=1.0, eta1=1.0, eta2=1.0, alpha=alpha, hrs=1,
+                           lam_x=lam_age, lam_y=lam_bmi, lam_s=lam_age, lam_o=lam_bmi, lam_r=float("nan"),
+                           delta=1.0 / n, nsim=nsim, X=X.data_ptr(), Y=Y.data_ptr(), xy_stride=0)
+    arr = (_lib.HrsSegment * len(rowsegs))(*[
+        _lib.HrsSegment(eps=e, seed_ni=sn, seed_int=si, rep_begin=r0, reps=c, out_row=row)
+        for e, sn, si, r0, c, row in rowsegs])
+    _lib.check(_lib.lib.dcor_hrs_sweep_launch(C.byref(base), pn, arr, len(rowsegs),
+                                              C.c_void_p(out.data_ptr()), C.c_void_p(stream.cuda_stream)))
+
+
+_SIDE = {}
+
+
+def _side_streams(ns):
+    """ns HIP streams of the current device, created once per process (stream creation and
+    destruction cost more than a sweep's launches)."""
+    import torch
+    dev = torch.cuda.current_device()
+    pool = _SIDE.setdefault(dev, [])
+    while len(pool) < ns:
+        pool.append(torch.cuda.Stream(device=dev))
+    return pool[:ns]
+
+
 def sweep_segments(age_z, bmi_z, lam_age, lam_bmi, eps_grid, segs, nsim=2000, alpha=0.05, streams=1):
     """Philox pre-materialised runs of several (eps index 0-based, first run, count) segments of
     an eps sweep on one shared panel -> [sum(count), 6] float64 in segment order.  Each segment's
@@ -239,23 +283,15 @@ def sweep_segments(age_z, bmi_z, lam_age, lam_bmi, eps_grid, segs, nsim=2000, al
     _lib.check(_lib.lib.dcor_panel_create(C.c_void_p(X.data_ptr()), C.c_void_p(Y.data_ptr()), n,
                                           C.c_void_p(main.cuda_stream), C.byref(pn)))
     out = torch.empty((max(total, 1), 6), dtype=torch.float64, device="cuda")
-    base = _lib.PrematSubg(n=n, reps=0, eps1=1.0, eps2=1.0, eta1=1.0, eta2=1.0, alpha=alpha, hrs=1,
-                           lam_x=lam_age, lam_y=lam_bmi, lam_s=lam_age, lam_o=lam_bmi, lam_r=float("nan"),
-                           delta=1.0 / n, nsim=nsim, X=X.data_ptr(), Y=Y.data_ptr(), xy_stride=0)
-    arr = (_lib.HrsSegment * max(1, len(segs)))()
-    for j, (e, r0, c) in enumerate(segs):
-        arr[j] = _lib.HrsSegment(eps=eps_grid[e], seed_ni=10 + 1000 * (e + 1), seed_int=20 + 1000 * (e + 1),
-                                 rep_begin=r0, reps=c, out_row=int(rows[j]))
+    rowsegs = [(eps_grid[e], 10 + 1000 * (e + 1), 20 + 1000 * (e + 1), r0, c, int(rows[j]))
+               for j, (e, r0, c) in enumerate(segs)]
     ns = max(1, min(streams, len(segs)))
-    side = [torch.cuda.Stream() for _ in range(ns)] if ns > 1 else [main]
+    side = _side_streams(ns) if ns > 1 else [main]
     try:
         for j, s in enumerate(side):
             if s is not main:
                 s.wait_stream(main)              # X, Y, the panel and out exist before any launch
-            mine = list(range(j, len(segs), ns))
-            part = (_lib.HrsSegment * max(1, len(mine)))(*[arr[i] for i in mine])
-            _lib.check(_lib.lib.dcor_hrs_sweep_launch(C.byref(base), pn, part, len(mine),
-                                                      C.c_void_p(out.data_ptr()), C.c_void_p(s.cuda_stream)))
+            _native_segments(X, Y, pn, lam_age, lam_bmi, nsim, alpha, rowsegs[j::ns], out, s)
         for s in side:
             if s is not main:
                 main.wait_stream(s)

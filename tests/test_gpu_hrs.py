@@ -139,16 +139,17 @@ def test_eps_sweep_summaries(panel):
 
 @pytest.mark.parametrize("kind", ["coded", "continuous"])
 def test_sweep_segments_equal_per_eps_calls(panel, kind):
-    """hrs.sweep_segments (one encoded panel, launch chains spread over HIP streams, one wait)
-    equals one hrs_replicates call per segment with the sweep's keys, byte for byte, whatever the
-    number of streams; segments start mid-eps (rep_begin > 0) as a rank's shard does."""
+    """hrs.sweep_segments (one encoded panel, the native launch chain dcor_hrs_sweep_launch with
+    its one-launch noise kernel, optionally over HIP streams, one wait) equals the host-driven
+    chain (hrs_replicates with keep_noise: the seven noise launches from Python) per segment with
+    the sweep's keys, byte for byte; segments start mid-eps (rep_begin > 0) as a rank's shard does."""
     from dcor import hrs
     z = panel if kind == "coded" else _continuous(2501, seed=9)
     args = (z["age_z"], z["bmi_z"], z["lambda_age_z"], z["lambda_bmi_z"])
     grid = (0.25, 1.05, 2.45)
     segs = [(0, 3, 5), (1, 0, 7), (2, 2, 1), (0, 8, 2), (1, 7, 3)]
     want = np.concatenate([hrs.hrs_replicates(*args, grid[e], c, seed_ni=10 + 1000 * (e + 1),
-                                              seed_int=20 + 1000 * (e + 1), rep_begin=r0)
+                                              seed_int=20 + 1000 * (e + 1), rep_begin=r0, keep_noise=True)[0]
                            for e, r0, c in segs])
     for streams in (1, 4):
         got = hrs.sweep_segments(*args, grid, segs, streams=streams)
@@ -160,13 +161,27 @@ def test_sweep_segments_equal_per_eps_calls(panel, kind):
 
 
 def test_sweep_segments_past_one_launch(panel):
-    """A segment longer than one launch (8192 runs) splits like hrs_replicates' chunks."""
+    """A segment longer than one launch chain (8192 runs) splits like the host-driven chunks."""
     from dcor import hrs
     z = panel
     args = (z["age_z"], z["bmi_z"], z["lambda_age_z"], z["lambda_bmi_z"])
     got = hrs.sweep_segments(*args, (2.0,), [(0, 5, 8195)], streams=2)
-    want = hrs.hrs_replicates(*args, 2.0, 8195, seed_ni=1010, seed_int=1020, rep_begin=5)
+    want = hrs.hrs_replicates(*args, 2.0, 8195, seed_ni=1010, seed_int=1020, rep_begin=5, keep_noise=True)[0]
     np.testing.assert_array_equal(got.view(np.int64), want.view(np.int64))
+
+
+@pytest.mark.parametrize("kind", ["coded", "continuous"])
+def test_native_chain_equals_host_chain(panel, kind):
+    """hrs_replicates' native chain (rng='philox', no keep_noise) equals the host-driven chain
+    (keep_noise=True: perm + six draw launches from Python, each checked against the oracle in
+    _check_against_oracle) byte for byte, chunked or not."""
+    from dcor import hrs
+    z = panel if kind == "coded" else _continuous(2501, seed=4)
+    args = (z["age_z"], z["bmi_z"], z["lambda_age_z"], z["lambda_bmi_z"], 0.85)
+    host = hrs.hrs_replicates(*args, 7, seed_ni=5, seed_int=6, rep_begin=2, keep_noise=True)[0]
+    for chunk in (3, 8192):
+        nat = hrs.hrs_replicates(*args, 7, seed_ni=5, seed_int=6, rep_begin=2, chunk=chunk)
+        np.testing.assert_array_equal(nat.view(np.int64), host.view(np.int64), err_msg=f"chunk={chunk}")
 
 
 def test_panel_pipelined_halves_bitexact(panel):
