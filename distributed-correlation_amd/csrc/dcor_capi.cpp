@@ -1635,8 +1635,8 @@ int dcor_draws_launch(int kind, uint64_t seed, int site, int64_t rep_begin, int6
   if (kind < 0 || kind > 2 || reps < 0 || count < 0 || (reps * count > 0 && !d_out))
     return fail(DCOR_EINVAL, "bad draws arguments");
   if (reps > 65535) return fail(DCOR_EINVAL, "draws: at most 65535 replicates per launch");
-  if (rep_begin < 0 || rep_begin + reps > 0xffffffffLL || (count + 1) / 2 > 0xffffffffLL)
-    return fail(DCOR_EINVAL, "draws: counter range exceeds 2^32");
+  if (rep_begin < 0 || rep_begin + reps > 0xffffffffLL || count > 0x7fffffffLL)
+    return fail(DCOR_EINVAL, "draws: need rep_begin + reps <= 2^32 and count < 2^31");
   if (int st = need_device()) return st;
   const int rc = launch_draws(kind, (uint32_t)seed, (uint32_t)(seed >> 32), (uint32_t)site,
                               rep_begin, reps, count, d_out, stream);

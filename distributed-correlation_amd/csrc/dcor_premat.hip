@@ -1396,12 +1396,15 @@ __global__ __launch_bounds__(DCOR_BLOCK) void k_mvrnorm_apply(const double* z0, 
 // ============================================================== draws ===
 // Pairs b = b0, b0 + bstride, ... of one replicate row: element 2b and 2b + 1 from Philox block
 // (b, rep, site).  The row's values do not depend on how the pairs are dealt to lanes.
+// 32-bit pair indices: count < 2^31 (the launchers' rows), so the loop and its store offsets need
+// no 64-bit arithmetic.
 __device__ __forceinline__ void draws_span(int kind, uint32_t k0, uint32_t k1, uint32_t site,
                                            uint32_t rep, int64_t count, double* __restrict__ o,
-                                           int64_t b0, int64_t bstride) {
-  const int64_t npair = (count + 1) / 2;
-  for (int64_t b = b0; b < npair; b += bstride) {
-    const U4 w = draw((uint32_t)b, rep, site, k0, k1);
+                                           int64_t b0_, int64_t bstride_) {
+  const uint32_t npair = (uint32_t)((count + 1) / 2), bstride = (uint32_t)bstride_;
+  const uint32_t cnt = (uint32_t)count;
+  for (uint32_t b = (uint32_t)b0_; b < npair; b += bstride) {
+    const U4 w = draw(b, rep, site, k0, k1);
     double a, c;
     if (kind == 1) {
       normal_pair(w, &a, &c);
@@ -1412,8 +1415,8 @@ __device__ __forceinline__ void draws_span(int kind, uint32_t k0, uint32_t k1, u
       a = u53(w.w0, w.w1);
       c = u53(w.w2, w.w3);
     }
-    o[2 * b] = a;
-    if (2 * b + 1 < count) o[2 * b + 1] = c;
+    o[2u * b] = a;
+    if (2u * b + 1u < cnt) o[2u * b + 1u] = c;
   }
 }
 

@@ -435,7 +435,8 @@ int dcor_mix_gaussian(const double* z0, int64_t n0, const double* z1, int64_t n1
 /* On-device unit draws from the engine's Philox streams (pre-materialised inputs
  * generated in HBM, e.g. the HRS noise of BASELINE config C5).  kind: 0 unit Laplace,
  * 1 standard normal (Box-Muller pairs), 2 uniform (0,1).  Element e of replicate r uses
- * block (e/2, r, site) and words (0,1) / (2,3) for e even / odd.  d_out: [reps][count]. */
+ * block (e/2, r, site) and words (0,1) / (2,3) for e even / odd.  d_out: [reps][count];
+ * count < 2^31, rep_begin + reps <= 2^32, reps <= 65535. */
 int dcor_draws_launch(int kind, uint64_t seed, int site, int64_t rep_begin, int64_t reps,
                       int64_t count, double* d_out, void* stream);
 
