@@ -170,6 +170,48 @@ def test_sweep_segments_past_one_launch(panel):
     np.testing.assert_array_equal(got.view(np.int64), want.view(np.int64))
 
 
+def test_sweep_launch_checks_every_segment_first(panel):
+    """dcor_hrs_sweep_launch rejects a bad segment (eps <= 0, negative counts) or a base that is
+    not the panel's before it enqueues anything: the output rows stay untouched; an empty segment
+    list or zero-run segments are no-ops."""
+    import ctypes as C
+
+    import torch
+    from dcor import _lib
+    z = panel
+    X = torch.as_tensor(z["age_z"], device="cuda")
+    Y = torch.as_tensor(z["bmi_z"], device="cuda")
+    n = int(X.shape[0])
+    s = torch.cuda.current_stream()
+    sp = C.c_void_p(s.cuda_stream)
+    pn = C.c_void_p()
+    _lib.check(_lib.lib.dcor_panel_create(C.c_void_p(X.data_ptr()), C.c_void_p(Y.data_ptr()), n, sp, C.byref(pn)))
+    try:
+        out = torch.full((8, 6), 7.0, dtype=torch.float64, device="cuda")
+        base = _lib.PrematSubg(n=n, eta1=1.0, eta2=1.0, alpha=0.05, hrs=1, lam_x=z["lambda_age_z"],
+                               lam_y=z["lambda_bmi_z"], lam_s=z["lambda_age_z"], lam_o=z["lambda_bmi_z"],
+                               delta=1.0 / n, nsim=2000, X=X.data_ptr(), Y=Y.data_ptr())
+        good = _lib.HrsSegment(eps=2.0, seed_ni=1, seed_int=2, rep_begin=0, reps=4, out_row=0)
+        for bad in (dict(eps=0.0), dict(eps=-1.0), dict(reps=-1), dict(rep_begin=-2), dict(out_row=-1)):
+            seg = _lib.HrsSegment(**{**dict(eps=1.0, seed_ni=1, seed_int=2, rep_begin=0, reps=4, out_row=4), **bad})
+            arr = (_lib.HrsSegment * 2)(good, seg)
+            st = _lib.lib.dcor_hrs_sweep_launch(C.byref(base), pn, arr, 2, C.c_void_p(out.data_ptr()), sp)
+            assert st == _lib.DCOR_EINVAL, bad
+        other = _lib.PrematSubg.from_buffer_copy(bytes(base))
+        other.n = n - 1
+        arr = (_lib.HrsSegment * 1)(good)
+        assert _lib.lib.dcor_hrs_sweep_launch(C.byref(other), pn, arr, 1, C.c_void_p(out.data_ptr()), sp) == _lib.DCOR_EINVAL
+        torch.cuda.synchronize()
+        assert bool((out == 7.0).all())
+        empty = (_lib.HrsSegment * 1)(_lib.HrsSegment(eps=2.0, reps=0, out_row=0))
+        _lib.check(_lib.lib.dcor_hrs_sweep_launch(C.byref(base), pn, empty, 0, C.c_void_p(out.data_ptr()), sp))
+        _lib.check(_lib.lib.dcor_hrs_sweep_launch(C.byref(base), pn, empty, 1, C.c_void_p(out.data_ptr()), sp))
+        torch.cuda.synchronize()
+        assert bool((out == 7.0).all())
+    finally:
+        _lib.lib.dcor_panel_destroy(pn)
+
+
 @pytest.mark.parametrize("kind", ["coded", "continuous"])
 def test_native_chain_equals_host_chain(panel, kind):
     """hrs_replicates' native chain (rng='philox', no keep_noise) equals the host-driven chain
