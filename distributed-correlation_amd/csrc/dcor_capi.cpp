@@ -1223,9 +1223,12 @@ int dcor_hrs_sweep_launch(const dcor_premat_subg* base, const dcor_panel* panel,
     return fail(DCOR_EINVAL, "hrs_sweep: X, Y, n must be the panel's and xy_stride 0");
   if (!base->hrs) return fail(DCOR_EINVAL, "hrs_sweep: the HRS variant only (hrs = 1)");
   if (!(base->delta > 0.0)) return fail(DCOR_EINVAL, "hrs_sweep: delta must be positive");
-  // every segment's geometry first: nothing is enqueued for an invalid sweep
-  std::vector<dcor_premat_subg> qs((size_t)nseg);
-  std::vector<int64_t> ks((size_t)nseg), ms((size_t)nseg);
+  // every segment's constants and geometry first: nothing is enqueued for an invalid sweep
+  struct SegPlan {
+    dcor_premat_subg q;
+    int64_t k, m, cr;
+  };
+  std::vector<SegPlan> plan((size_t)nseg);
   size_t need = 0;
   int64_t cap = 0;
   // noise of up to 8192 replicates per launch chain (C5's 8192 x 420 KB: 3.4 GB), at most 4 GB
@@ -1235,17 +1238,22 @@ int dcor_hrs_sweep_launch(const dcor_premat_subg* base, const dcor_panel* panel,
     if (g.reps < 0 || g.rep_begin < 0 || g.out_row < 0 || !(g.eps > 0.0))
       return fail(DCOR_EINVAL, "hrs_sweep: segment %lld: need eps > 0, reps, rep_begin, out_row >= 0",
                   (long long)i);
-    dcor_premat_subg& q = qs[(size_t)i];
+    if (g.rep_begin + g.reps > 0xffffffffLL)
+      return fail(DCOR_EINVAL, "hrs_sweep: segment %lld: replicate range exceeds 2^32", (long long)i);
+    SegPlan& sp = plan[(size_t)i];
+    dcor_premat_subg& q = sp.q;
     q = *base;
     q.reps = g.reps;
     q.eps1 = q.eps2 = g.eps;
     q.eta1 = q.eta2 = 1.0;
     q.lam_r = dcor_lambda_receiver_from_noise(base->lam_s, base->lam_o, g.eps, base->delta);
+    PrematSubgConst pc;   // the launch constants' own checks, here rather than mid-sweep
+    if (int st = premat_subg_const(&q, pc)) return st;
     size_t per;
-    if (int st = hrs_noise_geometry(&q, &ks[(size_t)i], &ms[(size_t)i], &per)) return st;
-    const int64_t cr = hrs_chunk(per, g.reps, budget, 8192);
-    need = std::max(need, per * (size_t)cr);
-    cap = std::max(cap, cr);
+    if (int st = hrs_noise_geometry(&q, &sp.k, &sp.m, &per)) return st;
+    sp.cr = hrs_chunk(per, g.reps, budget, 8192);
+    need = std::max(need, per * (size_t)sp.cr);
+    cap = std::max(cap, sp.cr);
   }
   if (need == 0) return DCOR_OK;
   if (int st = need_device()) return st;
@@ -1263,13 +1271,10 @@ int dcor_hrs_sweep_launch(const dcor_premat_subg* base, const dcor_panel* panel,
   int e = DCOR_OK;
   for (int64_t i = 0; i < nseg && !e; ++i) {
     const dcor_hrs_segment& g = segs[i];
+    const SegPlan& sp = plan[(size_t)i];
     if (g.reps == 0) continue;
-    size_t per;
-    int64_t k, m;
-    if ((e = hrs_noise_geometry(&qs[(size_t)i], &k, &m, &per))) break;
-    const int64_t cr = hrs_chunk(per, g.reps, budget, 8192);
-    e = hrs_premat_chunks(&qs[(size_t)i], panel, g.seed_ni, g.seed_int, g.rep_begin,
-                          d_out + g.out_row, buf, cr, k, m, stream, buf + need, scr_b);
+    e = hrs_premat_chunks(&sp.q, panel, g.seed_ni, g.seed_int, g.rep_begin, d_out + g.out_row, buf,
+                          sp.cr, sp.k, sp.m, stream, buf + need, scr_b);
   }
   (void)hipFreeAsync(buf, st);
   return e;

@@ -171,9 +171,9 @@ def test_sweep_segments_past_one_launch(panel):
 
 
 def test_sweep_launch_checks_every_segment_first(panel):
-    """dcor_hrs_sweep_launch rejects a bad segment (eps <= 0, negative counts) or a base that is
-    not the panel's before it enqueues anything: the output rows stay untouched; an empty segment
-    list or zero-run segments are no-ops."""
+    """dcor_hrs_sweep_launch rejects a bad segment (eps <= 0, negative counts, a replicate range past
+    2^32) or a bad base (not the panel's n, nsim 0, delta 0, not HRS) before it enqueues anything:
+    the output rows stay untouched; an empty segment list or zero-run segments are no-ops."""
     import ctypes as C
 
     import torch
@@ -197,10 +197,14 @@ def test_sweep_launch_checks_every_segment_first(panel):
             arr = (_lib.HrsSegment * 2)(good, seg)
             st = _lib.lib.dcor_hrs_sweep_launch(C.byref(base), pn, arr, 2, C.c_void_p(out.data_ptr()), sp)
             assert st == _lib.DCOR_EINVAL, bad
-        other = _lib.PrematSubg.from_buffer_copy(bytes(base))
-        other.n = n - 1
         arr = (_lib.HrsSegment * 1)(good)
-        assert _lib.lib.dcor_hrs_sweep_launch(C.byref(other), pn, arr, 1, C.c_void_p(out.data_ptr()), sp) == _lib.DCOR_EINVAL
+        for field, value in (("n", n - 1), ("nsim", 0), ("delta", 0.0), ("hrs", 0)):
+            other = _lib.PrematSubg.from_buffer_copy(bytes(base))
+            setattr(other, field, value)
+            st = _lib.lib.dcor_hrs_sweep_launch(C.byref(other), pn, arr, 1, C.c_void_p(out.data_ptr()), sp)
+            assert st == _lib.DCOR_EINVAL, field
+        far = (_lib.HrsSegment * 1)(_lib.HrsSegment(eps=2.0, seed_ni=1, seed_int=2, rep_begin=2**32 - 2, reps=4))
+        assert _lib.lib.dcor_hrs_sweep_launch(C.byref(base), pn, far, 1, C.c_void_p(out.data_ptr()), sp) == _lib.DCOR_EINVAL
         torch.cuda.synchronize()
         assert bool((out == 7.0).all())
         empty = (_lib.HrsSegment * 1)(_lib.HrsSegment(eps=2.0, reps=0, out_row=0))
